@@ -1,0 +1,230 @@
+"""Headline benchmark: query faces/sec, Fisherfaces projection + 1-NN against a 1M-image gallery.
+
+Workload (BASELINE.json configs[2], which fits one MI355X: the 1M x 9999 fp32
+gallery is 40 GB of the 288 GB HBM): synthetic 100x100 uint8 faces (D=10000),
+a Fisherfaces projection to d=9999 (= c-1 for 10k identities, thetrainer.py
+get_model defaults), a 1M-row gallery (100k identities x 10 images), batches of
+B=4096 query faces, k=1, Euclidean distance.  One step = project the batch
+(ofr_project_u8) + MFMA search pass (ofr_knn_tiles_f32) + merge / exact fp64
+re-rank (ofr_knn_merge_f32) [+ all-gather + ofr_topk_merge when sharded].
+Inputs are resident in HBM before the timed region.  W is random (no trained
+checkpoint exists at this scale), gallery/queries are synthetic (see
+opencv_facerecognizer_amd/synthetic.py).
+
+Multi-GPU (torch.distributed.run, one process per GPU): the 1M gallery is
+sharded by rows over the ranks, the query batch is replicated, and the per-rank
+top-k lists are merged after one RCCL all-gather -> strong scaling (total work
+fixed).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from opencv_facerecognizer_amd import _lib  # noqa: E402
+from opencv_facerecognizer_amd._device import FloatGallery, Projection, round_up  # noqa: E402
+from opencv_facerecognizer_amd.parallel import exchange_topk, merge_topk, shard_range  # noqa: E402
+from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
+
+PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
+PEAK_HBM = 8.0e12           # HBM3E 8 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--gallery", type=int, default=1_000_000)
+    ap.add_argument("--per-id", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--dim", type=int, default=9999)
+    ap.add_argument("--side", type=int, default=100)
+    ap.add_argument("--k", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build_projection(D, d, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(SEED + 5)
+    P = Projection.__new__(Projection)
+    P.D, P.d = D, d
+    P.ldw = max(32, round_up(D, 32))
+    P.Wt = torch.zeros((d, P.ldw), dtype=torch.float32, device=device)
+    P.Wt[:, :D] = torch.randn((d, D), generator=g, device=device) / np.sqrt(D)
+    P.shift = None
+    P.ldy = max(32, round_up(d, 32))
+    return P
+
+
+def cpu_baseline(P, gallery, Xq, ids_q, N_total, seconds):
+    """Reference-faithful oracle (classifier.py:104-108 loop, 1 Python thread) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import facerec_oracle as O  # the checker; timed here as the CPU baseline
+    n_s = min(4000, gallery.N)
+    G_s = gallery.G[:n_s, : gallery.d].double().cpu().numpy() + gallery.shift.double().cpu().numpy()
+    W = P.Wt[:, : P.D].double().cpu().numpy().T.copy()      # D x d, float64 like the reference
+    X = Xq.cpu().numpy()
+    t_proj, t_item, nq = 0.0, 0.0, 0
+    deadline = time.perf_counter() + seconds
+    while time.perf_counter() < deadline and nq < len(X):
+        t0 = time.perf_counter()
+        q = O.fisherfaces_project(W, X[nq])                  # feature.py:241-242
+        t1 = time.perf_counter()
+        for gi in G_s:                                       # classifier.py:104-108
+            O.euclidean(gi.reshape(-1, 1), q)
+        t2 = time.perf_counter()
+        t_proj += t1 - t0
+        t_item += (t2 - t1) / n_s
+        nq += 1
+    per_query = t_proj / nq + (t_item / nq) * N_total
+    # vectorised float64 mode (BLAS, all cores) on the same sample
+    t0 = time.perf_counter()
+    Qv = X[: min(64, len(X))].astype(np.float64) @ W
+    O.nn_search_vectorized("EuclideanDistance", Qv, G_s, 1)
+    tv = (time.perf_counter() - t0) / len(Qv)
+    per_query_vec = tv * (N_total / n_s)   # dominated by the distance pass, linear in N
+    return {
+        "value": 1.0 / per_query, "unit": "queries/s", "cores": 1, "kind": "port",
+        "sample": f"{nq} queries x {n_s} gallery rows, d={gallery.d}, D={P.D}: reference-faithful per-item "
+                  f"distance loop + W^T x, extrapolated linearly to N={N_total}",
+        "per_item_us": 1e6 * t_item / nq, "projection_ms": 1e3 * t_proj / nq,
+        "vectorized_f64": {"value": 1.0 / per_query_vec, "unit": "queries/s", "cores": os.cpu_count(),
+                           "sample": f"{len(Qv)} queries x {n_s} rows, BLAS, extrapolated to N={N_total}"},
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    _lib.device()
+
+    H = W = args.side
+    D, d, k, B = H * W, args.dim, args.k, args.batch
+    N = args.gallery
+    n_ids = (N + args.per_id - 1) // args.per_id
+    n0, n1 = shard_range(N, rank, world)
+    nl = n1 - n0
+
+    # ---- setup (untimed): W, gallery shard, queries -------------------------------------
+    t0 = time.perf_counter()
+    P = build_projection(D, d, device)
+    bank = IdentityBank(n_ids, H, W, device=device)
+    ld = max(32, round_up(d, 32))
+    G = torch.zeros((nl, ld), dtype=torch.float32, device=device)
+    chunk = 8192
+    for c0 in range(0, nl, chunk):
+        c1 = min(nl, c0 + chunk)
+        rows = torch.arange(n0 + c0, n0 + c1, device=device)
+        imgs = bank.images(rows // args.per_id, seed=SEED + 1000 + (n0 + c0) // chunk)
+        P.project_u8(imgs, out=G[c0:c1])
+    gallery = FloatGallery(G, _lib.METRIC_EUCLIDEAN, d=d, device=device)
+    gq = torch.Generator(device=device)
+    gq.manual_seed(SEED + 7)
+    ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
+    Xq = bank.images(ids_q, seed=SEED + 99)
+    Qd = torch.zeros((B, ld), dtype=torch.float32, device=device)
+    out = (torch.empty((B, k), dtype=torch.float64, device=device), torch.empty((B, k), dtype=torch.int64, device=device))
+    torch.cuda.synchronize()
+    log(rank, f"setup {time.perf_counter() - t0:.1f}s: gallery rows {nl}/{N} per rank, d={d}, D={D}, B={B}")
+
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+
+    def step(events=None):
+        if events:
+            events[0].record()
+        P.project_u8(Xq, out=Qd, shift=gallery.shift)              # W^T x - mu (centred for Euclidean)
+        if events:
+            events[1].record()
+        gallery.search_phase("tiles", Qd, k)
+        if events:
+            events[2].record()
+        gallery.search_phase("merge", Qd, k, index_base=n0, out=out)
+        if events:
+            events[3].record()
+        if world > 1:
+            gd, gi = exchange_topk(out[0], out[1])
+            return merge_topk(gd, gi, world, k, k)
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for s in range(args.steps):
+        res = step(ev[s])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_proj = np.mean([e[0].elapsed_time(e[1]) for e in ev])
+    ms_tiles = np.mean([e[1].elapsed_time(e[2]) for e in ev])
+    ms_merge = np.mean([e[2].elapsed_time(e[3]) for e in ev])
+    idx = res[1][:, 0]
+    acc = float(((idx // args.per_id) == ids_q).double().mean().item())
+
+    flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
+    achieved = flops_tiles / (ms_tiles * 1e-3)
+    alg_bytes_tiles = nl * d * 4 + B * d * 4                         # gallery + queries read once
+
+    if rank == 0:
+        value = B * args.steps / elapsed
+        result = {
+            "metric": "query faces/sec (Fisherfaces proj + 1-NN, 1M gallery) at 1/2/4/8 GPUs",
+            "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32 (fp32 MFMA scores, fp64 exact re-rank)", "data": "synthetic",
+            "config": {"workload": "configs[2]: Fisherfaces projection + 1-NN, 1M-image gallery (100k ids x 10), "
+                                   "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1",
+                       "gallery": N, "global_batch": B, "d": d, "D": D, "k": k,
+                       "parallelism": f"gallery-rows/{world} + RCCL all-gather of top-k" if world > 1 else "1 GPU"},
+            "roofline": {"kernel": "knn_tile_kernel (ofr_knn_tiles_f32)", "bound": "mfma",
+                         "achieved": achieved / 1e12, "peak": PEAK_FP32_MFMA / 1e12, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP32_MFMA, "traffic": None,
+                         "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
+                         "launch_ms": ms_tiles},
+            "kernels_ms": {"project_u8": ms_proj, "knn_tiles": ms_tiles, "knn_merge_rerank": ms_merge},
+            "top1_identity_acc": acc,
+        }
+        if world == 1 and not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(P, gallery, Xq, ids_q, N, args.cpu_seconds)
+            result["speedup_vs_cpu"] = value / result["cpu_baseline"]["value"]
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,193 @@
+/*
+ * ofr.h — C ABI of libocvf_hip.so, the MI355X (gfx950) implementation of the
+ * ocvfacerec / bytefish-facerec recognition hot path.
+ *
+ * The reference (sandykindy/opencv_facerecognizer, Python 2.7 + numpy) has no
+ * FFI: its hot path is the Python class API of src/ocvfacerec/facerec/.
+ * Each entry point below replaces the numpy expression cited next to it; the
+ * Python host package (opencv_facerecognizer_amd/, importable as
+ * `ocvfacerec`) keeps the reference's classes and calls these functions
+ * through ctypes.  Reference paths are relative to
+ * /root/reference/src/ocvfacerec/.
+ *
+ * Conventions
+ *   - Every function returns int: 0 = OFR_OK, negative = ofr error code
+ *     (enum below), positive = hipError_t passed through.  The library never
+ *     aborts or exits.  ofr_last_error() returns a thread-local message.
+ *   - All array arguments are caller-owned DEVICE pointers (e.g. torch
+ *     tensor data_ptr()); the library keeps no pointer past a call.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *     calls are stream-ordered and asynchronous.
+ *   - Matrices are row-major with an explicit leading dimension `ld*` in
+ *     ELEMENTS.  Float operands of the MFMA GEMMs use ld % 32 == 0 and the
+ *     columns [K, round_up(K,32)) of every row must be zero (the padding is
+ *     part of the device layout the host package owns).
+ */
+#ifndef OFR_H
+#define OFR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum ofr_status {
+  OFR_OK = 0,
+  OFR_E_INVALID = -1,     /* bad argument (shape, stride, alignment, null) */
+  OFR_E_UNSUPPORTED = -2, /* valid but not implemented (e.g. k > OFR_MAX_K) */
+  OFR_E_DEVICE = -3,      /* no usable gfx950 device */
+};
+
+enum ofr_metric {
+  OFR_METRIC_EUCLIDEAN = 0, /* distance.py:53-60  sqrt(sum((p-q)^2))            */
+  OFR_METRIC_COSINE = 1,    /* distance.py:63-77  -p.q / sqrt((p.p)(q.q))        */
+  OFR_METRIC_CHISQUARE = 2, /* distance.py:101-116 sum((p-q)^2/(p+q+eps))        */
+};
+
+#define OFR_MAX_K 16          /* largest k of the fused search (classifier.py:53-129) */
+#define OFR_TILE_ROWS 256     /* gallery rows per search tile                          */
+
+/* Library / context ------------------------------------------------------ */
+int ofr_version(void);                 /* (major<<16)|(minor<<8)|patch */
+const char* ofr_last_error(void);      /* thread-local, never NULL      */
+int ofr_device_check(int device);      /* OFR_OK iff `device` is gfx950 */
+
+/* Projection ---------------------------------------------------------------
+ * Y[b][j] = sum_i X[b][i] * Wt[j][i] - shift[j]     (b < B, j < d, i < D)
+ * Replaces Fisherfaces.project  feature.py:241-242 (np.dot(W.T, x), shift=NULL),
+ *          PCA.project          feature.py:114-116 (shift = P^T mu),
+ *          LDA.project          feature.py:184-185, and the per-sample
+ *          projection loops feature.py:104-108, 178-182, 231-235.
+ * X : uint8 [B][ldx], ldx % 16 == 0, bytes [D, ldx) ignored.
+ * Wt: fp32 [d][ldw] (= W transposed), ldw % 32 == 0, zero beyond D.
+ * Y : fp32 [B][ldy]; only columns j < d are written.
+ * fp32 MFMA (v_mfma_f32_32x32x2_f32), exact f32 products, f32 accumulation. */
+int ofr_project_u8(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx,
+                   const float* Wt, int64_t d, int64_t ldw, const float* shift, float* Y,
+                   int64_t ldy);
+
+/* Same with fp32 inputs X [B][ldx] (ldx % 32 == 0, zero beyond D).          */
+int ofr_project_f32(void* stream, const float* X, int64_t B, int64_t D, int64_t ldx,
+                    const float* Wt, int64_t d, int64_t ldw, const float* shift, float* Y,
+                    int64_t ldy);
+
+/* Gallery preparation ------------------------------------------------------
+ * For the search kernels: aux[n] = ||G[n]||^2 (EUCLIDEAN) or 1/||G[n]|| (COSINE),
+ * computed in fp64 and stored fp32.  G [N][ldg] fp32.                       */
+int ofr_row_aux(void* stream, int metric, const float* G, int64_t N, int64_t d, int64_t ldg,
+                float* aux);
+/* mean[j] = (1/N) sum_n G[n][j] in fp64 (column means of the gallery).      */
+int ofr_col_mean(void* stream, const float* G, int64_t N, int64_t d, int64_t ldg, double* mean);
+/* G[n][j] -= shift[j] for j < d (fp32).                                     */
+int ofr_sub_rows(void* stream, float* G, int64_t N, int64_t d, int64_t ldg, const float* shift);
+
+/* k-nearest-neighbour search ----------------------------------------------
+ * Replaces NearestNeighbor.predict classifier.py:76-129 (the per-item
+ * distance loop :104-108, argsort :113 and top-k slice :118-119) for a
+ * BATCH of B queries against N gallery rows.
+ *   pass 1  (MFMA tile kernel): coarse scores s = aux[n] - 2 q.g (EUCLIDEAN,
+ *           on centred features) or -(q.g) aux[n] (COSINE); per 256-row
+ *           gallery tile, the best OFR_KC candidates per query.
+ *   pass 2  merge of the tile candidates, EXACT fp64 re-evaluation of the
+ *           reference distance on the R best candidates, sort by
+ *           (distance, index) — ties resolve to the lowest gallery index.
+ * Outputs: out_d [B][k] fp64 distances, out_i [B][k] int64 gallery indices
+ * (+ index_base); entries beyond N are (+inf, -1).
+ * workspace: device scratch of ofr_knn_workspace_bytes(B, N, k) bytes.      */
+size_t ofr_knn_workspace_bytes(int64_t B, int64_t N, int k);
+int ofr_knn_f32(void* stream, int metric, const float* Q, int64_t B, int64_t ldq, const float* G,
+                int64_t N, int64_t ldg, int64_t d, const float* aux, int k, int64_t index_base,
+                double* out_d, int64_t* out_i, void* workspace, size_t workspace_bytes);
+/* The two passes of ofr_knn_f32 as separate launches (same arguments; pass 1
+ * ignores index_base/out_*, pass 2 reads the candidates pass 1 left in the
+ * workspace).  Lets a caller time the MFMA pass alone on its stream.         */
+int ofr_knn_tiles_f32(void* stream, int metric, const float* Q, int64_t B, int64_t ldq, const float* G,
+                      int64_t N, int64_t ldg, int64_t d, const float* aux, int k, int64_t index_base,
+                      double* out_d, int64_t* out_i, void* workspace, size_t workspace_bytes);
+int ofr_knn_merge_f32(void* stream, int metric, const float* Q, int64_t B, int64_t ldq, const float* G,
+                      int64_t N, int64_t ldg, int64_t d, const float* aux, int k, int64_t index_base,
+                      double* out_d, int64_t* out_i, void* workspace, size_t workspace_bytes);
+
+/* Merge P sorted (distance, index) lists per query into the best k:
+ * in_d/in_i [B][P*kin] (list p at columns [p*kin, (p+1)*kin)), ascending by
+ * (distance, index); out [B][k].  Used after the RCCL all-gather of per-rank
+ * results (gallery sharded across GPUs).                                     */
+int ofr_topk_merge(void* stream, const double* in_d, const int64_t* in_i, int64_t B, int P,
+                   int kin, int k, double* out_d, int64_t* out_i);
+
+/* ExtendedLBP + SpatialHistogram --------------------------------------------
+ * Replaces ExtendedLBP.__call__ lbp.py:80-130 and
+ *          SpatialHistogram.spatially_enhanced_histogram feature.py:286-302.
+ * imgs: uint8 [n][H][W] contiguous.  Geometry (from the host, lbp.py:84-121):
+ * P sample points, offs[P][4] = (fy, fx, cy, cx) int32, w[P][4] fp64
+ * (w1..w4), origin (oy, ox), block (by, bx).  The interpolated neighbour is
+ * evaluated in the reference's fp64 order without contraction:
+ *   N = w1*X[fy][fx]; N += w2*X[fy][cx]; N += w3*X[cy][fx]; N += w4*X[cy][cx]
+ * and bit i of the code is (N >= C), C = uint8 centre pixel.
+ * codes: uint32 [n][H-by+1][W-bx+1].                                         */
+int ofr_elbp_codes(void* stream, const uint8_t* imgs, int64_t n, int H, int W, int P,
+                   const int32_t* offs_host, const double* w_host, int oy, int ox, int by, int bx,
+                   uint32_t* codes);
+/* counts: [n][gr*gc][2^P] of `count_bytes` (1, 2 or 4) unsigned integers;
+ * cell (r,c) covers code rows [r*py,(r+1)*py) x cols [c*px,(c+1)*px),
+ * py = floor(dy/gr), px = floor(dx/gc).  The float histogram of the
+ * reference is count / (py*px) exactly (np.histogram density=True).  P <= 15. */
+int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H, int W, int P,
+                  const int32_t* offs_host, const double* w_host, int oy, int ox, int by, int bx,
+                  int gr, int gc, void* counts, int count_bytes);
+
+/* Chi-square search ----------------------------------------------------------
+ * Replaces ChiSquareDistance distance.py:112-116 inside NearestNeighbor.predict.
+ * Q [B][ldq], G [N][ldg] rows of `nbins` values of type dtype (OFR_DT_*); the
+ * reference value of an element is x / denom (denom = py*px for the counts
+ * of ofr_elbp_hist, whose float histogram is count/(py*px); 1.0 for fp32).
+ * Rows must be 16-byte aligned.  Coarse fp32 VALU pass + exact fp64
+ * re-evaluation of the reference formula on the best candidates; outputs as
+ * ofr_knn_f32.                                                                */
+enum ofr_dtype { OFR_DT_U8 = 0, OFR_DT_U16 = 1, OFR_DT_U32 = 2, OFR_DT_F32 = 3 };
+size_t ofr_chi2_workspace_bytes(int64_t B, int64_t N, int k);
+int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
+                 int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
+                 int64_t* out_i, void* workspace, size_t workspace_bytes);
+
+/* Training (PCA Gram / LDA scatter) ----------------------------------------
+ * C[M][N] = alpha * op(A) op(B) + beta * C in fp64 on the fp64 MFMA
+ * (v_mfma_f64_16x16x4_f64); op(X) = X or X^T (row-major storage).  Replaces
+ * the fp64 products of PCA.compute feature.py:91-94 (Gram / covariance of the
+ * centred data for the eigensolve that replaces np.linalg.svd), LDA.compute
+ * feature.py:162-168 (Sw = Fc^T Fc, Sb = Mc^T diag(n) Mc), Fisherfaces.compute
+ * feature.py:229 (W = P.L) and the training projections.                    */
+int ofr_gemm_f64(void* stream, int transA, int transB, int64_t M, int64_t N, int64_t K,
+                 double alpha, const double* A, int64_t lda, const double* B, int64_t ldb,
+                 double beta, double* C, int64_t ldc);
+/* mean[j] = (1/N) sum_n X[n][j] for uint8 X (exact integer sums; equals
+ * numpy's XC.mean(axis=1) of the uint8 column matrix, feature.py:91).        */
+int ofr_col_mean_u8(void* stream, const uint8_t* X, int64_t N, int64_t D, int64_t ldx,
+                    double* mean);
+/* mean[j] = (1/N) sum_n X[n][j] for fp64 X (row chunks summed in fixed order). */
+int ofr_col_mean_f64(void* stream, const double* X, int64_t N, int64_t D, int64_t ldx,
+                     double* mean);
+/* out[n][j] = X[n][j] - mean[j] (uint8 X -> fp64), feature.py:92.            */
+int ofr_center_u8_f64(void* stream, const uint8_t* X, int64_t N, int64_t D, int64_t ldx,
+                      const double* mean, double* out, int64_t ldo);
+/* out[n][j] = X[n][j] - mean[j] (fp64).                                      */
+int ofr_sub_mean_f64(void* stream, const double* X, int64_t N, int64_t D, int64_t ldx,
+                     const double* mean, double* out, int64_t ldo);
+/* Scale every column of U [rows][ldu] to unit 2-norm (zero columns stay zero):
+ * the left singular vectors from the Gram eigenvectors, U = XC^T V / sigma.   */
+int ofr_normalize_cols_f64(void* stream, double* U, int64_t rows, int64_t cols, int64_t ldu);
+/* Class means and class-centred rows for LDA (feature.py:164-167):
+ * perm [N] = row indices grouped by class, offsets [c+1] (device int64),
+ * means [c][D] = mean of each class's rows, Fc [N][D] = F - means[y] and
+ * Mc [c][D] = means[i] - total_mean, Mc_n [c][D] = n_i * Mc[i]; total_mean [D] given. */
+int ofr_class_center_f64(void* stream, const double* F, int64_t N, int64_t D, int64_t ldf,
+                         const int64_t* perm, const int64_t* offsets, int64_t c,
+                         const double* total_mean, double* means, double* Fc, double* Mc,
+                         double* Mc_n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OFR_H */

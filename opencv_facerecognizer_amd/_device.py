@@ -1,0 +1,347 @@
+"""Device-resident layouts and the host side of every kernel call.
+
+torch is used only for device memory, the current stream and (in
+``parallel.py``) torch.distributed; all arithmetic of the hot path runs in the
+HIP kernels of libocvf_hip.so.
+
+Layouts:
+* fp32 feature rows  [rows][ld], ld = round_up(d, 32), columns >= d zero
+* projection matrix  W^T [d][ldw], ldw = round_up(D, 32), fp32, pad zero
+* uint8 image rows   [rows][ldx], ldx = round_up(D, 16)
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+
+
+def round_up(x, m):
+    return (int(x) + m - 1) // m * m
+
+
+def dev():
+    return _lib.device()
+
+
+# ---------------------------------------------------------------------------
+# uploads
+# ---------------------------------------------------------------------------
+def f32_rows(a, ld=None, device=None):
+    """2-D float array (host or device) -> zero-padded fp32 [rows][ld] device tensor."""
+    device = device or dev()
+    if isinstance(a, torch.Tensor):
+        t = a.to(device=device, dtype=torch.float32)
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float32))).to(device)
+    rows, d = t.shape
+    ld = ld or max(32, round_up(d, 32))
+    out = torch.zeros((rows, ld), dtype=torch.float32, device=device)
+    out[:, :d] = t
+    return out
+
+
+def u8_rows(a, device=None):
+    """Stack of uint8 images (n, ...) -> [n][round_up(D,16)] device tensor (D = prod of the image shape)."""
+    device = device or dev()
+    if isinstance(a, torch.Tensor):
+        t = a.to(device=device, dtype=torch.uint8).reshape(a.shape[0], -1)
+    else:
+        arr = np.asarray(a)
+        if arr.dtype != np.uint8:
+            raise TypeError("image batch must be uint8")
+        t = torch.from_numpy(np.ascontiguousarray(arr.reshape(arr.shape[0], -1))).to(device)
+    n, D = t.shape
+    ldx = round_up(max(D, 1), 16)
+    if ldx == D:
+        return t.contiguous()
+    out = torch.zeros((n, ldx), dtype=torch.uint8, device=device)
+    out[:, :D] = t
+    return out
+
+
+def u8_images(a, device=None):
+    """uint8 image stack (n, H, W) -> contiguous device tensor."""
+    device = device or dev()
+    if isinstance(a, torch.Tensor):
+        return a.to(device=device, dtype=torch.uint8).contiguous()
+    arr = np.asarray(a)
+    if arr.dtype != np.uint8 or arr.ndim != 3:
+        raise TypeError("expected a uint8 image stack (n, H, W)")
+    return torch.from_numpy(np.ascontiguousarray(arr)).to(device)
+
+
+def f64_dev(a, device=None):
+    device = device or dev()
+    if isinstance(a, torch.Tensor):
+        return a.to(device=device, dtype=torch.float64).contiguous()
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float64))).to(device)
+
+
+# ---------------------------------------------------------------------------
+# projection  (feature.py:114-116, 184-185, 241-242)
+# ---------------------------------------------------------------------------
+class Projection:
+    """Device copy of a projection matrix W (D x d), stored as fp32 W^T [d][ldw]."""
+
+    def __init__(self, W, shift=None):
+        W = np.asarray(W, dtype=np.float64)
+        self.D, self.d = W.shape
+        self.ldw = max(32, round_up(self.D, 32))
+        self.Wt = f32_rows(W.T, self.ldw)
+        self.shift = None if shift is None else torch.from_numpy(np.asarray(shift, np.float32).reshape(-1)).to(self.Wt.device)
+        self.ldy = max(32, round_up(self.d, 32))
+
+    def project_u8(self, Xd, out=None, shift=None):
+        """Xd: uint8 [B][ldx] device rows -> fp32 [B][ldy] (pad columns zero)."""
+        B = Xd.shape[0]
+        if out is None:
+            out = torch.zeros((B, self.ldy), dtype=torch.float32, device=Xd.device)
+        sh = self.shift if shift is None else shift
+        call("ofr_project_u8", stream(), ptr(Xd), B, self.D, Xd.shape[1], ptr(self.Wt), self.d, self.ldw,
+             ptr(sh), ptr(out), out.shape[1])
+        return out
+
+    def project_f32(self, Xd, out=None, shift=None):
+        B = Xd.shape[0]
+        if out is None:
+            out = torch.zeros((B, self.ldy), dtype=torch.float32, device=Xd.device)
+        sh = self.shift if shift is None else shift
+        call("ofr_project_f32", stream(), ptr(Xd), B, self.D, Xd.shape[1], ptr(self.Wt), self.d, self.ldw,
+             ptr(sh), ptr(out), out.shape[1])
+        return out
+
+
+# ---------------------------------------------------------------------------
+# search  (classifier.py:76-129)
+# ---------------------------------------------------------------------------
+class Workspace:
+    """Grow-only device scratch buffer (candidate lists of the search kernels)."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes, device):
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        return self.buf
+
+
+class FloatGallery:
+    """Device gallery for Euclidean / Cosine search.
+
+    Euclidean: rows are stored CENTRED on the gallery mean (distances are
+    translation invariant; centring removes the cancellation of the
+    ||q||^2 + ||g||^2 - 2 q.g coarse score), queries are centred with the
+    same shift.  Cosine: raw rows (cosine is not translation invariant).
+    """
+
+    def __init__(self, feats, metric, d=None, device=None):
+        device = device or dev()
+        self.metric = metric
+        if isinstance(feats, torch.Tensor) and feats.dtype == torch.float32 and feats.shape[1] % 32 == 0 and d:
+            G = feats if feats.device == device else feats.to(device)
+            self.d = int(d)
+        else:
+            arr = feats if isinstance(feats, torch.Tensor) else np.asarray(feats, np.float64)
+            self.d = int(arr.shape[1])
+            G = f32_rows(arr, device=device)
+        self.N = int(G.shape[0])
+        self.ld = int(G.shape[1])
+        self.shift = None
+        if metric == _lib.METRIC_EUCLIDEAN and self.N > 0:
+            mean = torch.empty(self.d, dtype=torch.float64, device=device)
+            call("ofr_col_mean", stream(), ptr(G), self.N, self.d, self.ld, ptr(mean))
+            self.shift = mean.to(torch.float32)
+            call("ofr_sub_rows", stream(), ptr(G), self.N, self.d, self.ld, ptr(self.shift))
+        self.G = G
+        self.aux = torch.empty(max(self.N, 1), dtype=torch.float32, device=device)
+        if self.N > 0:
+            call("ofr_row_aux", stream(), metric, ptr(G), self.N, self.d, self.ld, ptr(self.aux))
+        self.ws = Workspace()
+
+    def prepare_queries(self, Qd):
+        """Centre fp32 query rows in place (Euclidean)."""
+        if self.shift is not None and Qd.shape[0] > 0:
+            call("ofr_sub_rows", stream(), ptr(Qd), Qd.shape[0], self.d, Qd.shape[1], ptr(self.shift))
+        return Qd
+
+    def search_phase(self, phase, Qd, k, index_base=0, out=None):
+        """One pass of the search: phase "tiles" (MFMA pass) or "merge" (merge + exact re-rank)."""
+        B = Qd.shape[0]
+        if out is None:
+            out = (torch.empty((B, k), dtype=torch.float64, device=Qd.device),
+                   torch.empty((B, k), dtype=torch.int64, device=Qd.device))
+        lib = _lib.load()
+        ws = self.ws.get(lib.ofr_knn_workspace_bytes(B, self.N, k), Qd.device)
+        name = "ofr_knn_tiles_f32" if phase == "tiles" else "ofr_knn_merge_f32"
+        call(name, stream(), self.metric, ptr(Qd), B, Qd.shape[1], ptr(self.G), self.N, self.ld, self.d,
+             ptr(self.aux), k, index_base, ptr(out[0]), ptr(out[1]), ptr(ws), ws.numel())
+        return out
+
+    def search(self, Qd, k, index_base=0, prepared=False):
+        """Qd: fp32 [B][ld] device rows (same d).  Returns (dist fp64 [B,k], idx int64 [B,k]) device tensors."""
+        if Qd.shape[1] != self.ld:
+            raise ValueError(f"query row stride {Qd.shape[1]} != gallery stride {self.ld}")
+        if not prepared:
+            self.prepare_queries(Qd)
+        B = Qd.shape[0]
+        out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
+        out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)
+        lib = _lib.load()
+        nbytes = lib.ofr_knn_workspace_bytes(B, self.N, k)
+        ws = self.ws.get(nbytes, Qd.device)
+        call("ofr_knn_f32", stream(), self.metric, ptr(Qd), B, Qd.shape[1], ptr(self.G), self.N, self.ld, self.d,
+             ptr(self.aux), k, index_base, ptr(out_d), ptr(out_i), ptr(ws), ws.numel())
+        return out_d, out_i
+
+
+class Chi2Gallery:
+    """Device gallery for ChiSquare search: fp32 values, or integer counts with a denominator."""
+
+    def __init__(self, rows, dtype=_lib.DT_F32, denom=1.0, nbins=None, device=None):
+        device = device or dev()
+        self.dtype = dtype
+        self.denom = float(denom)
+        if isinstance(rows, torch.Tensor):
+            self.G = rows.to(device).contiguous()
+            self.nbins = int(nbins or rows.shape[1])
+        else:
+            arr = np.asarray(rows, np.float64)
+            self.nbins = int(arr.shape[1])
+            self.G = f32_rows(arr, ld=max(4, round_up(self.nbins, 4)), device=device)
+        self.N = int(self.G.shape[0])
+        self.ws = Workspace()
+
+    def search(self, Qd, k, index_base=0):
+        B = Qd.shape[0]
+        out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
+        out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)
+        lib = _lib.load()
+        ws = self.ws.get(lib.ofr_chi2_workspace_bytes(B, self.N, k), Qd.device)
+        call("ofr_chi2_knn", stream(), self.dtype, ptr(Qd), B, Qd.shape[1], ptr(self.G), self.N, self.G.shape[1],
+             self.nbins, self.denom, k, index_base, ptr(out_d), ptr(out_i), ptr(ws), ws.numel())
+        return out_d, out_i
+
+    def query_rows(self, arr):
+        return f32_rows(np.asarray(arr, np.float64), ld=self.G.shape[1])
+
+
+def topk_merge(in_d, in_i, P, kin, k):
+    B = in_d.shape[0]
+    out_d = torch.empty((B, k), dtype=torch.float64, device=in_d.device)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=in_d.device)
+    call("ofr_topk_merge", stream(), ptr(in_d), ptr(in_i), B, P, kin, k, ptr(out_d), ptr(out_i))
+    return out_d, out_i
+
+
+# ---------------------------------------------------------------------------
+# LBP  (lbp.py:80-130, feature.py:286-302)
+# ---------------------------------------------------------------------------
+def elbp_codes(imgs_u8, geom):
+    """imgs: uint8 [n][H][W] device tensor; geom: lbp geometry tuple -> uint32 codes as int64 [n][dy][dx]."""
+    (oy, ox), (by, bx), offs, wts = geom
+    n, H, W = imgs_u8.shape
+    dy, dx = H - by + 1, W - bx + 1
+    out = torch.empty((n, max(dy, 0), max(dx, 0)), dtype=torch.int32, device=imgs_u8.device)
+    offs32 = np.ascontiguousarray(offs, dtype=np.int32)
+    w64 = np.ascontiguousarray(wts, dtype=np.float64)
+    call("ofr_elbp_codes", stream(), ptr(imgs_u8), n, H, W, len(offs32), offs32.ctypes.data_as(_lib.c_vp),
+         w64.ctypes.data_as(_lib.c_vp), oy, ox, by, bx, ptr(out))
+    return out  # int32 storage of uint32 codes (reinterpret on host)
+
+
+def elbp_hist(imgs_u8, geom, grid, count_bytes=None):
+    """-> (counts device tensor [n][gr*gc][2^P] of uint8/int16/int32 storage, cell pixel count)."""
+    (oy, ox), (by, bx), offs, wts = geom
+    n, H, W = imgs_u8.shape
+    P = len(offs)
+    gr, gc = grid
+    dy, dx = H - by + 1, W - bx + 1
+    py = dy // gr if dy > 0 else 0
+    px = dx // gc if dx > 0 else 0
+    cell = py * px
+    if count_bytes is None:
+        count_bytes = 1 if cell <= 255 else (2 if cell <= 65535 else 4)
+    tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[count_bytes]
+    out = torch.empty((n, gr * gc, 1 << P), dtype=tdt, device=imgs_u8.device)
+    offs32 = np.ascontiguousarray(offs, dtype=np.int32)
+    w64 = np.ascontiguousarray(wts, dtype=np.float64)
+    call("ofr_elbp_hist", stream(), ptr(imgs_u8), n, H, W, P, offs32.ctypes.data_as(_lib.c_vp),
+         w64.ctypes.data_as(_lib.c_vp), oy, ox, by, bx, gr, gc, ptr(out), count_bytes)
+    return out, cell, count_bytes
+
+
+# ---------------------------------------------------------------------------
+# training products  (feature.py:91-94, 162-168, 229)
+# ---------------------------------------------------------------------------
+def gemm_f64(A, B, transA=False, transB=False, alpha=1.0):
+    """op(A) @ op(B) in fp64 on the MFMA; A, B contiguous fp64 device tensors."""
+    M = A.shape[1] if transA else A.shape[0]
+    K = A.shape[0] if transA else A.shape[1]
+    N = B.shape[0] if transB else B.shape[1]
+    Kb = B.shape[1] if transB else B.shape[0]
+    if K != Kb:
+        raise ValueError(f"gemm_f64: inner dimensions {K} != {Kb}")
+    C = torch.empty((M, N), dtype=torch.float64, device=A.device)
+    call("ofr_gemm_f64", stream(), int(transA), int(transB), M, N, K, float(alpha), ptr(A), A.shape[1], ptr(B),
+         B.shape[1], 0.0, ptr(C), N)
+    return C
+
+
+def col_mean_u8(Xd, D):
+    mean = torch.empty(D, dtype=torch.float64, device=Xd.device)
+    call("ofr_col_mean_u8", stream(), ptr(Xd), Xd.shape[0], D, Xd.shape[1], ptr(mean))
+    return mean
+
+
+def col_mean_f64(F):
+    mean = torch.empty(F.shape[1], dtype=torch.float64, device=F.device)
+    call("ofr_col_mean_f64", stream(), ptr(F), F.shape[0], F.shape[1], F.shape[1], ptr(mean))
+    return mean
+
+
+def center_u8_f64(Xd, D, mean):
+    out = torch.empty((Xd.shape[0], D), dtype=torch.float64, device=Xd.device)
+    call("ofr_center_u8_f64", stream(), ptr(Xd), Xd.shape[0], D, Xd.shape[1], ptr(mean), ptr(out), D)
+    return out
+
+
+def center_f64(X, mean):
+    out = torch.empty_like(X)
+    call("ofr_sub_mean_f64", stream(), ptr(X), X.shape[0], X.shape[1], X.shape[1], ptr(mean), ptr(out), X.shape[1])
+    return out
+
+
+def normalize_columns(U):
+    U = U.contiguous()
+    call("ofr_normalize_cols_f64", stream(), ptr(U), U.shape[0], U.shape[1], U.shape[1])
+    return U
+
+
+def counts_numpy(counts, count_bytes):
+    """Device count tensor (uint8 / int16 / int32 storage) -> unsigned numpy array."""
+    a = counts.cpu().numpy()
+    return a.view({1: np.uint8, 2: np.uint16, 4: np.uint32}[count_bytes])
+
+
+def class_center_f64(F, y):
+    """F: fp64 [N][d] device; y: int labels 0..c-1 (host) -> (means [c][d], Fc [N][d], Mc, Mc_n [c][d])."""
+    y = np.asarray(y).astype(np.int64)
+    N, d = F.shape
+    c = int(y.max()) + 1 if len(y) else 0
+    perm = np.argsort(y, kind="stable")
+    counts = np.bincount(y, minlength=c)
+    offsets = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    perm_d = torch.from_numpy(perm.astype(np.int64)).to(F.device)
+    off_d = torch.from_numpy(offsets).to(F.device)
+    total = col_mean_f64(F)
+    means = torch.empty((c, d), dtype=torch.float64, device=F.device)
+    Fc = torch.empty((N, d), dtype=torch.float64, device=F.device)
+    Mc = torch.empty((c, d), dtype=torch.float64, device=F.device)
+    Mc_n = torch.empty((c, d), dtype=torch.float64, device=F.device)
+    call("ofr_class_center_f64", stream(), ptr(F), N, d, F.shape[1], ptr(perm_d), ptr(off_d), c, ptr(total),
+         ptr(means), ptr(Fc), ptr(Mc), ptr(Mc_n))
+    return total, means, Fc, Mc, Mc_n

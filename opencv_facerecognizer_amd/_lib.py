@@ -1,0 +1,123 @@
+"""ctypes binding of libocvf_hip.so (the gfx950 C ABI declared in include/ofr.h).
+
+torch is imported FIRST so that its bundled HIP runtime (soname
+libamdhip64.so.7) is the one our library binds to: device pointers and
+streams handed over from torch tensors are then valid in our kernels.
+
+The product path has no CPU fallback: every compute entry point raises if the
+library is missing or no gfx950 device is visible.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OFR_LIB", os.path.join(_HERE, "libocvf_hip.so"))
+
+METRIC_EUCLIDEAN = 0
+METRIC_COSINE = 1
+METRIC_CHISQUARE = 2
+MAX_K = 16
+DT_U8, DT_U16, DT_U32, DT_F32 = 0, 1, 2, 3
+
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_vp = ctypes.c_void_p
+c_dbl = ctypes.c_double
+c_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/ofr.h
+SIGNATURES = {
+    "ofr_version": (c_int, []),
+    "ofr_last_error": (ctypes.c_char_p, []),
+    "ofr_device_check": (c_int, [c_int]),
+    "ofr_project_u8": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]),
+    "ofr_project_f32": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]),
+    "ofr_row_aux": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "ofr_col_mean": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "ofr_sub_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "ofr_knn_workspace_bytes": (c_sz, [c_i64, c_i64, c_int]),
+    "ofr_knn_f32": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_i64,
+                            c_vp, c_vp, c_vp, c_sz]),
+    "ofr_knn_tiles_f32": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_i64,
+                                  c_vp, c_vp, c_vp, c_sz]),
+    "ofr_knn_merge_f32": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_int, c_i64,
+                                  c_vp, c_vp, c_vp, c_sz]),
+    "ofr_topk_merge": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp]),
+    "ofr_elbp_codes": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                               c_vp]),
+    "ofr_elbp_hist": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                              c_int, c_int, c_vp, c_int]),
+    "ofr_chi2_workspace_bytes": (c_sz, [c_i64, c_i64, c_int]),
+    "ofr_chi2_knn": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_dbl, c_int, c_i64, c_vp,
+                             c_vp, c_vp, c_sz]),
+    "ofr_gemm_f64": (c_int, [c_vp, c_int, c_int, c_i64, c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp, c_i64, c_dbl, c_vp,
+                             c_i64]),
+    "ofr_center_u8_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
+    "ofr_col_mean_u8": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "ofr_col_mean_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "ofr_sub_mean_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
+    "ofr_normalize_cols_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64]),
+    "ofr_class_center_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp]),
+}
+
+
+class OfrError(RuntimeError):
+    """A libocvf_hip call failed (message from ofr_last_error())."""
+
+
+_lib = None
+_lock = threading.Lock()
+_checked_devices = set()
+
+
+def load():
+    """Load the shared library (no GPU needed) and bind every declared symbol."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise OfrError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().ofr_last_error().decode(errors="replace")
+        raise OfrError(f"{what or 'ofr'} failed ({rc}): {msg}")
+
+
+def device():
+    """The torch device the kernels run on (raises without a gfx950 GPU)."""
+    if not torch.cuda.is_available():
+        raise OfrError("ocvfacerec (MI355X build): no HIP device visible — this implementation has no CPU path")
+    idx = torch.cuda.current_device()
+    if idx not in _checked_devices:
+        check(load().ofr_device_check(idx), "ofr_device_check")
+        _checked_devices.add(idx)
+    return torch.device("cuda", idx)
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args), name)

@@ -1,0 +1,266 @@
+// Chi-square nearest-neighbour search on gfx950 (VALU tile kernel).
+//
+// Replaces ChiSquareDistance (reference distance.py:112-116,
+// sum((p-q)^2 / (p+q+eps))) inside NearestNeighbor.predict
+// (classifier.py:104-119) for LBP spatial histograms (feature.py:286-302).
+//
+// chi^2 has no bilinear form, so it runs on the vector ALUs: one workgroup
+// computes a 64-query x 64-gallery tile, 4x4 pairs per thread, histogram bins
+// streamed through LDS in [bin][row] panels of 64 bins (uint8/16/32 counts or
+// fp32 values widened once on the LDS write).  Coarse fp32 score per pair:
+//     S = sum_b (a-c)^2 * rcp(a+c+tiny)      (tiny makes empty bins exact 0)
+// The best KC rows per query per tile go to cand[tile][query][KC]; the merge
+// kernel then re-evaluates the reference formula EXACTLY in fp64 on the
+// survivors, with p = value/denom (denom = cell pixel count for counts, the
+// reference histogram being count/(py*px)) and eps = 2^-52.
+#include "ofr_topk.h"
+
+namespace ofr {
+
+enum { DT_U8 = 0, DT_U16 = 1, DT_U32 = 2, DT_F32 = 3 };
+constexpr int C2_TQ = 64, C2_TG = 64, C2_BB = 64;
+
+template <int DT>
+__device__ __forceinline__ void load16(const void* base, int64_t ld, int64_t row, int64_t b0, float (&v)[16]) {
+  if constexpr (DT == DT_U8) {
+    const uint4 x = *reinterpret_cast<const uint4*>((const uint8_t*)base + row * ld + b0);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = (float)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
+  } else if constexpr (DT == DT_U16) {
+    const uint4* p = reinterpret_cast<const uint4*>((const uint16_t*)base + row * ld + b0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint4 x = p[h];
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[8 * h + i] = (float)((w[i >> 1] >> (16 * (i & 1))) & 0xffff);
+    }
+  } else if constexpr (DT == DT_U32) {
+    const uint4* p = reinterpret_cast<const uint4*>((const uint32_t*)base + row * ld + b0);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const uint4 x = p[h];
+      v[4 * h + 0] = (float)x.x;
+      v[4 * h + 1] = (float)x.y;
+      v[4 * h + 2] = (float)x.z;
+      v[4 * h + 3] = (float)x.w;
+    }
+  } else {
+    const f32x4* p = reinterpret_cast<const f32x4*>((const float*)base + row * ld + b0);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const f32x4 x = p[h];
+      v[4 * h + 0] = x[0];
+      v[4 * h + 1] = x[1];
+      v[4 * h + 2] = x[2];
+      v[4 * h + 3] = x[3];
+    }
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ double load1(const void* base, int64_t idx) {
+  if constexpr (DT == DT_U8) return (double)((const uint8_t*)base)[idx];
+  else if constexpr (DT == DT_U16) return (double)((const uint16_t*)base)[idx];
+  else if constexpr (DT == DT_U32) return (double)((const uint32_t*)base)[idx];
+  else return (double)((const float*)base)[idx];
+}
+
+struct Chi2Args {
+  const void* Q;
+  int64_t B, ldq;
+  const void* G;
+  int64_t N, ldg;
+  int64_t nbins;
+  Cand* cand;  // [T][B][KC]
+  int64_t ntq, ntg;
+};
+
+template <int DT, int KC>
+__global__ void __launch_bounds__(256) chi2_tile_kernel(Chi2Args p) {
+  __shared__ __attribute__((aligned(16))) float Qs[C2_BB][C2_TQ];
+  __shared__ __attribute__((aligned(16))) float Gs[C2_BB][C2_TG];
+  __shared__ float S[C2_TQ][C2_TG + 1];
+  const int64_t t = blockIdx.x;
+  const int64_t gt = t / p.ntq, qt = t % p.ntq;  // consecutive blocks share the gallery tile
+  const int64_t q0 = qt * C2_TQ, g0 = gt * C2_TG;
+  const int tid = threadIdx.x;
+  const int tq = tid >> 4, tg = tid & 15;       // compute: queries tq*4.., gallery tg*4..
+  const int lrow = tid >> 2, lseg = tid & 3;    // staging: row, 16-bin segment
+  const int64_t qrow = min(q0 + lrow, p.B - 1);
+  const int64_t grow = min(g0 + lrow, p.N - 1);
+
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+
+  float vq[16], vg[16];
+  const int nsteps = (int)(p.nbins / C2_BB);
+  if (nsteps > 0) {
+    load16<DT>(p.Q, p.ldq, qrow, lseg * 16, vq);
+    load16<DT>(p.G, p.ldg, grow, lseg * 16, vg);
+  }
+  for (int s = 0; s < nsteps; ++s) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      Qs[lseg * 16 + i][lrow] = vq[i];
+      Gs[lseg * 16 + i][lrow] = vg[i];
+    }
+    __syncthreads();
+    if (s + 1 < nsteps) {
+      load16<DT>(p.Q, p.ldq, qrow, (int64_t)(s + 1) * C2_BB + lseg * 16, vq);
+      load16<DT>(p.G, p.ldg, grow, (int64_t)(s + 1) * C2_BB + lseg * 16, vg);
+    }
+#pragma unroll 4
+    for (int b = 0; b < C2_BB; ++b) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(&Qs[b][tq * 4]);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(&Gs[b][tg * 4]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float df = a[i] - c[j];
+          const float sm = (a[i] + c[j]) + 1e-30f;
+          acc[i][j] = __builtin_fmaf(df * df, __builtin_amdgcn_rcpf(sm), acc[i][j]);
+        }
+    }
+  }
+  // tail bins (nbins % 64): plain loads
+  for (int64_t b = (int64_t)nsteps * C2_BB; b < p.nbins; ++b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = (float)load1<DT>(p.Q, min(q0 + tq * 4 + i, p.B - 1) * p.ldq + b);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float c = (float)load1<DT>(p.G, min(g0 + tg * 4 + j, p.N - 1) * p.ldg + b);
+        const float df = a - c;
+        acc[i][j] = __builtin_fmaf(df * df, __builtin_amdgcn_rcpf((a + c) + 1e-30f), acc[i][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) S[tq * 4 + i][tg * 4 + j] = acc[i][j];
+  __syncthreads();
+  if (tid < C2_TQ) {
+    const int64_t q = q0 + tid;
+    TopList<KC> L;
+    L.init();
+    for (int j = 0; j < C2_TG; ++j) {
+      const int64_t g = g0 + j;
+      if (g < p.N) L.insert(S[tid][j], (int)g);
+    }
+    if (q < p.B) {
+      Cand* out = p.cand + ((size_t)gt * p.B + q) * KC;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) out[j] = Cand{L.d[j], L.i[j]};
+    }
+  }
+}
+
+struct Chi2MergeArgs {
+  const Cand* cand;
+  int64_t T, B;
+  const void* Q;
+  int64_t ldq;
+  const void* G;
+  int64_t ldg, nbins;
+  double denom;
+  int k;
+  int64_t index_base;
+  double* out_d;
+  int64_t* out_i;
+};
+
+template <int DT, int KC>
+__global__ void __launch_bounds__(256) chi2_merge_rerank_kernel(Chi2MergeArgs p) {
+  __shared__ Cand lists[256 * KC];
+  __shared__ double exact[KC];
+  __shared__ double red[4];
+  const int64_t q = blockIdx.x;
+  select_candidates<KC>(p.cand, p.T, p.B, q, lists);
+  const double eps = 2.220446049250313e-16;  // np.finfo('float').eps, distance.py:115
+  for (int c = 0; c < KC; ++c) {
+    const Cand cc = lists[c];
+    double val = __builtin_inf();
+    if (cc.i != CAND_EMPTY) {
+      double a = 0;
+      for (int64_t b = threadIdx.x; b < p.nbins; b += blockDim.x) {
+        const double x = load1<DT>(p.Q, q * p.ldq + b) / p.denom;
+        const double y = load1<DT>(p.G, (int64_t)cc.i * p.ldg + b) / p.denom;
+        const double df = x - y;
+        a += (df * df) / (x + y + eps);
+      }
+      val = block_sum_f64(a, red);
+    }
+    if (threadIdx.x == 0) exact[c] = val;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) sort_and_write<KC>(lists, exact, p.k, p.index_base, p.out_d + q * p.k, p.out_i + q * p.k);
+}
+
+template <int DT, int KC>
+static int launch_chi2(hipStream_t st, const Chi2Args& a, const Chi2MergeArgs& m) {
+  if (a.N > 0) {
+    hipLaunchKernelGGL((chi2_tile_kernel<DT, KC>), dim3((unsigned)(a.ntq * a.ntg)), dim3(256), 0, st, a);
+    OFR_LAUNCH_CHECK("chi2_tile_kernel");
+  }
+  hipLaunchKernelGGL((chi2_merge_rerank_kernel<DT, KC>), dim3((unsigned)m.B), dim3(256), 0, st, m);
+  OFR_LAUNCH_CHECK("chi2_merge_rerank_kernel");
+  return OFR_OK;
+}
+
+template <int DT>
+static int chi2_dispatch(hipStream_t st, int kc, const Chi2Args& a, const Chi2MergeArgs& m) {
+  return kc == 8 ? launch_chi2<DT, 8>(st, a, m) : launch_chi2<DT, 16>(st, a, m);
+}
+
+}  // namespace ofr
+
+using namespace ofr;
+
+extern "C" size_t ofr_chi2_workspace_bytes(int64_t B, int64_t N, int k) {
+  const int kc = pick_kc(k);
+  const int64_t T = cdiv(N > 0 ? N : 1, C2_TG);
+  return (size_t)T * (size_t)B * kc * sizeof(Cand) + 256;
+}
+
+extern "C" int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
+                            int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
+                            int64_t* out_i, void* workspace, size_t workspace_bytes) {
+  OFR_CHECK_ARG(dtype >= DT_U8 && dtype <= DT_F32, "ofr_chi2_knn: dtype must be 0 (u8), 1 (u16), 2 (u32) or 3 (f32)");
+  OFR_CHECK_ARG(B >= 0 && N >= 0 && nbins >= 1 && denom > 0, "ofr_chi2_knn: bad sizes");
+  if (k < 1 || k > OFR_MAX_K) return fail(OFR_E_UNSUPPORTED, "ofr_chi2_knn: k must be in [1, 16]");
+  if (B == 0) return OFR_OK;
+  const int esz = dtype == DT_U8 ? 1 : dtype == DT_U16 ? 2 : 4;
+  OFR_CHECK_ARG(Q && out_d && out_i && workspace, "ofr_chi2_knn: null pointer");
+  OFR_CHECK_ARG(ldq >= nbins && (ldq * esz) % 16 == 0 && ((uintptr_t)Q % 16) == 0,
+                "ofr_chi2_knn: query rows must be 16-byte aligned (ldq*elem % 16 == 0)");
+  if (N > 0) {
+    OFR_CHECK_ARG(G, "ofr_chi2_knn: null gallery");
+    OFR_CHECK_ARG(ldg >= nbins && (ldg * esz) % 16 == 0 && ((uintptr_t)G % 16) == 0,
+                  "ofr_chi2_knn: gallery rows must be 16-byte aligned (ldg*elem % 16 == 0)");
+    OFR_CHECK_ARG(N < 0x7fffffffLL - C2_TG, "ofr_chi2_knn: N too large for one shard");
+  }
+  const int kc = pick_kc(k);
+  OFR_CHECK_ARG(workspace_bytes >= ofr_chi2_workspace_bytes(B, N, k), "ofr_chi2_knn: workspace too small");
+  Chi2Args a;
+  a.Q = Q; a.B = B; a.ldq = ldq; a.G = G; a.N = N; a.ldg = ldg; a.nbins = nbins;
+  a.cand = reinterpret_cast<Cand*>(workspace);
+  a.ntq = cdiv(B, C2_TQ);
+  a.ntg = N > 0 ? cdiv(N, C2_TG) : 0;
+  OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_chi2_knn: grid too large");
+  Chi2MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, nbins, denom, k, index_base, out_d, out_i};
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case DT_U8: return chi2_dispatch<DT_U8>(st, kc, a, m);
+    case DT_U16: return chi2_dispatch<DT_U16>(st, kc, a, m);
+    case DT_U32: return chi2_dispatch<DT_U32>(st, kc, a, m);
+    default: return chi2_dispatch<DT_F32>(st, kc, a, m);
+  }
+}

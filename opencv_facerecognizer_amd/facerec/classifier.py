@@ -1,0 +1,165 @@
+"""k-nearest-neighbour classifier (reference ``src/ocvfacerec/facerec/classifier.py``).
+
+``NearestNeighbor`` keeps the reference's interface and pickled state
+(``X`` list of features, ``y`` labels, ``k``, ``dist_metric``;
+classifier.py:53-74) and return format ``[label, {'labels', 'distances'}]``
+(classifier.py:129).  The search — the per-gallery-item distance loop
+(:104-108), the argsort (:113) and the top-k slice (:118-119) — runs on the
+GPU: the gallery is uploaded once into a device-resident layout (derived
+state, never pickled) and every query batch is one kernel pipeline
+(``_device.FloatGallery`` / ``Chi2Gallery``).  The label vote (:121-123) is a
+k-element host operation, as in the reference.
+
+Tie order: exact distance ties resolve to the lowest gallery index (the
+reference's quicksort leaves their order unspecified).
+
+Out of scope: ``SVM`` (classifier.py:150-222) needs the absent libsvm.
+"""
+from __future__ import annotations
+
+import operator as op
+import threading
+
+import numpy as np
+
+from .. import _lib
+from .._device import Chi2Gallery, FloatGallery, f32_rows
+from .distance import EuclideanDistance
+
+
+class AbstractClassifier(object):
+    """classifier.py:42-50."""
+
+    def compute(self, X, y):
+        raise NotImplementedError("Every AbstractClassifier must implement the compute method.")
+
+    def predict(self, X):
+        raise NotImplementedError("Every AbstractClassifier must implement the predict method.")
+
+    def update(self, X, y):
+        raise NotImplementedError("This Classifier is cannot be updated.")
+
+
+def vote(sorted_y):
+    """classifier.py:121-123: most frequent label among the k nearest, ties -> smallest label."""
+    hist = dict((key, val) for key, val in enumerate(np.bincount(sorted_y)) if val)
+    return max(hist.items(), key=op.itemgetter(1))[0]
+
+
+class NearestNeighbor(AbstractClassifier):
+    """classifier.py:53-132 on the GPU."""
+
+    def __init__(self, dist_metric=EuclideanDistance(), k=1):
+        AbstractClassifier.__init__(self)
+        self.k = k
+        self.dist_metric = dist_metric
+        self.X = []
+        self.y = np.array([], dtype=np.int32)
+
+    # -- reference API ----------------------------------------------------
+    def update(self, X, y):
+        """classifier.py:65-70."""
+        self.X.append(X)
+        self.y = np.append(self.y, y)
+
+    def compute(self, X, y):
+        """classifier.py:72-74."""
+        self.X = X
+        self.y = np.asarray(y)
+        self._invalidate()
+
+    def predict(self, q):
+        """classifier.py:76-129 for one query."""
+        return self.predict_batch([q])[0]
+
+    # -- batch API (new) --------------------------------------------------
+    def predict_batch(self, Q):
+        """Predict a batch: Q is a list of features or a 2-D array [B, d]."""
+        d_all, i_all = self.search(Q)
+        y = np.asarray(self.y)
+        out = []
+        for dist, idx in zip(d_all, i_all):
+            valid = idx >= 0
+            sorted_y = y[idx[valid]]
+            sorted_distances = dist[valid]
+            out.append([vote(sorted_y), {"labels": sorted_y, "distances": sorted_distances}])
+        return out
+
+    def search(self, Q, k=None):
+        """Top-k gallery rows of every query: (distances fp64 [B,k], gallery indices int64 [B,k]) on host."""
+        k = int(self.k if k is None else k)
+        Qd, B = self._queries(Q)
+        if B == 0:
+            return np.zeros((0, k)), np.zeros((0, k), np.int64)
+        dist, idx = self._search_device(Qd, k)
+        return dist.cpu().numpy(), idx.cpu().numpy()
+
+    # -- device state ----------------------------------------------------------
+    def _metric(self):
+        mid = getattr(self.dist_metric, "metric_id", None)
+        if mid is None:
+            raise NotImplementedError(
+                f"{self.dist_metric!r} has no device kernel (supported: Euclidean, Cosine, ChiSquare)")
+        return mid
+
+    def _invalidate(self):
+        self.__dict__.pop("_dev", None)
+
+    def _gallery(self):
+        mid = self._metric()
+        key = (mid, len(self.X), id(self.X), _lib.device())
+        cache = self.__dict__.get("_dev")
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        if len(self.X) > len(self.y):
+            raise Exception("More distances than classes. Is your distance metric correct?")  # classifier.py:109-110
+        feats = np.stack([np.asarray(x, dtype=np.float64).reshape(-1) for x in self.X]) if len(self.X) else \
+            np.zeros((0, 1))
+        if mid == _lib.METRIC_CHISQUARE:
+            g = Chi2Gallery(feats)
+        else:
+            g = FloatGallery(feats, mid)
+        self.__dict__["_dev"] = (key, g)
+        return g
+
+    def _queries(self, Q):
+        g = self._gallery()
+        if isinstance(Q, np.ndarray) and Q.ndim == 2 and not isinstance(Q, np.matrix):
+            arr = np.asarray(Q, np.float64)
+        else:
+            arr = np.stack([np.asarray(q, dtype=np.float64).reshape(-1) for q in Q]) if len(Q) else np.zeros((0, 1))
+        B = arr.shape[0]
+        if B and len(self.X) and arr.shape[1] != (g.nbins if isinstance(g, Chi2Gallery) else g.d):
+            raise ValueError(f"query dimension {arr.shape[1]} does not match the gallery")
+        if isinstance(g, Chi2Gallery):
+            return g.query_rows(arr), B
+        return f32_rows(arr, ld=g.ld), B
+
+    def _search_device(self, Qd, k):
+        g = self._gallery()
+        with _DEVICE_LOCK:
+            return g.search(Qd, k)
+
+    def _search_prepared(self, Qd, k):
+        """Qd already in the gallery's query layout (centred for Euclidean)."""
+        g = self._gallery()
+        if Qd.shape[1] != g.ld:
+            raise ValueError("query layout does not match the gallery")
+        with _DEVICE_LOCK:
+            return g.search(Qd, k, prepared=True)
+
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st.pop("_dev", None)
+        return st
+
+    def __repr__(self):
+        return "NearestNeighbor (k=%s, dist_metric=%s)" % (self.k, repr(self.dist_metric))
+
+
+# the ROS recognizer calls predict from a rospy callback thread (ocvf_recognizer_ros.py:96-116)
+_DEVICE_LOCK = threading.RLock()
+
+
+for _c in (AbstractClassifier, NearestNeighbor):
+    _c.__module__ = "ocvfacerec.facerec.classifier"

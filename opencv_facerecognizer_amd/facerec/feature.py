@@ -1,0 +1,390 @@
+"""Feature extraction (reference ``src/ocvfacerec/facerec/feature.py``).
+
+Same classes, constructor arguments, attributes (pickled state), return types
+and errors as the reference:
+
+* ``PCA`` (feature.py:78-139): ``_num_components``, ``_mean`` (np.matrix D x 1),
+  ``_eigenvectors`` (np.matrix D x k), ``_eigenvalues`` (k,).
+* ``LDA`` (feature.py:142-203): float32 ``_eigenvectors`` / ``_eigenvalues``.
+* ``Fisherfaces`` (feature.py:206-260): ``_eigenvectors`` W (np.matrix D x d,
+  float64), ``_eigenvalues``, ``_num_components``; ``extract`` is W^T x with
+  NO mean subtraction (feature.py:237-242).
+* ``SpatialHistogram`` (feature.py:266-305).
+
+What moves to the GPU: the centring and Gram/covariance products of PCA
+(the SVD of the centred data, feature.py:91-94, becomes an fp64-MFMA Gram
+matrix + host ``np.linalg.eigh``), the scatter matrices of LDA (feature.py:
+160-168 as fp64-MFMA GEMMs; ``inv`` and ``eig`` stay on host LAPACK exactly
+as the reference calls them, :170), W = P.L (:229), every projection loop
+(:104-108, :178-182, :231-235 and ``extract``) as the fp32-MFMA projection
+kernel, and the LBP + per-cell histograms (:286-302).
+
+Eigenvector signs: an eigensolver may return any column sign; distances and
+the Fisherfaces W are invariant to PCA column signs, and the LDA/Fisherfaces
+column signs are as arbitrary in the reference as here.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import _device
+
+
+class AbstractFeature(object):
+    """feature.py:38-52."""
+
+    def compute(self, X, y):
+        raise NotImplementedError("Every AbstractFeature must implement the compute method.")
+
+    def extract(self, X):
+        raise NotImplementedError("Every AbstractFeature must implement the extract method.")
+
+    def save(self):
+        raise NotImplementedError("Not implemented yet (TODO).")
+
+    def load(self):
+        raise NotImplementedError("Not implemented yet (TODO).")
+
+    def __repr__(self):
+        return "AbstractFeature"
+
+
+class Identity(AbstractFeature):
+    """feature.py:55-71 (forwards the data)."""
+
+    def __init__(self):
+        AbstractFeature.__init__(self)
+
+    def compute(self, X, y):
+        return X
+
+    def extract(self, X):
+        return X
+
+    def __repr__(self):
+        return "Identity"
+
+
+from .operators import ChainOperator  # noqa: E402  (feature.py:74-75 import order)
+from .util import as_column_matrix  # noqa: E402,F401
+
+
+def _stack_rows(X):
+    """List of equally-shaped items -> 2-D host array [N][D] (the rows of the reference's column matrix)."""
+    return np.stack([np.asarray(x).reshape(-1) for x in X])
+
+
+def _device_rows(X):
+    """Items -> (device rows, D, kind): uint8 images use the u8 layout, everything else fp64."""
+    A = _stack_rows(X)
+    if A.dtype == np.uint8:
+        return _device.u8_rows(A), A.shape[1], "u8"
+    return _device.f64_dev(A.astype(np.float64)), A.shape[1], "f64"
+
+
+class _DeviceProjMixin:
+    """Cached device projection (derived state; dropped from pickles)."""
+
+    def _proj_matrix(self):  # -> (W D x d, shift or None)
+        raise NotImplementedError
+
+    def _proj(self):
+        W, shift = self._proj_matrix()
+        src = self._eigenvectors
+        cache = self.__dict__.get("_dev_proj")
+        if cache is None or cache[0] is not src or cache[1] is not shift:
+            cache = (src, shift, _device.Projection(W, shift))   # holds src/shift: identity stays valid
+            self.__dict__["_dev_proj"] = cache
+        return cache[2]
+
+    def project_device(self, X, shift=None):
+        """Batch of items -> fp32 device rows [B][ldy] = W^T x - shift."""
+        P = self._proj()
+        A = _stack_rows(X) if not isinstance(X, np.ndarray) or X.ndim != 2 else X
+        if A.dtype == np.uint8:
+            return P.project_u8(_device.u8_rows(A), shift=shift)
+        return P.project_f32(_device.f32_rows(A.astype(np.float64), ld=P.ldw), shift=shift)
+
+    def _project_host(self, X):
+        """Batch -> list of (d,1) float64 np.matrix features (reference return type)."""
+        P = self._proj()
+        Y = self.project_device(X).cpu().numpy()[:, : P.d].astype(np.float64)
+        return [np.asmatrix(r.reshape(-1, 1)) for r in Y]
+
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st.pop("_dev_proj", None)
+        return st
+
+
+class PCA(_DeviceProjMixin, AbstractFeature):
+    """feature.py:78-139."""
+
+    def __init__(self, num_components=0):
+        AbstractFeature.__init__(self)
+        self._num_components = num_components
+
+    def compute(self, X, y):
+        Xd, D, kind = _device_rows(X)
+        y = np.asarray(y)
+        n = Xd.shape[0]
+        if self._num_components <= 0 or (self._num_components > n - 1):     # feature.py:88-89
+            self._num_components = n - 1
+        # centre the data on the device (feature.py:91-92)
+        if kind == "u8":
+            mean = _device.col_mean_u8(Xd, D)
+            XC = _device.center_u8_f64(Xd, D, mean)
+        else:
+            mean = _device.col_mean_f64(Xd)
+            XC = _device.center_f64(Xd, mean)
+        # economy SVD of the D x N centred matrix (feature.py:94) via the smaller Gram matrix
+        if n <= D:
+            G = _device.gemm_f64(XC, XC, transB=True).cpu().numpy()            # N x N = XC XC^T (rows)
+            lam, V = np.linalg.eigh(G)
+            order = np.argsort(-lam, kind="stable")
+            lam, V = lam[order], V[:, order]
+            U = _device.gemm_f64(XC, _device.f64_dev(V), transA=True)          # D x N, columns ~ sigma_i u_i
+            U = _device.normalize_columns(U)
+        else:
+            C = _device.gemm_f64(XC, XC, transA=True).cpu().numpy()            # D x D covariance * N
+            lam, V = np.linalg.eigh(C)
+            order = np.argsort(-lam, kind="stable")
+            lam, V = lam[order], V[:, order]
+            U = _device.f64_dev(V)
+        k = min(self._num_components, U.shape[1])
+        lam = np.maximum(lam[:k], 0.0)
+        Ud = U[:, :k].contiguous()
+        self._eigenvectors = np.asmatrix(Ud.cpu().numpy())                      # feature.py:99
+        self._eigenvalues = lam / n                                              # feature.py:102 (sigma^2 / N)
+        self._mean = np.asmatrix(mean.cpu().numpy().reshape(-1, 1))              # feature.py:91
+        # features = U^T (x - mean) for every sample (feature.py:104-108): XC @ U on the MFMA
+        F = _device.gemm_f64(XC, Ud).cpu().numpy()
+        return [np.asmatrix(f.reshape(-1, 1)) for f in F]
+
+    def extract(self, X):
+        """feature.py:110-112."""
+        return self._project_host([np.asarray(X).reshape(-1)])[0]
+
+    def project(self, X):
+        """feature.py:114-116: U^T (X - mean) for a column (D,1)."""
+        return self._project_host([np.asarray(X).reshape(-1)])[0]
+
+    def _proj_matrix(self):
+        W = np.asarray(self._eigenvectors)
+        shift = self.__dict__.get("_shift_cache")
+        if shift is None or shift[0] is not self._mean or shift[1] is not self._eigenvectors:
+            mu = _device.f64_dev(np.asarray(self._mean).reshape(-1, 1))
+            s = _device.gemm_f64(_device.f64_dev(W), mu, transA=True).cpu().numpy().reshape(-1)   # U^T mu
+            shift = (self._mean, self._eigenvectors, s)
+            self.__dict__["_shift_cache"] = shift
+        return W, shift[2]
+
+    def reconstruct(self, X):
+        return np.dot(self._eigenvectors, X) + self._mean
+
+    def __getstate__(self):
+        st = _DeviceProjMixin.__getstate__(self)
+        st.pop("_shift_cache", None)
+        return st
+
+    @property
+    def num_components(self):
+        return self._num_components
+
+    @property
+    def eigenvalues(self):
+        return self._eigenvalues
+
+    @property
+    def eigenvectors(self):
+        return self._eigenvectors
+
+    @property
+    def mean(self):
+        return self._mean
+
+    def __repr__(self):
+        return "PCA (num_components=%d)" % (self._num_components)
+
+
+class LDA(_DeviceProjMixin, AbstractFeature):
+    """feature.py:142-203."""
+
+    def __init__(self, num_components=0):
+        AbstractFeature.__init__(self)
+        self._num_components = num_components
+
+    @staticmethod
+    def scatter(X, y):
+        """Sw, Sb (float64 host arrays) of the items X with labels y (feature.py:160-168), on the device."""
+        F = _device.f64_dev(_stack_rows(X).astype(np.float64))
+        y = np.asarray(y)
+        c = len(np.unique(y))
+        if len(y) and (y.min() < 0 or y.max() != c - 1):
+            raise ValueError("LDA: labels must be the integers 0..c-1 (feature.py:164-165 iterates range(c))")
+        total, means, Fc, Mc, Mc_n = _device.class_center_f64(F, y)
+        Sw = _device.gemm_f64(Fc, Fc, transA=True)           # sum_i (Xi - mi)(Xi - mi)^T
+        Sb = _device.gemm_f64(Mc, Mc_n, transA=True)         # sum_i n_i (mi - m)(mi - m)^T
+        return Sw.cpu().numpy(), Sb.cpu().numpy(), F
+
+    def compute(self, X, y):
+        y = np.asarray(y)
+        c = len(np.unique(y))
+        if self._num_components <= 0:                          # feature.py:155-158
+            self._num_components = c - 1
+        elif self._num_components > (c - 1):
+            self._num_components = c - 1
+        Sw, Sb, F = self.scatter(X, y)
+        # solve eigenvalue problem for a general matrix (feature.py:170-176), host LAPACK
+        evals, evecs = np.linalg.eig(np.linalg.inv(Sw) @ Sb)
+        idx = np.argsort(-evals.real)
+        evals, evecs = evals[idx], evecs[:, idx]
+        self._eigenvalues = np.array(evals[0:self._num_components].real, dtype=np.float32, copy=True)
+        self._eigenvectors = np.matrix(evecs[0:, 0:self._num_components].real, dtype=np.float32, copy=True)
+        # features = L^T x (feature.py:178-182) on the MFMA
+        L = _device.f64_dev(np.asarray(self._eigenvectors, dtype=np.float64))
+        Y = _device.gemm_f64(F, L).cpu().numpy()
+        return [np.asmatrix(r.reshape(-1, 1)) for r in Y]
+
+    def extract(self, X):
+        return self.project(X)
+
+    def project(self, X):
+        """feature.py:184-185."""
+        return self._project_host([np.asarray(X).reshape(-1)])[0]
+
+    def _proj_matrix(self):
+        return np.asarray(self._eigenvectors, dtype=np.float64), None
+
+    def reconstruct(self, X):
+        return np.dot(self._eigenvectors, X)
+
+    @property
+    def num_components(self):
+        return self._num_components
+
+    @property
+    def eigenvectors(self):
+        return self._eigenvectors
+
+    @property
+    def eigenvalues(self):
+        return self._eigenvalues
+
+    def __repr__(self):
+        return "LDA (num_components=%d)" % (self._num_components)
+
+
+class Fisherfaces(_DeviceProjMixin, AbstractFeature):
+    """feature.py:206-260."""
+
+    def __init__(self, num_components=0):
+        AbstractFeature.__init__(self)
+        self._num_components = num_components
+
+    def compute(self, X, y):
+        y = np.asarray(y)
+        n = len(y)                                             # feature.py:216-217
+        c = len(np.unique(y))
+        pca = PCA(num_components=(n - c))                      # :219-224
+        lda = LDA(num_components=self._num_components)
+        model = ChainOperator(pca, lda)
+        model.compute(X, y)
+        self._eigenvalues = lda.eigenvalues                    # :226-227
+        self._num_components = lda.num_components
+        # W = P . L (:229) on the fp64 MFMA
+        P = _device.f64_dev(np.asarray(pca.eigenvectors))
+        L = _device.f64_dev(np.asarray(lda.eigenvectors, dtype=np.float64))
+        self._eigenvectors = np.asmatrix(_device.gemm_f64(P, L).cpu().numpy())
+        self.__dict__.pop("_dev_proj", None)
+        # features of the training set (:231-235): one batched projection
+        return self._project_host(X)
+
+    def extract(self, X):
+        """feature.py:237-239."""
+        return self._project_host([np.asarray(X).reshape(-1)])[0]
+
+    def project(self, X):
+        """feature.py:241-242: W^T X, no mean subtraction."""
+        return self._project_host([np.asarray(X).reshape(-1)])[0]
+
+    def extract_batch(self, X):
+        """Batch version of extract: list of (d,1) float64 matrices."""
+        return self._project_host(X)
+
+    def _proj_matrix(self):
+        return np.asarray(self._eigenvectors), None
+
+    def reconstruct(self, X):
+        return np.dot(self._eigenvectors, X)
+
+    @property
+    def num_components(self):
+        return self._num_components
+
+    @property
+    def eigenvalues(self):
+        return self._eigenvalues
+
+    @property
+    def eigenvectors(self):
+        return self._eigenvectors
+
+    def __repr__(self):
+        return "Fisherfaces (num_components=%s)" % (self.num_components)
+
+
+from .lbp import ExtendedLBP, LocalDescriptor  # noqa: E402  (feature.py:263)
+
+
+class SpatialHistogram(AbstractFeature):
+    """feature.py:266-305: per-cell LBP histograms, concatenated row-major over the grid."""
+
+    def __init__(self, lbp_operator=ExtendedLBP(), sz=(8, 8)):
+        AbstractFeature.__init__(self)
+        if not isinstance(lbp_operator, LocalDescriptor):
+            raise TypeError("Only an operator of type facerec.lbp.LocalDescriptor is a valid lbp_operator.")
+        self.lbp_operator = lbp_operator
+        self.sz = sz
+
+    def compute(self, X, y):
+        return list(self.histograms(X))
+
+    def extract(self, X):
+        return self.histograms([X])[0]
+
+    def spatially_enhanced_histogram(self, X):
+        return self.histograms([X])[0]
+
+    def counts_device(self, imgs):
+        """uint8 image stack (n,H,W) (host or device) -> (counts device tensor [n][cells][2^P], cell pixels, bytes)."""
+        if not isinstance(self.lbp_operator, ExtendedLBP):
+            raise NotImplementedError("SpatialHistogram (MI355X build) runs ExtendedLBP operators only")
+        from .lbp import as_u8_images
+        if not hasattr(imgs, "device"):
+            imgs = as_u8_images(np.stack([np.asarray(x) for x in imgs]))
+        counts, cell, cb = _device.elbp_hist(_device.u8_images(imgs), self.lbp_operator.geometry(), tuple(self.sz))
+        return counts, cell, cb
+
+    def histograms(self, X):
+        """List of images -> list of float64 histograms = count/(py*px) (np.histogram density, :298-299)."""
+        if len(X) == 0:
+            return []
+        shapes = {np.asarray(x).shape for x in X}
+        out = [None] * len(X)
+        for shp in shapes:   # images of one size per launch
+            sel = [i for i, x in enumerate(X) if np.asarray(x).shape == shp]
+            counts, cell, cb = self.counts_device([X[i] for i in sel])
+            c = _device.counts_numpy(counts, cb).astype(np.int64).reshape(len(sel), -1)
+            with np.errstate(invalid="ignore", divide="ignore"):
+                h = c.astype(np.float64) / float(cell)
+            for j, i in enumerate(sel):
+                out[i] = h[j]
+        return out
+
+    def __repr__(self):
+        return "SpatialHistogram (operator=%s, grid=%s)" % (repr(self.lbp_operator), str(self.sz))
+
+
+for _c in (AbstractFeature, Identity, PCA, LDA, Fisherfaces, SpatialHistogram):
+    _c.__module__ = "ocvfacerec.facerec.feature"

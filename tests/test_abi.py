@@ -1,0 +1,34 @@
+"""The C-ABI library loads without a GPU and exports every symbol include/ofr.h declares."""
+import os
+import re
+
+from opencv_facerecognizer_amd import _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "ofr.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\b(ofr_[a-z0-9_]+)\s*\(", src))
+
+
+def test_header_matches_bindings():
+    assert declared() == set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    lib = _lib.load()
+    for name in declared():
+        assert hasattr(lib, name), name
+    assert lib.ofr_version() == (0 << 16) | (1 << 8)
+
+
+def test_error_paths_without_device():
+    lib = _lib.load()
+    # argument validation happens before any device work and reports through ofr_last_error
+    rc = lib.ofr_knn_f32(None, 7, None, 1, 32, None, 1, 32, 3, None, 1, 0, None, None, None, 0)
+    assert rc == -1 and b"metric" in lib.ofr_last_error()
+    rc = lib.ofr_knn_f32(None, 0, None, 1, 32, None, 1, 32, 3, None, 99, 0, None, None, None, 0)
+    assert rc == -2 and b"k must be" in lib.ofr_last_error()
+    assert lib.ofr_knn_workspace_bytes(4096, 1000000, 1) >= 4096 * (1000000 // 256) * 8 * 8

@@ -1,0 +1,315 @@
+"""Parity of the HIP path (through the C ABI) against the CPU oracle and the reference's golden vectors.
+
+Tolerances (north_star): LBP codes and histogram counts bit-exact; projections
+and distances within 1e-4 relative of numpy float64 (projections norm-relative
+per row; a distance may also carry an absolute 1e-6*||q|| term, the size of the
+fp32 rounding of the features it is computed from); labels identical except
+on near-ties, (d2-d1)/d1 <= 1e-4 between distinct gallery rows in the oracle.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import facerec_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    torch.cuda.set_device(0)
+    from opencv_facerecognizer_amd import _lib
+    _lib.device()
+
+
+def _rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def _check_search(metric_name, Q, G, d_got, i_got, k, near_rel=1e-4):
+    """Compare device top-k with the float64 oracle on the same (fp32-representable) inputs."""
+    Dref = O.pairwise(metric_name, Q, G)
+    order = np.argsort(Dref, axis=1, kind="stable")
+    n_ties = 0
+    for b in range(Q.shape[0]):
+        kk = min(k, G.shape[0])
+        ref_i = order[b, :kk]
+        ref_d = Dref[b, ref_i]
+        got_i = i_got[b, :kk]
+        got_d = d_got[b, :kk]
+        assert np.all(i_got[b, kk:] == -1)
+        qn = np.linalg.norm(Q[b])
+        tol = 1e-4 * np.abs(ref_d) + 1e-6 * max(qn, 1e-30)
+        assert np.all(np.abs(got_d - ref_d) <= tol), (b, got_d, ref_d)
+        # every returned row is really at the reported oracle distance
+        np.testing.assert_allclose(Dref[b, got_i], got_d, rtol=1e-4, atol=1e-6 * max(qn, 1e-30))
+        if not np.array_equal(got_i, ref_i):
+            # allowed only where the oracle itself has near-ties at the differing ranks
+            for j in np.nonzero(got_i != ref_i)[0]:
+                a, c = Dref[b, got_i[j]], Dref[b, ref_i[j]]
+                assert abs(a - c) <= near_rel * max(abs(c), 1e-300) + 1e-6 * qn, (b, j, a, c)
+                n_ties += 1
+    return n_ties
+
+
+# ---------------------------------------------------------------------------
+# search kernel (ofr_knn_f32) — Euclidean / Cosine
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("metric", ["EuclideanDistance", "CosineDistance"])
+@pytest.mark.parametrize("B,N,d,k", [(1, 31, 3, 1), (7, 1000, 99, 5), (300, 5000, 3, 1), (257, 3000, 300, 16),
+                                     (600, 20000, 64, 3), (5, 4, 10, 8)])
+def test_knn_vs_oracle(metric, B, N, d, k):
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery, f32_rows
+    r = _rng(B * 7 + N + d)
+    G = r.normal(100, 40, (N, d)).astype(np.float32).astype(np.float64)
+    Q = r.normal(100, 40, (B, d)).astype(np.float32).astype(np.float64)
+    if N > 10:
+        Q[0] = G[N // 2]           # exact match -> distance 0
+        G[N - 1] = G[3]            # duplicate rows -> lowest index first
+    mid = _lib.METRIC_EUCLIDEAN if metric == "EuclideanDistance" else _lib.METRIC_COSINE
+    g = FloatGallery(G, mid)
+    dd, ii = g.search(f32_rows(Q, ld=g.ld), k)
+    ties = _check_search(metric, Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
+    assert ties <= max(1, B // 100)
+
+
+def test_knn_exact_duplicates_tie_to_lowest_index():
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery, f32_rows
+    r = _rng(5)
+    base = r.normal(0, 1, (40, 16)).astype(np.float32)
+    G = np.concatenate([base, base, base]).astype(np.float64)     # every row appears 3 times
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    dd, ii = g.search(f32_rows(base.astype(np.float64), ld=g.ld), 3)
+    ii = ii.cpu().numpy()
+    assert np.array_equal(ii, np.stack([np.arange(40), np.arange(40) + 40, np.arange(40) + 80], 1))
+    assert np.all(dd.cpu().numpy() == 0)
+
+
+def test_knn_golden_reference_predictions(golden):
+    """NearestNeighbor.predict vs the reference's own outputs (tests/golden/dist_golden.npz)."""
+    from ocvfacerec.facerec.classifier import NearestNeighbor
+    from ocvfacerec.facerec.distance import ChiSquareDistance, CosineDistance, EuclideanDistance
+    d = golden("dist_golden.npz")
+    mets = {"EuclideanDistance": EuclideanDistance, "CosineDistance": CosineDistance,
+            "ChiSquareDistance": ChiSquareDistance}
+    for s in ("d3", "d99", "hist"):
+        for mname, cls in mets.items():
+            if f"{s}_{mname}_D" not in d.files:
+                continue
+            for k in (1, 3, 5):
+                c = NearestNeighbor(dist_metric=cls(), k=k)
+                c.compute([g.reshape(-1, 1) for g in d[s + "_G"]], d[s + "_y"])
+                preds = c.predict_batch([q.reshape(-1, 1) for q in d[s + "_Q"]])
+                for qi, p in enumerate(preds):
+                    ref_l = d[f"{s}_{mname}_k{k}_labels"][qi]
+                    ref_d = d[f"{s}_{mname}_k{k}_dists"][qi]
+                    qn = np.linalg.norm(d[s + "_Q"][qi])
+                    np.testing.assert_allclose(p[1]["distances"], ref_d, rtol=1e-4, atol=1e-6 * qn)
+                    if not np.array_equal(p[1]["labels"], ref_l):
+                        # exact duplicate gallery rows: the reference's quicksort order is unspecified
+                        assert np.allclose(np.sort(p[1]["distances"]), np.sort(ref_d), rtol=1e-6)
+                    assert p[0] == d[f"{s}_{mname}_k{k}_label"][qi] or len(set(ref_d)) < len(ref_d)
+    # the single-pair metric call (distance.py:57-116) runs the same kernels
+    for mname, cls in mets.items():
+        s = "hist" if mname == "ChiSquareDistance" else "d99"
+        D = d[f"{s}_{mname}_D"]
+        assert cls()(d[s + "_G"][3], d[s + "_Q"][1]) == pytest.approx(D[1, 3], rel=1e-4, abs=1e-9)
+
+
+# ---------------------------------------------------------------------------
+# projection kernel (ofr_project_u8 / _f32)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("B,D,d", [(1, 4900, 3), (31, 4900, 3), (300, 10000, 99), (513, 777, 260)])
+def test_projection_vs_oracle(B, D, d):
+    from opencv_facerecognizer_amd._device import Projection, u8_rows
+    r = _rng(B + D + d)
+    W = r.normal(0, 1.0 / np.sqrt(D), (D, d))
+    X = r.integers(0, 256, (B, D), dtype=np.uint8)
+    P = Projection(W)
+    Y = P.project_u8(u8_rows(X)).cpu().numpy()
+    assert np.all(Y[:, d:] == 0)
+    ref = X.astype(np.float64) @ W
+    err = np.linalg.norm(Y[:, :d] - ref, axis=1) / np.linalg.norm(ref, axis=1)
+    assert err.max() < 1e-4, err.max()
+    # with a shift (PCA.project form, feature.py:114-116)
+    mu = r.normal(128, 5, D)
+    P2 = Projection(W, shift=(mu @ W))
+    Y2 = P2.project_u8(u8_rows(X)).cpu().numpy()[:, :d]
+    ref2 = (X - mu) @ W
+    err2 = np.linalg.norm(Y2 - ref2, axis=1) / np.linalg.norm(ref2, axis=1)
+    assert err2.max() < 1e-4, err2.max()
+
+
+def test_pickled_model_predict_matches_reference(golden):
+    """Bundled individuals.pkl: predictions on the 31 bundled faces equal the reference's (golden)."""
+    from ocvfacerec.facerec.serialization import load_model
+    m = load_model(os.path.join(GOLDEN, "individuals.pkl"))
+    f = golden("individuals_faces.npz")
+    preds = m.predict_batch(list(f["X"]))
+    labels = np.array([p[0] for p in preds])
+    dists = np.array([p[1]["distances"][0] for p in preds])
+    assert np.array_equal(labels, f["pkl_pred_labels"])
+    np.testing.assert_allclose(dists, f["pkl_pred_dist"], rtol=1e-4)
+    # single-face API (one face per call, as the recognizer loops use it)
+    p0 = m.predict(f["X"][5])
+    assert p0[0] == f["pkl_pred_labels"][5] and p0[1]["distances"][0] == pytest.approx(f["pkl_pred_dist"][5], rel=1e-4)
+    q = m.feature.extract(f["X"][5])
+    assert isinstance(q, np.matrix) and q.shape == (3, 1) and q.dtype == np.float64
+    np.testing.assert_allclose(np.asarray(q).ravel(), O.fisherfaces_project(np.asarray(m.feature._eigenvectors),
+                                                                            f["X"][5]).A.ravel(), rtol=1e-5)
+
+
+# ---------------------------------------------------------------------------
+# LBP + histograms (bit-exact)
+# ---------------------------------------------------------------------------
+def test_lbp_codes_bit_exact_vs_reference(golden):
+    from ocvfacerec.facerec.lbp import ExtendedLBP
+    g = golden("lbp_golden.npz")
+    names = sorted(k[4:] for k in g.files if k.startswith("img_"))
+    for nm in names:
+        im = g["img_" + nm]
+        for r, P in ((1, 8), (2, 8), (2, 16), (3, 4)):
+            got = ExtendedLBP(radius=r, neighbors=P)(im)
+            assert got.dtype == np.uint32
+            assert np.array_equal(got, g[f"codes_{nm}_r{r}p{P}"]), (nm, r, P)
+
+
+def test_spatial_histogram_bit_exact_vs_reference(golden):
+    from ocvfacerec.facerec.feature import SpatialHistogram
+    from ocvfacerec.facerec.lbp import ExtendedLBP
+    g = golden("lbp_golden.npz")
+    names = [k[4:] for k in g.files if k.startswith("img_") and f"hist_{k[4:]}_r1p8_g8" in g.files]
+    imgs = [g["img_" + n] for n in names]
+    h8 = SpatialHistogram(ExtendedLBP(1, 8), (8, 8)).compute(imgs, None)
+    h45 = SpatialHistogram(ExtendedLBP(2, 8), (4, 5)).compute(imgs, None)
+    for n, a, b in zip(names, h8, h45):
+        assert np.array_equal(a, g[f"hist_{n}_r1p8_g8"]), n
+        assert np.array_equal(b, g[f"hist_{n}_r2p8_g4x5"]), n
+
+
+def test_lbp_hist_counts_batch_vs_oracle():
+    from ocvfacerec.facerec.feature import SpatialHistogram
+    from opencv_facerecognizer_amd._device import counts_numpy
+    r = _rng(11)
+    imgs = r.integers(0, 256, (200, 128, 128), dtype=np.uint8)
+    imgs[:50] = (imgs[:50] // 64) * 64 + 100          # tie-heavy
+    sh = SpatialHistogram()
+    counts, cell, cb = sh.counts_device(imgs)
+    c = counts_numpy(counts, cb).astype(np.int64)
+    assert cell == 225 and cb == 1
+    for i in range(0, 200, 13):
+        ref, _ = O.spatial_histogram_counts(O.elbp(imgs[i]), 8, (8, 8))
+        assert np.array_equal(c[i], ref), i
+
+
+# ---------------------------------------------------------------------------
+# chi-square search
+# ---------------------------------------------------------------------------
+def test_chi2_counts_search_vs_oracle():
+    from ocvfacerec.facerec.feature import SpatialHistogram
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import Chi2Gallery, counts_numpy
+    r = _rng(12)
+    protos = r.integers(0, 256, (20, 16, 16)).astype(np.float64)
+    up = np.kron(protos, np.ones((8, 8)))
+    gal = np.clip(up[np.arange(300) % 20] + r.normal(0, 20, (300, 128, 128)), 0, 255).astype(np.uint8)
+    qry = np.clip(up[np.arange(70) % 20] + r.normal(0, 20, (70, 128, 128)), 0, 255).astype(np.uint8)
+    sh = SpatialHistogram()
+    gc, cell, cb = sh.counts_device(gal)
+    qc, _, _ = sh.counts_device(qry)
+    n, nb = gc.shape[0], gc.shape[1] * gc.shape[2]
+    g = Chi2Gallery(gc.reshape(n, nb), dtype=_lib.DT_U8, denom=float(cell), nbins=nb)
+    dd, ii = g.search(qc.reshape(qc.shape[0], nb).contiguous(), 5)
+    Gh = counts_numpy(gc, cb).reshape(n, nb).astype(np.float64) / cell
+    Qh = counts_numpy(qc, cb).reshape(-1, nb).astype(np.float64) / cell
+    _check_search("ChiSquareDistance", Qh, Gh, dd.cpu().numpy(), ii.cpu().numpy(), 5)
+
+
+def test_chi2_float_search_vs_oracle():
+    from opencv_facerecognizer_amd._device import Chi2Gallery
+    r = _rng(13)
+    G = r.random((500, 300)) ** 3
+    Q = r.random((40, 300)) ** 3
+    G = G.astype(np.float32).astype(np.float64)
+    Q = Q.astype(np.float32).astype(np.float64)
+    g = Chi2Gallery(G)
+    dd, ii = g.search(g.query_rows(Q), 4)
+    _check_search("ChiSquareDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 4)
+
+
+# ---------------------------------------------------------------------------
+# training (Fisherfaces.compute on the bundled faces)
+# ---------------------------------------------------------------------------
+def test_fisherfaces_compute_bundled(golden):
+    from ocvfacerec.facerec.classifier import NearestNeighbor
+    from ocvfacerec.facerec.distance import EuclideanDistance
+    from ocvfacerec.facerec.feature import LDA, PCA, Fisherfaces
+    from ocvfacerec.facerec.model import PredictableModel
+    f = golden("individuals_faces.npz")
+    X, y = list(f["X"]), f["y"]
+    # PCA: mean exact, eigenvalues and subspace match the reference SVD
+    pca = PCA(len(y) - 4)
+    pf = pca.compute(X, y)
+    assert np.array_equal(np.asarray(pca.mean).ravel(), f["pca_mean"])
+    np.testing.assert_allclose(pca.eigenvalues, f["pca_eigenvalues"], rtol=1e-6)
+    U, Ur = np.asarray(pca.eigenvectors), f["pca_eigenvectors"]
+    cos = np.abs(np.sum(U * Ur, 0))
+    assert cos.min() > 1 - 1e-6, cos
+    # PCA features equal the reference's up to column sign
+    sgn = np.sign(np.sum(U * Ur, 0))
+    pfa = np.stack([np.asarray(p).ravel() for p in pf]) * sgn
+    np.testing.assert_allclose(pfa, f["pca_features"], rtol=0, atol=1e-6 * np.abs(f["pca_features"]).max())
+    # LDA scatter matrices equal the oracle's (on the reference PCA features)
+    Sw, Sb, _ = LDA.scatter(list(f["pca_features"]), y)
+    _, Sw_ref, Sb_ref = O.lda_scatter(f["pca_features"].T, y)
+    np.testing.assert_allclose(Sw, Sw_ref, rtol=0, atol=1e-10 * np.abs(Sw_ref).max())
+    np.testing.assert_allclose(Sb, Sb_ref, rtol=0, atol=1e-10 * np.abs(Sb_ref).max())
+    # full model: resubstitution labels equal the reference's
+    m = PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=1))
+    m.compute(X, list(y))
+    W = np.asarray(m.feature.eigenvectors)
+    assert W.shape == (4900, 3) and m.feature.num_components == 3
+    labels = [p[0] for p in m.predict_batch(X)]
+    assert np.array_equal(labels, f["resub_labels"])
+    # gallery features are W^T x of the model's own W (feature.py:231-235)
+    feats = np.stack([np.asarray(x).ravel() for x in m.classifier.X])
+    ref = f["X"].reshape(31, -1).astype(np.float64) @ W
+    assert (np.linalg.norm(feats - ref, axis=1) / np.linalg.norm(ref, axis=1)).max() < 1e-4
+
+
+def test_gemm_f64_vs_numpy():
+    from opencv_facerecognizer_amd._device import f64_dev, gemm_f64
+    r = _rng(3)
+    for (M, N, K) in [(31, 31, 4900), (100, 7, 33), (130, 257, 64)]:
+        A = r.normal(size=(M, K))
+        Bm = r.normal(size=(K, N))
+        C = gemm_f64(f64_dev(A), f64_dev(Bm)).cpu().numpy()
+        np.testing.assert_allclose(C, A @ Bm, rtol=1e-12, atol=1e-12 * np.abs(A @ Bm).max())
+        Ct = gemm_f64(f64_dev(A.T.copy()), f64_dev(Bm.T.copy()), transA=True, transB=True).cpu().numpy()
+        np.testing.assert_allclose(Ct, A @ Bm, rtol=1e-12, atol=1e-12 * np.abs(A @ Bm).max())
+
+
+def test_topk_merge_kernel():
+    from opencv_facerecognizer_amd._device import topk_merge
+    r = _rng(4)
+    B, P, kin, k = 50, 4, 5, 7
+    d = np.sort(r.random((B, P, kin)), axis=2)
+    d[:, 1, 0] = d[:, 0, 0]                      # cross-list ties
+    i = r.integers(0, 10**6, (B, P, kin))
+    i[:, 2, 3:] = -1                             # short list
+    d[:, 2, 3:] = np.inf
+    od, oi = topk_merge(torch.from_numpy(d.reshape(B, -1)).cuda(), torch.from_numpy(i.reshape(B, -1)).cuda(), P, kin, k)
+    od, oi = od.cpu().numpy(), oi.cpu().numpy()
+    for b in range(B):
+        cand = [(d[b, p, j], i[b, p, j]) for p in range(P) for j in range(kin) if i[b, p, j] >= 0]
+        cand.sort()
+        ref = cand[:k]
+        assert [x[1] for x in ref] == list(oi[b, :len(ref)])
+        assert np.array_equal([x[0] for x in ref], od[b, :len(ref)])
