@@ -5,8 +5,9 @@ gallery is 40 GB of the 288 GB HBM): synthetic 100x100 uint8 faces (D=10000),
 a Fisherfaces projection to d=9999 (= c-1 for 10k identities, thetrainer.py
 get_model defaults), a 1M-row gallery (100k identities x 10 images), batches of
 B=4096 query faces, k=1, Euclidean distance.  One step = project the batch
-(ofr_project_u8) + MFMA search pass (ofr_knn_tiles_f32) + merge / exact fp64
-re-rank (ofr_knn_merge_f32) [+ all-gather + ofr_topk_merge when sharded].
+(ofr_project_u8_exact: int8-slice MFMA, exact) + fp32-MFMA search pass
+(ofr_knn_tiles_f32) + merge / exact fp64 re-rank (ofr_knn_merge_f32)
+[+ all-gather + ofr_topk_merge when sharded].
 Inputs are resident in HBM before the timed region.  W is random (no trained
 checkpoint exists at this scale), gallery/queries are synthetic (see
 opencv_facerecognizer_amd/synthetic.py).
@@ -32,7 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from opencv_facerecognizer_amd import _lib  # noqa: E402
-from opencv_facerecognizer_amd._device import FloatGallery, Projection, round_up  # noqa: E402
+from opencv_facerecognizer_amd._device import FloatGallery, Projection, col_mean_u8, round_up  # noqa: E402
 from opencv_facerecognizer_amd.parallel import exchange_topk, merge_topk, shard_range  # noqa: E402
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 
@@ -62,25 +63,21 @@ def log(rank, *a):
 
 
 def build_projection(D, d, device):
+    """Random W (no trained checkpoint exists at this scale): N(0, 1/D), prepared for the exact int8 kernel."""
     g = torch.Generator(device=device)
     g.manual_seed(SEED + 5)
-    P = Projection.__new__(Projection)
-    P.D, P.d = D, d
-    P.ldw = max(32, round_up(D, 32))
-    P.Wt = torch.zeros((d, P.ldw), dtype=torch.float32, device=device)
-    P.Wt[:, :D] = torch.randn((d, D), generator=g, device=device) / np.sqrt(D)
-    P.shift = None
-    P.ldy = max(32, round_up(d, 32))
-    return P
+    Wt = torch.randn((d, D), generator=g, device=device) / np.sqrt(D)
+    P = Projection(Wt_device=Wt, D=D, device=device)
+    return P, Wt
 
 
-def cpu_baseline(P, gallery, Xq, ids_q, N_total, seconds):
+def cpu_baseline(Wt, gallery, Xq, N_total, seconds):
     """Reference-faithful oracle (classifier.py:104-108 loop, 1 Python thread) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import facerec_oracle as O  # the checker; timed here as the CPU baseline
     n_s = min(4000, gallery.N)
-    G_s = gallery.G[:n_s, : gallery.d].double().cpu().numpy() + gallery.shift.double().cpu().numpy()
-    W = P.Wt[:, : P.D].double().cpu().numpy().T.copy()      # D x d, float64 like the reference
+    G_s = gallery.G[:n_s, : gallery.d].double().cpu().numpy() + gallery.shift64.cpu().numpy()
+    W = Wt.double().cpu().numpy().T.copy()                   # D x d, float64 like the reference
     X = Xq.cpu().numpy()
     t_proj, t_item, nq = 0.0, 0.0, 0
     deadline = time.perf_counter() + seconds
@@ -95,19 +92,24 @@ def cpu_baseline(P, gallery, Xq, ids_q, N_total, seconds):
         t_item += (t2 - t1) / n_s
         nq += 1
     per_query = t_proj / nq + (t_item / nq) * N_total
-    # vectorised float64 mode (BLAS, all cores) on the same sample
+    # vectorised float64 mode (BLAS dgemm, all BLAS threads) on the same sample: projection of a batch
+    # and ||q||^2 + ||g||^2 - 2 q.g distances, extrapolated linearly in N
+    nv = min(256, len(X))
     t0 = time.perf_counter()
-    Qv = X[: min(64, len(X))].astype(np.float64) @ W
-    O.nn_search_vectorized("EuclideanDistance", Qv, G_s, 1)
-    tv = (time.perf_counter() - t0) / len(Qv)
-    per_query_vec = tv * (N_total / n_s)   # dominated by the distance pass, linear in N
+    Qv = X[:nv].astype(np.float64) @ W
+    t1 = time.perf_counter()
+    O.nn_search_blas(Qv, G_s, 1)
+    t2 = time.perf_counter()
+    per_query_vec = (t1 - t0) / nv + (t2 - t1) / nv * (N_total / n_s)
+    blas_threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {
         "value": 1.0 / per_query, "unit": "queries/s", "cores": 1, "kind": "port",
-        "sample": f"{nq} queries x {n_s} gallery rows, d={gallery.d}, D={P.D}: reference-faithful per-item "
+        "sample": f"{nq} queries x {n_s} gallery rows, d={gallery.d}, D={W.shape[0]}: reference-faithful per-item "
                   f"distance loop + W^T x, extrapolated linearly to N={N_total}",
         "per_item_us": 1e6 * t_item / nq, "projection_ms": 1e3 * t_proj / nq,
-        "vectorized_f64": {"value": 1.0 / per_query_vec, "unit": "queries/s", "cores": os.cpu_count(),
-                           "sample": f"{len(Qv)} queries x {n_s} rows, BLAS, extrapolated to N={N_total}"},
+        "vectorized_f64": {"value": 1.0 / per_query_vec, "unit": "queries/s", "cores": blas_threads,
+                           "sample": f"{nv} queries x {n_s} rows, float64 BLAS (dgemm) projection + distances, "
+                                     f"extrapolated to N={N_total}"},
     }
 
 
@@ -131,17 +133,24 @@ def main():
 
     # ---- setup (untimed): W, gallery shard, queries -------------------------------------
     t0 = time.perf_counter()
-    P = build_projection(D, d, device)
+    P, Wt = build_projection(D, d, device)
     bank = IdentityBank(n_ids, H, W, device=device)
     ld = max(32, round_up(d, 32))
     G = torch.zeros((nl, ld), dtype=torch.float32, device=device)
     chunk = 8192
+    centre = None
     for c0 in range(0, nl, chunk):
         c1 = min(nl, c0 + chunk)
         rows = torch.arange(n0 + c0, n0 + c1, device=device)
         imgs = bank.images(rows // args.per_id, seed=SEED + 1000 + (n0 + c0) // chunk)
-        P.project_u8(imgs, out=G[c0:c1])
-    gallery = FloatGallery(G, _lib.METRIC_EUCLIDEAN, d=d, device=device)
+        if centre is None:
+            # centring vector c = W^T round(mean image of the first chunk), exact fp64: rows are stored as
+            # fp32(W^T x - c), rounded after centring (FloatGallery docstring)
+            m = col_mean_u8(imgs, D)
+            m_img = torch.clamp(torch.round(m), 0, 255).to(torch.uint8).reshape(1, -1).contiguous()
+            centre = P.project(m_img, f64=True)[0].contiguous()
+        P.project(imgs, shift64=centre, out=G[c0:c1])
+    gallery = FloatGallery.from_device_rows(G, d, _lib.METRIC_EUCLIDEAN, shift64=centre)
     gq = torch.Generator(device=device)
     gq.manual_seed(SEED + 7)
     ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
@@ -156,7 +165,7 @@ def main():
     def step(events=None):
         if events:
             events[0].record()
-        P.project_u8(Xq, out=Qd, shift=gallery.shift)              # W^T x - mu (centred for Euclidean)
+        P.project(Xq, shift64=gallery.shift64, out=Qd)            # fp32(W^T x - c), exact int8 MFMA
         if events:
             events[1].record()
         gallery.search_phase("tiles", Qd, k)
@@ -215,11 +224,11 @@ def main():
                          "frac": achieved / PEAK_FP32_MFMA, "traffic": None,
                          "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
                          "launch_ms": ms_tiles},
-            "kernels_ms": {"project_u8": ms_proj, "knn_tiles": ms_tiles, "knn_merge_rerank": ms_merge},
+            "kernels_ms": {"project_u8_exact": ms_proj, "knn_tiles": ms_tiles, "knn_merge_rerank": ms_merge},
             "top1_identity_acc": acc,
         }
         if world == 1 and not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(P, gallery, Xq, ids_q, N, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(Wt, gallery, Xq, N, args.cpu_seconds)
             result["speedup_vs_cpu"] = value / result["cpu_baseline"]["value"]
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -22,6 +22,7 @@
  *     ELEMENTS.  Float operands of the MFMA GEMMs use ld % 32 == 0 and the
  *     columns [K, round_up(K,32)) of every row must be zero (the padding is
  *     part of the device layout the host package owns).
+ *   - Element types are named by enum ofr_dtype where a function takes several.
  */
 #ifndef OFR_H
 #define OFR_H
@@ -46,6 +47,8 @@ enum ofr_metric {
   OFR_METRIC_CHISQUARE = 2, /* distance.py:101-116 sum((p-q)^2/(p+q+eps))        */
 };
 
+enum ofr_dtype { OFR_DT_U8 = 0, OFR_DT_U16 = 1, OFR_DT_U32 = 2, OFR_DT_F32 = 3, OFR_DT_F64 = 4 };
+
 #define OFR_MAX_K 16          /* largest k of the fused search (classifier.py:53-129) */
 #define OFR_TILE_ROWS 256     /* gallery rows per search tile                          */
 
@@ -55,29 +58,38 @@ const char* ofr_last_error(void);      /* thread-local, never NULL      */
 int ofr_device_check(int device);      /* OFR_OK iff `device` is gfx950 */
 
 /* Projection ---------------------------------------------------------------
- * Y[b][j] = sum_i X[b][i] * Wt[j][i] - shift[j]     (b < B, j < d, i < D)
+ * Y[b][j] = sum_i X[b][i] * W[i][j] - shift[j]      (b < B, j < d, i < D)
  * Replaces Fisherfaces.project  feature.py:241-242 (np.dot(W.T, x), shift=NULL),
  *          PCA.project          feature.py:114-116 (shift = P^T mu),
  *          LDA.project          feature.py:184-185, and the per-sample
  *          projection loops feature.py:104-108, 178-182, 231-235.
- * X : uint8 [B][ldx], ldx % 16 == 0, bytes [D, ldx) ignored.
- * Wt: fp32 [d][ldw] (= W transposed), ldw % 32 == 0, zero beyond D.
- * Y : fp32 [B][ldy]; only columns j < d are written.
- * fp32 MFMA (v_mfma_f32_32x32x2_f32), exact f32 products, f32 accumulation. */
-int ofr_project_u8(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx,
-                   const float* Wt, int64_t d, int64_t ldw, const float* shift, float* Y,
-                   int64_t ldy);
-
-/* Same with fp32 inputs X [B][ldx] (ldx % 32 == 0, zero beyond D).          */
-int ofr_project_f32(void* stream, const float* X, int64_t B, int64_t D, int64_t ldx,
-                    const float* Wt, int64_t d, int64_t ldw, const float* shift, float* Y,
-                    int64_t ldy);
+ * EXACT integer path on v_mfma_i32_32x32x32_i8: W is prepared once into four
+ * int8 slices with a power-of-two scale per output feature
+ * (W[i][j] = s_j (q1 + q2/2^7 + q3/2^14 + q4/2^21), exact for every fp32
+ * element within 2^4 of its column maximum); (x-128) . q is accumulated in
+ * int32 without rounding and combined in fp64 without rounding; the shift is
+ * subtracted in fp64 and the result rounded once to fp32 or fp64.
+ * Wt: W transposed, [d][ldw] of OFR_DT_F32 or OFR_DT_F64.
+ * Aq: int8 [ceil(d/64)*256][ldk], ldk % 64 == 0, ldk >= round_up(D,64)
+ *     (ofr_qproj_bytes(D,d) bytes with ldk = round_up(D,64)); scale, K: fp64 [d].
+ * X : uint8 [B][ldx], 16-byte aligned rows, ldx >= D.
+ * Y : [B][ldy] of y_dtype (OFR_DT_F32 / OFR_DT_F64); columns j < d written.   */
+size_t ofr_qproj_bytes(int64_t D, int64_t d);
+int ofr_qproj_prepare(void* stream, int dtype, const void* Wt, int64_t d, int64_t D, int64_t ldw,
+                      int8_t* Aq, int64_t ldk, double* scale, double* K);
+int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx,
+                         const int8_t* Aq, int64_t ldk, const double* scale, const double* K,
+                         int64_t d, const double* shift, void* Y, int64_t ldy, int y_dtype);
 
 /* Gallery preparation ------------------------------------------------------
  * For the search kernels: aux[n] = ||G[n]||^2 (EUCLIDEAN) or 1/||G[n]|| (COSINE),
  * computed in fp64 and stored fp32.  G [N][ldg] fp32.                       */
 int ofr_row_aux(void* stream, int metric, const float* G, int64_t N, int64_t d, int64_t ldg,
                 float* aux);
+/* out[n][j] = (float)(F[n][j] - shift[j]) for j < d: fp64 features -> the
+ * fp32 search layout, centred BEFORE the rounding (shift may be NULL).       */
+int ofr_center_round_f64(void* stream, const double* F, int64_t N, int64_t d, int64_t ldf,
+                         const double* shift, float* out, int64_t ldo);
 /* mean[j] = (1/N) sum_n G[n][j] in fp64 (column means of the gallery).      */
 int ofr_col_mean(void* stream, const float* G, int64_t N, int64_t d, int64_t ldg, double* mean);
 /* G[n][j] -= shift[j] for j < d (fp32).                                     */
@@ -146,7 +158,7 @@ int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H, int W, in
  * Rows must be 16-byte aligned.  Coarse fp32 VALU pass + exact fp64
  * re-evaluation of the reference formula on the best candidates; outputs as
  * ofr_knn_f32.                                                                */
-enum ofr_dtype { OFR_DT_U8 = 0, OFR_DT_U16 = 1, OFR_DT_U32 = 2, OFR_DT_F32 = 3 };
+
 size_t ofr_chi2_workspace_bytes(int64_t B, int64_t N, int k);
 int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
                  int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,

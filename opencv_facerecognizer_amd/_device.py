@@ -84,34 +84,53 @@ def f64_dev(a, device=None):
 # projection  (feature.py:114-116, 184-185, 241-242)
 # ---------------------------------------------------------------------------
 class Projection:
-    """Device copy of a projection matrix W (D x d), stored as fp32 W^T [d][ldw]."""
+    """Device form of a projection matrix W (D x d) for the exact int8-slice kernel.
 
-    def __init__(self, W, shift=None):
-        W = np.asarray(W, dtype=np.float64)
-        self.D, self.d = W.shape
-        self.ldw = max(32, round_up(self.D, 32))
-        self.Wt = f32_rows(W.T, self.ldw)
-        self.shift = None if shift is None else torch.from_numpy(np.asarray(shift, np.float32).reshape(-1)).to(self.Wt.device)
+    W is given as a host array (fp64 model weights) or as a device tensor Wt
+    (d x >=D, fp32/fp64).  ``project(Xd, shift64, out_dtype)`` returns
+    (x . W - shift) rounded once to fp32 (search layout, [B][ldy] with zero pad
+    columns) or fp64.
+    """
+
+    def __init__(self, W=None, Wt_device=None, D=None, device=None):
+        device = device or dev()
+        if Wt_device is not None:
+            Wt = Wt_device
+            self.d = int(Wt.shape[0])
+            self.D = int(D if D is not None else Wt.shape[1])
+        else:
+            W = np.asarray(W, dtype=np.float64)
+            self.D, self.d = W.shape
+            Wt = torch.from_numpy(np.ascontiguousarray(W.T)).to(device)
+        dt = {torch.float32: _lib.DT_F32, torch.float64: _lib.DT_F64}[Wt.dtype]
+        self.ldk = round_up(self.D, 64)
+        nbytes = _lib.load().ofr_qproj_bytes(self.D, self.d)
+        self.Aq = torch.empty(nbytes, dtype=torch.int8, device=device)
+        self.scale = torch.empty(self.d, dtype=torch.float64, device=device)
+        self.K = torch.empty(self.d, dtype=torch.float64, device=device)
+        call("ofr_qproj_prepare", stream(), dt, ptr(Wt), self.d, self.D, Wt.shape[1], ptr(self.Aq), self.ldk,
+             ptr(self.scale), ptr(self.K))
         self.ldy = max(32, round_up(self.d, 32))
 
-    def project_u8(self, Xd, out=None, shift=None):
-        """Xd: uint8 [B][ldx] device rows -> fp32 [B][ldy] (pad columns zero)."""
+    def project(self, Xd, shift64=None, out=None, f64=False):
+        """Xd: uint8 [B][ldx] device rows.  fp32 [B][ldy] (zero pad) or fp64 [B][d]."""
         B = Xd.shape[0]
         if out is None:
-            out = torch.zeros((B, self.ldy), dtype=torch.float32, device=Xd.device)
-        sh = self.shift if shift is None else shift
-        call("ofr_project_u8", stream(), ptr(Xd), B, self.D, Xd.shape[1], ptr(self.Wt), self.d, self.ldw,
-             ptr(sh), ptr(out), out.shape[1])
+            out = torch.empty((B, self.d), dtype=torch.float64, device=Xd.device) if f64 else \
+                torch.zeros((B, self.ldy), dtype=torch.float32, device=Xd.device)
+        ydt = _lib.DT_F64 if out.dtype == torch.float64 else _lib.DT_F32
+        call("ofr_project_u8_exact", stream(), ptr(Xd), B, self.D, Xd.shape[1], ptr(self.Aq), self.ldk,
+             ptr(self.scale), ptr(self.K), self.d, ptr(shift64), ptr(out), out.shape[1], ydt)
         return out
 
-    def project_f32(self, Xd, out=None, shift=None):
-        B = Xd.shape[0]
-        if out is None:
-            out = torch.zeros((B, self.ldy), dtype=torch.float32, device=Xd.device)
-        sh = self.shift if shift is None else shift
-        call("ofr_project_f32", stream(), ptr(Xd), B, self.D, Xd.shape[1], ptr(self.Wt), self.d, self.ldw,
-             ptr(sh), ptr(out), out.shape[1])
-        return out
+
+def center_round(F64, shift64, ld, out=None):
+    """fp64 rows [N][d] -> fp32 [N][ld] = rows - shift (pad columns zero), rounded once."""
+    N, d = F64.shape
+    if out is None:
+        out = torch.zeros((N, ld), dtype=torch.float32, device=F64.device)
+    call("ofr_center_round_f64", stream(), ptr(F64), N, d, F64.stride(0), ptr(shift64), ptr(out), out.shape[1])
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -132,41 +151,49 @@ class Workspace:
 class FloatGallery:
     """Device gallery for Euclidean / Cosine search.
 
-    Euclidean: rows are stored CENTRED on the gallery mean (distances are
-    translation invariant; centring removes the cancellation of the
-    ||q||^2 + ||g||^2 - 2 q.g coarse score), queries are centred with the
-    same shift.  Cosine: raw rows (cosine is not translation invariant).
+    Euclidean: rows are stored CENTRED on a shift c (the gallery mean, fp64)
+    and rounded to fp32 AFTER centring, so the stored values carry
+    eps*|g - c| instead of eps*|g| of error (Fisherfaces features share a large
+    common component); distances are translation invariant and queries are
+    centred on the same c.  Cosine: raw rows (cosine is not translation
+    invariant), shift None.
     """
 
-    def __init__(self, feats, metric, d=None, device=None):
+    def __init__(self, feats, metric, device=None):
+        """feats: host array [N][d] (any float type; used in fp64)."""
         device = device or dev()
         self.metric = metric
-        if isinstance(feats, torch.Tensor) and feats.dtype == torch.float32 and feats.shape[1] % 32 == 0 and d:
-            G = feats if feats.device == device else feats.to(device)
-            self.d = int(d)
-        else:
-            arr = feats if isinstance(feats, torch.Tensor) else np.asarray(feats, np.float64)
-            self.d = int(arr.shape[1])
-            G = f32_rows(arr, device=device)
-        self.N = int(G.shape[0])
-        self.ld = int(G.shape[1])
-        self.shift = None
+        F = f64_dev(np.asarray(feats, np.float64), device=device) if not isinstance(feats, torch.Tensor) else \
+            feats.to(device=device, dtype=torch.float64).contiguous()
+        self.N, self.d = int(F.shape[0]), int(F.shape[1])
+        self.ld = max(32, round_up(self.d, 32))
+        self.shift64 = None
         if metric == _lib.METRIC_EUCLIDEAN and self.N > 0:
-            mean = torch.empty(self.d, dtype=torch.float64, device=device)
-            call("ofr_col_mean", stream(), ptr(G), self.N, self.d, self.ld, ptr(mean))
-            self.shift = mean.to(torch.float32)
-            call("ofr_sub_rows", stream(), ptr(G), self.N, self.d, self.ld, ptr(self.shift))
+            self.shift64 = col_mean_f64(F)
+        self.G = center_round(F, self.shift64, self.ld)
+        self._finish(device)
+
+    @classmethod
+    def from_device_rows(cls, G, d, metric, shift64=None):
+        """Adopt fp32 rows [N][ld] that are already centred on shift64 (fp64 [d]) — e.g. written by Projection."""
+        self = cls.__new__(cls)
+        self.metric = metric
         self.G = G
+        self.N, self.ld, self.d = int(G.shape[0]), int(G.shape[1]), int(d)
+        self.shift64 = shift64
+        self._finish(G.device)
+        return self
+
+    def _finish(self, device):
         self.aux = torch.empty(max(self.N, 1), dtype=torch.float32, device=device)
         if self.N > 0:
-            call("ofr_row_aux", stream(), metric, ptr(G), self.N, self.d, self.ld, ptr(self.aux))
+            call("ofr_row_aux", stream(), self.metric, ptr(self.G), self.N, self.d, self.ld, ptr(self.aux))
         self.ws = Workspace()
 
-    def prepare_queries(self, Qd):
-        """Centre fp32 query rows in place (Euclidean)."""
-        if self.shift is not None and Qd.shape[0] > 0:
-            call("ofr_sub_rows", stream(), ptr(Qd), Qd.shape[0], self.d, Qd.shape[1], ptr(self.shift))
-        return Qd
+    def query_rows(self, Q64):
+        """Host or device fp64 query features [B][d] -> centred fp32 search rows [B][ld]."""
+        Q = Q64 if isinstance(Q64, torch.Tensor) else f64_dev(np.asarray(Q64, np.float64), device=self.G.device)
+        return center_round(Q.to(torch.float64).contiguous(), self.shift64, self.ld)
 
     def search_phase(self, phase, Qd, k, index_base=0, out=None):
         """One pass of the search: phase "tiles" (MFMA pass) or "merge" (merge + exact re-rank)."""
@@ -181,12 +208,10 @@ class FloatGallery:
              ptr(self.aux), k, index_base, ptr(out[0]), ptr(out[1]), ptr(ws), ws.numel())
         return out
 
-    def search(self, Qd, k, index_base=0, prepared=False):
-        """Qd: fp32 [B][ld] device rows (same d).  Returns (dist fp64 [B,k], idx int64 [B,k]) device tensors."""
+    def search(self, Qd, k, index_base=0):
+        """Qd: centred fp32 search rows [B][ld] (see query_rows / Projection.project with shift64)."""
         if Qd.shape[1] != self.ld:
             raise ValueError(f"query row stride {Qd.shape[1]} != gallery stride {self.ld}")
-        if not prepared:
-            self.prepare_queries(Qd)
         B = Qd.shape[0]
         out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
         out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)

@@ -22,7 +22,7 @@ METRIC_EUCLIDEAN = 0
 METRIC_COSINE = 1
 METRIC_CHISQUARE = 2
 MAX_K = 16
-DT_U8, DT_U16, DT_U32, DT_F32 = 0, 1, 2, 3
+DT_U8, DT_U16, DT_U32, DT_F32, DT_F64 = 0, 1, 2, 3, 4
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
@@ -35,8 +35,11 @@ SIGNATURES = {
     "ofr_version": (c_int, []),
     "ofr_last_error": (ctypes.c_char_p, []),
     "ofr_device_check": (c_int, [c_int]),
-    "ofr_project_u8": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]),
-    "ofr_project_f32": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64]),
+    "ofr_qproj_bytes": (c_sz, [c_i64, c_i64]),
+    "ofr_qproj_prepare": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "ofr_project_u8_exact": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                     c_i64, c_int]),
+    "ofr_center_round_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
     "ofr_row_aux": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "ofr_col_mean": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "ofr_sub_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),

@@ -23,7 +23,7 @@ import threading
 import numpy as np
 
 from .. import _lib
-from .._device import Chi2Gallery, FloatGallery, f32_rows
+from .._device import Chi2Gallery, FloatGallery
 from .distance import EuclideanDistance
 
 
@@ -131,9 +131,7 @@ class NearestNeighbor(AbstractClassifier):
         B = arr.shape[0]
         if B and len(self.X) and arr.shape[1] != (g.nbins if isinstance(g, Chi2Gallery) else g.d):
             raise ValueError(f"query dimension {arr.shape[1]} does not match the gallery")
-        if isinstance(g, Chi2Gallery):
-            return g.query_rows(arr), B
-        return f32_rows(arr, ld=g.ld), B
+        return g.query_rows(arr), B
 
     def _search_device(self, Qd, k):
         g = self._gallery()
@@ -146,7 +144,7 @@ class NearestNeighbor(AbstractClassifier):
         if Qd.shape[1] != g.ld:
             raise ValueError("query layout does not match the gallery")
         with _DEVICE_LOCK:
-            return g.search(Qd, k, prepared=True)
+            return g.search(Qd, k)
 
     def __getstate__(self):
         st = dict(self.__dict__)

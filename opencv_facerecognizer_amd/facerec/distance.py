@@ -38,7 +38,7 @@ class AbstractDistance(object):
 
 
 def _pair(metric, p, q):
-    from .._device import Chi2Gallery, FloatGallery, f32_rows
+    from .._device import Chi2Gallery, FloatGallery
     p = np.asarray(p, dtype=np.float64).reshape(1, -1)
     q = np.asarray(q, dtype=np.float64).reshape(1, -1)
     if p.shape != q.shape:
@@ -48,7 +48,7 @@ def _pair(metric, p, q):
         d, _ = g.search(g.query_rows(q), 1)
     else:
         g = FloatGallery(p, metric)
-        d, _ = g.search(f32_rows(q, ld=g.ld), 1)
+        d, _ = g.search(g.query_rows(q), 1)
     return np.float64(d.cpu().numpy()[0, 0])
 
 

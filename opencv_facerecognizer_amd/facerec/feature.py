@@ -83,9 +83,13 @@ def _device_rows(X):
 
 
 class _DeviceProjMixin:
-    """Cached device projection (derived state; dropped from pickles)."""
+    """Cached device projection (derived state; dropped from pickles).
 
-    def _proj_matrix(self):  # -> (W D x d, shift or None)
+    uint8 inputs (faces) use the exact int8-slice MFMA kernel; any other input
+    dtype uses the fp64 MFMA GEMM.  Both give fp64-accurate W^T x - shift.
+    """
+
+    def _proj_matrix(self):  # -> (W D x d, own shift (fp64 [d] host array) or None)
         raise NotImplementedError
 
     def _proj(self):
@@ -93,22 +97,34 @@ class _DeviceProjMixin:
         src = self._eigenvectors
         cache = self.__dict__.get("_dev_proj")
         if cache is None or cache[0] is not src or cache[1] is not shift:
-            cache = (src, shift, _device.Projection(W, shift))   # holds src/shift: identity stays valid
+            P = _device.Projection(W)
+            P.W64 = _device.f64_dev(np.asarray(W, np.float64))
+            P.own_shift = None if shift is None else _device.f64_dev(np.asarray(shift, np.float64).reshape(-1))
+            cache = (src, shift, P)   # holds src/shift so that the identity check stays valid
             self.__dict__["_dev_proj"] = cache
         return cache[2]
 
-    def project_device(self, X, shift=None):
-        """Batch of items -> fp32 device rows [B][ldy] = W^T x - shift."""
+    def _shift(self, P, extra):
+        """Own shift (PCA mean term) plus an extra centring shift (search layout), fp64 device or None."""
+        if P.own_shift is None:
+            return extra
+        return P.own_shift if extra is None else P.own_shift + extra
+
+    def project_device(self, X, shift64=None, f64=False, ld=None):
+        """Batch of items -> (W^T x - own shift - shift64): fp32 search rows [B][ldy] or fp64 [B][d]."""
         P = self._proj()
-        A = _stack_rows(X) if not isinstance(X, np.ndarray) or X.ndim != 2 else X
+        A = X if isinstance(X, np.ndarray) and X.ndim == 2 and not isinstance(X, np.matrix) else _stack_rows(X)
+        sh = self._shift(P, shift64)
         if A.dtype == np.uint8:
-            return P.project_u8(_device.u8_rows(A), shift=shift)
-        return P.project_f32(_device.f32_rows(A.astype(np.float64), ld=P.ldw), shift=shift)
+            return P.project(_device.u8_rows(A), shift64=sh, f64=f64)
+        Y = _device.gemm_f64(_device.f64_dev(A.astype(np.float64)), P.W64)
+        if sh is not None:
+            Y = _device.center_f64(Y, sh)
+        return Y if f64 else _device.center_round(Y, None, P.ldy)
 
     def _project_host(self, X):
         """Batch -> list of (d,1) float64 np.matrix features (reference return type)."""
-        P = self._proj()
-        Y = self.project_device(X).cpu().numpy()[:, : P.d].astype(np.float64)
+        Y = self.project_device(X, f64=True).cpu().numpy()
         return [np.asmatrix(r.reshape(-1, 1)) for r in Y]
 
     def __getstate__(self):
@@ -174,7 +190,7 @@ class PCA(_DeviceProjMixin, AbstractFeature):
         shift = self.__dict__.get("_shift_cache")
         if shift is None or shift[0] is not self._mean or shift[1] is not self._eigenvectors:
             mu = _device.f64_dev(np.asarray(self._mean).reshape(-1, 1))
-            s = _device.gemm_f64(_device.f64_dev(W), mu, transA=True).cpu().numpy().reshape(-1)   # U^T mu
+            s = _device.gemm_f64(_device.f64_dev(W), mu, transA=True).cpu().numpy().reshape(-1)   # U^T mu (fp64)
             shift = (self._mean, self._eigenvectors, s)
             self.__dict__["_shift_cache"] = shift
         return W, shift[2]

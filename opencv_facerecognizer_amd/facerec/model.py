@@ -47,8 +47,8 @@ class PredictableModel(object):
         g = clf._gallery()
         if g.N and g.d != self.feature._proj().d:
             raise ValueError("feature dimension does not match the classifier gallery")
-        # Euclidean: fold the gallery centring into the projection shift (W^T x - mu)
-        Qd = self.feature.project_device(X, shift=g.shift)
+        # Euclidean: the gallery centring is folded into the projection (W^T x - c, fp64, rounded once)
+        Qd = self.feature.project_device(X, shift64=g.shift64)
         return clf._search_prepared(Qd, k)
 
     def predict_batch(self, X):

@@ -281,6 +281,16 @@ def nn_search_vectorized(metric, Q, G, k):
     return np.take_along_axis(D, idx, 1), idx
 
 
+def nn_search_blas(Q, G, k):
+    """Vectorised float64 1-NN with BLAS: ||q||^2 + ||g||^2 - 2 Q G^T (CPU-baseline timing only; the
+    GEMM form cancels, so parity checks use ``nn_search_vectorized``)."""
+    Q = np.asarray(Q, np.float64)
+    G = np.asarray(G, np.float64)
+    D2 = np.einsum("ij,ij->i", Q, Q)[:, None] + np.einsum("ij,ij->i", G, G)[None, :] - 2.0 * (Q @ G.T)
+    idx = np.argsort(D2, axis=1, kind="stable")[:, :k]
+    return np.sqrt(np.maximum(np.take_along_axis(D2, idx, 1), 0)), idx
+
+
 def near_tie_mask(metric, Q, G, rel=1e-4):
     """Queries whose best and second-best oracle distances are within ``rel``."""
     D = pairwise(metric, Q, G)

@@ -65,7 +65,7 @@ def _check_search(metric_name, Q, G, d_got, i_got, k, near_rel=1e-4):
                                      (600, 20000, 64, 3), (5, 4, 10, 8)])
 def test_knn_vs_oracle(metric, B, N, d, k):
     from opencv_facerecognizer_amd import _lib
-    from opencv_facerecognizer_amd._device import FloatGallery, f32_rows
+    from opencv_facerecognizer_amd._device import FloatGallery
     r = _rng(B * 7 + N + d)
     G = r.normal(100, 40, (N, d)).astype(np.float32).astype(np.float64)
     Q = r.normal(100, 40, (B, d)).astype(np.float32).astype(np.float64)
@@ -74,19 +74,19 @@ def test_knn_vs_oracle(metric, B, N, d, k):
         G[N - 1] = G[3]            # duplicate rows -> lowest index first
     mid = _lib.METRIC_EUCLIDEAN if metric == "EuclideanDistance" else _lib.METRIC_COSINE
     g = FloatGallery(G, mid)
-    dd, ii = g.search(f32_rows(Q, ld=g.ld), k)
+    dd, ii = g.search(g.query_rows(Q), k)
     ties = _check_search(metric, Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
     assert ties <= max(1, B // 100)
 
 
 def test_knn_exact_duplicates_tie_to_lowest_index():
     from opencv_facerecognizer_amd import _lib
-    from opencv_facerecognizer_amd._device import FloatGallery, f32_rows
+    from opencv_facerecognizer_amd._device import FloatGallery
     r = _rng(5)
     base = r.normal(0, 1, (40, 16)).astype(np.float32)
     G = np.concatenate([base, base, base]).astype(np.float64)     # every row appears 3 times
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
-    dd, ii = g.search(f32_rows(base.astype(np.float64), ld=g.ld), 3)
+    dd, ii = g.search(g.query_rows(base.astype(np.float64)), 3)
     ii = ii.cpu().numpy()
     assert np.array_equal(ii, np.stack([np.arange(40), np.arange(40) + 40, np.arange(40) + 80], 1))
     assert np.all(dd.cpu().numpy() == 0)
@@ -126,25 +126,45 @@ def test_knn_golden_reference_predictions(golden):
 # ---------------------------------------------------------------------------
 # projection kernel (ofr_project_u8 / _f32)
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("B,D,d", [(1, 4900, 3), (31, 4900, 3), (300, 10000, 99), (513, 777, 260)])
+@pytest.mark.parametrize("B,D,d", [(1, 4900, 3), (31, 4900, 3), (300, 10000, 99), (513, 777, 260), (5, 100, 70)])
 def test_projection_vs_oracle(B, D, d):
-    from opencv_facerecognizer_amd._device import Projection, u8_rows
+    """ofr_project_u8_exact: exact int8-slice MFMA projection vs numpy float64 (feature.py:241-242)."""
+    from opencv_facerecognizer_amd._device import Projection, f64_dev, u8_rows
     r = _rng(B + D + d)
     W = r.normal(0, 1.0 / np.sqrt(D), (D, d))
     X = r.integers(0, 256, (B, D), dtype=np.uint8)
+    X[0] = 255
     P = Projection(W)
-    Y = P.project_u8(u8_rows(X)).cpu().numpy()
-    assert np.all(Y[:, d:] == 0)
     ref = X.astype(np.float64) @ W
-    err = np.linalg.norm(Y[:, :d] - ref, axis=1) / np.linalg.norm(ref, axis=1)
-    assert err.max() < 1e-4, err.max()
-    # with a shift (PCA.project form, feature.py:114-116)
+    Y64 = P.project(u8_rows(X), f64=True).cpu().numpy()
+    # 4 int8 slices represent W to 2^-28 of each column maximum: far below the 1e-4 bound
+    err = np.abs(Y64 - ref).max(axis=1) / np.linalg.norm(ref, axis=1)
+    assert err.max() < 1e-8, err.max()
+    Y = P.project(u8_rows(X)).cpu().numpy()
+    assert Y.shape[1] == max(32, -(-d // 32) * 32) and np.all(Y[:, d:] == 0)
+    np.testing.assert_array_equal(Y[:, :d], Y64.astype(np.float32))   # rounded once from the exact value
+    # with a shift, subtracted in fp64 before the rounding (PCA.project form, feature.py:114-116)
     mu = r.normal(128, 5, D)
-    P2 = Projection(W, shift=(mu @ W))
-    Y2 = P2.project_u8(u8_rows(X)).cpu().numpy()[:, :d]
+    c = mu @ W
+    Y2 = P.project(u8_rows(X), shift64=f64_dev(c), f64=True).cpu().numpy()
     ref2 = (X - mu) @ W
-    err2 = np.linalg.norm(Y2 - ref2, axis=1) / np.linalg.norm(ref2, axis=1)
-    assert err2.max() < 1e-4, err2.max()
+    err2 = np.abs(Y2 - ref2).max(axis=1) / np.linalg.norm(ref2, axis=1)
+    assert err2.max() < 1e-8, err2.max()
+
+
+def test_projection_fp32_weights_exact():
+    """fp32 weights within 2^4 of their column maximum are represented exactly: the result equals the
+    correctly rounded float64 dot product of the fp32 W."""
+    import torch
+    from opencv_facerecognizer_amd._device import Projection, u8_rows
+    r = _rng(21)
+    D, d, B = 2000, 40, 64
+    W32 = (r.uniform(0.5, 1.0, (d, D)) * r.choice([-1.0, 1.0], (d, D))).astype(np.float32)
+    X = r.integers(0, 256, (B, D), dtype=np.uint8)
+    P = Projection(Wt_device=torch.from_numpy(W32).cuda(), D=D)
+    Y = P.project(u8_rows(X), f64=True).cpu().numpy()
+    ref = X.astype(np.float64) @ W32.T.astype(np.float64)   # exact in float64 here (small integers x 24-bit)
+    np.testing.assert_array_equal(Y, ref)
 
 
 def test_pickled_model_predict_matches_reference(golden):
