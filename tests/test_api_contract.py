@@ -1,0 +1,79 @@
+"""Reference API conventions that need no GPU (model.py:40-44, feature.py:269-270, reprs, pickled state),
+and the loud failure of the compute path when no HIP device is visible (no CPU fallback)."""
+import numpy as np
+import pytest
+import torch
+
+from ocvfacerec.facerec.classifier import AbstractClassifier, NearestNeighbor
+from ocvfacerec.facerec.distance import ChiSquareDistance, CosineDistance, EuclideanDistance
+from ocvfacerec.facerec.feature import LDA, PCA, AbstractFeature, Fisherfaces, Identity, SpatialHistogram
+from ocvfacerec.facerec.lbp import ExtendedLBP, LocalDescriptor
+from ocvfacerec.facerec.model import PredictableModel
+from ocvfacerec.facerec.operators import ChainOperator
+from ocvfacerec.trainer.thetrainer import ExtendedPredictableModel, TheTrainer
+
+
+def test_type_checks():
+    with pytest.raises(TypeError, match="feature must be of type AbstractFeature"):
+        PredictableModel(object(), NearestNeighbor())
+    with pytest.raises(TypeError, match="classifier must be of type AbstractClassifier"):
+        PredictableModel(Fisherfaces(), object())
+    with pytest.raises(TypeError, match="LocalDescriptor"):
+        SpatialHistogram(lbp_operator=object())
+    with pytest.raises(Exception, match="FeatureOperator only works"):
+        ChainOperator(PCA(), object())
+
+
+def test_abstract_methods_raise():
+    with pytest.raises(NotImplementedError):
+        AbstractFeature().compute([], [])
+    with pytest.raises(NotImplementedError):
+        AbstractClassifier().predict(None)
+    with pytest.raises(NotImplementedError):
+        AbstractClassifier().update(None, None)
+    with pytest.raises(NotImplementedError):
+        LocalDescriptor(8)(np.zeros((3, 3)))
+
+
+def test_reprs_and_defaults():
+    assert repr(Fisherfaces()) == "Fisherfaces (num_components=0)"
+    assert repr(PCA(5)) == "PCA (num_components=5)" and repr(LDA(2)) == "LDA (num_components=2)"
+    assert repr(NearestNeighbor()) == "NearestNeighbor (k=1, dist_metric=EuclideanDistance)"
+    assert repr(ExtendedLBP()) == "ExtendedLBP (neighbors=8, radius=1)"
+    assert repr(SpatialHistogram()) == "SpatialHistogram (operator=ExtendedLBP (neighbors=8, radius=1), grid=(8, 8))"
+    assert [m().name for m in (EuclideanDistance, CosineDistance, ChiSquareDistance)] == \
+        ["EuclideanDistance", "CosineDistance", "ChiSquareDistance"]
+    m = TheTrainer.get_model((70, 70), {0: "a"})
+    assert isinstance(m, ExtendedPredictableModel) and isinstance(m.feature, Fisherfaces)
+    assert m.classifier.k == 1 and isinstance(m.classifier.dist_metric, EuclideanDistance)
+    assert Identity().extract(5) == 5
+
+
+def test_classes_pickle_under_reference_paths():
+    assert Fisherfaces.__module__ == "ocvfacerec.facerec.feature"
+    assert NearestNeighbor.__module__ == "ocvfacerec.facerec.classifier"
+    assert ExtendedPredictableModel.__module__ == "ocvfacerec.trainer.thetrainer"
+    import ocvfacerec.facerec.feature as f
+    import opencv_facerecognizer_amd.facerec.feature as g
+    assert f is g
+
+
+def test_nearest_neighbor_update_and_state():
+    c = NearestNeighbor(k=3)
+    c.update(np.ones((4, 1)), 2)
+    assert len(c.X) == 1 and list(c.y) == [2]
+    c.__dict__["_dev"] = object()
+    assert "_dev" not in c.__getstate__()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device failure mode")
+def test_compute_path_fails_loudly_without_gpu():
+    from opencv_facerecognizer_amd._lib import OfrError
+    c = NearestNeighbor()
+    c.compute([np.ones((3, 1)), np.zeros((3, 1))], [0, 1])
+    with pytest.raises(OfrError, match="no HIP device"):
+        c.predict(np.ones((3, 1)))
+    with pytest.raises(OfrError, match="no HIP device"):
+        ExtendedLBP()(np.zeros((5, 5), np.uint8))
+    with pytest.raises(OfrError, match="no HIP device"):
+        EuclideanDistance()(np.ones(3), np.zeros(3))
