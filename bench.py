@@ -113,6 +113,21 @@ def cpu_baseline(Wt, gallery, Xq, N_total, seconds):
     }
 
 
+def committed_traffic(cfg):
+    """HBM-side bytes per launch of the search pass from the committed rocprofv3 PMC passes
+    (profiles/*_pmc_summary.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 guide), if measured at this config."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+        try:
+            s = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if s.get("config") == cfg:
+            best = (s["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -210,6 +225,7 @@ def main():
 
     if rank == 0:
         value = B * args.steps / elapsed
+        tr = committed_traffic({"gallery": nl, "batch": B, "d": d, "D": D, "k": k})
         result = {
             "metric": "query faces/sec (Fisherfaces proj + 1-NN, 1M gallery) at 1/2/4/8 GPUs",
             "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -221,7 +237,8 @@ def main():
                        "parallelism": f"gallery-rows/{world} + RCCL all-gather of top-k" if world > 1 else "1 GPU"},
             "roofline": {"kernel": "knn_tile_kernel (ofr_knn_tiles_f32)", "bound": "mfma",
                          "achieved": achieved / 1e12, "peak": PEAK_FP32_MFMA / 1e12, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_MFMA, "traffic": None,
+                         "frac": achieved / PEAK_FP32_MFMA, "traffic": tr[0] if tr else None,
+                         "traffic_source": tr[1] if tr else None,
                          "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
                          "launch_ms": ms_tiles},
             "kernels_ms": {"project_u8_exact": ms_proj, "knn_tiles": ms_tiles, "knn_merge_rerank": ms_merge},
