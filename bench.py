@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--k", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--small-batches", default="32,1", help="extra HBM-regime measurements (B <= 32); '' to skip")
     return ap.parse_args()
 
 
@@ -219,6 +220,37 @@ def main():
     idx = res[1][:, 0]
     acc = float(((idx // args.per_id) == ids_q).double().mean().item())
 
+    # ---- small-batch regime (the recognizers send one face per call): HBM-bound streaming of the gallery ----
+    small = []
+    for bs in [int(x) for x in args.small_batches.split(",") if x.strip()]:
+        Qs = torch.zeros((bs, ld), dtype=torch.float32, device=device)
+        P.project(Xq[:bs], shift64=gallery.shift64, out=Qs)
+        for _ in range(2):
+            gallery.search_phase("tiles", Qs, k)
+        reps = 10
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            gallery.search_phase("tiles", Qs, k)
+        e1.record()
+        torch.cuda.synchronize()
+        ms_t = e0.elapsed_time(e1) / reps
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            P.project(Xq[:bs], shift64=gallery.shift64, out=Qs)
+            gallery.search_phase("tiles", Qs, k)
+            gallery.search_phase("merge", Qs, k, index_base=n0)
+        torch.cuda.synchronize()
+        ms_step = (time.perf_counter() - t1) * 1e3 / reps
+        bytes_t = nl * d * 4 + bs * d * 4                            # gallery streamed once per batch
+        small.append({"batch": bs, "queries_per_s": bs / (ms_step * 1e-3), "ms_per_batch": ms_step,
+                      "roofline": {"kernel": "knn_tile_kernel<Cfg<32,4,1,4>> (ofr_knn_tiles_f32, B<=32)",
+                                   "bound": "hbm", "achieved": bytes_t / (ms_t * 1e-3) / 1e9,
+                                   "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                                   "frac": bytes_t / (ms_t * 1e-3) / PEAK_HBM, "launch_ms": ms_t,
+                                   "algorithmic_bytes_per_launch": bytes_t}})
+
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
     alg_bytes_tiles = nl * d * 4 + B * d * 4                         # gallery + queries read once
@@ -243,6 +275,7 @@ def main():
                          "launch_ms": ms_tiles},
             "kernels_ms": {"project_u8_exact": ms_proj, "knn_tiles": ms_tiles, "knn_merge_rerank": ms_merge},
             "top1_identity_acc": acc,
+            "small_batch": small,
         }
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(Wt, gallery, Xq, N, args.cpu_seconds)

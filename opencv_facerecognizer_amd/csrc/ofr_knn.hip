@@ -33,44 +33,41 @@ struct KnnTileArgs {
   int64_t ntg;     // gallery tiles
 };
 
-template <int METRIC, int KC>
+template <class C, int METRIC, int KC>
 __global__ void __launch_bounds__(256, 1) knn_tile_kernel(KnnTileArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int64_t t = tile::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   const int64_t gt = t / p.ntb;  // gallery tile (consecutive t share it)
   const int64_t qt = t % p.ntb;
-  const int64_t g0 = gt * tile::TM, q0 = qt * tile::TN;
+  const int64_t g0 = gt * tile::TM, q0 = qt * C::TN;
 
-  tile::LoaderF32 la{p.G, p.ldg, p.N, g0};
-  tile::LoaderF32 lb{p.Q, p.ldq, p.B, q0};
-  f32x16 acc[4][4];
-  tile::mainloop(smem, la, lb, p.nk, acc);
+  f32x16 acc[C::RT][C::CT];
+  tile::mainloop<C>(smem, p.G, p.ldg, p.N, g0, p.Q, p.ldq, p.B, q0, p.nk, acc);
 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / C::WN, wc = wave % C::WN;
   const int h = lane >> 5;
-  Cand* buf = reinterpret_cast<Cand*>(smem);  // [2][256][KC]
+  Cand* buf = reinterpret_cast<Cand*>(smem);  // [WM][TN][KC]
 
-  // per-lane aux of its 64 gallery rows
-  float gaux[4][16];
+  float gaux[C::RT][16];
 #pragma unroll
-  for (int rt = 0; rt < 4; ++rt)
+  for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int64_t g = g0 + wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int64_t g = g0 + wr * (C::RT * 32) + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
       gaux[rt][r] = g < p.N ? p.aux[g] : __builtin_nanf("");
     }
 
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
+  for (int ct = 0; ct < C::CT; ++ct) {
     TopList<KC> L;
     L.init();
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt)
+    for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int gl = wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int gl = wr * (C::RT * 32) + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float dot = acc[rt][ct][r];
         float s;
         if (METRIC == OFR_METRIC_EUCLIDEAN) s = __builtin_fmaf(-2.f, dot, gaux[rt][r]);
@@ -86,29 +83,35 @@ __global__ void __launch_bounds__(256, 1) knn_tile_kernel(KnnTileArgs p) {
     }
     L.merge(od, oi);
     if (h == 0) {
-      const int ql = wc * 128 + ct * 32 + (lane & 31);
-      Cand* dst = buf + ((size_t)wr * 256 + ql) * KC;
+      const int ql = wc * (C::CT * 32) + ct * 32 + (lane & 31);
+      Cand* dst = buf + ((size_t)wr * C::TN + ql) * KC;
 #pragma unroll
       for (int j = 0; j < KC; ++j) dst[j] = Cand{L.d[j], L.i[j]};
     }
   }
   __syncthreads();
-  {
+  if ((int)threadIdx.x < C::TN) {
     const int ql = threadIdx.x;
     const int64_t q = q0 + ql;
     TopList<KC> L;
-    float od[KC];
-    int oi[KC];
     const Cand* s0 = buf + (size_t)ql * KC;
-    const Cand* s1 = buf + ((size_t)256 + ql) * KC;
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
       L.d[j] = s0[j].d;
       L.i[j] = s0[j].i;
-      od[j] = s1[j].d;
-      oi[j] = s1[j].i;
     }
-    L.merge(od, oi);
+#pragma unroll
+    for (int w = 1; w < C::WM; ++w) {
+      float od[KC];
+      int oi[KC];
+      const Cand* sw = buf + ((size_t)w * C::TN + ql) * KC;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        od[j] = sw[j].d;
+        oi[j] = sw[j].i;
+      }
+      L.merge(od, oi);
+    }
     if (q < p.B) {
       Cand* out = p.cand + ((size_t)gt * p.B + q) * KC;
 #pragma unroll
@@ -265,19 +268,30 @@ extern "C" size_t ofr_knn_workspace_bytes(int64_t B, int64_t N, int k) {
   return (size_t)T * (size_t)B * kc * sizeof(Cand) + 256;
 }
 
-template <int METRIC, int KC>
-static int launch_knn(hipStream_t st, const KnnTileArgs& a, const MergeArgs& m, int phases) {
+template <class C, int METRIC, int KC>
+static int launch_tiles(hipStream_t st, KnnTileArgs a) {
   static bool attr_done = false;
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)knn_tile_kernel<METRIC, KC>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, tile::LDS_BYTES);
+    hipError_t e = hipFuncSetAttribute((const void*)knn_tile_kernel<C, METRIC, KC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(knn_tile)");
     attr_done = true;
   }
+  a.ntb = cdiv(a.B, C::TN);
+  const int64_t nblocks = a.ntb * a.ntg;
+  if (nblocks >= 0x7fffffffLL) return fail(OFR_E_INVALID, "ofr_knn_f32: grid too large");
+  hipLaunchKernelGGL((knn_tile_kernel<C, METRIC, KC>), dim3((unsigned)nblocks), dim3(256), C::LDS, st, a);
+  OFR_LAUNCH_CHECK("knn_tile_kernel");
+  return OFR_OK;
+}
+
+template <int METRIC, int KC>
+static int launch_knn(hipStream_t st, const KnnTileArgs& a, const MergeArgs& m, int phases) {
   if (phases & 1) {
-    const int64_t nblocks = a.ntb * a.ntg;
-    hipLaunchKernelGGL((knn_tile_kernel<METRIC, KC>), dim3((unsigned)nblocks), dim3(256), tile::LDS_BYTES, st, a);
-    OFR_LAUNCH_CHECK("knn_tile_kernel");
+    // narrow query tiles stream the gallery once per batch (HBM-bound regime); wide tiles are MFMA-bound
+    const int rc = a.B <= tile::CfgSmall::TN ? launch_tiles<tile::CfgSmall, METRIC, KC>(st, a)
+                                             : launch_tiles<tile::CfgBig, METRIC, KC>(st, a);
+    if (rc) return rc;
   }
   if (phases & 2) {
     hipLaunchKernelGGL((knn_merge_rerank_kernel<KC>), dim3((unsigned)m.B), dim3(256), 0, st, m);
@@ -315,9 +329,8 @@ static int knn_impl(void* stream, int metric, const float* Q, int64_t B, int64_t
   a.nk = (int)cdiv(d, tile::BK);
   a.aux = aux;
   a.cand = reinterpret_cast<Cand*>(workspace);
-  a.ntb = cdiv(B, tile::TN);
+  a.ntb = 0;  // set per tile configuration
   a.ntg = cdiv(N, tile::TM);
-  OFR_CHECK_ARG(a.ntb * a.ntg < 0x7fffffffLL, "ofr_knn_f32: grid too large");
   MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, metric, k, index_base, out_d, out_i};
   if (metric == OFR_METRIC_EUCLIDEAN)
     return kc == 8 ? launch_knn<OFR_METRIC_EUCLIDEAN, 8>(st, a, m, phases)
