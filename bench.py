@@ -38,6 +38,7 @@ from opencv_facerecognizer_amd.parallel import exchange_topk, merge_topk, shard_
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 
 PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
+PEAK_I8_MFMA = 5.0e15       # int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, matrix cores)
 PEAK_HBM = 8.0e12           # HBM3E 8 TB/s (spec)
 
 
@@ -55,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--small-batches", default="32,1", help="extra HBM-regime measurements (B <= 32); '' to skip")
+    ap.add_argument("--search", choices=["q8", "fp32"], default="q8",
+                    help="q8: certified int8 coarse pass (+fp32 fallback for uncertified queries); fp32: fp32-MFMA pass")
     return ap.parse_args()
 
 
@@ -177,17 +180,32 @@ def main():
     log(rank, f"setup {time.perf_counter() - t0:.1f}s: gallery rows {nl}/{N} per rank, d={d}, D={D}, B={B}")
 
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    use_q8 = args.search == "q8"
+    if use_q8:
+        gallery._q8_gallery()                                     # gallery int8 slices (once, untimed)
+    qq = None
+    fallbacks = []
 
     def step(events=None):
+        nonlocal qq
         if events:
             events[0].record()
         P.project(Xq, shift64=gallery.shift64, out=Qd)            # fp32(W^T x - c), exact int8 MFMA
+        if use_q8:
+            qq = gallery.quantize_queries(Qd, qq)
         if events:
             events[1].record()
-        gallery.search_phase("tiles", Qd, k)
+        if use_q8:
+            gallery.search_q8_phase(1, Qd, qq, k)
+        else:
+            gallery.search_phase("tiles", Qd, k)
         if events:
             events[2].record()
-        gallery.search_phase("merge", Qd, k, index_base=n0, out=out)
+        if use_q8:
+            gallery.search_q8_phase(2, Qd, qq, k, index_base=n0, out=out)
+            fallbacks.append(gallery.fallback(Qd, qq, k, out, index_base=n0))
+        else:
+            gallery.search_phase("merge", Qd, k, index_base=n0, out=out)
         if events:
             events[3].record()
         if world > 1:
@@ -253,11 +271,18 @@ def main():
 
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
-    alg_bytes_tiles = nl * d * 4 + B * d * 4                         # gallery + queries read once
+    if use_q8:
+        peak, kname = PEAK_I8_MFMA, "q8s::tile_kernel (ofr_knn_q8 phase 1, int8 slices)"
+        alg_bytes_tiles = nl * d * 2 + B * d * 2                     # two int8 slices of gallery + queries
+        executed = 3 * flops_tiles                                   # x1.y1 + x1.y2 + x2.y1 int8 products
+    else:
+        peak, kname = PEAK_FP32_MFMA, "knn_tile_kernel (ofr_knn_tiles_f32)"
+        alg_bytes_tiles = nl * d * 4 + B * d * 4                     # gallery + queries read once
+        executed = flops_tiles
 
     if rank == 0:
         value = B * args.steps / elapsed
-        tr = committed_traffic({"gallery": nl, "batch": B, "d": d, "D": D, "k": k})
+        tr = committed_traffic({"gallery": nl, "batch": B, "d": d, "D": D, "k": k, "search": args.search})
         result = {
             "metric": "query faces/sec (Fisherfaces proj + 1-NN, 1M gallery) at 1/2/4/8 GPUs",
             "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -267,13 +292,16 @@ def main():
                                    "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1",
                        "gallery": N, "global_batch": B, "d": d, "D": D, "k": k,
                        "parallelism": f"gallery-rows/{world} + RCCL all-gather of top-k" if world > 1 else "1 GPU"},
-            "roofline": {"kernel": "knn_tile_kernel (ofr_knn_tiles_f32)", "bound": "mfma",
-                         "achieved": achieved / 1e12, "peak": PEAK_FP32_MFMA / 1e12, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_MFMA, "traffic": tr[0] if tr else None,
+            "roofline": {"kernel": kname, "bound": "mfma",
+                         "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s" if not use_q8 else "TOPS",
+                         "frac": achieved / peak, "traffic": tr[0] if tr else None,
+                         "executed_ops_per_launch": executed, "executed_frac": executed / (ms_tiles * 1e-3) / peak,
                          "traffic_source": tr[1] if tr else None,
                          "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
                          "launch_ms": ms_tiles},
-            "kernels_ms": {"project_u8_exact": ms_proj, "knn_tiles": ms_tiles, "knn_merge_rerank": ms_merge},
+            "kernels_ms": {"project_u8_exact" + ("+q8_quantize" if use_q8 else ""): ms_proj, "knn_tiles": ms_tiles,
+                           "knn_merge_rerank" + ("+certificate+fallback" if use_q8 else ""): ms_merge},
+            "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
             "top1_identity_acc": acc,
             "small_batch": small,
         }

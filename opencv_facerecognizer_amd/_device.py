@@ -11,11 +11,16 @@ Layouts:
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
 from . import _lib
 from ._lib import call, ptr, stream
+
+
+SMALL_BATCH = 32   # B <= 32: HBM-streaming fp32 tiles; larger batches: certified int8 tiles (Euclidean)
 
 
 def round_up(x, m):
@@ -189,6 +194,67 @@ class FloatGallery:
         if self.N > 0:
             call("ofr_row_aux", stream(), self.metric, ptr(self.G), self.N, self.d, self.ld, ptr(self.aux))
         self.ws = Workspace()
+        self.q8 = None
+        self.last_fallbacks = 0
+
+    # -- certified int8 coarse pass (Euclidean, B > 32) ------------------------------------------
+    def use_q8(self, B, k):
+        mode = os.environ.get("OFR_SEARCH", "auto")
+        return (mode != "fp32" and self.metric == _lib.METRIC_EUCLIDEAN and self.N > 0
+                and B > SMALL_BATCH and k <= 16)
+
+    def _q8_gallery(self):
+        if self.q8 is None:
+            dev_ = self.G.device
+            ldk = round_up(self.d, 64)
+            G1 = torch.empty((self.N, ldk), dtype=torch.int8, device=dev_)
+            G2 = torch.empty((self.N, ldk), dtype=torch.int8, device=dev_)
+            gs = torch.empty(self.N, dtype=torch.float32, device=dev_)
+            st = torch.empty((self.N, 3), dtype=torch.float64, device=dev_)
+            gmax = torch.empty(4, dtype=torch.float64, device=dev_)
+            call("ofr_q8_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, ptr(G1), ptr(G2), ldk,
+                 ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
+            self.q8 = dict(G1=G1, G2=G2, scale=gs, stats=st, gmax=gmax, ldk=ldk)
+        return self.q8
+
+    def quantize_queries(self, Qd, out=None):
+        g = self._q8_gallery()
+        B = Qd.shape[0]
+        if out is None or out["Q1"].shape[0] != B:
+            out = dict(Q1=torch.empty((B, g["ldk"]), dtype=torch.int8, device=Qd.device),
+                       Q2=torch.empty((B, g["ldk"]), dtype=torch.int8, device=Qd.device),
+                       scale=torch.empty(B, dtype=torch.float32, device=Qd.device),
+                       stats=torch.empty((B, 3), dtype=torch.float64, device=Qd.device),
+                       cert=torch.empty(B, dtype=torch.int32, device=Qd.device))
+        call("ofr_q8_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Q1"]), ptr(out["Q2"]),
+             g["ldk"], ptr(out["scale"]), ptr(out["stats"]), None, None)
+        return out
+
+    def search_q8_phase(self, phases, Qd, qq, k, index_base=0, out=None):
+        """phases 1 = int8 tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"])."""
+        g = self._q8_gallery()
+        B = Qd.shape[0]
+        if out is None:
+            out = (torch.empty((B, k), dtype=torch.float64, device=Qd.device),
+                   torch.empty((B, k), dtype=torch.int64, device=Qd.device))
+        ws = self.ws.get(_lib.load().ofr_knn_q8_workspace_bytes(B, self.N), Qd.device)
+        call("ofr_knn_q8", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Q1"]), ptr(qq["Q2"]), ptr(qq["scale"]),
+             ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["G1"]), ptr(g["G2"]), g["ldk"],
+             ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
+             ptr(ws), ws.numel())
+        return out
+
+    def fallback(self, Qd, qq, k, out, index_base=0):
+        """Re-run uncertified queries on the fp32 path; returns how many there were (host sync)."""
+        bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
+        n = int(bad.numel())
+        self.last_fallbacks = n
+        if n:
+            sub = Qd.index_select(0, bad).contiguous()
+            d2, i2 = self._search_f32(sub, k, index_base)
+            out[0].index_copy_(0, bad, d2)
+            out[1].index_copy_(0, bad, i2)
+        return n
 
     def query_rows(self, Q64):
         """Host or device fp64 query features [B][d] -> centred fp32 search rows [B][ld]."""
@@ -212,6 +278,15 @@ class FloatGallery:
         """Qd: centred fp32 search rows [B][ld] (see query_rows / Projection.project with shift64)."""
         if Qd.shape[1] != self.ld:
             raise ValueError(f"query row stride {Qd.shape[1]} != gallery stride {self.ld}")
+        B = Qd.shape[0]
+        if self.use_q8(B, k):
+            qq = self.quantize_queries(Qd)
+            out = self.search_q8_phase(3, Qd, qq, k, index_base)
+            self.fallback(Qd, qq, k, out, index_base)
+            return out
+        return self._search_f32(Qd, k, index_base)
+
+    def _search_f32(self, Qd, k, index_base=0):
         B = Qd.shape[0]
         out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
         out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)

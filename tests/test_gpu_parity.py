@@ -79,6 +79,45 @@ def test_knn_vs_oracle(metric, B, N, d, k):
     assert ties <= max(1, B // 100)
 
 
+@pytest.mark.parametrize("B,N,d,k", [(33, 300, 3, 1), (300, 5000, 99, 5), (257, 3000, 300, 16), (600, 20000, 64, 3),
+                                     (1000, 70000, 130, 1)])
+@pytest.mark.parametrize("mode", ["q8", "fp32"])
+def test_knn_euclidean_paths_vs_oracle(monkeypatch, mode, B, N, d, k):
+    """Batches > 32 take the certified int8 pass (ofr_knn_q8) unless OFR_SEARCH=fp32."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto" if mode == "q8" else "fp32")
+    r = _rng(B * 11 + N + d)
+    protos = r.normal(0, 30, (max(N // 10, 1), d))
+    G = (protos[np.arange(N) % len(protos)] + r.normal(0, 5, (N, d))).astype(np.float32).astype(np.float64)
+    Q = (protos[r.integers(0, len(protos), B)] + r.normal(0, 5, (B, d))).astype(np.float32).astype(np.float64)
+    Q[0] = G[N // 2]
+    G[N - 1] = G[3]
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    assert g.use_q8(B, k) == (mode == "q8")
+    dd, ii = g.search(g.query_rows(Q), k)
+    ties = _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
+    assert ties <= max(1, B // 100)
+    if mode == "q8":
+        assert g.last_fallbacks <= B // 10     # well-separated data: nearly every query certifies
+
+
+def test_knn_q8_certificate_forces_fallback(monkeypatch):
+    """Rows that differ by far less than the int8 slice resolution cannot be certified: the
+    uncertified queries must be re-run on the fp32 path and still match the oracle."""
+    from opencv_facerecognizer_amd._device import FloatGallery
+    from opencv_facerecognizer_amd import _lib
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(99)
+    base = r.normal(0, 50, 64)
+    G = (base + r.normal(0, 1e-3, (2000, 64))).astype(np.float32).astype(np.float64)
+    Q = (base + r.normal(0, 1e-3, (100, 64))).astype(np.float32).astype(np.float64)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    dd, ii = g.search(g.query_rows(Q), 3)
+    assert g.last_fallbacks > 0
+    _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
+
+
 def test_knn_exact_duplicates_tie_to_lowest_index():
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
