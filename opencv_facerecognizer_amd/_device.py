@@ -21,6 +21,9 @@ from ._lib import call, ptr, stream
 
 
 SMALL_BATCH = 32   # B <= 32: HBM-streaming fp32 tiles; larger batches: certified int8 tiles (Euclidean)
+# the int8 pass keeps 16 candidates per query; a certificate needs slack between the k-th
+# exact distance and the 16th coarse score, so k is limited to half of that
+Q8_MAX_K = 8
 
 
 def round_up(x, m):
@@ -201,7 +204,7 @@ class FloatGallery:
     def use_q8(self, B, k):
         mode = os.environ.get("OFR_SEARCH", "auto")
         return (mode != "fp32" and self.metric == _lib.METRIC_EUCLIDEAN and self.N > 0
-                and B > SMALL_BATCH and k <= 16)
+                and B > SMALL_BATCH and k <= Q8_MAX_K)
 
     def _q8_gallery(self):
         if self.q8 is None:

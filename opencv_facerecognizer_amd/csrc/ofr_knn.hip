@@ -16,6 +16,7 @@
 //         the REFERENCE distance recomputed exactly in fp64 for those R rows
 //         (direct (q-g)^2 sum / -q.g/sqrt(q.q g.g)), sorted by (distance,
 //         index), best k written as fp64 + int64.
+#include <type_traits>
 #include "ofr_gemm_tile.h"
 #include "ofr_topk.h"
 
@@ -50,17 +51,19 @@ __global__ void __launch_bounds__(256, 1) knn_tile_kernel(KnnTileArgs p) {
   const int h = lane >> 5;
   Cand* buf = reinterpret_cast<Cand*>(smem);  // [WM][TN][KC]
 
-  float gaux[C::RT][16];
-#pragma unroll
-  for (int rt = 0; rt < C::RT; ++rt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t g = g0 + wr * (C::RT * 32) + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      gaux[rt][r] = g < p.N ? p.aux[g] : __builtin_nanf("");
-    }
+  // gallery aux of the tile staged once in LDS (past the candidate buffer): keeps
+  // the epilogue free of per-element global loads and of a 16*RT register table
+  float* gtab = reinterpret_cast<float*>(smem + C::LDS - tile::TM * 4);
+  static_assert((size_t)C::WM * C::TN * KC * sizeof(Cand) + tile::TM * 4 <= (size_t)C::LDS, "epilogue LDS");
+  {
+    const int64_t g = g0 + threadIdx.x;
+    gtab[threadIdx.x] = g < p.N ? p.aux[g] : __builtin_nanf("");
+  }
+  __syncthreads();
 
-#pragma unroll
-  for (int ct = 0; ct < C::CT; ++ct) {
+  // one instantiation per query block: a constant ct keeps acc[][ct] in registers
+  auto epi = [&](auto ctc) {
+    constexpr int ct = decltype(ctc)::value;
     TopList<KC> L;
     L.init();
 #pragma unroll
@@ -69,9 +72,10 @@ __global__ void __launch_bounds__(256, 1) knn_tile_kernel(KnnTileArgs p) {
       for (int r = 0; r < 16; ++r) {
         const int gl = wr * (C::RT * 32) + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float dot = acc[rt][ct][r];
+        const float ga = gtab[gl];
         float s;
-        if (METRIC == OFR_METRIC_EUCLIDEAN) s = __builtin_fmaf(-2.f, dot, gaux[rt][r]);
-        else s = -dot * gaux[rt][r];
+        if (METRIC == OFR_METRIC_EUCLIDEAN) s = __builtin_fmaf(-2.f, dot, ga);
+        else s = -dot * ga;
         L.insert(s, (int)(g0 + gl));   // NaN (masked rows) never inserts
       }
     float od[KC];
@@ -88,7 +92,12 @@ __global__ void __launch_bounds__(256, 1) knn_tile_kernel(KnnTileArgs p) {
 #pragma unroll
       for (int j = 0; j < KC; ++j) dst[j] = Cand{L.d[j], L.i[j]};
     }
-  }
+  };
+  static_assert(C::CT <= 4, "epilogue unroll");
+  epi(std::integral_constant<int, 0>{});
+  if constexpr (C::CT > 1) epi(std::integral_constant<int, 1>{});
+  if constexpr (C::CT > 2) epi(std::integral_constant<int, 2>{});
+  if constexpr (C::CT > 3) epi(std::integral_constant<int, 3>{});
   __syncthreads();
   if ((int)threadIdx.x < C::TN) {
     const int ql = threadIdx.x;
