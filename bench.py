@@ -182,7 +182,8 @@ def main():
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     use_q8 = args.search == "q8"
     if use_q8:
-        gallery._q8_gallery()                                     # gallery int8 slices (once, untimed)
+        gallery._q8_gallery(1)                                    # gallery int8 slices (once, untimed)
+        gallery._q8_gallery(2)
     qq = None
     fallbacks = []
 
@@ -192,7 +193,7 @@ def main():
             events[0].record()
         P.project(Xq, shift64=gallery.shift64, out=Qd)            # fp32(W^T x - c), exact int8 MFMA
         if use_q8:
-            qq = gallery.quantize_queries(Qd, qq)
+            qq = gallery.quantize_queries(Qd, qq, slices=1)
         if events:
             events[1].record()
         if use_q8:
@@ -272,9 +273,9 @@ def main():
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
     if use_q8:
-        peak, kname = PEAK_I8_MFMA, "q8s::tile_kernel (ofr_knn_q8 phase 1, int8 slices)"
-        alg_bytes_tiles = nl * d * 2 + B * d * 2                     # two int8 slices of gallery + queries
-        executed = 3 * flops_tiles                                   # x1.y1 + x1.y2 + x2.y1 int8 products
+        peak, kname = PEAK_I8_MFMA, "q8s::tile_kernel<1> (ofr_knn_q8 phase 1, one int8 slice)"
+        alg_bytes_tiles = nl * d + B * d                             # one int8 slice of gallery + queries
+        executed = flops_tiles                                       # x1.y1
     else:
         peak, kname = PEAK_FP32_MFMA, "knn_tile_kernel (ofr_knn_tiles_f32)"
         alg_bytes_tiles = nl * d * 4 + B * d * 4                     # gallery + queries read once
@@ -287,7 +288,9 @@ def main():
             "metric": "query faces/sec (Fisherfaces proj + 1-NN, 1M gallery) at 1/2/4/8 GPUs",
             "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f32 (fp32 MFMA scores, fp64 exact re-rank)", "data": "synthetic",
+            "vs_baseline": None,
+            "dtype": ("i8 (int8 MFMA coarse scores, certified; fp64 exact re-rank)" if use_q8 else
+                      "f32 (fp32 MFMA scores, fp64 exact re-rank)"), "data": "synthetic",
             "config": {"workload": "configs[2]: Fisherfaces projection + 1-NN, 1M-image gallery (100k ids x 10), "
                                    "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1",
                        "gallery": N, "global_batch": B, "d": d, "D": D, "k": k,
@@ -302,6 +305,7 @@ def main():
             "kernels_ms": {"project_u8_exact" + ("+q8_quantize" if use_q8 else ""): ms_proj, "knn_tiles": ms_tiles,
                            "knn_merge_rerank" + ("+certificate+fallback" if use_q8 else ""): ms_merge},
             "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
+            "uncertified_after_two_slices": (list(gallery.last_fallbacks)[1] if use_q8 else None),
             "top1_identity_acc": acc,
             "small_batch": small,
         }

@@ -123,28 +123,31 @@ int ofr_knn_merge_f32(void* stream, int metric, const float* Q, int64_t B, int64
                       double* out_d, int64_t* out_i, void* workspace, size_t workspace_bytes);
 
 /* Certified int8 coarse pass (Euclidean, B > 32) -----------------------------
- * Rows (gallery once, query batch per call) are split into two int8 slices
- * with a power-of-two scale: x~ = s (x1 + x2/2^7); per row stats[3] = (||x~||,
- * ||x - x~||, s 2^-7 ||x2||) in fp64.  ofr_q8_quantize_rows also reduces the
- * gallery-wide maxima (A, E, T, max aux) into maxima[4] when maxima != NULL.
- * X1, X2: int8 [R][ldk], ldk % 64 == 0, ldk >= round_up(d, 64).               */
-int ofr_q8_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int8_t* X1,
-                         int8_t* X2, int64_t ldk, float* scale, double* stats, const float* aux,
+ * Rows (gallery once, query batch per call) are cut into int8 slices with a
+ * power-of-two scale s (max|x|/s in (63.5, 127]):
+ *   slices = 1:  x~ = s x1                 Xs [R][ld], ld % 128 == 0, ld >= round_up(d, 128)
+ *   slices = 2:  x~ = s (x1 + x2/2^7)      Xs [R][ld], ld % 128 == 0, ld >= 2 round_up(d, 64);
+ *                per 64 features, 64 bytes of x1 then 64 bytes of x2 (one 128-B line)
+ * Per row stats[3] = (||x~||, ||x - x~||, s 2^-7 ||x2||) in fp64 (third = 0 for
+ * one slice).  With maxima != NULL the gallery-wide maxima (A, E, T, max aux)
+ * are reduced into maxima[4].                                                  */
+int ofr_q8_quantize_rows(void* stream, int slices, const float* X, int64_t R, int64_t d, int64_t ldx,
+                         int8_t* Xs, int64_t ld, float* scale, double* stats, const float* aux,
                          double* maxima);
-/* The search: v_mfma_i32_32x32x32_i8 sums x1.y1 and x1.y2 + x2.y1 exactly, the
- * coarse score ||g||^2 - 2 s_q s_g (P0 + P1/2^7) keeps the best 16 rows per
- * 256-row tile and query; the merge re-ranks the best 16 with the exact fp64
- * distance (distance.py:60) and writes cert[q] = 1 iff the rigorous bound
+/* The search: v_mfma_i32_32x32x32_i8 sums x1.y1 (and x1.y2 + x2.y1) exactly,
+ * the coarse score ||g||^2 - 2 s_q s_g (P0 + P1/2^7) keeps the best 16 rows
+ * per 256-row tile and query; the merge re-ranks the best 16 with the exact
+ * fp64 distance (distance.py:60) and writes cert[q] = 1 iff the rigorous bound
  * |S - S~| <= dS(q) proves that no other row can reach the k-th neighbour
- * (DESIGN.md §3).  Queries with cert[q] == 0 must be re-run on ofr_knn_f32.
- * Q/G: the fp32 rows the slices were made from (centred), for the re-rank.
- * phases: 1 = tiles, 2 = merge, 3 = both.  k <= 16.                          */
+ * (DESIGN.md §3).  Queries with cert[q] == 0 must be re-run with more slices
+ * or on ofr_knn_f32.  Q/G: the fp32 rows the slices were made from (centred),
+ * for the re-rank.  phases: 1 = tiles, 2 = merge, 3 = both.  k <= 16.        */
 size_t ofr_knn_q8_workspace_bytes(int64_t B, int64_t N);
-int ofr_knn_q8(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const int8_t* Q1,
-               const int8_t* Q2, const float* qscale, const double* qstats, const float* G, int64_t N,
-               int64_t ldg, int64_t d, const int8_t* G1, const int8_t* G2, int64_t ldk,
-               const float* gscale, const float* aux, const double* gmax, int k, int64_t index_base,
-               double* out_d, int64_t* out_i, int* cert, void* workspace, size_t workspace_bytes);
+int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, int64_t ldq, const int8_t* Qs,
+               const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
+               const int8_t* Gs, int64_t ld, const float* gscale, const float* aux, const double* gmax,
+               int k, int64_t index_base, double* out_d, int64_t* out_i, int* cert, void* workspace,
+               size_t workspace_bytes);
 
 /* Merge P sorted (distance, index) lists per query into the best k:
  * in_d/in_i [B][P*kin] (list p at columns [p*kin, (p+1)*kin)), ascending by

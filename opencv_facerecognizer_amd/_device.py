@@ -201,63 +201,83 @@ class FloatGallery:
         self.last_fallbacks = 0
 
     # -- certified int8 coarse pass (Euclidean, B > 32) ------------------------------------------
+    # Tier 1: one int8 slice (x~ = s x1), 256x256 tiles.  Tier 2, for the queries tier 1 could
+    # not certify: two slices (x~ = s (x1 + x2/2^7)).  Tier 3: the fp32 path.  Every tier ends in
+    # the exact fp64 re-rank; tiers 1-2 only answer where the certificate proves the result exact.
     def use_q8(self, B, k):
         mode = os.environ.get("OFR_SEARCH", "auto")
         return (mode != "fp32" and self.metric == _lib.METRIC_EUCLIDEAN and self.N > 0
                 and B > SMALL_BATCH and k <= Q8_MAX_K)
 
-    def _q8_gallery(self):
+    @staticmethod
+    def _q8_ld(d, slices):
+        return round_up(d, 128) if slices == 1 else 2 * round_up(d, 64)
+
+    def _q8_gallery(self, slices=1):
         if self.q8 is None:
+            self.q8 = {}
+        if slices not in self.q8:
             dev_ = self.G.device
-            ldk = round_up(self.d, 64)
-            G1 = torch.empty((self.N, ldk), dtype=torch.int8, device=dev_)
-            G2 = torch.empty((self.N, ldk), dtype=torch.int8, device=dev_)
+            ld = self._q8_ld(self.d, slices)
+            Gs = torch.empty((self.N, ld), dtype=torch.int8, device=dev_)
             gs = torch.empty(self.N, dtype=torch.float32, device=dev_)
             st = torch.empty((self.N, 3), dtype=torch.float64, device=dev_)
             gmax = torch.empty(4, dtype=torch.float64, device=dev_)
-            call("ofr_q8_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, ptr(G1), ptr(G2), ldk,
+            call("ofr_q8_quantize_rows", stream(), slices, ptr(self.G), self.N, self.d, self.ld, ptr(Gs), ld,
                  ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
-            self.q8 = dict(G1=G1, G2=G2, scale=gs, stats=st, gmax=gmax, ldk=ldk)
-        return self.q8
+            self.q8[slices] = dict(Gs=Gs, scale=gs, stats=st, gmax=gmax, ld=ld)
+        return self.q8[slices]
 
-    def quantize_queries(self, Qd, out=None):
-        g = self._q8_gallery()
+    def quantize_queries(self, Qd, out=None, slices=1):
+        ld = self._q8_ld(self.d, slices)
         B = Qd.shape[0]
-        if out is None or out["Q1"].shape[0] != B:
-            out = dict(Q1=torch.empty((B, g["ldk"]), dtype=torch.int8, device=Qd.device),
-                       Q2=torch.empty((B, g["ldk"]), dtype=torch.int8, device=Qd.device),
+        if out is None or out["Qs"].shape[0] != B or out["slices"] != slices:
+            out = dict(Qs=torch.empty((B, ld), dtype=torch.int8, device=Qd.device),
                        scale=torch.empty(B, dtype=torch.float32, device=Qd.device),
                        stats=torch.empty((B, 3), dtype=torch.float64, device=Qd.device),
-                       cert=torch.empty(B, dtype=torch.int32, device=Qd.device))
-        call("ofr_q8_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Q1"]), ptr(out["Q2"]),
-             g["ldk"], ptr(out["scale"]), ptr(out["stats"]), None, None)
+                       cert=torch.empty(B, dtype=torch.int32, device=Qd.device), slices=slices)
+        call("ofr_q8_quantize_rows", stream(), slices, ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]), ld,
+             ptr(out["scale"]), ptr(out["stats"]), None, None)
         return out
 
     def search_q8_phase(self, phases, Qd, qq, k, index_base=0, out=None):
-        """phases 1 = int8 tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"])."""
-        g = self._q8_gallery()
+        """phases 1 = int8 tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"]), 3 = both."""
+        g = self._q8_gallery(qq["slices"])
         B = Qd.shape[0]
         if out is None:
             out = (torch.empty((B, k), dtype=torch.float64, device=Qd.device),
                    torch.empty((B, k), dtype=torch.int64, device=Qd.device))
         ws = self.ws.get(_lib.load().ofr_knn_q8_workspace_bytes(B, self.N), Qd.device)
-        call("ofr_knn_q8", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Q1"]), ptr(qq["Q2"]), ptr(qq["scale"]),
-             ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["G1"]), ptr(g["G2"]), g["ldk"],
-             ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
-             ptr(ws), ws.numel())
+        call("ofr_knn_q8", stream(), phases, qq["slices"], ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
+             ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), g["ld"],
+             ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]),
+             ptr(qq["cert"]), ptr(ws), ws.numel())
         return out
 
     def fallback(self, Qd, qq, k, out, index_base=0):
-        """Re-run uncertified queries on the fp32 path; returns how many there were (host sync)."""
+        """Re-run the queries tier 1 left uncertified: two slices, then fp32 for what remains.
+        Returns the number of tier-1 failures (host sync); self.last_fallbacks = (tier-1, tier-2) failures."""
         bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
-        n = int(bad.numel())
-        self.last_fallbacks = n
-        if n:
+        n1 = int(bad.numel())
+        n2 = 0
+        if n1:
             sub = Qd.index_select(0, bad).contiguous()
-            d2, i2 = self._search_f32(sub, k, index_base)
+            if qq["slices"] == 1:
+                q2 = self.quantize_queries(sub, slices=2)
+                d2, i2 = self.search_q8_phase(3, sub, q2, k, index_base)
+                bad2 = torch.nonzero(q2["cert"] == 0).reshape(-1)
+                n2 = int(bad2.numel())
+                if n2:
+                    d3, i3 = self._search_f32(sub.index_select(0, bad2).contiguous(), k, index_base)
+                    d2.index_copy_(0, bad2, d3)
+                    i2.index_copy_(0, bad2, i3)
+            else:
+                n2 = n1
+                d2, i2 = self._search_f32(sub, k, index_base)
             out[0].index_copy_(0, bad, d2)
             out[1].index_copy_(0, bad, i2)
-        return n
+        self.last_fallbacks = (n1, n2)
+        return n1
 
     def query_rows(self, Q64):
         """Host or device fp64 query features [B][d] -> centred fp32 search rows [B][ld]."""
@@ -283,7 +303,8 @@ class FloatGallery:
             raise ValueError(f"query row stride {Qd.shape[1]} != gallery stride {self.ld}")
         B = Qd.shape[0]
         if self.use_q8(B, k):
-            qq = self.quantize_queries(Qd)
+            # OFR_SEARCH=q8x2 starts at the two-slice tier (tests / hard data)
+            qq = self.quantize_queries(Qd, slices=2 if os.environ.get("OFR_SEARCH") == "q8x2" else 1)
             out = self.search_q8_phase(3, Qd, qq, k, index_base)
             self.fallback(Qd, qq, k, out, index_base)
             return out

@@ -19,9 +19,10 @@
 // gives a per-query bound dS(q).
 //
 // Certificate.  Each 256-row gallery tile keeps its best KC=16 coarse scores
-// per query; the merge keeps the best R=16 overall (tau = the 16th).  Every
-// row outside the final list has S~ >= tau (a tile contributing < 16 rows
-// below tau cannot hide one).  After the EXACT fp64 re-rank of the 16
+// per query (as keys: the score truncated toward -inf by < 256 ulp, ties by
+// row); the merge keeps the best R=16 overall (tau = the 16th, truncated).
+// Every row outside the final list has S~ >= tau (a tile contributing < 16
+// rows below tau cannot hide one; truncation only lowers tau).  After the EXACT fp64 re-rank of the 16
 // candidates, the top-k is proven equal to the exact top-k when
 //     S_k(exact) < tau - dS(q)
 // (strictly: no excluded row can reach or tie the k-th).  cert[q] = 1 then;
@@ -37,29 +38,57 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int KC = 16;
-constexpr int TG = 256, TQ = 128, BK = 64, NST = 3;
-constexpr int PG = TG * BK, PQ = TQ * BK;          // 16 KiB, 8 KiB per slice panel
-constexpr int STAGE = 2 * PG + 2 * PQ;             // 48 KiB
-constexpr int LDS = NST * STAGE;                   // 144 KiB
-constexpr int IPW = 4 + 4 + 2 + 2;                 // DMA wave-instructions per wave per panel
+constexpr int TG = 256;                            // gallery rows per tile
+constexpr int ROWB = 128;                          // LDS/global bytes per row and k step (one 128-B line)
+constexpr int GROUP_G = 4;                         // gallery tiles per tile group (tile_coords)
 
-__device__ __forceinline__ int off(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 2) & 3)) << 4); }
+// Two tile shapes share the engine (SL = int8 slices per row):
+//   SL = 1: 256 x 256 tile, k step 128 (x1 only), 2 LDS stages of 64 KiB, acc 4x4 blocks/wave
+//   SL = 2: 256 x 128 tile, k step 64 (x1 | x2 per 128-B line), 3 stages of 48 KiB, acc 2 x 4x2
+template <int SL>
+struct Shape {
+  static constexpr int TQ = SL == 1 ? 256 : 128;
+  static constexpr int BK = ROWB / SL;             // features per k step
+  static constexpr int NST = SL == 1 ? 2 : 3;
+  static constexpr int CT = TQ / 64;               // 32-query blocks per wave (2 x 2 wave grid)
+  static constexpr int NKS = BK / 32;              // MFMA k-halves per step (each MFMA: k = 32)
+  static constexpr int PG = TG * ROWB, PQ = TQ * ROWB;
+  static constexpr int STAGE = PG + PQ;
+  static constexpr int LDS = NST * STAGE;          // 128 / 144 KiB
+  static constexpr int IPW = (TG + TQ) / 8 / 4;    // DMA wave-instructions per wave per stage (16 / 12)
+  static constexpr int YOUNG = (NST - 2) * IPW;    // DMAs allowed in flight at the stage wait
+  static constexpr int NFRAG = 4 + CT;             // fragment reads per k-half per slice
+  static constexpr int MF_PER_KS = 4 * CT * (SL == 1 ? 1 : 3);
+};
 
+// 128-B LDS rows = 8 chunks of 16 B, XOR-swizzled by ((row >> 1) & 7) so that the 16
+// rows of a ds_read_b128 lane group hit 16 distinct bank quads.  SL = 1: chunk c holds
+// features 16c..16c+15 of the step; SL = 2: chunks 0-3 slice 1, 4-7 slice 2.
+__device__ __forceinline__ int off(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// rows [r0, r0 + ROWS) of a slice matrix, k step kt -> LDS panel.
+// One wave-instruction moves 8 full rows (8 x 128 B = 1 KiB, one 128-B line per row).
 template <int ROWS>
-__device__ __forceinline__ void dma(const int8_t* base, int64_t ldk, int64_t rows, int64_t r0, char* panel, int kt) {
-  constexpr int NINS = ROWS / 16;        // 16 rows x 64 B per wave-instruction
-  constexpr int PER = NINS / 4;
+__device__ __forceinline__ void dma(const int8_t* base, int64_t ld, int64_t rows, int64_t r0, char* panel, int kt) {
+  constexpr int PER = ROWS / 8 / 4;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int t = 0; t < PER; ++t) {
     const int ins = wave * PER + t;
-    const int row = ins * 16 + (lane >> 2);
-    const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+    const int row = ins * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
     int64_t gr = r0 + row;
     gr = gr < rows ? gr : rows - 1;
-    const int8_t* src = base + gr * ldk + (int64_t)kt * BK + chunk * 16;
+    const int8_t* src = base + gr * ld + (int64_t)kt * ROWB + chunk * 16;
     __builtin_amdgcn_global_load_lds((const OFR_GLOBAL void*)src, (OFR_LDS void*)(panel + ins * 1024), 16, 0, 0);
   }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else static_assert(N == 0 || N == 12, "vmcnt");
 }
 
 __device__ __forceinline__ void barrier() {
@@ -69,16 +98,17 @@ __device__ __forceinline__ void barrier() {
 }
 
 struct TileArgs {
-  const int8_t *G1, *G2;
-  int64_t N, ldk;
+  const int8_t* G;     // gallery slices [N][ld]
+  int64_t N, ld;
   const float* gscale;
   const float* aux;
-  const int8_t *Q1, *Q2;
+  const int8_t* Q;     // query slices [B][ld]
   int64_t B;
   const float* qscale;
   int nk;
   Cand* cand;   // [T][B][KC]
   int64_t ntq, ntg;
+  int64_t gg;   // gallery tiles per tile group (see tile_coords)
 };
 
 __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblocks) {
@@ -87,74 +117,187 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblocks) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + s;
 }
 
+// Tile order.  Tiles come in groups of gg gallery tiles x all query tiles; inside
+// a group the gallery tile varies fastest.  With the XCD-contiguous remap, the
+// ~32 workgroups resident on one XCD then cover gg gallery panels x 32/gg query
+// panels, so both operands are shared in that XCD's L2.
+__device__ __forceinline__ void tile_coords(int64_t t, const TileArgs& p, int64_t& gt, int64_t& qt) {
+  const int64_t group = t / (p.gg * p.ntq), within = t % (p.gg * p.ntq);
+  const int64_t gbase = group * p.gg;
+  const int64_t gg = p.ntg - gbase < p.gg ? p.ntg - gbase : p.gg;
+  qt = within / gg;
+  gt = gbase + within % gg;
+}
+
+// ---- keys of the tile epilogue --------------------------------------------------------
+// A coarse score becomes an order-preserving u32 whose low 8 bits are replaced by
+// the row's index inside the 256-row tile: u32 order = (score, index) order with the
+// score truncated by < 256 ulp toward -inf.  A sorted list of keys takes a new key
+// with one v_med3_u32 per slot, no compares on indices, no branches.
+// The truncated value is a LOWER bound of the fp32 coarse score, which is the side
+// the certificate needs (tau below).
+constexpr uint32_t KEY_NONE = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t score_key(float sc, int local) {
+  const uint32_t b = __float_as_uint(sc);
+  const uint32_t m = (uint32_t)((int32_t)b >> 31) | 0x80000000u;
+  return ((b ^ m) & ~0xffu) | (uint32_t)local;
+}
+__device__ __forceinline__ float key_score(uint32_t k) {
+  const uint32_t t = k & ~0xffu;
+  return __uint_as_float((t & 0x80000000u) ? (t ^ 0x80000000u) : ~t);
+}
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a < b ? b : a; }
+// median of three = clamp(v, lo, hi) for lo <= hi (the compiler cannot prove lo <= hi itself)
+__device__ __forceinline__ uint32_t med3(uint32_t v, uint32_t lo, uint32_t hi) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(lo), "v"(hi));
+  return r;
+}
+
+struct KeyList {
+  uint32_t k[KC];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) k[j] = KEY_NONE;
+  }
+  __device__ __forceinline__ void insert(uint32_t v) {
+#pragma unroll
+    for (int j = KC - 1; j > 0; --j) k[j] = med3(v, k[j - 1], k[j]);
+    k[0] = umin(v, k[0]);
+  }
+  // best KC of this ascending list and another ascending list (bitonic merge)
+  __device__ __forceinline__ void merge(const uint32_t (&o)[KC]) {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) k[j] = umin(k[j], o[KC - 1 - j]);
+#pragma unroll
+    for (int s = KC / 2; s > 0; s >>= 1)
+#pragma unroll
+      for (int j = 0; j < KC; ++j)
+        if ((j & s) == 0) {
+          const uint32_t x = k[j], y = k[j + s];
+          k[j] = umin(x, y);
+          k[j + s] = umax(x, y);
+        }
+  }
+};
+
+// MODE 0 is the search; 1 (no k-loop DMA) and 2 (no MFMA) exist only for the
+// feed/compute probe in tools/ and are never instantiated by the library.
+template <int SL, int MODE>
 __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
+  using S = Shape<SL>;
+  constexpr int CT = S::CT, NKS = S::NKS, TQ = S::TQ;
+  constexpr int NACC1 = SL == 2 ? CT : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int64_t t = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
-  const int64_t gt = t / p.ntq, qt = t % p.ntq;     // consecutive tiles share the gallery tile
+  int64_t gt, qt;
+  tile_coords(t, p, gt, qt);
   const int64_t g0 = gt * TG, q0 = qt * TQ;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
 
-  i32x16 acc0[4][2], acc1[4][2];
+  i32x16 acc0[4][CT], acc1[4][NACC1];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int r = 0; r < 16; ++r) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc0[i][j][r] = 0;
-        acc1[i][j][r] = 0;
-      }
+      for (int j = 0; j < CT; ++j) acc0[i][j][r] = 0;
+#pragma unroll
+      for (int j = 0; j < NACC1; ++j) acc1[i][j][r] = 0;
+    }
 
   auto issue = [&](int kt) {
-    char* st = smem + (kt % NST) * STAGE;
-    dma<TG>(p.G1, p.ldk, p.N, g0, st, kt);
-    dma<TG>(p.G2, p.ldk, p.N, g0, st + PG, kt);
-    dma<TQ>(p.Q1, p.ldk, p.B, q0, st + 2 * PG, kt);
-    dma<TQ>(p.Q2, p.ldk, p.B, q0, st + 2 * PG + PQ, kt);
+    char* st = smem + (kt % S::NST) * S::STAGE;
+    dma<TG>(p.G, p.ld, p.N, g0, st, kt);
+    dma<TQ>(p.Q, p.ld, p.B, q0, st + S::PG, kt);
   };
+  // Branch-free k loop (one scheduling region): the step issued at kt is
+  // min(kt + NST - 1, nk - 1); past the end it re-loads the last step into the
+  // stage nobody reads any more, which keeps the vmcnt bookkeeping constant.
+  const int last = p.nk - 1;
 #pragma unroll
-  for (int s = 0; s < NST - 1; ++s)
-    if (s < p.nk) issue(s);
+  for (int s = 0; s < S::NST - 1; ++s) issue(s < last ? s : last);
 
-  for (int kt = 0; kt < p.nk; ++kt) {
-    if (kt + 1 < p.nk) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // (NST-2) panels x IPW in flight
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier();
-    if (kt + NST - 1 < p.nk) issue(kt + NST - 1);
-    const char* st = smem + (kt % NST) * STAGE;
+  // fragments of one k-half, double-buffered by k-half parity
+  i32x4 g1[2][4], q1[2][CT], g2[2][4], q2[2][CT];
+  auto frags = [&](const char* st, int ks) {
+    const int b = ks & 1;
+    const int c = 2 * ks + h;   // 16-B chunk; SL = 2: slice 2 at c + 4
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int chunk = 2 * ks + h;
-      i32x4 g1[4], g2[4], q1[2], q2[2];
+    for (int j = 0; j < CT; ++j) q1[b][j] = *reinterpret_cast<const i32x4*>(st + S::PG + off(wc * (TQ / 2) + j * 32 + r32, c));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wr * 128 + i * 32 + r32;
-        g1[i] = *reinterpret_cast<const i32x4*>(st + off(row, chunk));
-        g2[i] = *reinterpret_cast<const i32x4*>(st + PG + off(row, chunk));
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 128 + i * 32 + r32;
+      g1[b][i] = *reinterpret_cast<const i32x4*>(st + off(row, c));
+      if constexpr (SL == 2) g2[b][i] = *reinterpret_cast<const i32x4*>(st + off(row, c + 4));
+    }
+    if constexpr (SL == 2) {
+#pragma unroll
+      for (int j = 0; j < CT; ++j)
+        q2[b][j] = *reinterpret_cast<const i32x4*>(st + S::PG + off(wc * (TQ / 2) + j * 32 + r32, c + 4));
+    }
+  };
+  // SL = 2: the two products into acc1 sit 8 instructions apart (no RAW stall)
+  auto mfmas = [&](int ks) {
+    const int b = ks & 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) {
+        acc0[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g1[b][i], q1[b][j], acc0[i][j], 0, 0, 0);
+        if constexpr (SL == 2)
+          acc1[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g2[b][i], q1[b][j], acc1[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = wc * 64 + j * 32 + r32;
-        q1[j] = *reinterpret_cast<const i32x4*>(st + 2 * PG + off(row, chunk));
-        q2[j] = *reinterpret_cast<const i32x4*>(st + 2 * PG + PQ + off(row, chunk));
-      }
+    if constexpr (SL == 2) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc0[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g1[i], q1[j], acc0[i][j], 0, 0, 0);
-          acc1[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g2[i], q1[j], acc1[i][j], 0, 0, 0);
-          acc1[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g1[i], q2[j], acc1[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < CT; ++j)
+          acc1[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g1[b][i], q2[b][j], acc1[i][j], 0, 0, 0);
     }
+  };
+
+  constexpr int NFR = S::NFRAG * SL;          // ds_read_b128 per k-half
+  constexpr int MF = S::MF_PER_KS;            // MFMAs per k-half
+  static_assert(MF % NFR == 0, "MFMA : read interleave");
+  for (int kt = 0; kt < p.nk; ++kt) {
+    if constexpr (MODE == 1) wait_vm<0>();
+    else wait_vm<S::YOUNG>();   // step kt landed; younger steps may stay in flight
+    barrier();
+    const char* st = smem + (kt % S::NST) * S::STAGE;
+    frags(st, 0);
+    if constexpr (MODE != 1) {
+      const int nx = kt + S::NST - 1;
+      issue(nx < last ? nx : last);
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (ks + 1 < NKS) frags(st, ks + 1);
+      if constexpr (MODE != 2) mfmas(ks);
+    }
+    // schedule: k-half-0 reads, the DMAs, then each k-half's MFMAs with the next
+    // k-half's reads threaded between them, then the last k-half's MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, NFR, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, S::IPW, 0);
+#pragma unroll
+    for (int ks = 0; ks + 1 < NKS; ++ks)
+#pragma unroll
+      for (int r = 0; r < NFR; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, MF / NFR, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
   }
+  wait_vm<0>();
   barrier();
 
-  // epilogue: coarse scores, per-lane top-16 over the lane's 64 gallery rows, merges.
-  // The tile's gallery aux / scale go through LDS (one coalesced load, no per-element global waits).
-  Cand* buf = reinterpret_cast<Cand*>(smem);                       // [2][TQ][KC]  (32 KiB)
-  float* gtab = reinterpret_cast<float*>(smem + 2 * TQ * KC * sizeof(Cand));   // [TG][2]
+  // epilogue: coarse scores -> keys, per-lane best 16 of the lane's 64 gallery rows,
+  // merge with the partner half-wave, then across the two row-waves through LDS.
+  uint32_t* kbuf = reinterpret_cast<uint32_t*>(smem);                      // [2][TQ][KC]
+  float* gtab = reinterpret_cast<float*>(smem + 2 * TQ * KC * 4);          // [TG][2]
   {
     const int64_t g = g0 + threadIdx.x;
     const bool ok = g < p.N;
@@ -162,63 +305,70 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
     gtab[2 * threadIdx.x + 1] = ok ? p.gscale[g] : 0.f;
   }
   __syncthreads();
+  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
   // one body per query block (ct is a template constant: a runtime index would send acc to scratch)
   auto epi = [&](auto ctc) {
     constexpr int ct = decltype(ctc)::value;
-    int64_t q = q0 + wc * 64 + ct * 32 + r32;
-    const float sq2 = 2.0f * p.qscale[q < p.B ? q : p.B - 1];
-    TopList<KC> L;
-    L.init();
+    if constexpr (ct < CT) {
+      const int ql = wc * (TQ / 2) + ct * 32 + r32;
+      const int64_t q = q0 + ql;
+      const float sq2 = 2.0f * p.qscale[q < p.B ? q : p.B - 1];
+      KeyList L;
+      L.init();
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt)
+      for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int gl = wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float c = (float)acc0[rt][ct][r] + (float)acc1[rt][ct][r] * 0x1p-7f;
-        const float sc = gtab[2 * gl] - sq2 * gtab[2 * gl + 1] * c;
-        // rows past N get NaN: never inserted
-        L.insert(g0 + gl < p.N ? sc : __builtin_nanf(""), (int)(g0 + gl));
+        for (int r = 0; r < 16; ++r) {
+          const int gl = wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          float c = (float)acc0[rt][ct][r];
+          if constexpr (SL == 2) c += (float)acc1[rt][ct][r] * 0x1p-7f;
+          const float sc = gtab[2 * gl] - sq2 * gtab[2 * gl + 1] * c;
+          L.insert(gl < nvalid ? score_key(sc, gl) : KEY_NONE);
+        }
+      uint32_t o[KC];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) o[j] = (uint32_t)__shfl_xor((int)L.k[j], 32);
+      L.merge(o);
+      if (h == 0) {
+        uint32_t* dst = kbuf + ((size_t)wr * TQ + ql) * KC;
+#pragma unroll
+        for (int j = 0; j < KC; j += 4)
+          *reinterpret_cast<uint4*>(dst + j) = make_uint4(L.k[j], L.k[j + 1], L.k[j + 2], L.k[j + 3]);
       }
-    float od[KC];
-    int oi[KC];
-#pragma unroll
-    for (int j = 0; j < KC; ++j) {
-      od[j] = __shfl_xor(L.d[j], 32);
-      oi[j] = __shfl_xor(L.i[j], 32);
-    }
-    L.merge(od, oi);
-    if (h == 0) {
-      Cand* dst = buf + ((size_t)wr * TQ + wc * 64 + ct * 32 + r32) * KC;
-#pragma unroll
-      for (int j = 0; j < KC; ++j) dst[j] = Cand{L.d[j], L.i[j]};
     }
   };
+  static_assert(CT <= 4, "epilogue unroll");
   epi(std::integral_constant<int, 0>{});
   epi(std::integral_constant<int, 1>{});
+  epi(std::integral_constant<int, 2>{});
+  epi(std::integral_constant<int, 3>{});
   __syncthreads();
   if ((int)threadIdx.x < TQ) {
     const int ql = threadIdx.x;
     const int64_t q = q0 + ql;
-    TopList<KC> L;
-    float od[KC];
-    int oi[KC];
-    const Cand* s0 = buf + (size_t)ql * KC;
-    const Cand* s1 = buf + ((size_t)TQ + ql) * KC;
+    KeyList L;
+    uint32_t o[KC];
+    const uint32_t* s0 = kbuf + (size_t)ql * KC;
+    const uint32_t* s1 = kbuf + ((size_t)TQ + ql) * KC;
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      L.d[j] = s0[j].d;
-      L.i[j] = s0[j].i;
-      od[j] = s1[j].d;
-      oi[j] = s1[j].i;
+      L.k[j] = s0[j];
+      o[j] = s1[j];
     }
-    L.merge(od, oi);
+    L.merge(o);
     if (q < p.B) {
       Cand* out = p.cand + ((size_t)gt * p.B + q) * KC;
 #pragma unroll
-      for (int j = 0; j < KC; ++j) out[j] = Cand{L.d[j], L.i[j]};
+      for (int j = 0; j < KC; ++j) {
+        const uint32_t kk = L.k[j];
+        out[j] = kk == KEY_NONE ? Cand{__builtin_inff(), CAND_EMPTY}
+                                : Cand{key_score(kk), (int)(g0 + (kk & 0xffu))};
+      }
     }
   }
 }
+
+// ---- pass 2 ----------------------------------------------------------------------------
 
 struct MergeArgs {
   const Cand* cand;
@@ -290,8 +440,11 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
 }
 
 // ---- quantization of fp32 rows ----------------------------------------------------------
-__global__ void __launch_bounds__(256) quantize_kernel(const float* X, int64_t ldx, int64_t d, int8_t* X1, int8_t* X2,
-                                                       int64_t ldk, float* scale, double* stats) {
+// SL = 1: x~ = s x1, row layout plain [ld];  SL = 2: x~ = s (x1 + 2^-7 x2), per 64
+// features 64 bytes of x1 then 64 bytes of x2 (one 128-B line).
+template <int SL>
+__global__ void __launch_bounds__(256) quantize_kernel(const float* X, int64_t ldx, int64_t d, int8_t* Xs,
+                                                       int64_t ld, float* scale, double* stats) {
   __shared__ double red[4][3];
   const int64_t row = blockIdx.x;
   const float* x = X + row * ldx;
@@ -312,15 +465,15 @@ __global__ void __launch_bounds__(256) quantize_kernel(const float* X, int64_t l
     if ((double)mx / s > 127.0) s *= 2.0;
   }
   double sa = 0, se = 0, st = 0;
-  int8_t* o1 = X1 + row * ldk;
-  int8_t* o2 = X2 + row * ldk;
-  for (int64_t i = threadIdx.x; i < ldk; i += blockDim.x) {
+  int8_t* o = Xs + row * ld;
+  const int64_t dk = ld / SL;
+  for (int64_t i = threadIdx.x; i < dk; i += blockDim.x) {
     int v1 = 0, v2 = 0;
     if (i < d) {
       const double xv = (double)x[i];
       const double r = xv / s;                // exact (power of two)
       const double f1 = rint(r);
-      const double f2 = rint((r - f1) * 128.0);
+      const double f2 = SL == 2 ? rint((r - f1) * 128.0) : 0.0;
       v1 = (int)f1;
       v2 = (int)f2;
       const double xt = s * (f1 + f2 * 0x1p-7);  // exact
@@ -328,8 +481,13 @@ __global__ void __launch_bounds__(256) quantize_kernel(const float* X, int64_t l
       se += (xv - xt) * (xv - xt);
       st += f2 * f2;
     }
-    o1[i] = (int8_t)v1;
-    o2[i] = (int8_t)v2;
+    if constexpr (SL == 1) {
+      o[i] = (int8_t)v1;
+    } else {
+      const int64_t at = (i >> 6) * 128 + (i & 63);
+      o[at] = (int8_t)v1;
+      o[at + 64] = (int8_t)v2;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -380,16 +538,23 @@ __global__ void __launch_bounds__(256) maxima_kernel(const double* stats, const 
 
 using namespace ofr;
 
-extern "C" int ofr_q8_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int8_t* X1,
-                                    int8_t* X2, int64_t ldk, float* scale, double* stats, const float* aux,
+static int64_t q8_min_ld(int slices, int64_t d) { return slices == 1 ? round_up(d, 128) : 2 * round_up(d, 64); }
+
+extern "C" int ofr_q8_quantize_rows(void* stream, int slices, const float* X, int64_t R, int64_t d, int64_t ldx,
+                                    int8_t* Xs, int64_t ld, float* scale, double* stats, const float* aux,
                                     double* maxima) {
-  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d && ldk >= round_up(d, 64) && ldk % 64 == 0,
-                "ofr_q8_quantize_rows: bad sizes (ldk must be a multiple of 64 >= round_up(d,64))");
+  OFR_CHECK_ARG(slices == 1 || slices == 2, "ofr_q8_quantize_rows: slices must be 1 or 2");
+  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d && ld >= q8_min_ld(slices, d) && ld % 128 == 0,
+                "ofr_q8_quantize_rows: bad sizes (ld: multiple of 128, >= round_up(d,128) for 1 slice, "
+                ">= 2 round_up(d,64) for 2)");
   if (R == 0) return OFR_OK;
-  OFR_CHECK_ARG(X && X1 && X2 && scale && stats, "ofr_q8_quantize_rows: null pointer");
+  OFR_CHECK_ARG(X && Xs && scale && stats, "ofr_q8_quantize_rows: null pointer");
   OFR_CHECK_ARG(R < 0x7fffffffLL, "ofr_q8_quantize_rows: too many rows");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(q8s::quantize_kernel, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, X1, X2, ldk, scale, stats);
+  if (slices == 1)
+    hipLaunchKernelGGL(q8s::quantize_kernel<1>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, Xs, ld, scale, stats);
+  else
+    hipLaunchKernelGGL(q8s::quantize_kernel<2>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, Xs, ld, scale, stats);
   OFR_LAUNCH_CHECK("q8 quantize_kernel");
   if (maxima) {
     hipLaunchKernelGGL(q8s::maxima_kernel, dim3(1), dim3(256), 0, st, stats, aux, R, maxima);
@@ -402,41 +567,51 @@ extern "C" size_t ofr_knn_q8_workspace_bytes(int64_t B, int64_t N) {
   return (size_t)cdiv(N > 0 ? N : 1, q8s::TG) * (size_t)B * q8s::KC * sizeof(Cand) + 256;
 }
 
-extern "C" int ofr_knn_q8(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const int8_t* Q1,
-                          const int8_t* Q2, const float* qscale, const double* qstats, const float* G, int64_t N,
-                          int64_t ldg, int64_t d, const int8_t* G1, const int8_t* G2, int64_t ldk,
-                          const float* gscale, const float* aux, const double* gmax, int k, int64_t index_base,
-                          double* out_d, int64_t* out_i, int* cert, void* workspace, size_t workspace_bytes) {
+template <int SL>
+static int q8_tiles(hipStream_t st, q8s::TileArgs a) {
+  using S = q8s::Shape<SL>;
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel<SL, 0>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
+    if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(q8 tile)");
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((q8s::tile_kernel<SL, 0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(256), S::LDS, st, a);
+  OFR_LAUNCH_CHECK("q8 tile_kernel");
+  return OFR_OK;
+}
+
+extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, int64_t ldq,
+                          const int8_t* Qs, const float* qscale, const double* qstats, const float* G, int64_t N,
+                          int64_t ldg, int64_t d, const int8_t* Gs, int64_t ld, const float* gscale,
+                          const float* aux, const double* gmax, int k, int64_t index_base, double* out_d,
+                          int64_t* out_i, int* cert, void* workspace, size_t workspace_bytes) {
   OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_q8: phases must be 1 (tiles), 2 (merge) or 3");
+  OFR_CHECK_ARG(slices == 1 || slices == 2, "ofr_knn_q8: slices must be 1 or 2");
   OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_q8: bad sizes (empty galleries use ofr_knn_f32)");
   if (k < 1 || k > q8s::KC) return fail(OFR_E_UNSUPPORTED, "ofr_knn_q8: k must be in [1, 16]");
   if (B == 0) return OFR_OK;
-  OFR_CHECK_ARG(ldk % 64 == 0 && ldk >= round_up(d, 64), "ofr_knn_q8: bad ldk");
+  OFR_CHECK_ARG(ld % 128 == 0 && ld >= q8_min_ld(slices, d), "ofr_knn_q8: bad slice leading dimension");
   OFR_CHECK_ARG(ldq >= d && ldg >= d, "ofr_knn_q8: bad leading dimensions");
-  OFR_CHECK_ARG(Q && Q1 && Q2 && qscale && qstats && G && G1 && G2 && gscale && aux && gmax && workspace,
+  OFR_CHECK_ARG(Q && Qs && qscale && qstats && G && Gs && gscale && aux && gmax && workspace,
                 "ofr_knn_q8: null pointer");
-  OFR_CHECK_ARG(((uintptr_t)Q1 | (uintptr_t)Q2 | (uintptr_t)G1 | (uintptr_t)G2) % 16 == 0, "ofr_knn_q8: slices must be 16-byte aligned");
+  OFR_CHECK_ARG(((uintptr_t)Qs | (uintptr_t)Gs) % 16 == 0, "ofr_knn_q8: slices must be 16-byte aligned");
   OFR_CHECK_ARG(N < 0x7fffffffLL - q8s::TG, "ofr_knn_q8: N too large for one shard");
   OFR_CHECK_ARG(workspace_bytes >= ofr_knn_q8_workspace_bytes(B, N), "ofr_knn_q8: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   q8s::TileArgs a;
-  a.G1 = G1; a.G2 = G2; a.N = N; a.ldk = ldk; a.gscale = gscale; a.aux = aux;
-  a.Q1 = Q1; a.Q2 = Q2; a.B = B; a.qscale = qscale;
-  a.nk = (int)cdiv(d, q8s::BK);
+  a.G = Gs; a.N = N; a.ld = ld; a.gscale = gscale; a.aux = aux;
+  a.Q = Qs; a.B = B; a.qscale = qscale;
+  a.nk = (int)cdiv(d, slices == 1 ? q8s::Shape<1>::BK : q8s::Shape<2>::BK);
   a.cand = reinterpret_cast<Cand*>(workspace);
-  a.ntq = cdiv(B, q8s::TQ);
+  a.ntq = cdiv(B, slices == 1 ? q8s::Shape<1>::TQ : q8s::Shape<2>::TQ);
   a.ntg = cdiv(N, q8s::TG);
+  a.gg = a.ntg < q8s::GROUP_G ? a.ntg : q8s::GROUP_G;
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_q8: grid too large");
   if (phases & 1) {
-    static bool attr_done = false;
-    if (!attr_done) {
-      hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         q8s::LDS);
-      if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(q8 tile)");
-      attr_done = true;
-    }
-    hipLaunchKernelGGL(q8s::tile_kernel, dim3((unsigned)(a.ntq * a.ntg)), dim3(256), q8s::LDS, st, a);
-    OFR_LAUNCH_CHECK("q8 tile_kernel");
+    const int rc = slices == 1 ? q8_tiles<1>(st, a) : q8_tiles<2>(st, a);
+    if (rc) return rc;
   }
   if (phases & 2) {
     OFR_CHECK_ARG(out_d && out_i && cert, "ofr_knn_q8: null output");

@@ -81,12 +81,12 @@ def test_knn_vs_oracle(metric, B, N, d, k):
 
 @pytest.mark.parametrize("B,N,d,k", [(33, 300, 3, 1), (300, 5000, 99, 5), (257, 3000, 300, 16), (600, 20000, 64, 3),
                                      (1000, 70000, 130, 1)])
-@pytest.mark.parametrize("mode", ["q8", "fp32"])
+@pytest.mark.parametrize("mode", ["q8", "q8x2", "fp32"])
 def test_knn_euclidean_paths_vs_oracle(monkeypatch, mode, B, N, d, k):
-    """Batches > 32 take the certified int8 pass (ofr_knn_q8) unless OFR_SEARCH=fp32."""
+    """Batches > 32 take the certified int8 tiers (ofr_knn_q8, 1 then 2 slices) unless OFR_SEARCH=fp32."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
-    monkeypatch.setenv("OFR_SEARCH", "auto" if mode == "q8" else "fp32")
+    monkeypatch.setenv("OFR_SEARCH", {"q8": "auto"}.get(mode, mode))
     r = _rng(B * 11 + N + d)
     protos = r.normal(0, 30, (max(N // 10, 1), d))
     G = (protos[np.arange(N) % len(protos)] + r.normal(0, 5, (N, d))).astype(np.float32).astype(np.float64)
@@ -94,13 +94,13 @@ def test_knn_euclidean_paths_vs_oracle(monkeypatch, mode, B, N, d, k):
     Q[0] = G[N // 2]
     G[N - 1] = G[3]
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
-    q8 = mode == "q8" and k <= 8
+    q8 = mode != "fp32" and k <= 8
     assert g.use_q8(B, k) == q8
     dd, ii = g.search(g.query_rows(Q), k)
     ties = _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
     assert ties <= max(1, B // 100)
     if q8:
-        assert g.last_fallbacks <= B // 10     # well-separated data: nearly every query certifies
+        assert g.last_fallbacks[0] <= B // 10     # well-separated data: nearly every query certifies
 
 
 def test_knn_q8_certificate_forces_fallback(monkeypatch):
@@ -117,7 +117,7 @@ def test_knn_q8_certificate_forces_fallback(monkeypatch):
     Q = (c + r.normal(0, 1e-6, (100, 64))).astype(np.float32).astype(np.float64)   # every row ~equidistant
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     dd, ii = g.search(g.query_rows(Q), 3)
-    assert g.last_fallbacks > 0
+    assert g.last_fallbacks[0] > 0 and g.last_fallbacks[1] > 0
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
 
 
