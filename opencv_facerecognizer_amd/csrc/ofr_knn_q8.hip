@@ -43,19 +43,26 @@ constexpr int ROWB = 128;                          // LDS/global bytes per row a
 constexpr int GROUP_G = 4;                         // gallery tiles per tile group (tile_coords)
 
 // Two tile shapes share the engine (SL = int8 slices per row):
-//   SL = 1: 256 x 256 tile, k step 128 (x1 only), 2 LDS stages of 64 KiB, acc 4x4 blocks/wave
-//   SL = 2: 256 x 128 tile, k step 64 (x1 | x2 per 128-B line), 3 stages of 48 KiB, acc 2 x 4x2
+//   SL = 1: 256 x 256 tile, k step 128 (x1 only), 2 LDS stages of 64 KiB, 8 waves (2 per
+//           SIMD: one wave's LDS-DMA issue and barrier wait hide behind the other's MFMAs),
+//           each 128 x 64 (acc 4x2 blocks, 128 registers)
+//   SL = 2: 256 x 128 tile, k step 64 (x1 | x2 per 128-B line), 3 stages of 48 KiB, 4 waves,
+//           each 128 x 64 with two accumulator sets (256 registers)
 template <int SL>
 struct Shape {
   static constexpr int TQ = SL == 1 ? 256 : 128;
+  static constexpr int NW = SL == 1 ? 8 : 4;       // waves per workgroup
+  static constexpr int NT = NW * 64;
+  static constexpr int WQ = NW / 2;                // wave grid: 2 (gallery) x WQ (queries)
+  static constexpr int QW = TQ / WQ;               // queries per wave (64)
   static constexpr int BK = ROWB / SL;             // features per k step
   static constexpr int NST = SL == 1 ? 2 : 3;
-  static constexpr int CT = TQ / 64;               // 32-query blocks per wave (2 x 2 wave grid)
+  static constexpr int CT = QW / 32;               // 32-query blocks per wave
   static constexpr int NKS = BK / 32;              // MFMA k-halves per step (each MFMA: k = 32)
   static constexpr int PG = TG * ROWB, PQ = TQ * ROWB;
   static constexpr int STAGE = PG + PQ;
   static constexpr int LDS = NST * STAGE;          // 128 / 144 KiB
-  static constexpr int IPW = (TG + TQ) / 8 / 4;    // DMA wave-instructions per wave per stage (16 / 12)
+  static constexpr int IPW = (TG + TQ) / 8 / NW;   // DMA wave-instructions per wave per stage (8 / 12)
   static constexpr int YOUNG = (NST - 2) * IPW;    // DMAs allowed in flight at the stage wait
   static constexpr int NFRAG = 4 + CT;             // fragment reads per k-half per slice
   static constexpr int MF_PER_KS = 4 * CT * (SL == 1 ? 1 : 3);
@@ -68,9 +75,10 @@ __device__ __forceinline__ int off(int row, int chunk) { return row * ROWB + ((c
 
 // rows [r0, r0 + ROWS) of a slice matrix, k step kt -> LDS panel.
 // One wave-instruction moves 8 full rows (8 x 128 B = 1 KiB, one 128-B line per row).
-template <int ROWS>
+template <int ROWS, int NW>
 __device__ __forceinline__ void dma(const int8_t* base, int64_t ld, int64_t rows, int64_t r0, char* panel, int kt) {
-  constexpr int PER = ROWS / 8 / 4;
+  constexpr int PER = ROWS / 8 / NW;
+  static_assert(PER * 8 * NW == ROWS, "DMA split");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int t = 0; t < PER; ++t) {
@@ -186,9 +194,9 @@ struct KeyList {
 // MODE 0 is the search; 1 (no k-loop DMA) and 2 (no MFMA) exist only for the
 // feed/compute probe in tools/ and are never instantiated by the library.
 template <int SL, int MODE>
-__global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
+__global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
   using S = Shape<SL>;
-  constexpr int CT = S::CT, NKS = S::NKS, TQ = S::TQ;
+  constexpr int CT = S::CT, NKS = S::NKS, TQ = S::TQ, QW = S::QW;
   constexpr int NACC1 = SL == 2 ? CT : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int64_t t = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
@@ -196,7 +204,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
   tile_coords(t, p, gt, qt);
   const int64_t g0 = gt * TG, q0 = qt * TQ;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
+  const int wr = wave / S::WQ, wc = wave % S::WQ, h = lane >> 5, r32 = lane & 31;
 
   i32x16 acc0[4][CT], acc1[4][NACC1];
 #pragma unroll
@@ -211,8 +219,8 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
 
   auto issue = [&](int kt) {
     char* st = smem + (kt % S::NST) * S::STAGE;
-    dma<TG>(p.G, p.ld, p.N, g0, st, kt);
-    dma<TQ>(p.Q, p.ld, p.B, q0, st + S::PG, kt);
+    dma<TG, S::NW>(p.G, p.ld, p.N, g0, st, kt);
+    dma<TQ, S::NW>(p.Q, p.ld, p.B, q0, st + S::PG, kt);
   };
   // Branch-free k loop (one scheduling region): the step issued at kt is
   // min(kt + NST - 1, nk - 1); past the end it re-loads the last step into the
@@ -227,7 +235,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
     const int b = ks & 1;
     const int c = 2 * ks + h;   // 16-B chunk; SL = 2: slice 2 at c + 4
 #pragma unroll
-    for (int j = 0; j < CT; ++j) q1[b][j] = *reinterpret_cast<const i32x4*>(st + S::PG + off(wc * (TQ / 2) + j * 32 + r32, c));
+    for (int j = 0; j < CT; ++j) q1[b][j] = *reinterpret_cast<const i32x4*>(st + S::PG + off(wc * QW + j * 32 + r32, c));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = wr * 128 + i * 32 + r32;
@@ -237,7 +245,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
     if constexpr (SL == 2) {
 #pragma unroll
       for (int j = 0; j < CT; ++j)
-        q2[b][j] = *reinterpret_cast<const i32x4*>(st + S::PG + off(wc * (TQ / 2) + j * 32 + r32, c + 4));
+        q2[b][j] = *reinterpret_cast<const i32x4*>(st + S::PG + off(wc * QW + j * 32 + r32, c + 4));
     }
   };
   // SL = 2: the two products into acc1 sit 8 instructions apart (no RAW stall)
@@ -262,7 +270,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
 
   constexpr int NFR = S::NFRAG * SL;          // ds_read_b128 per k-half
   constexpr int MF = S::MF_PER_KS;            // MFMAs per k-half
-  static_assert(MF % NFR == 0, "MFMA : read interleave");
+  static_assert(MF >= NFR, "MFMA : read interleave");
   for (int kt = 0; kt < p.nk; ++kt) {
     if constexpr (MODE == 1) wait_vm<0>();
     else wait_vm<S::YOUNG>();   // step kt landed; younger steps may stay in flight
@@ -279,16 +287,19 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
       if constexpr (MODE != 2) mfmas(ks);
     }
     // schedule: k-half-0 reads, the DMAs, then each k-half's MFMAs with the next
-    // k-half's reads threaded between them, then the last k-half's MFMAs
+    // k-half's reads front-loaded between them (1 : 1, so they land before they are
+    // needed), then the last k-half's MFMAs
     __builtin_amdgcn_sched_group_barrier(0x100, NFR, 0);
     __builtin_amdgcn_sched_group_barrier(0x020, S::IPW, 0);
 #pragma unroll
-    for (int ks = 0; ks + 1 < NKS; ++ks)
+    for (int ks = 0; ks + 1 < NKS; ++ks) {
 #pragma unroll
       for (int r = 0; r < NFR; ++r) {
-        __builtin_amdgcn_sched_group_barrier(0x008, MF / NFR, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
+      __builtin_amdgcn_sched_group_barrier(0x008, MF - NFR, 0);
+    }
     __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
   }
   wait_vm<0>();
@@ -298,7 +309,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
   // merge with the partner half-wave, then across the two row-waves through LDS.
   uint32_t* kbuf = reinterpret_cast<uint32_t*>(smem);                      // [2][TQ][KC]
   float* gtab = reinterpret_cast<float*>(smem + 2 * TQ * KC * 4);          // [TG][2]
-  {
+  if (threadIdx.x < TG) {
     const int64_t g = g0 + threadIdx.x;
     const bool ok = g < p.N;
     gtab[2 * threadIdx.x + 0] = ok ? p.aux[g] : 0.f;
@@ -310,7 +321,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel(TileArgs p) {
   auto epi = [&](auto ctc) {
     constexpr int ct = decltype(ctc)::value;
     if constexpr (ct < CT) {
-      const int ql = wc * (TQ / 2) + ct * 32 + r32;
+      const int ql = wc * QW + ct * 32 + r32;
       const int64_t q = q0 + ql;
       const float sq2 = 2.0f * p.qscale[q < p.B ? q : p.B - 1];
       KeyList L;
@@ -577,7 +588,7 @@ static int q8_tiles(hipStream_t st, q8s::TileArgs a) {
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(q8 tile)");
     attr_done = true;
   }
-  hipLaunchKernelGGL((q8s::tile_kernel<SL, 0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(256), S::LDS, st, a);
+  hipLaunchKernelGGL((q8s::tile_kernel<SL, 0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(S::NT), S::LDS, st, a);
   OFR_LAUNCH_CHECK("q8 tile_kernel");
   return OFR_OK;
 }

@@ -21,6 +21,34 @@ __global__ void fill_f(float* p, size_t n, float v) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// ceiling: back-to-back v_mfma_i32_32x32x32_i8 on register operands, 16 accumulators per wave,
+// one wave per SIMD on every CU (what the matrix cores sustain at the clock they hold)
+__global__ void __launch_bounds__(256, 1) mfma_ceiling(const int* seed, int iters, int* out) {
+  typedef int v4 __attribute__((ext_vector_type(4)));
+  typedef int v16 __attribute__((ext_vector_type(16)));
+  v4 a[4], b[4];
+  for (int i = 0; i < 4; ++i)
+    for (int e = 0; e < 4; ++e) {
+      a[i][e] = seed[(threadIdx.x + 7 * i + e) & 255] * 0x01010101;
+      b[i][e] = seed[(threadIdx.x + 13 * i + 3 * e) & 255] * 0x01030507;
+    }
+  v16 acc[4][4];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+  int s = 0;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      for (int r = 0; r < 16; ++r) s += acc[i][j][r];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
 template <int SL, int MODE>
@@ -33,10 +61,10 @@ static int run(q8s::TileArgs a, int64_t d, int reps, const char* tag) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const unsigned grid = (unsigned)(a.ntq * a.ntg);
-  hipLaunchKernelGGL((q8s::tile_kernel<SL, MODE>), dim3(grid), dim3(256), S::LDS, 0, a);
+  hipLaunchKernelGGL((q8s::tile_kernel<SL, MODE>), dim3(grid), dim3(S::NT), S::LDS, 0, a);
   CK(hipGetLastError());
   CK(hipEventRecord(e0));
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((q8s::tile_kernel<SL, MODE>), dim3(grid), dim3(256), S::LDS, 0, a);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((q8s::tile_kernel<SL, MODE>), dim3(grid), dim3(S::NT), S::LDS, 0, a);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -70,6 +98,22 @@ int main(int argc, char** argv) {
   a.G = G; a.N = N; a.ld = ld; a.gscale = gs; a.aux = aux;
   a.Q = Q; a.B = B; a.qscale = qs; a.cand = cand; a.ntg = ntg;
   printf("N=%ld B=%ld d=%ld\n", (long)N, (long)B, (long)d);
+  {
+    int *seed, *outv;
+    CK(hipMalloc(&seed, 256 * 4)); CK(hipMalloc(&outv, 1024 * 256 * 4));
+    fill_f<<<1, 256>>>((float*)seed, 256, 1.2345f);
+    const int iters = 20000, grid = 1024;
+    hipLaunchKernelGGL(mfma_ceiling, dim3(grid), dim3(256), 0, 0, seed, 100, outv);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL(mfma_ceiling, dim3(grid), dim3(256), 0, 0, seed, iters, outv);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    const double ops = 2.0 * 32 * 32 * 32 * 16.0 * iters * 4.0 * grid;
+    printf("mfma ceiling (registers only): %.1f TOPS (%.1f%% of 5000)\n", ops / ms / 1e9, ops / ms / 1e9 / 50.0);
+  }
   const int ggs[] = {1, 2, 4, 8};
   for (int g : ggs) {
     a.gg = g < ntg ? g : ntg;
