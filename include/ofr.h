@@ -70,8 +70,8 @@ int ofr_device_check(int device);      /* OFR_OK iff `device` is gfx950 */
  * int32 without rounding and combined in fp64 without rounding; the shift is
  * subtracted in fp64 and the result rounded once to fp32 or fp64.
  * Wt: W transposed, [d][ldw] of OFR_DT_F32 or OFR_DT_F64.
- * Aq: int8 [ceil(d/64)*256][ldk], ldk % 64 == 0, ldk >= round_up(D,64)
- *     (ofr_qproj_bytes(D,d) bytes with ldk = round_up(D,64)); scale, K: fp64 [d].
+ * Aq: int8 [ceil(d/64)*256][ldk], ldk % 128 == 0, ldk >= round_up(D,128)
+ *     (ofr_qproj_bytes(D,d) bytes with ldk = round_up(D,128)); scale, K: fp64 [d].
  * X : uint8 [B][ldx], 16-byte aligned rows, ldx >= D.
  * Y : [B][ldy] of y_dtype (OFR_DT_F32 / OFR_DT_F64); columns j < d written.   */
 size_t ofr_qproj_bytes(int64_t D, int64_t d);

@@ -111,7 +111,7 @@ class Projection:
             self.D, self.d = W.shape
             Wt = torch.from_numpy(np.ascontiguousarray(W.T)).to(device)
         dt = {torch.float32: _lib.DT_F32, torch.float64: _lib.DT_F64}[Wt.dtype]
-        self.ldk = round_up(self.D, 64)
+        self.ldk = round_up(self.D, 128)
         nbytes = _lib.load().ofr_qproj_bytes(self.D, self.d)
         self.Aq = torch.empty(nbytes, dtype=torch.int8, device=device)
         self.scale = torch.empty(self.d, dtype=torch.float64, device=device)

@@ -21,33 +21,27 @@
 // The int8 path runs at 2x the bf16 MFMA rate, i.e. 4 slices cost half of one
 // bf16 pass and 1/8 of the fp32 MFMA projection.
 //
-// Layouts: Aq [ceil(d/64)*256][ldk] int8, ldk = round_up(D, 64); the rows of
-// feature block jb = j/32 are jb*128 + s*32 + j%32 (the four slices of 32
-// features are the four 32-row MFMA blocks of one wave).  A 256x256 tile =
-// 64 features x 4 slices by 256 images; 4 waves (2x2), each 128x128 =
-// 4 slices x 4 image blocks, int32 accumulators.  LDS: [256][64 B] panels,
-// 16-B chunks XOR-swizzled by ((row>>2)&3), A by LDS-DMA, images through
-// registers (x ^ 0x80 = x - 128 as int8), two stages.
-#include "ofr_common.h"
+// Layouts: Aq [ceil(d/64)*256][ldk] int8, ldk % 128 == 0, ldk >= round_up(D, 128);
+// the rows of feature block jb = j/32 are jb*128 + s*32 + j%32 (the four slices
+// of 32 features are the four 32-row MFMA blocks of one wave).  The product
+// runs on the int8 tile engine (ofr_i8_tile.h, one-slice shape): a 256x256
+// tile = 64 features x 4 slices by 256 images, 8 waves (2 per SIMD) of 128x64,
+// k step 128, both operands by LDS-DMA (the images as raw uint8 rows; the
+// fragments become x - 128 by an XOR with 0x80 after the LDS read).
+#include "ofr_i8_tile.h"
 
 namespace ofr {
 namespace q8 {
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int TM = 256, TN = 256, BK = 64;
-constexpr int PANEL = 256 * BK;          // 16 KiB
-constexpr int STAGE = 2 * PANEL;         // A + B
-constexpr int LDS_BYTES = 2 * STAGE;     // 64 KiB
-
-__device__ __forceinline__ int off(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 2) & 3)) << 4); }
+using i8t::i32x16;
+using S = i8t::Shape<1>;
+constexpr int GROUP_F = 4;   // feature tiles per tile group (i8t::tile_coords)
 
 struct Args {
   const uint8_t* X;
   int64_t B, D, ldx;
   const int8_t* Aq;
-  int64_t ldk;
+  int64_t ldk, arows;
   const double* scale;
   const double* K;
   const double* shift;
@@ -56,108 +50,32 @@ struct Args {
   int64_t ldy;
   int y_f64;
   int nk;
-  int64_t ntf, ntb;
+  int64_t ntf, ntb, gg;
 };
 
-__device__ __forceinline__ void issue_a(const Args& p, char* panel, int64_t arow0, int kt) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int ins = wave * 4 + t;        // 16 wave-instructions x 16 rows
-    const int row = ins * 16 + (lane >> 2);
-    const int chunk = (lane & 3) ^ ((row >> 2) & 3);
-    const int8_t* src = p.Aq + (arow0 + row) * p.ldk + (int64_t)kt * BK + chunk * 16;
-    __builtin_amdgcn_global_load_lds((const OFR_GLOBAL void*)src, (OFR_LDS void*)(panel + ins * 1024), 16, 0, 0);
-  }
-}
-
-__device__ __forceinline__ void load_b(const Args& p, int64_t b0, int kt, uint4 (&v)[4]) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int q = threadIdx.x + 256 * s;
-    const int row = q >> 2, c = q & 3;
-    int64_t b = b0 + row;
-    b = b < p.B ? b : p.B - 1;
-    const int64_t k = (int64_t)kt * BK + c * 16;
-    if (k < p.D) {
-      uint4 x = *reinterpret_cast<const uint4*>(p.X + b * p.ldx + k);
-      x.x ^= 0x80808080u; x.y ^= 0x80808080u; x.z ^= 0x80808080u; x.w ^= 0x80808080u;
-      v[s] = x;    // bytes >= D meet the zero pad of Aq
-    } else {
-      v[s] = make_uint4(0, 0, 0, 0);
-    }
-  }
-}
-
-__device__ __forceinline__ void store_b(char* panel, const uint4 (&v)[4]) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int q = threadIdx.x + 256 * s;
-    *reinterpret_cast<uint4*>(panel + off(q >> 2, q & 3)) = v[s];
-  }
-}
-
-__global__ void __launch_bounds__(256, 1) project_q8_kernel(Args p) {
+__global__ void __launch_bounds__(S::NT, 1) project_q8_kernel(Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // consecutive blocks share the weight tile: the 256-row W-slice panel is fetched from HBM once
-  // (the image panels of a 4096-image batch, 41 MB, stay in the Infinity Cache)
-  const int64_t t = blockIdx.x;
-  const int64_t ft = t / p.ntb, bt = t % p.ntb;
-  const int64_t f0 = ft * 64, b0 = bt * TN, arow0 = ft * TM;
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t ft, bt;
+  i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
+  const int64_t a0 = ft * i8t::TA, b0 = bt * S::TQ;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
+  const int wr = wave / S::WQ, wc = wave % S::WQ, h = lane >> 5, r32 = lane & 31;
 
-  i32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
-
-  uint4 vb[4];
-  issue_a(p, smem, arow0, 0);
-  load_b(p, b0, 0, vb);
-  store_b(smem + PANEL, vb);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < p.nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE;
-    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
-    const bool more = kt + 1 < p.nk;
-    if (more) {
-      issue_a(p, nxt, arow0, kt + 1);
-      load_b(p, b0, kt + 1, vb);
-    }
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int chunk = 2 * ks + h;
-      i32x4 a[4], b[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        a[s] = *reinterpret_cast<const i32x4*>(cur + off(wr * 128 + s * 32 + r32, chunk));
-        b[s] = *reinterpret_cast<const i32x4*>(cur + PANEL + off(wc * 128 + s * 32 + r32, chunk));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) store_b(nxt + PANEL, vb);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  i32x16 acc[4][S::CT], unused[4][1];
+  i8t::mainloop<1, 0, true>(smem, p.Aq, p.ldk, p.arows, a0, reinterpret_cast<const int8_t*>(p.X), p.ldx, p.B, b0,
+                            p.ldx, p.nk, acc, unused);
 
   // epilogue: rows (reg&3) + 8*(reg>>2) + 4*h of each 32-block are the same 32 features in all four slices
+  const int64_t fb = ft * 2 + wr;   // 32-feature block of this wave
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int64_t b = b0 + wc * 128 + ct * 32 + r32;
+  for (int ct = 0; ct < S::CT; ++ct) {
+    const int64_t b = b0 + wc * S::QW + ct * 32 + r32;
     if (b >= p.B) continue;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       double v[4];
-      const int64_t j0 = f0 + wr * 32 + 8 * g + 4 * h;
+      const int64_t j0 = fb * 32 + 8 * g + 4 * h;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e;
@@ -269,14 +187,14 @@ __global__ void center_round_kernel(const double* F, int64_t ldf, int64_t d, con
 using namespace ofr;
 
 extern "C" size_t ofr_qproj_bytes(int64_t D, int64_t d) {
-  return (size_t)(cdiv(d, 64) * 256) * (size_t)round_up(D, 64);
+  return (size_t)(cdiv(d, 64) * 256) * (size_t)round_up(D, 128);
 }
 
 extern "C" int ofr_qproj_prepare(void* stream, int dtype, const void* Wt, int64_t d, int64_t D, int64_t ldw, int8_t* Aq,
                                  int64_t ldk, double* scale, double* K) {
   OFR_CHECK_ARG(dtype == OFR_DT_F32 || dtype == OFR_DT_F64, "ofr_qproj_prepare: dtype must be F32 or F64");
-  OFR_CHECK_ARG(d >= 1 && D >= 1 && ldw >= D && ldk >= round_up(D, 64) && ldk % 64 == 0,
-                "ofr_qproj_prepare: bad sizes (ldk must be a multiple of 64 >= round_up(D,64))");
+  OFR_CHECK_ARG(d >= 1 && D >= 1 && ldw >= D && ldk >= round_up(D, 128) && ldk % 128 == 0,
+                "ofr_qproj_prepare: bad sizes (ldk must be a multiple of 128 >= round_up(D,128))");
   OFR_CHECK_ARG(Wt && Aq && scale && K && d < 0x7fffffffLL, "ofr_qproj_prepare: null pointer");
   hipStream_t st = (hipStream_t)stream;
   // the pad rows/columns of Aq must be zero: clear the whole operand first
@@ -300,23 +218,26 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   if (B == 0) return OFR_OK;
   OFR_CHECK_ARG(X && Aq && scale && K && Y, "ofr_project_u8_exact: null pointer");
   OFR_CHECK_ARG(ldx >= D && ldx % 16 == 0 && ((uintptr_t)X % 16) == 0, "ofr_project_u8_exact: X rows must be 16-byte aligned, ldx >= D");
-  OFR_CHECK_ARG(ldk >= round_up(D, 64) && ldk % 64 == 0 && ((uintptr_t)Aq % 16) == 0, "ofr_project_u8_exact: bad Aq layout");
+  OFR_CHECK_ARG(ldk >= round_up(D, 128) && ldk % 128 == 0 && ((uintptr_t)Aq % 16) == 0,
+                "ofr_project_u8_exact: bad Aq layout");
   OFR_CHECK_ARG(ldy >= d, "ofr_project_u8_exact: ldy < d");
   static bool attr_done = false;
   if (!attr_done) {
     hipError_t e = hipFuncSetAttribute((const void*)q8::project_q8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       q8::LDS_BYTES);
+                                       q8::S::LDS);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8)");
     attr_done = true;
   }
   q8::Args p;
   p.X = X; p.B = B; p.D = D; p.ldx = ldx; p.Aq = Aq; p.ldk = ldk; p.scale = scale; p.K = K; p.shift = shift;
   p.d = d; p.Y = Y; p.ldy = ldy; p.y_f64 = y_dtype == OFR_DT_F64;
-  p.nk = (int)cdiv(D, q8::BK);
+  p.nk = (int)cdiv(D, q8::S::BK);
   p.ntf = cdiv(d, 64);
-  p.ntb = cdiv(B, q8::TN);
+  p.arows = p.ntf * 256;
+  p.ntb = cdiv(B, q8::S::TQ);
+  p.gg = p.ntf < q8::GROUP_F ? p.ntf : q8::GROUP_F;
   OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-  hipLaunchKernelGGL(q8::project_q8_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(256), q8::LDS_BYTES,
+  hipLaunchKernelGGL(q8::project_q8_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(q8::S::NT), q8::S::LDS,
                      (hipStream_t)stream, p);
   OFR_LAUNCH_CHECK("project_q8_kernel");
   return OFR_OK;

@@ -1,0 +1,67 @@
+"""Summarise the rocprofv3 passes of tools/prof_q8.sh (gpurun_out/prof) into profiles/.
+
+    python tools/pmc_summary.py <name> [kernel-substring]
+
+writes profiles/<name>_kernel_stats.csv (the --stats table) and profiles/<name>_pmc_summary.json
+(per-launch counters of the search tile kernel; traffic = FETCH_SIZE x 2 + WRITE_SIZE, the gfx950
+correction of MI355X_MICROARCH.md §HBM).  bench.py reads traffic_bytes_per_launch back when the
+config matches its own run.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = os.path.join(ROOT, "gpurun_out", "prof")
+
+
+def counters(kname):
+    agg = collections.defaultdict(list)
+    for p in ("p1", "p2", "p3", "p4", "p5"):
+        f = os.path.join(P, p, f"{p}_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            if kname in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}, max((len(v) for v in agg.values()), default=0)
+
+
+def main():
+    name = sys.argv[1]
+    kname = sys.argv[2] if len(sys.argv) > 2 else "tile_kernel<1, 0>"
+    stats = os.path.join(P, "kt", "kt_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(ROOT, "profiles", f"{name}_kernel_stats.csv"))
+    avg_ns = None
+    for r in csv.DictReader(open(stats)):
+        if kname in r["Name"]:
+            avg_ns = float(r["AverageNs"])
+    c, n = counters(kname)
+    log = open(os.path.join(P, "kt.log")).read().strip().splitlines()
+    bench = json.loads([ln for ln in log if ln.startswith("{")][-1])
+    cfg = bench["config"]
+    out = {
+        "config": {"gallery": cfg["gallery"], "batch": cfg["global_batch"], "d": cfg["d"], "D": cfg["D"],
+                   "k": cfg["k"], "search": "q8" if "i8" in bench["dtype"] else "fp32"},
+        "kernel": kname, "launches": n, "rocprof_avg_ns": avg_ns,
+        "counters_per_launch": c,
+        "correction": "gfx950: FETCH_SIZE reports half of the bytes of wide coalesced streaming reads "
+                      "(MI355X_MICROARCH.md §HBM) -> x2; WRITE_SIZE exact for 16-B stores",
+    }
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["traffic_bytes_per_launch"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+    if "TCC_HIT_sum" in c:
+        out["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if "GRBM_GUI_ACTIVE" in c and avg_ns:
+        out["effective_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / avg_ns
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "SQ_WAVE_CYCLES" in c:
+        out["mfma_busy_per_wave_cycle"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * c["SQ_WAVE_CYCLES"])
+    json.dump(out, open(os.path.join(ROOT, "profiles", f"{name}_pmc_summary.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
