@@ -39,6 +39,7 @@ from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 
 PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
 PEAK_I8_MFMA = 5.0e15       # int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, matrix cores)
+PEAK_F6_MFMA = 10.0e15      # fp6 (block-scaled f8f6f4 MFMA): ~10 PF dense, the FP4 rate (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12           # HBM3E 8 TB/s (spec)
 
 
@@ -56,8 +57,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--small-batches", default="32,1", help="extra HBM-regime measurements (B <= 32); '' to skip")
-    ap.add_argument("--search", choices=["q8", "fp32"], default="q8",
-                    help="q8: certified int8 coarse pass (+fp32 fallback for uncertified queries); fp32: fp32-MFMA pass")
+    ap.add_argument("--search", choices=["f6", "q8", "fp32"], default="f6",
+                    help="f6: certified fp6 coarse pass (uncertified queries go down the int8 tiers, then fp32); "
+                         "q8: start at the certified int8 tier; fp32: fp32-MFMA pass")
     return ap.parse_args()
 
 
@@ -180,10 +182,11 @@ def main():
     log(rank, f"setup {time.perf_counter() - t0:.1f}s: gallery rows {nl}/{N} per rank, d={d}, D={D}, B={B}")
 
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    use_q8 = args.search == "q8"
+    use_q8 = args.search in ("f6", "q8")
+    tier0 = "f6" if args.search == "f6" else 1
     if use_q8:
-        gallery._q8_gallery(1)                                    # gallery int8 slices (once, untimed)
-        gallery._q8_gallery(2)
+        for t in FloatGallery.TIER_CHAIN[FloatGallery.TIER_CHAIN.index(tier0):-1]:
+            gallery._tier_gallery(t)                              # quantized gallery tiers (once, untimed)
     qq = None
     fallbacks = []
 
@@ -193,7 +196,7 @@ def main():
             events[0].record()
         P.project(Xq, shift64=gallery.shift64, out=Qd)            # fp32(W^T x - c), exact int8 MFMA
         if use_q8:
-            qq = gallery.quantize_queries(Qd, qq, slices=1)
+            qq = gallery.quantize_queries(Qd, qq, tier=tier0)
         if events:
             events[1].record()
         if use_q8:
@@ -272,7 +275,11 @@ def main():
 
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
-    if use_q8:
+    if args.search == "f6":
+        peak, kname = PEAK_F6_MFMA, "q8s::tile_kernel_f6 (ofr_knn_f6 phase 1, one fp6 e2m3 slice)"
+        alg_bytes_tiles = 0.75 * (nl * d + B * d)                    # 6 bits per feature, gallery + queries
+        executed = flops_tiles
+    elif use_q8:
         peak, kname = PEAK_I8_MFMA, "q8s::tile_kernel<1> (ofr_knn_q8 phase 1, one int8 slice)"
         alg_bytes_tiles = nl * d + B * d                             # one int8 slice of gallery + queries
         executed = flops_tiles                                       # x1.y1
@@ -289,8 +296,9 @@ def main():
             "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None,
-            "dtype": ("i8 (int8 MFMA coarse scores, certified; fp64 exact re-rank)" if use_q8 else
-                      "f32 (fp32 MFMA scores, fp64 exact re-rank)"), "data": "synthetic",
+            "dtype": {"f6": "fp6 e2m3 (fp6 MFMA coarse scores, certified; fp64 exact re-rank)",
+                      "q8": "i8 (int8 MFMA coarse scores, certified; fp64 exact re-rank)",
+                      "fp32": "f32 (fp32 MFMA scores, fp64 exact re-rank)"}[args.search], "data": "synthetic",
             "config": {"workload": "configs[2]: Fisherfaces projection + 1-NN, 1M-image gallery (100k ids x 10), "
                                    "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1",
                        "gallery": N, "global_batch": B, "d": d, "D": D, "k": k,
@@ -302,10 +310,10 @@ def main():
                          "traffic_source": tr[1] if tr else None,
                          "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
                          "launch_ms": ms_tiles},
-            "kernels_ms": {"project_u8_exact" + ("+q8_quantize" if use_q8 else ""): ms_proj, "knn_tiles": ms_tiles,
+            "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else ""): ms_proj, "knn_tiles": ms_tiles,
                            "knn_merge_rerank" + ("+certificate+fallback" if use_q8 else ""): ms_merge},
             "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
-            "uncertified_after_two_slices": (list(gallery.last_fallbacks)[1] if use_q8 else None),
+            "uncertified_after_each_tier": (list(gallery.last_fallbacks) if use_q8 else None),
             "top1_identity_acc": acc,
             "small_batch": small,
         }

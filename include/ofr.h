@@ -149,6 +149,26 @@ int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, 
                int k, int64_t index_base, double* out_d, int64_t* out_i, int* cert, void* workspace,
                size_t workspace_bytes);
 
+/* fp6 first tier of the certified search (same contract as ofr_knn_q8) -----
+ * Rows are cut into e2m3 fp6 values with a per-row fp32 scale s = max|x|/7.5
+ * (x~ = s v, |v| <= 7.5) and stored in the "f6 tiled" layout: 256-row panels x
+ * 128-feature stages, 24 KiB per (panel, stage) (layout: csrc/ofr_f6_tile.h);
+ * ofr_f6_tiles_bytes(R, d) bytes, rows past R in the last panel zeroed.
+ * stats[3] = (||x~||, ||x - x~||, 0); maxima as ofr_q8_quantize_rows.
+ * ofr_knn_f6: v_mfma_scale_f32_32x32x64_f8f6f4 (fp6 x fp6, unit block scales)
+ * sums v_q.v_g with fp32 accumulation, whose error (<= (2 nst + 64) 2^-23
+ * a_q A) is added to the certificate bound; otherwise exactly ofr_knn_q8
+ * (best 16 per 256-row tile, exact fp64 re-rank, cert[q]).  Workspace:
+ * ofr_knn_q8_workspace_bytes(B, N).                                          */
+size_t ofr_f6_tiles_bytes(int64_t R, int64_t d);
+int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
+                         size_t tiles_bytes, float* scale, double* stats, const float* aux, double* maxima);
+int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+               const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
+               const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
+               int64_t index_base, double* out_d, int64_t* out_i, int* cert, void* workspace,
+               size_t workspace_bytes);
+
 /* Merge P sorted (distance, index) lists per query into the best k:
  * in_d/in_i [B][P*kin] (list p at columns [p*kin, (p+1)*kin)), ascending by
  * (distance, index); out [B][k].  Used after the RCCL all-gather of per-rank

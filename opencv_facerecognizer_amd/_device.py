@@ -20,7 +20,7 @@ from . import _lib
 from ._lib import call, ptr, stream
 
 
-SMALL_BATCH = 32   # B <= 32: HBM-streaming fp32 tiles; larger batches: certified int8 tiles (Euclidean)
+SMALL_BATCH = 32   # B <= 32: HBM-streaming fp32 tiles; larger batches: certified fp6/int8 tiles (Euclidean)
 # the int8 pass keeps 16 candidates per query; a certificate needs slack between the k-th
 # exact distance and the 16th coarse score, so k is limited to half of that
 Q8_MAX_K = 8
@@ -200,84 +200,120 @@ class FloatGallery:
         self.q8 = None
         self.last_fallbacks = 0
 
-    # -- certified int8 coarse pass (Euclidean, B > 32) ------------------------------------------
-    # Tier 1: one int8 slice (x~ = s x1), 256x256 tiles.  Tier 2, for the queries tier 1 could
-    # not certify: two slices (x~ = s (x1 + x2/2^7)).  Tier 3: the fp32 path.  Every tier ends in
-    # the exact fp64 re-rank; tiers 1-2 only answer where the certificate proves the result exact.
+    # -- certified quantized coarse passes (Euclidean, B > 32) -------------------------------------
+    # Tier "f6": one fp6 (e2m3) slice per row with an fp32 row scale (x~ = s v), fp6 MFMA at twice
+    # the int8 rate.  Tier 1, for the queries tier "f6" could not certify: one int8 slice
+    # (x~ = s x1).  Tier 2: two int8 slices (x~ = s (x1 + x2/2^7)).  Last: the fp32 path.  Every
+    # tier ends in the exact fp64 re-rank; the quantized tiers only answer where the certificate
+    # proves the result exact.  OFR_SEARCH picks the first tier: auto (= f6), q8
+    # (tier 1), q8x2 (tier 2) or fp32.
+    TIER_CHAIN = ("f6", 1, 2, "fp32")
+
     def use_q8(self, B, k):
         mode = os.environ.get("OFR_SEARCH", "auto")
         return (mode != "fp32" and self.metric == _lib.METRIC_EUCLIDEAN and self.N > 0
                 and B > SMALL_BATCH and k <= Q8_MAX_K)
 
     @staticmethod
+    def first_tier():
+        return {"q8": 1, "q8x2": 2}.get(os.environ.get("OFR_SEARCH", "auto"), "f6")
+
+    @staticmethod
     def _q8_ld(d, slices):
         return round_up(d, 128) if slices == 1 else 2 * round_up(d, 64)
 
-    def _q8_gallery(self, slices=1):
+    def _tier_gallery(self, tier="f6"):
+        """Quantized gallery rows of one tier (built once, kept on the device)."""
         if self.q8 is None:
             self.q8 = {}
-        if slices not in self.q8:
+        if tier not in self.q8:
             dev_ = self.G.device
-            ld = self._q8_ld(self.d, slices)
-            Gs = torch.empty((self.N, ld), dtype=torch.int8, device=dev_)
             gs = torch.empty(self.N, dtype=torch.float32, device=dev_)
             st = torch.empty((self.N, 3), dtype=torch.float64, device=dev_)
             gmax = torch.empty(4, dtype=torch.float64, device=dev_)
-            call("ofr_q8_quantize_rows", stream(), slices, ptr(self.G), self.N, self.d, self.ld, ptr(Gs), ld,
-                 ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
-            self.q8[slices] = dict(Gs=Gs, scale=gs, stats=st, gmax=gmax, ld=ld)
-        return self.q8[slices]
+            if tier == "f6":
+                nbytes = _lib.load().ofr_f6_tiles_bytes(self.N, self.d)
+                Gs = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
+                call("ofr_f6_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, ptr(Gs), nbytes,
+                     ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
+                ld = 0
+            else:
+                ld = self._q8_ld(self.d, tier)
+                Gs = torch.empty((self.N, ld), dtype=torch.int8, device=dev_)
+                call("ofr_q8_quantize_rows", stream(), tier, ptr(self.G), self.N, self.d, self.ld, ptr(Gs), ld,
+                     ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
+            self.q8[tier] = dict(Gs=Gs, scale=gs, stats=st, gmax=gmax, ld=ld)
+        return self.q8[tier]
 
-    def quantize_queries(self, Qd, out=None, slices=1):
-        ld = self._q8_ld(self.d, slices)
+    def _q8_gallery(self, slices=1):   # kept for callers of the int8 tiers
+        return self._tier_gallery(slices)
+
+    def quantize_queries(self, Qd, out=None, tier="f6"):
+        """Centred fp32 query rows -> the tier's quantized rows, scales and stats (device)."""
         B = Qd.shape[0]
-        if out is None or out["Qs"].shape[0] != B or out["slices"] != slices:
-            out = dict(Qs=torch.empty((B, ld), dtype=torch.int8, device=Qd.device),
-                       scale=torch.empty(B, dtype=torch.float32, device=Qd.device),
-                       stats=torch.empty((B, 3), dtype=torch.float64, device=Qd.device),
-                       cert=torch.empty(B, dtype=torch.int32, device=Qd.device), slices=slices)
-        call("ofr_q8_quantize_rows", stream(), slices, ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]), ld,
-             ptr(out["scale"]), ptr(out["stats"]), None, None)
+        dev_ = Qd.device
+        if out is None or out["B"] != B or out["tier"] != tier:
+            if tier == "f6":
+                Qs = torch.empty(max(1, _lib.load().ofr_f6_tiles_bytes(B, self.d)), dtype=torch.uint8, device=dev_)
+            else:
+                Qs = torch.empty((B, self._q8_ld(self.d, tier)), dtype=torch.int8, device=dev_)
+            out = dict(Qs=Qs, scale=torch.empty(B, dtype=torch.float32, device=dev_),
+                       stats=torch.empty((B, 3), dtype=torch.float64, device=dev_),
+                       cert=torch.empty(B, dtype=torch.int32, device=dev_), tier=tier, B=B)
+        if tier == "f6":
+            call("ofr_f6_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
+                 out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None)
+        else:
+            call("ofr_q8_quantize_rows", stream(), tier, ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
+                 out["Qs"].shape[1], ptr(out["scale"]), ptr(out["stats"]), None, None)
         return out
 
     def search_q8_phase(self, phases, Qd, qq, k, index_base=0, out=None):
-        """phases 1 = int8 tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"]), 3 = both."""
-        g = self._q8_gallery(qq["slices"])
+        """phases 1 = quantized tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"]), 3 = both."""
+        tier = qq["tier"]
+        g = self._tier_gallery(tier)
         B = Qd.shape[0]
         if out is None:
             out = (torch.empty((B, k), dtype=torch.float64, device=Qd.device),
                    torch.empty((B, k), dtype=torch.int64, device=Qd.device))
         ws = self.ws.get(_lib.load().ofr_knn_q8_workspace_bytes(B, self.N), Qd.device)
-        call("ofr_knn_q8", stream(), phases, qq["slices"], ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
-             ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), g["ld"],
-             ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]),
-             ptr(qq["cert"]), ptr(ws), ws.numel())
+        if tier == "f6":
+            call("ofr_knn_f6", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
+                 ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),
+                 ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
+                 ptr(ws), ws.numel())
+        else:
+            call("ofr_knn_q8", stream(), phases, tier, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
+                 ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), g["ld"],
+                 ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]),
+                 ptr(qq["cert"]), ptr(ws), ws.numel())
         return out
 
     def fallback(self, Qd, qq, k, out, index_base=0):
-        """Re-run the queries tier 1 left uncertified: two slices, then fp32 for what remains.
-        Returns the number of tier-1 failures (host sync); self.last_fallbacks = (tier-1, tier-2) failures."""
+        """Re-run the queries the first tier left uncertified down the tier chain (then fp32).
+        Returns the number of first-tier failures (host sync); self.last_fallbacks = the number of
+        uncertified queries after each quantized tier that ran."""
+        chain = list(self.TIER_CHAIN[self.TIER_CHAIN.index(qq["tier"]) + 1:])
         bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
-        n1 = int(bad.numel())
-        n2 = 0
-        if n1:
-            sub = Qd.index_select(0, bad).contiguous()
-            if qq["slices"] == 1:
-                q2 = self.quantize_queries(sub, slices=2)
-                d2, i2 = self.search_q8_phase(3, sub, q2, k, index_base)
-                bad2 = torch.nonzero(q2["cert"] == 0).reshape(-1)
-                n2 = int(bad2.numel())
-                if n2:
-                    d3, i3 = self._search_f32(sub.index_select(0, bad2).contiguous(), k, index_base)
-                    d2.index_copy_(0, bad2, d3)
-                    i2.index_copy_(0, bad2, i3)
-            else:
-                n2 = n1
+        counts = [int(bad.numel())]
+        rows = bad                      # indices into the original batch still unresolved
+        while rows.numel():
+            tier = chain.pop(0)
+            sub = Qd.index_select(0, rows).contiguous()
+            if tier == "fp32":
                 d2, i2 = self._search_f32(sub, k, index_base)
-            out[0].index_copy_(0, bad, d2)
-            out[1].index_copy_(0, bad, i2)
-        self.last_fallbacks = (n1, n2)
-        return n1
+                out[0].index_copy_(0, rows, d2)
+                out[1].index_copy_(0, rows, i2)
+                break
+            q2 = self.quantize_queries(sub, tier=tier)
+            d2, i2 = self.search_q8_phase(3, sub, q2, k, index_base)
+            out[0].index_copy_(0, rows, d2)
+            out[1].index_copy_(0, rows, i2)
+            still = torch.nonzero(q2["cert"] == 0).reshape(-1)
+            counts.append(int(still.numel()))
+            rows = rows.index_select(0, still)
+        self.last_fallbacks = tuple(counts)
+        return counts[0]
 
     def query_rows(self, Q64):
         """Host or device fp64 query features [B][d] -> centred fp32 search rows [B][ld]."""
@@ -303,8 +339,7 @@ class FloatGallery:
             raise ValueError(f"query row stride {Qd.shape[1]} != gallery stride {self.ld}")
         B = Qd.shape[0]
         if self.use_q8(B, k):
-            # OFR_SEARCH=q8x2 starts at the two-slice tier (tests / hard data)
-            qq = self.quantize_queries(Qd, slices=2 if os.environ.get("OFR_SEARCH") == "q8x2" else 1)
+            qq = self.quantize_queries(Qd, tier=self.first_tier())
             out = self.search_q8_phase(3, Qd, qq, k, index_base)
             self.fallback(Qd, qq, k, out, index_base)
             return out

@@ -29,6 +29,7 @@
 // otherwise 0 and the caller re-runs that query on the fp32 path.
 #include <type_traits>
 
+#include "ofr_f6_tile.h"
 #include "ofr_i8_tile.h"
 #include "ofr_topk.h"
 
@@ -111,25 +112,16 @@ struct KeyList {
   }
 };
 
-// MODE 0 is the search; 1 (no k-loop DMA) and 2 (no MFMA) exist only for the
-// feed/compute probe in tools/ and are never instantiated by the library.
-template <int SL, int MODE>
-__global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
-  using S = Shape<SL>;
-  constexpr int CT = S::CT, TQ = S::TQ, QW = S::QW;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
-  int64_t gt, qt;
-  i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
-  const int64_t g0 = gt * TG, q0 = qt * TQ;
+// Tile epilogue shared by the int8 and fp6 engines: coarse scores -> keys, per-lane best
+// 16 of the lane's 64 gallery rows, merge with the partner half-wave, then across the two
+// row-waves through LDS; writes the tile's best KC per query to p.cand.
+// cval(rt, ctc, r): coarse product q~.g~ / (s_q s_g) of accumulator register r of row block
+// rt and query block ctc (an integral_constant: a runtime index would send acc to scratch).
+template <int CT, int TQ, int QW, int WQ, class CV>
+__device__ __forceinline__ void tile_epilogue(char* smem, const TileArgs& p, int64_t gt, int64_t g0, int64_t q0,
+                                              CV&& cval) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave / S::WQ, wc = wave % S::WQ, h = lane >> 5, r32 = lane & 31;
-
-  i32x16 acc0[4][CT], acc1[4][SL == 2 ? CT : 1];
-  i8t::mainloop<SL, MODE, false>(smem, p.G, p.ld, p.N, g0, p.Q, p.ld, p.B, q0, p.ld, p.nk, acc0, acc1);
-
-  // epilogue: coarse scores -> keys, per-lane best 16 of the lane's 64 gallery rows,
-  // merge with the partner half-wave, then across the two row-waves through LDS.
+  const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
   uint32_t* kbuf = reinterpret_cast<uint32_t*>(smem);                      // [2][TQ][KC]
   float* gtab = reinterpret_cast<float*>(smem + 2 * TQ * KC * 4);          // [TG][2]
   if (threadIdx.x < TG) {
@@ -140,7 +132,6 @@ __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
   }
   __syncthreads();
   const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
-  // one body per query block (ct is a template constant: a runtime index would send acc to scratch)
   auto epi = [&](auto ctc) {
     constexpr int ct = decltype(ctc)::value;
     if constexpr (ct < CT) {
@@ -154,8 +145,7 @@ __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int gl = wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float c = (float)acc0[rt][ct][r];
-          if constexpr (SL == 2) c += (float)acc1[rt][ct][r] * 0x1p-7f;
+          const float c = cval(rt, ctc, r);
           const float sc = gtab[2 * gl] - sq2 * gtab[2 * gl + 1] * c;
           L.insert(gl < nvalid ? score_key(sc, gl) : KEY_NONE);
         }
@@ -202,6 +192,45 @@ __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
   }
 }
 
+// MODE 0 is the search; 1 (no k-loop DMA) and 2 (no MFMA) exist only for the
+// feed/compute probe in tools/ and are never instantiated by the library.
+template <int SL, int MODE>
+__global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
+  using S = Shape<SL>;
+  constexpr int CT = S::CT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t gt, qt;
+  i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
+  const int64_t g0 = gt * TG, q0 = qt * S::TQ;
+
+  i32x16 acc0[4][CT], acc1[4][SL == 2 ? CT : 1];
+  i8t::mainloop<SL, MODE, false>(smem, p.G, p.ld, p.N, g0, p.Q, p.ld, p.B, q0, p.ld, p.nk, acc0, acc1);
+  tile_epilogue<CT, S::TQ, S::QW, S::WQ>(smem, p, gt, g0, q0, [&](int rt, auto ctc, int r) {
+    constexpr int ct = decltype(ctc)::value;
+    float c = (float)acc0[rt][ct][r];
+    if constexpr (SL == 2) c += (float)acc1[rt][ct][r] * 0x1p-7f;
+    return c;
+  });
+}
+
+// fp6 tier: p.G / p.Q are f6 tiled buffers (ofr_f6_tile.h), p.nk = stages.
+template <int MODE>
+__global__ void __launch_bounds__(f6t::NT, 1) tile_kernel_f6(TileArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t gt, qt;
+  i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
+  const int64_t g0 = gt * TG, q0 = qt * f6t::TQ;
+  f6t::f32x16 acc[4][f6t::CT];
+  f6t::mainloop<MODE>(smem, reinterpret_cast<const char*>(p.G), gt, reinterpret_cast<const char*>(p.Q), qt, p.nk,
+                      acc);
+  tile_epilogue<f6t::CT, f6t::TQ, f6t::QW, f6t::WQ>(smem, p, gt, g0, q0, [&](int rt, auto ctc, int r) {
+    constexpr int ct = decltype(ctc)::value;
+    return acc[rt][ct][r];
+  });
+}
+
 // ---- pass 2 ----------------------------------------------------------------------------
 
 struct MergeArgs {
@@ -213,6 +242,7 @@ struct MergeArgs {
   int64_t ldg, d;
   const double* qstats;   // [B][3]: a, e, t
   const double* gmax;     // [4]: A, E, T, auxmax
+  double gamma;           // fp32 accumulation bound of the coarse products / (a_q A): 0 for int8
   int k;
   int64_t index_base;
   double* out_d;
@@ -262,7 +292,8 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
       const double tau = (double)lists[KC - 1].d;
       const double a = p.qstats[q * 3 + 0], e = p.qstats[q * 3 + 1], tq = p.qstats[q * 3 + 2];
       const double A = p.gmax[0], E = p.gmax[1], T = p.gmax[2], auxmax = p.gmax[3];
-      double dS = 2.0 * (a * E + e * A + e * E + tq * T) + 0x1p-20 * (auxmax + 2.0 * a * A);
+      double dS = 2.0 * (a * E + e * A + e * E + tq * T) + 0x1p-20 * (auxmax + 2.0 * a * A) +
+                  2.0 * p.gamma * a * A;
       dS = dS * (1.0 + 1e-6) + 1e-300;
       const int kk = p.k < KC ? p.k : KC;
       const double dk = od[kk - 1];
@@ -344,6 +375,109 @@ __global__ void __launch_bounds__(256) quantize_kernel(const float* X, int64_t l
     stats[row * 3 + 0] = sqrt(A) * (1.0 + 1e-12);
     stats[row * 3 + 1] = sqrt(E) * (1.0 + 1e-12);
     stats[row * 3 + 2] = s * 0x1p-7 * sqrt(T) * (1.0 + 1e-12);
+  }
+}
+
+// fp6 tier: x~ = s v, v in e2m3 (|v| <= 7.5: m/8 below 2, steps 1/4 in [2,4), 1/2 in [4,7.5]),
+// s = max|x| / 7.5 as an fp32 number (any real scale is allowed: it is applied in the
+// epilogue, not by the MFMA), rounded up so that every |x|/s <= 7.5.  One block per row;
+// thread t writes the 24 bytes of the 32-feature groups g = t, t + 256, ... into the f6
+// tiled layout (ofr_f6_tile.h).  stats as quantize_kernel (third = 0).
+__device__ __forceinline__ uint32_t e2m3_code(double r, double& q) {
+  const double a = fabs(r);
+  double v;
+  if (a < 2.0) v = rint(a * 8.0) * 0.125;
+  else if (a < 4.0) v = rint(a * 4.0) * 0.25;
+  else v = rint(a * 2.0) * 0.5;
+  uint32_t code;
+  if (v < 1.0) code = (uint32_t)(v * 8.0);
+  else {
+    const int e = v < 2.0 ? 1 : (v < 4.0 ? 2 : 3);
+    code = ((uint32_t)e << 3) | (uint32_t)((v / (double)(1 << (e - 1)) - 1.0) * 8.0);
+  }
+  q = r < 0 ? -v : v;
+  return (r < 0 && v != 0.0) ? (code | 32u) : code;
+}
+
+__global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_t ldx, int64_t d, int64_t nst,
+                                                          char* tiles, float* scale, double* stats) {
+  __shared__ float redf[4];
+  __shared__ double red[4][2];
+  const int64_t row = blockIdx.x;
+  const float* x = X + row * ldx;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float mx = 0.f;
+  for (int64_t i = threadIdx.x; i < d; i += blockDim.x) mx = fmaxf(mx, fabsf(x[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) redf[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+  float s = 1.0f;
+  if (mx > 0.f) {
+    s = (float)((double)mx / 7.5);
+    while ((double)mx / (double)s > 7.5) s = __uint_as_float(__float_as_uint(s) + 1u);
+  }
+  const double sd = (double)s;
+  double sa = 0, se = 0;
+  const int64_t ngroups = nst * 4;
+  char* pbase = tiles + (row >> 8) * nst * (int64_t)f6t::PANEL;
+  const int rl = (int)(row & 255);
+  for (int64_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
+    uint32_t w[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+      const int64_t k = g * 32 + e;
+      if (k < d) {
+        const double xv = (double)x[k];
+        double qv;
+        const uint32_t c = e2m3_code(xv / sd, qv);
+        const double xt = sd * qv;   // exact: 24-bit s times a 4-bit significand
+        sa += xt * xt;
+        se += (xv - xt) * (xv - xt);
+        const int bit = 6 * e;
+        w[bit >> 5] |= c << (bit & 31);
+        if ((bit & 31) > 26) w[(bit >> 5) + 1] |= c >> (32 - (bit & 31));
+      }
+    }
+    const int64_t st = g >> 2;
+    const int jh = (int)(g & 3);   // 2 j + h
+    char* sb = pbase + st * f6t::PANEL + jh * 6144;
+    *reinterpret_cast<uint4*>(sb + rl * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<uint2*>(sb + 4096 + rl * 8) = make_uint2(w[4], w[5]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sa += __shfl_xor(sa, o);
+    se += __shfl_xor(se, o);
+  }
+  if (lane == 0) {
+    red[wave][0] = sa;
+    red[wave][1] = se;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double A = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    const double E = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    scale[row] = s;
+    stats[row * 3 + 0] = sqrt(A) * (1.0 + 1e-12);
+    stats[row * 3 + 1] = sqrt(E) * (1.0 + 1e-12);
+    stats[row * 3 + 2] = 0.0;
+  }
+}
+
+// zero rows of the last panel past R (they are never selected: the epilogue masks rows >= N)
+__global__ void f6_zero_tail(char* tiles, int64_t R, int64_t nst) {
+  const int64_t p = R >> 8;
+  const int r0 = (int)(R & 255);
+  char* pbase = tiles + p * nst * (int64_t)f6t::PANEL;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nst * 4 * (256 - r0);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t sjh = i / (256 - r0);
+    const int rl = r0 + (int)(i % (256 - r0));
+    char* sb = pbase + (sjh >> 2) * f6t::PANEL + (sjh & 3) * 6144;
+    *reinterpret_cast<uint4*>(sb + rl * 16) = make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint2*>(sb + 4096 + rl * 8) = make_uint2(0, 0);
   }
 }
 
@@ -449,9 +583,88 @@ extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, 
   }
   if (phases & 2) {
     OFR_CHECK_ARG(out_d && out_i && cert, "ofr_knn_q8: null output");
-    q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, k, index_base, out_d, out_i, cert};
+    q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, 0.0, k, index_base, out_d, out_i, cert};
     hipLaunchKernelGGL(q8s::merge_kernel, dim3((unsigned)B), dim3(256), 0, st, m);
     OFR_LAUNCH_CHECK("q8 merge_kernel");
+  }
+  return OFR_OK;
+}
+
+/* ---- fp6 tier ------------------------------------------------------------------------- */
+
+extern "C" size_t ofr_f6_tiles_bytes(int64_t R, int64_t d) {
+  return R <= 0 || d <= 0 ? 0 : (size_t)f6t::tiles_bytes(R, d);
+}
+
+extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
+                                    size_t tiles_bytes, float* scale, double* stats, const float* aux,
+                                    double* maxima) {
+  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d, "ofr_f6_quantize_rows: bad sizes");
+  if (R == 0) return OFR_OK;
+  OFR_CHECK_ARG(X && tiles && scale && stats, "ofr_f6_quantize_rows: null pointer");
+  OFR_CHECK_ARG(R < 0x7fffffffLL, "ofr_f6_quantize_rows: too many rows");
+  OFR_CHECK_ARG(tiles_bytes >= ofr_f6_tiles_bytes(R, d), "ofr_f6_quantize_rows: tile buffer too small");
+  OFR_CHECK_ARG((uintptr_t)tiles % 16 == 0, "ofr_f6_quantize_rows: tiles must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nst = f6t::stages(d);
+  hipLaunchKernelGGL(q8s::quantize_f6_kernel, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, (char*)tiles,
+                     scale, stats);
+  OFR_LAUNCH_CHECK("f6 quantize_kernel");
+  if (R % 256) {
+    hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)tiles, R, nst);
+    OFR_LAUNCH_CHECK("f6 zero_tail");
+  }
+  if (maxima) {
+    hipLaunchKernelGGL(q8s::maxima_kernel, dim3(1), dim3(256), 0, st, stats, aux, R, maxima);
+    OFR_LAUNCH_CHECK("q8 maxima_kernel");
+  }
+  return OFR_OK;
+}
+
+extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                          const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
+                          int64_t d, const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
+                          int64_t index_base, double* out_d, int64_t* out_i, int* cert, void* workspace,
+                          size_t workspace_bytes) {
+  OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_f6: phases must be 1 (tiles), 2 (merge) or 3");
+  OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_f6: bad sizes (empty galleries use ofr_knn_f32)");
+  if (k < 1 || k > q8s::KC) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6: k must be in [1, 16]");
+  if (B == 0) return OFR_OK;
+  OFR_CHECK_ARG(ldq >= d && ldg >= d, "ofr_knn_f6: bad leading dimensions");
+  OFR_CHECK_ARG(Q && Qt && qscale && qstats && G && Gt && gscale && aux && gmax && workspace,
+                "ofr_knn_f6: null pointer");
+  OFR_CHECK_ARG(((uintptr_t)Qt | (uintptr_t)Gt) % 16 == 0, "ofr_knn_f6: tiles must be 16-byte aligned");
+  OFR_CHECK_ARG(N < 0x7fffffffLL - q8s::TG, "ofr_knn_f6: N too large for one shard");
+  OFR_CHECK_ARG(workspace_bytes >= ofr_knn_q8_workspace_bytes(B, N), "ofr_knn_f6: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  q8s::TileArgs a;
+  a.G = (const int8_t*)Gt; a.N = N; a.ld = 0; a.gscale = gscale; a.aux = aux;
+  a.Q = (const int8_t*)Qt; a.B = B; a.qscale = qscale;
+  a.nk = (int)f6t::stages(d);
+  a.cand = reinterpret_cast<Cand*>(workspace);
+  a.ntq = f6t::panels(B);
+  a.ntg = f6t::panels(N);
+  a.gg = a.ntg < q8s::GROUP_G ? a.ntg : q8s::GROUP_G;
+  OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
+  if (phases & 1) {
+    static bool attr_done = false;
+    if (!attr_done) {
+      hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel_f6<0>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
+      if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
+      attr_done = true;
+    }
+    hipLaunchKernelGGL((q8s::tile_kernel_f6<0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::NT), f6t::LDS, st, a);
+    OFR_LAUNCH_CHECK("f6 tile_kernel");
+  }
+  if (phases & 2) {
+    OFR_CHECK_ARG(out_d && out_i && cert, "ofr_knn_f6: null output");
+    // fp32 accumulation over nst * 2 MFMAs: |err| <= (n + 64) 2^-23 sum|q~ g~| / (s_q s_g),
+    // sum|q~ g~| <= a_q a_g <= a_q A (tools/mx_probe.hip measures <= 3 * 2^-24 at n = 160)
+    const double gamma = (double)(2 * a.nk + 64) * 0x1p-23;
+    q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, gamma, k, index_base, out_d, out_i, cert};
+    hipLaunchKernelGGL(q8s::merge_kernel, dim3((unsigned)B), dim3(256), 0, st, m);
+    OFR_LAUNCH_CHECK("f6 merge_kernel");
   }
   return OFR_OK;
 }

@@ -81,12 +81,13 @@ def test_knn_vs_oracle(metric, B, N, d, k):
 
 @pytest.mark.parametrize("B,N,d,k", [(33, 300, 3, 1), (300, 5000, 99, 5), (257, 3000, 300, 16), (600, 20000, 64, 3),
                                      (1000, 70000, 130, 1)])
-@pytest.mark.parametrize("mode", ["q8", "q8x2", "fp32"])
+@pytest.mark.parametrize("mode", ["auto", "q8", "q8x2", "fp32"])
 def test_knn_euclidean_paths_vs_oracle(monkeypatch, mode, B, N, d, k):
-    """Batches > 32 take the certified int8 tiers (ofr_knn_q8, 1 then 2 slices) unless OFR_SEARCH=fp32."""
+    """Batches > 32 take the certified tiers (ofr_knn_f6, then ofr_knn_q8 with 1 and 2 slices) unless
+    OFR_SEARCH=fp32; OFR_SEARCH=q8 / q8x2 start at the int8 tiers."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
-    monkeypatch.setenv("OFR_SEARCH", {"q8": "auto"}.get(mode, mode))
+    monkeypatch.setenv("OFR_SEARCH", mode)
     r = _rng(B * 11 + N + d)
     protos = r.normal(0, 30, (max(N // 10, 1), d))
     G = (protos[np.arange(N) % len(protos)] + r.normal(0, 5, (N, d))).astype(np.float32).astype(np.float64)
@@ -104,9 +105,10 @@ def test_knn_euclidean_paths_vs_oracle(monkeypatch, mode, B, N, d, k):
 
 
 def test_knn_q8_certificate_forces_fallback(monkeypatch):
-    """A gallery on a sphere around the queries: more than 16 rows lie within the int8 pass's error
-    bound of the k-th distance, so no query can be certified; all of them must be re-run on the
-    fp32 path and still match the oracle (up to its own near-ties)."""
+    """A gallery on a sphere around the queries: more than 16 rows lie within the quantized passes'
+    error bounds of the k-th distance, so no query can be certified by any tier (fp6, int8 x1,
+    int8 x2); all of them must be re-run on the fp32 path and still match the oracle (up to its
+    own near-ties)."""
     from opencv_facerecognizer_amd._device import FloatGallery
     from opencv_facerecognizer_amd import _lib
     monkeypatch.setenv("OFR_SEARCH", "auto")
@@ -117,8 +119,91 @@ def test_knn_q8_certificate_forces_fallback(monkeypatch):
     Q = (c + r.normal(0, 1e-6, (100, 64))).astype(np.float32).astype(np.float64)   # every row ~equidistant
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     dd, ii = g.search(g.query_rows(Q), 3)
-    assert g.last_fallbacks[0] > 0 and g.last_fallbacks[1] > 0
+    assert len(g.last_fallbacks) == 3 and min(g.last_fallbacks) > 0
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
+
+
+def _e2m3_values():
+    return np.array([m / 8 for m in range(8)] + [(1 + m / 8) * 2.0 ** (e - 1) for e in (1, 2, 3) for m in range(8)])
+
+
+def _decode_f6_tiles(tiles, R, d):
+    """Host decode of the f6 tiled layout (csrc/ofr_f6_tile.h) -> e2m3 values [R][nst*128]."""
+    nst = -(-d // 128)
+    P = -(-R // 256)
+    t = tiles.reshape(P, nst, 4, 6144)                       # (panel, stage, 2j+h, sub-block)
+    p0 = t[..., :4096].reshape(P, nst, 4, 256, 16)
+    p1 = t[..., 4096:].reshape(P, nst, 4, 256, 8)
+    grp = np.concatenate([p0, p1], axis=-1)                  # 24 bytes = 32 x 6 bits per row and group
+    bits = np.unpackbits(grp, axis=-1, bitorder="little").reshape(P, nst, 4, 256, 32, 6)
+    code = (bits * (1 << np.arange(6))).sum(-1)
+    mag = _e2m3_values()[code & 31]
+    val = np.where(code & 32, -mag, mag)                     # (P, nst, 4, 256, 32)
+    val = val.transpose(0, 3, 1, 2, 4).reshape(P * 256, nst * 128)
+    return val[:R]
+
+
+@pytest.mark.parametrize("R,d", [(1, 3), (300, 99), (513, 260), (256, 128), (40, 1000)])
+def test_f6_quantize_rows_vs_host(R, d):
+    """ofr_f6_quantize_rows: every value is the nearest e2m3 value of x/s (ties either way), s = max|x|/7.5
+    rounded up, padding is zero, and the stats are ||x~|| and ||x - x~|| of x~ = s v."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._lib import call, ptr, stream
+    r = _rng(R * 7 + d)
+    X = r.normal(0, 3, (R, d)).astype(np.float32)
+    X[0, : d // 2] = 0
+    if R > 2:
+        X[2] = 0                                                          # all-zero row
+        X[1, 0] = 1e6                                                     # one huge feature
+    ldx = d + 5
+    Xd = torch.zeros((R, ldx), dtype=torch.float32, device="cuda")
+    Xd[:, :d] = torch.from_numpy(X).cuda()
+    nbytes = _lib.load().ofr_f6_tiles_bytes(R, d)
+    T = torch.full((nbytes,), 0xAB, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(R, dtype=torch.float32, device="cuda")
+    st = torch.empty((R, 3), dtype=torch.float64, device="cuda")
+    call("ofr_f6_quantize_rows", stream(), ptr(Xd), R, d, ldx, ptr(T), nbytes, ptr(sc), ptr(st), None, None)
+    torch.cuda.synchronize()
+    Vall = _decode_f6_tiles(T.cpu().numpy(), -(-R // 256) * 256, d)
+    assert np.all(Vall[R:] == 0)                                          # tail rows of the last panel
+    V = Vall[:R]
+    s = sc.cpu().numpy().astype(np.float64)
+    assert np.all(V[:, d:] == 0)
+    mx = np.abs(X).max(1).astype(np.float64)
+    assert np.all(np.where(mx > 0, mx / s, 0) <= 7.5)
+    assert np.all(np.where(mx > 0, s <= np.nextafter(np.float32(mx / 7.5), np.float32(np.inf)) * (1 + 1e-6), s == 1))
+    grid = _e2m3_values()
+    r_ = np.abs(X / s[:, None])
+    err = np.abs(np.abs(V[:, :d]) - r_)
+    best = np.abs(r_[..., None] - grid).min(-1)
+    assert np.all(err <= best + 1e-12)                                    # nearest representable value
+    assert np.all((np.sign(V[:, :d]) == np.sign(X)) | (V[:, :d] == 0))
+    Xt = s[:, None] * V[:, :d]
+    a = np.linalg.norm(Xt, axis=1)
+    e = np.linalg.norm(X.astype(np.float64) - Xt, axis=1)
+    got = st.cpu().numpy()
+    np.testing.assert_allclose(got[:, 0], a, rtol=1e-11, atol=0)
+    np.testing.assert_allclose(got[:, 1], e, rtol=1e-11, atol=0)
+    assert np.all(got[:, 0] >= a) and np.all(got[:, 1] >= e)             # rounded up, never shrinks the bound
+    assert np.all(got[:, 2] == 0)
+
+
+def test_knn_f6_tier_certifies_separated_data(monkeypatch):
+    """f6 tier on well-separated identities (integer prototypes, +-1 noise, 10 rows per identity so
+    that the 16 candidates reach past the query's own identity): the fp6 tier alone must certify
+    every query and return the oracle's neighbours."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(5)
+    N, B, d = 5000, 300, 200
+    protos = r.integers(-7, 8, (N // 10, d)).astype(np.float64)
+    G = protos[np.arange(N) % (N // 10)] + r.integers(-1, 2, (N, d))
+    Q = protos[r.integers(0, N // 10, B)] + r.integers(-1, 2, (B, d))
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    dd, ii = g.search(g.query_rows(Q), 4)
+    assert g.last_fallbacks[0] == 0
+    _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 4)
 
 
 def test_knn_exact_duplicates_tie_to_lowest_index():
