@@ -53,7 +53,7 @@ struct TileArgs {
   int64_t B;
   const float* qscale;
   int nk;
-  Cand* cand;   // [T][B][KC]
+  Cand* cand;   // [B][T][KC] (query-major)
   int64_t ntq, ntg;
   int64_t gg;   // gallery tiles per tile group (see tile_coords)
 };
@@ -181,7 +181,7 @@ __device__ __forceinline__ void tile_epilogue(char* smem, const TileArgs& p, int
     }
     L.merge(o);
     if (q < p.B) {
-      Cand* out = p.cand + ((size_t)gt * p.B + q) * KC;
+      Cand* out = p.cand + ((size_t)q * p.ntg + gt) * KC;   // query-major: the merge streams one query's lists
 #pragma unroll
       for (int j = 0; j < KC; ++j) {
         const uint32_t kk = L.k[j];
@@ -250,32 +250,82 @@ struct MergeArgs {
   int* cert;
 };
 
+// One block per query.  (1) best KC of the T tile lists, read as one contiguous stream
+// (candidate lists are query-major: cand[q][t][KC]; 16 B per lane and load, fully
+// coalesced) with a per-thread sorted list and a tree merge; (2) the exact fp64 distance
+// (distance.py:60) of the KC survivors, one wave per candidate (float4 loads, lane partial
+// sums, shuffle reduction); (3) sort by (distance, index) and the certificate.
 __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   __shared__ Cand lists[256 * KC];
   __shared__ double exact[KC];
   __shared__ double red[4];
   const int64_t q = blockIdx.x;
-  select_candidates<KC>(p.cand, p.T, p.B, q, lists);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  {
+    TopList<KC> L;
+    L.init();
+    const uint4* src = reinterpret_cast<const uint4*>(p.cand + (size_t)q * p.T * KC);
+    const int64_t n4 = p.T * KC / 2;   // two candidates per 16 B
+    for (int64_t e = threadIdx.x; e < n4; e += blockDim.x) {
+      const uint4 v = src[e];
+      const float d0 = __uint_as_float(v.x), d1 = __uint_as_float(v.z);
+      if (better_f(d0, (int)v.y, L.d[KC - 1], L.i[KC - 1])) L.insert(d0, (int)v.y);
+      if (better_f(d1, (int)v.w, L.d[KC - 1], L.i[KC - 1])) L.insert(d1, (int)v.w);
+    }
+#pragma unroll
+    for (int j = 0; j < KC; ++j) lists[threadIdx.x * KC + j] = Cand{L.d[j], L.i[j]};
+    __syncthreads();
+    for (int active = (int)blockDim.x / 2; active > 0; active >>= 1) {
+      if ((int)threadIdx.x < active) {
+        float od[KC];
+        int oi[KC];
+        const Cand* o = lists + (threadIdx.x + active) * KC;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+          od[j] = o[j].d;
+          oi[j] = o[j].i;
+        }
+        L.merge(od, oi);
+#pragma unroll
+        for (int j = 0; j < KC; ++j) lists[threadIdx.x * KC + j] = Cand{L.d[j], L.i[j]};
+      }
+      __syncthreads();
+    }
+  }
   const float* qr = p.Q + q * p.ldq;
+  const int64_t d4 = p.d >> 2;
+  const bool vec = ((p.ldq | p.ldg) & 3) == 0 && (((uintptr_t)p.Q | (uintptr_t)p.G) & 15) == 0;
   double qq = 0;
   for (int64_t j = threadIdx.x; j < p.d; j += blockDim.x) {
     const double x = qr[j];
     qq += x * x;
   }
   qq = block_sum_f64(qq, red);
-  for (int c = 0; c < KC; ++c) {
+  for (int c = wave; c < KC; c += 4) {
     const Cand cc = lists[c];
-    double val = __builtin_inf();
+    double a = 0;
     if (cc.i != CAND_EMPTY) {
       const float* gr = p.G + (int64_t)cc.i * p.ldg;
-      double a = 0;
-      for (int64_t j = threadIdx.x; j < p.d; j += blockDim.x) {   // distance.py:60
+      int64_t j0 = 0;
+      if (vec) {
+        const float4* q4 = reinterpret_cast<const float4*>(qr);
+        const float4* g4 = reinterpret_cast<const float4*>(gr);
+        for (int64_t j = lane; j < d4; j += 64) {   // distance.py:60, in fp64
+          const float4 x = q4[j], y = g4[j];
+          const double e0 = (double)x.x - (double)y.x, e1 = (double)x.y - (double)y.y;
+          const double e2 = (double)x.z - (double)y.z, e3 = (double)x.w - (double)y.w;
+          a += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+        }
+        j0 = d4 * 4;
+      }
+      for (int64_t j = j0 + lane; j < p.d; j += 64) {
         const double df = (double)qr[j] - (double)gr[j];
         a += df * df;
       }
-      val = sqrt(block_sum_f64(a, red));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
     }
-    if (threadIdx.x == 0) exact[c] = val;
+    if (lane == 0) exact[c] = cc.i != CAND_EMPTY ? sqrt(a) : __builtin_inf();
   }
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <vector>
+#include <algorithm>
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -39,7 +40,7 @@ __global__ void chain(const i32x8* a, const i32x8* b, const int* sa, const int* 
   for (int r = 0; r < 16; ++r) out[l * 16 + r] = acc[r];
 }
 
-__global__ void __launch_bounds__(512, 1) rate_fp6(const int* seed, int iters, float* out) {
+__global__ void __launch_bounds__(512, 1) rate_fp6(const int* seed, int iters, float* out, long long* stamps) {
   i32x8 a[4], b[2];
   for (int i = 0; i < 4; ++i)
     for (int e = 0; e < 8; ++e) a[i][e] = seed[(threadIdx.x + 7 * i + e) & 255];
@@ -50,12 +51,19 @@ __global__ void __launch_bounds__(512, 1) rate_fp6(const int* seed, int iters, f
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 2; ++j)
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+  const long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[i], b[j], acc[i][j], 2, 2, 0, s, 0, s);
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) {
+    const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    stamps[2 * w] = t1 - t0;
+    stamps[2 * w + 1] = r1 - r0;
   }
   float t = 0;
   for (int i = 0; i < 4; ++i)
@@ -64,7 +72,7 @@ __global__ void __launch_bounds__(512, 1) rate_fp6(const int* seed, int iters, f
   out[blockIdx.x * blockDim.x + threadIdx.x] = t;
 }
 
-__global__ void __launch_bounds__(512, 1) rate_i8(const int* seed, int iters, float* out) {
+__global__ void __launch_bounds__(512, 1) rate_i8(const int* seed, int iters, float* out, long long* stamps) {
   i32x4 a[4], b[2];
   for (int i = 0; i < 4; ++i)
     for (int e = 0; e < 4; ++e) a[i][e] = seed[(threadIdx.x + 7 * i + e) & 255];
@@ -74,11 +82,18 @@ __global__ void __launch_bounds__(512, 1) rate_i8(const int* seed, int iters, fl
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 2; ++j)
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+  const long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) {
+    const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    stamps[2 * w] = t1 - t0;
+    stamps[2 * w + 1] = r1 - r0;
   }
   int t = 0;
   for (int i = 0; i < 4; ++i)
@@ -211,6 +226,9 @@ int main(int argc, char** argv) {
   for (auto& v : hs) { s ^= s << 13; s ^= s >> 17; s ^= s << 5; v = (int)s; }
   CK(hipMemcpy(seed, hs.data(), 256 * 4, hipMemcpyHostToDevice));
   CK(hipMalloc(&out, (size_t)ncu * 512 * 4));
+  long long* stamps;
+  CK(hipMalloc(&stamps, (size_t)ncu * 8 * 2 * 8));
+  std::vector<long long> hst((size_t)ncu * 16);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int iters = 20000;
@@ -218,8 +236,8 @@ int main(int argc, char** argv) {
     for (int threads : {256, 512}) {
       for (int kind = 0; kind < 2; ++kind) {
         auto launch = [&]() {
-          if (kind == 0) hipLaunchKernelGGL(rate_fp6, dim3(ncu), dim3(threads), 0, 0, seed, iters, out);
-          else hipLaunchKernelGGL(rate_i8, dim3(ncu), dim3(threads), 0, 0, seed, iters, out);
+          if (kind == 0) hipLaunchKernelGGL(rate_fp6, dim3(ncu), dim3(threads), 0, 0, seed, iters, out, stamps);
+          else hipLaunchKernelGGL(rate_i8, dim3(ncu), dim3(threads), 0, 0, seed, iters, out, stamps);
         };
         launch();
         CK(hipEventRecord(e0));
@@ -230,8 +248,18 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double k = kind == 0 ? 64 : 32;
         const double ops = 2.0 * 32 * 32 * k * 8.0 * iters * (threads / 64) * ncu;
-        printf("rate %s, %d waves/CU: %.1f ms, %.0f TOPS\n", kind == 0 ? "fp6 scaled 32x32x64" : "i8 32x32x32",
-               threads / 64, ms, ops / ms * 1e-9);
+        const int nw = ncu * threads / 64;
+        CK(hipMemcpy(hst.data(), stamps, (size_t)nw * 16, hipMemcpyDeviceToHost));
+        std::vector<double> cyc, clk;
+        for (int w = 0; w < nw; ++w) {
+          cyc.push_back((double)hst[2 * w] / (8.0 * iters));
+          clk.push_back((double)hst[2 * w] / (double)hst[2 * w + 1] * 0.1);
+        }
+        std::sort(cyc.begin(), cyc.end());
+        std::sort(clk.begin(), clk.end());
+        printf("rate %s, %d waves/CU: %.1f ms, %.0f TOPS; per wave %.1f cycles per MFMA (median), clock %.2f GHz\n",
+               kind == 0 ? "fp6 scaled 32x32x64" : "i8 32x32x32", threads / 64, ms, ops / ms * 1e-9, cyc[nw / 2],
+               clk[nw / 2]);
       }
     }
   return 0;
