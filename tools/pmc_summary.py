@@ -1,4 +1,4 @@
-"""Summarise the rocprofv3 passes of tools/prof_q8.sh (gpurun_out/prof) into profiles/.
+"""Summarise the rocprofv3 passes of tools/prof_search.sh (gpurun_out/prof) into profiles/.
 
     python tools/pmc_summary.py <name> [kernel-substring]
 
@@ -32,7 +32,7 @@ def counters(kname):
 
 def main():
     name = sys.argv[1]
-    kname = sys.argv[2] if len(sys.argv) > 2 else "tile_kernel<1, 0>"
+    kname = sys.argv[2] if len(sys.argv) > 2 else "tile_kernel_f6<0>"
     stats = os.path.join(P, "kt", "kt_kernel_stats.csv")
     shutil.copy(stats, os.path.join(ROOT, "profiles", f"{name}_kernel_stats.csv"))
     avg_ns = None
@@ -45,7 +45,8 @@ def main():
     cfg = bench["config"]
     out = {
         "config": {"gallery": cfg["gallery"], "batch": cfg["global_batch"], "d": cfg["d"], "D": cfg["D"],
-                   "k": cfg["k"], "search": "q8" if "i8" in bench["dtype"] else "fp32"},
+                   "k": cfg["k"],
+                   "search": "f6" if "fp6" in bench["dtype"] else ("q8" if "i8" in bench["dtype"] else "fp32")},
         "kernel": kname, "launches": n, "rocprof_avg_ns": avg_ns,
         "counters_per_launch": c,
         "correction": "gfx950: FETCH_SIZE reports half of the bytes of wide coalesced streaming reads "
