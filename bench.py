@@ -13,9 +13,11 @@ checkpoint exists at this scale), gallery/queries are synthetic (see
 opencv_facerecognizer_amd/synthetic.py).
 
 Multi-GPU (torch.distributed.run, one process per GPU): the 1M gallery is
-sharded by rows over the ranks, the query batch is replicated, and the per-rank
-top-k lists are merged after one RCCL all-gather -> strong scaling (total work
-fixed).
+sharded by rows over the ranks; each rank projects and quantizes B/G of the
+query faces and the centred fp32 rows + fp6 panels are all-gathered (RCCL), every
+rank searches its shard for the whole batch, and the per-rank top-k lists are
+merged after one RCCL all-gather -> strong scaling (total work fixed).
+OFR_DIST_BACKEND=gloo OFR_ONE_DEVICE=1 rehearse the multi-rank path on one GPU.
 """
 from __future__ import annotations
 
@@ -34,7 +36,8 @@ sys.path.insert(0, ROOT)
 
 from opencv_facerecognizer_amd import _lib  # noqa: E402
 from opencv_facerecognizer_amd._device import FloatGallery, Projection, col_mean_u8, round_up  # noqa: E402
-from opencv_facerecognizer_amd.parallel import exchange_topk, merge_topk, shard_range  # noqa: E402
+from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, merge_topk,  # noqa: E402
+                                                shard_range)
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 
 PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
@@ -138,11 +141,15 @@ def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = 0 if os.environ.get("OFR_ONE_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("OFR_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     _lib.device()
 
     H = W = args.side
@@ -159,17 +166,17 @@ def main():
     ld = max(32, round_up(d, 32))
     G = torch.zeros((nl, ld), dtype=torch.float32, device=device)
     chunk = 8192
-    centre = None
+    # centring vector c = W^T round(mean image of the gallery's first chunk), exact fp64, the same on
+    # every rank (the query rows are centred once and shared): rows are stored as fp32(W^T x - c),
+    # rounded after centring (FloatGallery docstring)
+    rows = torch.arange(0, min(N, chunk), device=device)
+    m = col_mean_u8(bank.images(rows // args.per_id, seed=SEED + 1000), D)
+    m_img = torch.clamp(torch.round(m), 0, 255).to(torch.uint8).reshape(1, -1).contiguous()
+    centre = P.project(m_img, f64=True)[0].contiguous()
     for c0 in range(0, nl, chunk):
         c1 = min(nl, c0 + chunk)
         rows = torch.arange(n0 + c0, n0 + c1, device=device)
         imgs = bank.images(rows // args.per_id, seed=SEED + 1000 + (n0 + c0) // chunk)
-        if centre is None:
-            # centring vector c = W^T round(mean image of the first chunk), exact fp64: rows are stored as
-            # fp32(W^T x - c), rounded after centring (FloatGallery docstring)
-            m = col_mean_u8(imgs, D)
-            m_img = torch.clamp(torch.round(m), 0, 255).to(torch.uint8).reshape(1, -1).contiguous()
-            centre = P.project(m_img, f64=True)[0].contiguous()
         P.project(imgs, shift64=centre, out=G[c0:c1])
     gallery = FloatGallery.from_device_rows(G, d, _lib.METRIC_EUCLIDEAN, shift64=centre)
     gq = torch.Generator(device=device)
@@ -189,14 +196,28 @@ def main():
             gallery._tier_gallery(t)                              # quantized gallery tiers (once, untimed)
     qq = None
     fallbacks = []
+    last_counts = []
+    # sharded query preparation: rank r projects / quantizes faces [b0, b1) and the rows are
+    # all-gathered (fp6 panels need whole 256-row blocks per rank)
+    b0, b1 = shard_range(B, rank, world)
+    shard_prep = world > 1 and B % world == 0 and (tier0 != "f6" or (B // world) % 256 == 0)
+    Qd_loc = torch.zeros((b1 - b0, ld), dtype=torch.float32, device=device) if shard_prep else None
+    qq_loc = None
 
     def step(events=None):
-        nonlocal qq
+        nonlocal qq, qq_loc, Qd
         if events:
             events[0].record()
-        P.project(Xq, shift64=gallery.shift64, out=Qd)            # fp32(W^T x - c), exact int8 MFMA
-        if use_q8:
-            qq = gallery.quantize_queries(Qd, qq, tier=tier0)
+        if shard_prep:
+            P.project(Xq[b0:b1], shift64=gallery.shift64, out=Qd_loc)   # this rank's faces
+            if use_q8:
+                qq_loc = gallery.quantize_queries(Qd_loc, qq_loc, tier=tier0)
+                qq = gallery.gather_queries(qq_loc)
+            Qd = gather_rows(Qd_loc)                                    # RCCL all-gather
+        else:
+            P.project(Xq, shift64=gallery.shift64, out=Qd)              # fp32(W^T x - c), exact int8 MFMA
+            if use_q8:
+                qq = gallery.quantize_queries(Qd, qq, tier=tier0)
         if events:
             events[1].record()
         if use_q8:
@@ -207,7 +228,15 @@ def main():
             events[2].record()
         if use_q8:
             gallery.search_q8_phase(2, Qd, qq, k, index_base=n0, out=out)
+            if world > 1:      # global certificate: all-gather + merge + collective fallback
+                res, counts = certify_sharded(gallery, Qd, qq, k, out, n0)
+                fallbacks.append(counts[0])
+                last_counts[:] = counts
+                if events:
+                    events[3].record()
+                return res
             fallbacks.append(gallery.fallback(Qd, qq, k, out, index_base=n0))
+            last_counts[:] = list(gallery.last_fallbacks)
         else:
             gallery.search_phase("merge", Qd, k, index_base=n0, out=out)
         if events:
@@ -302,7 +331,10 @@ def main():
             "config": {"workload": "configs[2]: Fisherfaces projection + 1-NN, 1M-image gallery (100k ids x 10), "
                                    "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1",
                        "gallery": N, "global_batch": B, "d": d, "D": D, "k": k,
-                       "parallelism": f"gallery-rows/{world} + RCCL all-gather of top-k" if world > 1 else "1 GPU"},
+                       "parallelism": (f"gallery-rows/{world}, query prep sharded + RCCL all-gather of rows, RCCL all-gather of "
+                                       f"top-k + bounds (global certificate)" if shard_prep else
+                                       f"gallery-rows/{world} + RCCL all-gather of top-k")
+                       if world > 1 else "1 GPU"},
             "roofline": {"kernel": kname, "bound": "mfma",
                          "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s" if not use_q8 else "TOPS",
                          "frac": achieved / peak, "traffic": tr[0] if tr else None,
@@ -310,10 +342,11 @@ def main():
                          "traffic_source": tr[1] if tr else None,
                          "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
                          "launch_ms": ms_tiles},
-            "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else ""): ms_proj, "knn_tiles": ms_tiles,
+            "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else "") + ("+all_gather" if shard_prep else ""):
+                           ms_proj, "knn_tiles": ms_tiles,
                            "knn_merge_rerank" + ("+certificate+fallback" if use_q8 else ""): ms_merge},
             "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
-            "uncertified_after_each_tier": (list(gallery.last_fallbacks) if use_q8 else None),
+            "uncertified_after_each_tier": (list(last_counts) if use_q8 else None),
             "top1_identity_acc": acc,
             "small_batch": small,
         }

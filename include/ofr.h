@@ -140,14 +140,18 @@ int ofr_q8_quantize_rows(void* stream, int slices, const float* X, int64_t R, in
  * fp64 distance (distance.py:60) and writes cert[q] = 1 iff the rigorous bound
  * |S - S~| <= dS(q) proves that no other row can reach the k-th neighbour
  * (DESIGN.md §3).  Queries with cert[q] == 0 must be re-run with more slices
- * or on ofr_knn_f32.  Q/G: the fp32 rows the slices were made from (centred),
+ * or on ofr_knn_f32.  bound (nullable, [B]): a lower bound of the squared
+ * distance of every row outside the candidates (+inf if all rows were
+ * candidates); cert[q] = (d_k^2 < bound[q]).  A gallery sharded over ranks
+ * certifies the GLOBAL top-k when its k-th squared distance is below every
+ * rank's bound (opencv_facerecognizer_amd/parallel.py).  Q/G: the fp32 rows the slices were made from (centred),
  * for the re-rank.  phases: 1 = tiles, 2 = merge, 3 = both.  k <= 16.        */
 size_t ofr_knn_q8_workspace_bytes(int64_t B, int64_t N);
 int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, int64_t ldq, const int8_t* Qs,
                const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                const int8_t* Gs, int64_t ld, const float* gscale, const float* aux, const double* gmax,
-               int k, int64_t index_base, double* out_d, int64_t* out_i, int* cert, void* workspace,
-               size_t workspace_bytes);
+               int k, int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
+               void* workspace, size_t workspace_bytes);
 
 /* fp6 first tier of the certified search (same contract as ofr_knn_q8) -----
  * Rows are cut into e2m3 fp6 values with a per-row fp32 scale s = max|x|/7.5
@@ -166,8 +170,8 @@ int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int
 int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
-               int64_t index_base, double* out_d, int64_t* out_i, int* cert, void* workspace,
-               size_t workspace_bytes);
+               int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
+               void* workspace, size_t workspace_bytes);
 
 /* Merge P sorted (distance, index) lists per query into the best k:
  * in_d/in_i [B][P*kin] (list p at columns [p*kin, (p+1)*kin)), ascending by

@@ -259,7 +259,8 @@ class FloatGallery:
                 Qs = torch.empty((B, self._q8_ld(self.d, tier)), dtype=torch.int8, device=dev_)
             out = dict(Qs=Qs, scale=torch.empty(B, dtype=torch.float32, device=dev_),
                        stats=torch.empty((B, 3), dtype=torch.float64, device=dev_),
-                       cert=torch.empty(B, dtype=torch.int32, device=dev_), tier=tier, B=B)
+                       cert=torch.empty(B, dtype=torch.int32, device=dev_),
+                       bound=torch.empty(B, dtype=torch.float64, device=dev_), tier=tier, B=B)
         if tier == "f6":
             call("ofr_f6_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
                  out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None)
@@ -267,6 +268,19 @@ class FloatGallery:
             call("ofr_q8_quantize_rows", stream(), tier, ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
                  out["Qs"].shape[1], ptr(out["scale"]), ptr(out["stats"]), None, None)
         return out
+
+    def gather_queries(self, qq, group=None):
+        """Quantized query rows of this rank's block of the batch -> the whole batch (all-gather over
+        the ranks, rank-major).  The fp6 tiles concatenate only whole 256-row panels: every rank's
+        block must be a multiple of 256 rows (int8 tiers: any equal split)."""
+        from .parallel import gather_rows
+        if qq["tier"] == "f6" and qq["B"] % 256:
+            raise ValueError("fp6 query tiles gather whole 256-row panels: rows per rank must be a multiple of 256")
+        scale = gather_rows(qq["scale"], group)
+        B = scale.shape[0]
+        return dict(Qs=gather_rows(qq["Qs"], group), scale=scale, stats=gather_rows(qq["stats"], group),
+                    cert=torch.empty(B, dtype=torch.int32, device=scale.device),
+                    bound=torch.empty(B, dtype=torch.float64, device=scale.device), tier=qq["tier"], B=B)
 
     def search_q8_phase(self, phases, Qd, qq, k, index_base=0, out=None):
         """phases 1 = quantized tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"]), 3 = both."""
@@ -281,12 +295,12 @@ class FloatGallery:
             call("ofr_knn_f6", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
                  ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),
                  ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
-                 ptr(ws), ws.numel())
+                 ptr(qq["bound"]), ptr(ws), ws.numel())
         else:
             call("ofr_knn_q8", stream(), phases, tier, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
                  ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), g["ld"],
                  ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]),
-                 ptr(qq["cert"]), ptr(ws), ws.numel())
+                 ptr(qq["cert"]), ptr(qq["bound"]), ptr(ws), ws.numel())
         return out
 
     def fallback(self, Qd, qq, k, out, index_base=0):

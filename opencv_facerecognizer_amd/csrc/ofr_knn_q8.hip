@@ -248,6 +248,7 @@ struct MergeArgs {
   double* out_d;
   int64_t* out_i;
   int* cert;
+  double* bound;   // optional: squared-distance lower bound of every row outside the candidates
 };
 
 // One block per query.  (1) best KC of the T tile lists, read as one contiguous stream
@@ -332,25 +333,26 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     double* od = p.out_d + q * p.k;
     int64_t* oi = p.out_i + q * p.k;
     sort_and_write<KC>(lists, exact, p.k, p.index_base, od, oi);
-    // certificate
+    // certificate.  Every row outside the KC candidates has coarse score >= tau, hence exact
+    // score S = d^2 - |q|^2 >= tau - dS, i.e. d^2 >= bound = tau - dS + |q|^2 (less a relative
+    // 1e-12 for the fp64 evaluation); the local top-k is exact iff d_k^2 < bound.  A sharded
+    // search compares the GLOBAL k-th with every rank's bound instead (parallel.py).
     int nvalid = 0;
     for (int c = 0; c < KC; ++c) nvalid += lists[c].i != CAND_EMPTY;
-    int ok;
-    if (nvalid < KC) {
-      ok = 1;   // every gallery row was a candidate
-    } else {
+    double bnd = __builtin_inf();   // every gallery row was a candidate
+    if (nvalid == KC) {
       const double tau = (double)lists[KC - 1].d;
       const double a = p.qstats[q * 3 + 0], e = p.qstats[q * 3 + 1], tq = p.qstats[q * 3 + 2];
       const double A = p.gmax[0], E = p.gmax[1], T = p.gmax[2], auxmax = p.gmax[3];
       double dS = 2.0 * (a * E + e * A + e * E + tq * T) + 0x1p-20 * (auxmax + 2.0 * a * A) +
                   2.0 * p.gamma * a * A;
       dS = dS * (1.0 + 1e-6) + 1e-300;
-      const int kk = p.k < KC ? p.k : KC;
-      const double dk = od[kk - 1];
-      const double Sk = dk * dk - qq;
-      ok = (dk == dk) && (Sk + 1e-12 * (dk * dk + qq) < tau - dS);
+      bnd = (tau - dS + qq) - 1e-12 * (fabs(tau) + dS + 2.0 * qq);
     }
-    p.cert[q] = ok;
+    const int kk = p.k < KC ? p.k : KC;
+    const double dk = od[kk - 1];
+    p.cert[q] = (dk == dk) && (dk * dk < bnd);
+    if (p.bound) p.bound[q] = bnd;
   }
 }
 
@@ -604,7 +606,7 @@ extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, 
                           const int8_t* Qs, const float* qscale, const double* qstats, const float* G, int64_t N,
                           int64_t ldg, int64_t d, const int8_t* Gs, int64_t ld, const float* gscale,
                           const float* aux, const double* gmax, int k, int64_t index_base, double* out_d,
-                          int64_t* out_i, int* cert, void* workspace, size_t workspace_bytes) {
+                          int64_t* out_i, int* cert, double* bound, void* workspace, size_t workspace_bytes) {
   OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_q8: phases must be 1 (tiles), 2 (merge) or 3");
   OFR_CHECK_ARG(slices == 1 || slices == 2, "ofr_knn_q8: slices must be 1 or 2");
   OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_q8: bad sizes (empty galleries use ofr_knn_f32)");
@@ -633,7 +635,7 @@ extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, 
   }
   if (phases & 2) {
     OFR_CHECK_ARG(out_d && out_i && cert, "ofr_knn_q8: null output");
-    q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, 0.0, k, index_base, out_d, out_i, cert};
+    q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, 0.0, k, index_base, out_d, out_i, cert, bound};
     hipLaunchKernelGGL(q8s::merge_kernel, dim3((unsigned)B), dim3(256), 0, st, m);
     OFR_LAUNCH_CHECK("q8 merge_kernel");
   }
@@ -674,8 +676,8 @@ extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int
 extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                           const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
                           int64_t d, const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
-                          int64_t index_base, double* out_d, int64_t* out_i, int* cert, void* workspace,
-                          size_t workspace_bytes) {
+                          int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
+                          void* workspace, size_t workspace_bytes) {
   OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_f6: phases must be 1 (tiles), 2 (merge) or 3");
   OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_f6: bad sizes (empty galleries use ofr_knn_f32)");
   if (k < 1 || k > q8s::KC) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6: k must be in [1, 16]");
@@ -712,7 +714,7 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
     // fp32 accumulation over nst * 2 MFMAs: |err| <= (n + 64) 2^-23 sum|q~ g~| / (s_q s_g),
     // sum|q~ g~| <= a_q a_g <= a_q A (tools/mx_probe.hip measures <= 3 * 2^-24 at n = 160)
     const double gamma = (double)(2 * a.nk + 64) * 0x1p-23;
-    q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, gamma, k, index_base, out_d, out_i, cert};
+    q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, gamma, k, index_base, out_d, out_i, cert, bound};
     hipLaunchKernelGGL(q8s::merge_kernel, dim3((unsigned)B), dim3(256), 0, st, m);
     OFR_LAUNCH_CHECK("f6 merge_kernel");
   }

@@ -7,6 +7,10 @@ top-k (exact fp64 distances, global row indices via ``index_base``), and the
 only data-path exchange is ONE all-gather of the B x k (distance, index)
 lists (torch.distributed; backend "nccl" = RCCL over xGMI on MI355X, "gloo"
 on CPU for tests), followed by the ``ofr_topk_merge`` kernel.
+
+Query preparation can be sharded too (``gather_rows``): each rank projects and
+quantizes B/G of the faces and the rows are all-gathered, so at G GPUs the
+projection costs 1/G instead of being replicated.
 """
 from __future__ import annotations
 
@@ -14,15 +18,30 @@ import torch
 import torch.distributed as dist
 
 
-def world():
+def world(group=None):
     if dist.is_available() and dist.is_initialized():
-        return dist.get_rank(), dist.get_world_size()
+        return dist.get_rank(group), dist.get_world_size(group)
     return 0, 1
 
 
 def shard_range(N, rank, world_size):
     """Contiguous, disjoint, covering row ranges."""
     return (N * rank) // world_size, (N * (rank + 1)) // world_size
+
+
+def gather_rows(x, group=None):
+    """All-gather equal-size row blocks (dim 0) of every rank, rank-major: [G * rows, ...]."""
+    _, ws = world()
+    if ws == 1:
+        return x
+    x = x.contiguous()
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((ws * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x, group=group)
+        return out
+    parts = [torch.empty_like(x) for _ in range(ws)]
+    dist.all_gather(parts, x, group=group)
+    return torch.cat(parts, 0)
 
 
 def exchange_topk(d, i, group=None):
@@ -51,3 +70,53 @@ def sharded_search(local_search, k, group=None):
     _, ws = world()
     gd, gi = exchange_topk(d, i, group)
     return merge_topk(gd, gi, ws, k, k)
+
+
+def certify_sharded(gallery, Qd, qq, k, out, index_base, group=None):
+    """Global certificate + collective fallback of the certified tiers on a sharded gallery.
+
+    ``out`` is this rank's local top-k (exact fp64 distances, global row indices) of the whole
+    batch from the tier of ``qq``; the merge kernel left in ``qq["bound"]`` a lower bound of the
+    squared distance of every local row outside its candidates.  After the all-gather + merge,
+    query q is certified iff its GLOBAL k-th squared distance is below every rank's bound: a row
+    that is not among its rank's candidates is then farther than the global k-th, and one that is
+    a candidate but not in its rank's top-k has k better rows on that rank, so the merged list is
+    the exact global top-k.  (A per-rank certificate would fail for every query whose identity
+    lives on another rank: its local neighbours are not separated from its 16th candidate.)
+    Uncertified queries -- the same set on every rank, it is computed from gathered data -- go
+    down the tier chain on every rank, each stage with its own exchange; the fp32 stage is exact.
+    Returns ((d, i) global top-k, [uncertified after each quantized tier]).
+    """
+    _, ws = world(group)
+
+    def merged(d, i, bound):
+        gd, gi = exchange_topk(d, i, group)
+        md, mi = merge_topk(gd, gi, ws, k, k)
+        if bound is None:
+            return md, mi, None
+        minb = gather_rows(bound.reshape(1, -1), group).min(0).values
+        kth = md[:, k - 1]
+        return md, mi, (kth * kth < minb) | torch.isinf(minb)
+
+    md, mi, cert = merged(out[0], out[1], qq["bound"])
+    chain = list(gallery.TIER_CHAIN[gallery.TIER_CHAIN.index(qq["tier"]) + 1:])
+    rows = torch.nonzero(~cert).reshape(-1)
+    counts = [int(rows.numel())]
+    while rows.numel():
+        tier = chain.pop(0)
+        sub = Qd.index_select(0, rows).contiguous()
+        if tier == "fp32":
+            d2, i2 = gallery._search_f32(sub, k, index_base)
+            md2, mi2, _ = merged(d2, i2, None)
+        else:
+            q2 = gallery.quantize_queries(sub, tier=tier)
+            d2, i2 = gallery.search_q8_phase(3, sub, q2, k, index_base)
+            md2, mi2, c2 = merged(d2, i2, q2["bound"])
+        md.index_copy_(0, rows, md2)
+        mi.index_copy_(0, rows, mi2)
+        if tier == "fp32":
+            break
+        still = torch.nonzero(~c2).reshape(-1)
+        counts.append(int(still.numel()))
+        rows = rows.index_select(0, still)
+    return (md, mi), counts

@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import facerec_oracle as O
-from opencv_facerecognizer_amd.parallel import exchange_topk, shard_range, world
+from opencv_facerecognizer_amd.parallel import exchange_topk, gather_rows, shard_range, world
 
 
 def _free_port():
@@ -76,3 +76,108 @@ def test_two_rank_exchange_reproduces_global_topk(k):
         o = np.lexsort((gi[b], gd[b]))[:k]          # merge by (distance, index)
         assert np.array_equal(gi[b][o], ref_i[b]), b
         assert np.array_equal(gd[b][o], ref_d[b]), b
+
+
+def _gather_worker(rank, ws, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        x = torch.arange(6 * 5, dtype=torch.float32).reshape(6, 5) + 1000 * rank   # this rank's row block
+        g = gather_rows(x)
+        if rank == 0:
+            out.put(g.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_rows_rank_major():
+    """Sharded query preparation: every rank's row block, concatenated in rank order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    g = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    base = np.arange(30, dtype=np.float32).reshape(6, 5)
+    assert np.array_equal(g, np.concatenate([base, base + 1000]))
+
+
+class _MockShardGallery:
+    """CPU stand-in for FloatGallery on one shard: every tier returns the exact local top-k (global
+    indices) and, as its certificate bound, the squared distance of the 16th local candidate shrunk
+    by a tier-dependent slack -- a valid lower bound for every row outside the candidates, loose
+    at the first tier so that the collective fallback chain runs."""
+    TIER_CHAIN = ("f6", 1, 2, "fp32")
+    SLACK = {"f6": 0.5, 1: 0.97, 2: 0.999}
+
+    def __init__(self, G, n0):
+        self.G, self.n0 = G, n0
+
+    def _local(self, Q, k):
+        d, i = O.nn_search_vectorized("EuclideanDistance", Q, self.G, min(16, len(self.G)))
+        return d, i + self.n0
+
+    def quantize_queries(self, sub, tier):
+        return {"tier": tier, "Q": sub.numpy()}
+
+    def search_q8_phase(self, phases, sub, q2, k, index_base):
+        d, i = self._local(q2["Q"], k)
+        b = d[:, -1] ** 2 * self.SLACK[q2["tier"]] if d.shape[1] == 16 else np.full(len(d), np.inf)
+        q2["bound"] = torch.from_numpy(b)
+        return torch.from_numpy(d[:, :k].copy()), torch.from_numpy(i[:, :k].copy())
+
+    def _search_f32(self, sub, k, index_base):
+        d, i = self._local(sub.numpy(), k)
+        return torch.from_numpy(d[:, :k].copy()), torch.from_numpy(i[:, :k].copy())
+
+
+def _cert_worker(rank, ws, port, k, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        import opencv_facerecognizer_amd.parallel as par
+        par.merge_topk = _host_merge                      # the device merge kernel needs a GPU
+        Q, G = _data()
+        n0, n1 = shard_range(len(G), rank, ws)
+        g = _MockShardGallery(G[n0:n1], n0)
+        Qt = torch.from_numpy(Q)
+        qq = g.quantize_queries(Qt, "f6")
+        d, i = g.search_q8_phase(3, Qt, qq, k, n0)
+        (md, mi), counts = par.certify_sharded(g, Qt, qq, k, (d, i), n0)
+        if rank == 0:
+            out.put((md.numpy(), mi.numpy(), counts))
+    finally:
+        dist.destroy_process_group()
+
+
+def _host_merge(gd, gi, nlists, kin, k):
+    d, i = gd.numpy(), gi.numpy()
+    od, oi = np.empty((len(d), k)), np.empty((len(d), k), np.int64)
+    for b in range(len(d)):
+        o = np.lexsort((i[b], d[b]))[:k]
+        od[b], oi[b] = d[b][o], i[b][o]
+    return torch.from_numpy(od), torch.from_numpy(oi)
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_sharded_global_certificate_and_collective_fallback(k):
+    """parallel.certify_sharded on 2 ranks: the merged result is the exact global top-k whatever tier
+    certifies each query, and both ranks run the same collectives down the chain (no deadlock)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cert_worker, args=(r, 2, port, k, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    md, mi, counts = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    Q, G = _data()
+    ref_d, ref_i = O.nn_search_vectorized("EuclideanDistance", Q, G, k)
+    assert np.array_equal(mi, ref_i) and np.allclose(md, ref_d, rtol=0, atol=0)
+    assert counts[0] > 0 and len(counts) >= 2            # the loose first-tier bound forced fallbacks
