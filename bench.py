@@ -274,30 +274,50 @@ def main():
     # ---- small-batch regime (the recognizers send one face per call): HBM-bound streaming of the gallery ----
     small = []
     for bs in [int(x) for x in args.small_batches.split(",") if x.strip()]:
+        # HBM regime (the recognizers send one face per call): the fp6 streaming pass for B <= 32
         Qs = torch.zeros((bs, ld), dtype=torch.float32, device=device)
         P.project(Xq[:bs], shift64=gallery.shift64, out=Qs)
+        f6_small = args.search == "f6" and gallery.use_q8(bs, k)
+        qs = gallery.quantize_queries(Qs, tier="f6") if f6_small else None
+
+        def small_pass():
+            if f6_small:
+                gallery.search_q8_phase(1, Qs, qs, k)
+            else:
+                gallery.search_phase("tiles", Qs, k)
+
         for _ in range(2):
-            gallery.search_phase("tiles", Qs, k)
+            small_pass()
         reps = 10
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record()
         for _ in range(reps):
-            gallery.search_phase("tiles", Qs, k)
+            small_pass()
         e1.record()
         torch.cuda.synchronize()
         ms_t = e0.elapsed_time(e1) / reps
         t1 = time.perf_counter()
-        for _ in range(reps):
+        for _ in range(reps):                 # the whole small-batch step: project, search, merge, certificate
             P.project(Xq[:bs], shift64=gallery.shift64, out=Qs)
-            gallery.search_phase("tiles", Qs, k)
-            gallery.search_phase("merge", Qs, k, index_base=n0)
+            if f6_small:
+                qs = gallery.quantize_queries(Qs, qs, tier="f6")
+                o = gallery.search_q8_phase(3, Qs, qs, k, index_base=n0)
+                gallery.fallback(Qs, qs, k, o, index_base=n0)
+            else:
+                gallery.search_phase("tiles", Qs, k)
+                gallery.search_phase("merge", Qs, k, index_base=n0)
         torch.cuda.synchronize()
         ms_step = (time.perf_counter() - t1) * 1e3 / reps
-        bytes_t = nl * d * 4 + bs * d * 4                            # gallery streamed once per batch
+        if f6_small:
+            kern = "q8s::stream_kernel_f6 (ofr_knn_f6 phase 1, B<=32)"
+            bytes_t = 0.75 * (nl * d + bs * d)                       # fp6 tiles streamed once per batch
+        else:
+            kern = "knn_tile_kernel<Cfg<32,4,1,4>> (ofr_knn_tiles_f32, B<=32)"
+            bytes_t = nl * d * 4 + bs * d * 4                        # fp32 rows streamed once per batch
         small.append({"batch": bs, "queries_per_s": bs / (ms_step * 1e-3), "ms_per_batch": ms_step,
-                      "roofline": {"kernel": "knn_tile_kernel<Cfg<32,4,1,4>> (ofr_knn_tiles_f32, B<=32)",
-                                   "bound": "hbm", "achieved": bytes_t / (ms_t * 1e-3) / 1e9,
+                      "uncertified": (list(gallery.last_fallbacks) if f6_small else None),
+                      "roofline": {"kernel": kern, "bound": "hbm", "achieved": bytes_t / (ms_t * 1e-3) / 1e9,
                                    "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                    "frac": bytes_t / (ms_t * 1e-3) / PEAK_HBM, "launch_ms": ms_t,
                                    "algorithmic_bytes_per_launch": bytes_t}})

@@ -20,7 +20,7 @@ from . import _lib
 from ._lib import call, ptr, stream
 
 
-SMALL_BATCH = 32   # B <= 32: HBM-streaming fp32 tiles; larger batches: certified fp6/int8 tiles (Euclidean)
+SMALL_BATCH = 32   # B <= 32: HBM-streaming passes (fp6 first tier, fp32); larger batches: fp6/int8 tiles
 # the int8 pass keeps 16 candidates per query; a certificate needs slack between the k-th
 # exact distance and the 16th coarse score, so k is limited to half of that
 Q8_MAX_K = 8
@@ -211,8 +211,15 @@ class FloatGallery:
 
     def use_q8(self, B, k):
         mode = os.environ.get("OFR_SEARCH", "auto")
-        return (mode != "fp32" and self.metric == _lib.METRIC_EUCLIDEAN and self.N > 0
-                and B > SMALL_BATCH and k <= Q8_MAX_K)
+        return (mode != "fp32" and self.metric == _lib.METRIC_EUCLIDEAN and self.N > 0 and B > 0
+                and k <= Q8_MAX_K)
+
+    def next_tier(self, tier, nrows):
+        """Stage after `tier` for `nrows` uncertified queries.  The int8 tiers run 256-query tiles
+        over 10-30 GB of slices: for <= 32 queries the exact fp32 streaming pass is as cheap, so
+        small sets go straight to it (and a small-batch workload never builds the int8 slices)."""
+        nxt = self.TIER_CHAIN[self.TIER_CHAIN.index(tier) + 1]
+        return "fp32" if nxt != "fp32" and nrows <= SMALL_BATCH else nxt
 
     @staticmethod
     def first_tier():
@@ -307,12 +314,12 @@ class FloatGallery:
         """Re-run the queries the first tier left uncertified down the tier chain (then fp32).
         Returns the number of first-tier failures (host sync); self.last_fallbacks = the number of
         uncertified queries after each quantized tier that ran."""
-        chain = list(self.TIER_CHAIN[self.TIER_CHAIN.index(qq["tier"]) + 1:])
         bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
         counts = [int(bad.numel())]
         rows = bad                      # indices into the original batch still unresolved
+        tier = qq["tier"]
         while rows.numel():
-            tier = chain.pop(0)
+            tier = self.next_tier(tier, int(rows.numel()))
             sub = Qd.index_select(0, rows).contiguous()
             if tier == "fp32":
                 d2, i2 = self._search_f32(sub, k, index_base)

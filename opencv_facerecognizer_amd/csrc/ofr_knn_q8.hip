@@ -231,6 +231,93 @@ __global__ void __launch_bounds__(f6t::NT, 1) tile_kernel_f6(TileArgs p) {
   });
 }
 
+// ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
+// One workgroup per 256-row gallery panel, wave w owns rows 32w..32w+31 against the (single)
+// 32-row query block, loading its fragments straight to VGPRs from the f6 tiled layout (each
+// gallery byte is used once: no LDS staging; the 243 KB of query fragments stay in L2).
+// SU steps of loads are in flight per wave and 16 waves per CU, so the pass streams HBM.
+// Epilogue: the 32 x 32 scores of each wave -> per-query best 16 (keys, as tile_epilogue),
+// merged over the 8 waves through LDS -> the panel's best 16 rows per query.
+constexpr int SU = 4;
+
+__device__ __forceinline__ f6t::i32x8 stream_frag(const char* stage, int j, int h, int row) {
+  const char* sb = stage + (2 * j + h) * 6144;
+  const f6t::i32x4 p0 = *reinterpret_cast<const f6t::i32x4*>(sb + row * 16);
+  const f6t::i32x2 p1 = *reinterpret_cast<const f6t::i32x2*>(sb + 4096 + row * 8);
+  f6t::i32x8 f;
+  f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3];
+  f[4] = p1[0]; f[5] = p1[1]; f[6] = 0; f[7] = 0;
+  return f;
+}
+
+__global__ void __launch_bounds__(512, 2) stream_kernel_f6(TileArgs p) {
+  __shared__ uint32_t kbuf[8][32][KC];
+  __shared__ float gtab[TG][2];
+  const int64_t gt = blockIdx.x, g0 = gt * TG;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r32 = lane & 31;
+  if (threadIdx.x < TG) {
+    const int64_t g = g0 + threadIdx.x;
+    const bool ok = g < p.N;
+    gtab[threadIdx.x][0] = ok ? p.aux[g] : 0.f;
+    gtab[threadIdx.x][1] = ok ? p.gscale[g] : 0.f;
+  }
+  const char* gpan = reinterpret_cast<const char*>(p.G) + gt * (int64_t)p.nk * f6t::PANEL;
+  const char* qpan = reinterpret_cast<const char*>(p.Q);
+  const int nsteps = 2 * p.nk, grow = wave * 32 + r32;
+  f6t::f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int k0 = 0; k0 < nsteps; k0 += SU) {
+    f6t::i32x8 a[SU], b[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int k = k0 + u < nsteps ? k0 + u : nsteps - 1;
+      a[u] = stream_frag(gpan + (k >> 1) * (int64_t)f6t::PANEL, k & 1, h, grow);
+      b[u] = stream_frag(qpan + (k >> 1) * (int64_t)f6t::PANEL, k & 1, h, r32);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u)
+      if (k0 + u < nsteps)
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[u], b[u], acc, 2, 2, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+  }
+  __syncthreads();
+  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
+  const float sq2 = 2.0f * p.qscale[r32 < p.B ? r32 : p.B - 1];
+  KeyList L;
+  L.init();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int gl = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const float sc = gtab[gl][0] - sq2 * gtab[gl][1] * acc[r];
+    L.insert(gl < nvalid ? score_key(sc, gl) : KEY_NONE);
+  }
+  uint32_t o[KC];
+#pragma unroll
+  for (int j = 0; j < KC; ++j) o[j] = (uint32_t)__shfl_xor((int)L.k[j], 32);
+  L.merge(o);
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) kbuf[wave][r32][j] = L.k[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < 32 && (int64_t)threadIdx.x < p.B) {
+    const int q = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < KC; ++j) L.k[j] = kbuf[0][q][j];
+    for (int w = 1; w < 8; ++w) {
+#pragma unroll
+      for (int j = 0; j < KC; ++j) o[j] = kbuf[w][q][j];
+      L.merge(o);
+    }
+    Cand* out = p.cand + ((size_t)q * p.ntg + gt) * KC;
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const uint32_t kk = L.k[j];
+      out[j] = kk == KEY_NONE ? Cand{__builtin_inff(), CAND_EMPTY} : Cand{key_score(kk), (int)(g0 + (kk & 0xffu))};
+    }
+  }
+}
+
 // ---- pass 2 ----------------------------------------------------------------------------
 
 struct MergeArgs {
@@ -699,15 +786,21 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
   a.gg = a.ntg < q8s::GROUP_G ? a.ntg : q8s::GROUP_G;
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
   if (phases & 1) {
-    static bool attr_done = false;
-    if (!attr_done) {
-      hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel_f6<0>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
-      if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
-      attr_done = true;
+    if (B <= 32) {   // HBM regime: one 32-query block, gallery streamed straight to VGPRs
+      hipLaunchKernelGGL(q8s::stream_kernel_f6, dim3((unsigned)a.ntg), dim3(512), 0, st, a);
+      OFR_LAUNCH_CHECK("f6 stream_kernel");
+    } else {
+      static bool attr_done = false;
+      if (!attr_done) {
+        hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel_f6<0>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
+        if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
+        attr_done = true;
+      }
+      hipLaunchKernelGGL((q8s::tile_kernel_f6<0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::NT), f6t::LDS, st,
+                         a);
+      OFR_LAUNCH_CHECK("f6 tile_kernel");
     }
-    hipLaunchKernelGGL((q8s::tile_kernel_f6<0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::NT), f6t::LDS, st, a);
-    OFR_LAUNCH_CHECK("f6 tile_kernel");
   }
   if (phases & 2) {
     OFR_CHECK_ARG(out_d && out_i && cert, "ofr_knn_f6: null output");

@@ -99,11 +99,11 @@ def certify_sharded(gallery, Qd, qq, k, out, index_base, group=None):
         return md, mi, (kth * kth < minb) | torch.isinf(minb)
 
     md, mi, cert = merged(out[0], out[1], qq["bound"])
-    chain = list(gallery.TIER_CHAIN[gallery.TIER_CHAIN.index(qq["tier"]) + 1:])
     rows = torch.nonzero(~cert).reshape(-1)
     counts = [int(rows.numel())]
+    tier = qq["tier"]
     while rows.numel():
-        tier = chain.pop(0)
+        tier = gallery.next_tier(tier, int(rows.numel()))
         sub = Qd.index_select(0, rows).contiguous()
         if tier == "fp32":
             d2, i2 = gallery._search_f32(sub, k, index_base)

@@ -79,12 +79,14 @@ def test_knn_vs_oracle(metric, B, N, d, k):
     assert ties <= max(1, B // 100)
 
 
-@pytest.mark.parametrize("B,N,d,k", [(33, 300, 3, 1), (300, 5000, 99, 5), (257, 3000, 300, 16), (600, 20000, 64, 3),
+@pytest.mark.parametrize("B,N,d,k", [(1, 3000, 99, 1), (5, 257, 64, 8), (32, 20000, 200, 3), (33, 300, 3, 1),
+                                     (300, 5000, 99, 5), (257, 3000, 300, 16), (600, 20000, 64, 3),
                                      (1000, 70000, 130, 1)])
 @pytest.mark.parametrize("mode", ["auto", "q8", "q8x2", "fp32"])
 def test_knn_euclidean_paths_vs_oracle(monkeypatch, mode, B, N, d, k):
-    """Batches > 32 take the certified tiers (ofr_knn_f6, then ofr_knn_q8 with 1 and 2 slices) unless
-    OFR_SEARCH=fp32; OFR_SEARCH=q8 / q8x2 start at the int8 tiers."""
+    """Euclidean searches with k <= 8 take the certified tiers (ofr_knn_f6 -- the streaming kernel for
+    B <= 32, the tile kernel above -- then ofr_knn_q8 with 1 and 2 slices) unless OFR_SEARCH=fp32;
+    OFR_SEARCH=q8 / q8x2 start at the int8 tiers."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
     monkeypatch.setenv("OFR_SEARCH", mode)

@@ -117,6 +117,9 @@ class _MockShardGallery:
     def __init__(self, G, n0):
         self.G, self.n0 = G, n0
 
+    def next_tier(self, tier, nrows):
+        return self.TIER_CHAIN[self.TIER_CHAIN.index(tier) + 1]
+
     def _local(self, Q, k):
         d, i = O.nn_search_vectorized("EuclideanDistance", Q, self.G, min(16, len(self.G)))
         return d, i + self.n0
