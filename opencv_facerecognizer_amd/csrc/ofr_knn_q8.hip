@@ -235,22 +235,34 @@ __global__ void __launch_bounds__(f6t::NT, 1) tile_kernel_f6(TileArgs p) {
 // One workgroup per 256-row gallery panel, wave w owns rows 32w..32w+31 against the (single)
 // 32-row query block, loading its fragments straight to VGPRs from the f6 tiled layout (each
 // gallery byte is used once: no LDS staging; the 243 KB of query fragments stay in L2).
-// SU steps of loads are in flight per wave and 16 waves per CU, so the pass streams HBM.
+// SU steps of loads (96 B per lane each) are in flight per wave: enough to stream HBM even at
+// one 8-wave workgroup per CU.
 // Epilogue: the 32 x 32 scores of each wave -> per-query best 16 (keys, as tile_epilogue),
 // merged over the 8 waves through LDS -> the panel's best 16 rows per query.
-constexpr int SU = 4;
+constexpr int SU = 8;   // loads in flight per wave (tools/f6_probe.hip: 8 + non-temporal = 74 % of HBM peak, 4 = 68 %)
 
+template <bool NT = false>
 __device__ __forceinline__ f6t::i32x8 stream_frag(const char* stage, int j, int h, int row) {
   const char* sb = stage + (2 * j + h) * 6144;
-  const f6t::i32x4 p0 = *reinterpret_cast<const f6t::i32x4*>(sb + row * 16);
-  const f6t::i32x2 p1 = *reinterpret_cast<const f6t::i32x2*>(sb + 4096 + row * 8);
+  f6t::i32x4 p0;
+  f6t::i32x2 p1;
+  if constexpr (NT) {   // streamed once: non-temporal, keeps L2 for the query fragments
+    p0 = __builtin_nontemporal_load(reinterpret_cast<const f6t::i32x4*>(sb + row * 16));
+    p1 = __builtin_nontemporal_load(reinterpret_cast<const f6t::i32x2*>(sb + 4096 + row * 8));
+  } else {
+    p0 = *reinterpret_cast<const f6t::i32x4*>(sb + row * 16);
+    p1 = *reinterpret_cast<const f6t::i32x2*>(sb + 4096 + row * 8);
+  }
   f6t::i32x8 f;
   f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3];
   f[4] = p1[0]; f[5] = p1[1]; f[6] = 0; f[7] = 0;
   return f;
 }
 
-__global__ void __launch_bounds__(512, 2) stream_kernel_f6(TileArgs p) {
+// U loads in flight per wave, NT non-temporal gallery loads (the library uses <SU, true>; other
+// values are probe variants)
+template <int U = SU, bool NT = false>
+__global__ void __launch_bounds__(512) stream_kernel_f6(TileArgs p) {
   __shared__ uint32_t kbuf[8][32][KC];
   __shared__ float gtab[TG][2];
   const int64_t gt = blockIdx.x, g0 = gt * TG;
@@ -267,16 +279,16 @@ __global__ void __launch_bounds__(512, 2) stream_kernel_f6(TileArgs p) {
   f6t::f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  for (int k0 = 0; k0 < nsteps; k0 += SU) {
-    f6t::i32x8 a[SU], b[SU];
+  for (int k0 = 0; k0 < nsteps; k0 += U) {
+    f6t::i32x8 a[U], b[U];
 #pragma unroll
-    for (int u = 0; u < SU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int k = k0 + u < nsteps ? k0 + u : nsteps - 1;
-      a[u] = stream_frag(gpan + (k >> 1) * (int64_t)f6t::PANEL, k & 1, h, grow);
-      b[u] = stream_frag(qpan + (k >> 1) * (int64_t)f6t::PANEL, k & 1, h, r32);
+      a[u] = stream_frag<NT>(gpan + (k >> 1) * (int64_t)f6t::PANEL, k & 1, h, grow);
+      b[u] = stream_frag<false>(qpan + (k >> 1) * (int64_t)f6t::PANEL, k & 1, h, r32);
     }
 #pragma unroll
-    for (int u = 0; u < SU; ++u)
+    for (int u = 0; u < U; ++u)
       if (k0 + u < nsteps)
         acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[u], b[u], acc, 2, 2, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
   }
@@ -787,7 +799,7 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
   if (phases & 1) {
     if (B <= 32) {   // HBM regime: one 32-query block, gallery streamed straight to VGPRs
-      hipLaunchKernelGGL(q8s::stream_kernel_f6, dim3((unsigned)a.ntg), dim3(512), 0, st, a);
+      hipLaunchKernelGGL((q8s::stream_kernel_f6<q8s::SU, true>), dim3((unsigned)a.ntg), dim3(512), 0, st, a);
       OFR_LAUNCH_CHECK("f6 stream_kernel");
     } else {
       static bool attr_done = false;

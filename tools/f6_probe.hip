@@ -46,6 +46,27 @@ static int run(q8s::TileArgs a, int reps, const char* tag) {
   return 0;
 }
 
+template <int U, bool NT>
+static int run_stream(q8s::TileArgs a, int reps, const char* tag) {
+  a.ntq = 1;
+  a.B = 32;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((q8s::stream_kernel_f6<U, NT>), dim3((unsigned)a.ntg), dim3(512), 0, 0, a);
+  CK(hipGetLastError());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((q8s::stream_kernel_f6<U, NT>), dim3((unsigned)a.ntg), dim3(512), 0, 0, a);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  const double bytes = (double)a.ntg * f6t::TA * a.nk * 96.0;
+  printf("stream %-10s U=%d nt=%d ms=%7.3f  %6.0f GB/s (%.1f%% of 8000)\n", tag, U, (int)NT, ms, bytes / ms / 1e6,
+         bytes / ms / 1e6 / 80.0);
+  fflush(stdout);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int64_t N = argc > 1 ? atoll(argv[1]) : 1000000;
   const int64_t B = argc > 2 ? atoll(argv[2]) : 4096;
@@ -70,6 +91,13 @@ int main(int argc, char** argv) {
   a.ntq = f6t::panels(B);
   a.nk = (int)f6t::stages(d);
   printf("N=%ld B=%ld d=%ld\n", (long)N, (long)B, (long)d);
+  if (getenv("STREAM_ONLY")) {
+    for (int rep = 0; rep < 2; ++rep)
+      if (run_stream<4, false>(a, 20, "base") || run_stream<8, false>(a, 20, "u8") || run_stream<2, false>(a, 20, "u2") ||
+          run_stream<4, true>(a, 20, "nt") || run_stream<8, true>(a, 20, "u8+nt"))
+        return 1;
+    return 0;
+  }
   const int ggs[] = {1, 2, 4, 8, 16};
   for (int g : ggs) {
     a.gg = g < ntg ? g : ntg;
