@@ -102,6 +102,93 @@ __global__ void __launch_bounds__(256) elbp_hist_kernel(const uint8_t* __restric
   }
 }
 
+// Whole-image variant: one 1024-thread workgroup per image, the image staged in LDS (16-B loads)
+// behind the u32 counters of all cells, codes computed from LDS (same fp64 arithmetic, same
+// order) over a division-free 2-D walk, counts written four per 32-bit store.  Used when counters + image fit in 80 KiB, so two
+// workgroups (32 waves) share a CU.
+constexpr int LDS_IMG_BUDGET = 80 * 1024;
+
+__global__ void __launch_bounds__(1024) elbp_hist_lds_kernel(const uint8_t* __restrict__ imgs, LbpGeom g, HistArgs a,
+                                                             void* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+  const int64_t img = blockIdx.x;
+  const int nb = 1 << a.nbins_log2;
+  const int ncell = a.gr * a.gc;
+  uint8_t* im = reinterpret_cast<uint8_t*>(hist + ncell * nb);
+  const int npix = g.H * g.W;
+  for (int i = threadIdx.x; i < ncell * nb; i += blockDim.x) hist[i] = 0;
+  const uint8_t* src = imgs + img * (int64_t)npix;
+  if ((npix & 15) == 0 && ((uintptr_t)src & 15) == 0) {
+    for (int i = threadIdx.x; i < npix / 16; i += blockDim.x)
+      reinterpret_cast<uint4*>(im)[i] = reinterpret_cast<const uint4*>(src)[i];
+  } else {
+    for (int i = threadIdx.x; i < npix; i += blockDim.x) im[i] = src[i];
+  }
+  __syncthreads();
+  const int wpx = a.gc * a.px;                 // covered code columns
+  const int hpx = a.gr * a.py;                 // covered code rows
+  // 2-D walk: thread (tx, ty) takes column x = tx (+128 ...) and RB rows ty, ty + 8, ... at a time.
+  // Points outer, pixels inner: each (weight, offset) of the geometry is read once per RB pixels
+  // (a runtime-indexed kernel-argument read is a scalar load whose lgkmcnt wait would also drain
+  // the pending LDS atomics), and the atomics are issued after all codes of the group.
+  constexpr int RB = 5;   // 8 x 5 = 40 rows per pass (120 code rows of a 128x128 face: 3 passes), <= 64 VGPRs
+  const int tx = threadIdx.x & 127, ty = threadIdx.x >> 7;
+  for (int x = tx; x < wpx; x += 128) {
+    const int cx = x / a.px;
+    for (int y0 = ty; y0 < hpx; y0 += 8 * RB) {
+      uint32_t code[RB];
+      double C[RB], N[RB];
+      int base[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int y = min(y0 + 8 * r, hpx - 1);
+        base[r] = y * g.W + x;
+        C[r] = (double)im[base[r] + g.oy * g.W + g.ox];
+        code[r] = 0;
+      }
+      for (int i = 0; i < g.P; ++i) {
+        const int nt = g.nterm[i];
+        {
+          const int off = g.toff[i][0];
+          const double w = g.tw[i][0];
+#pragma unroll
+          for (int r = 0; r < RB; ++r) N[r] = w * (double)im[base[r] + off];
+        }
+        for (int t = 1; t < nt; ++t) {   // lbp.py:123-126 order, no contraction
+          const int off = g.toff[i][t];
+          const double w = g.tw[i][t];
+#pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const double prod = w * (double)im[base[r] + off];
+            N[r] = N[r] + prod;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) code[r] |= (N[r] >= C[r] ? 1u : 0u) << i;
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int y = y0 + 8 * r;
+        if (y < hpx) atomicAdd(&hist[((y / a.py) * a.gc + cx) * nb + (int)code[r]], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  const int total = ncell * nb;
+  const int64_t base = img * (int64_t)total;
+  if (a.count_bytes == 1) {
+    uint32_t* o = reinterpret_cast<uint32_t*>((uint8_t*)counts + base);
+    for (int i = threadIdx.x; i < total / 4; i += blockDim.x)
+      o[i] = hist[4 * i] | (hist[4 * i + 1] << 8) | (hist[4 * i + 2] << 16) | (hist[4 * i + 3] << 24);
+  } else if (a.count_bytes == 2) {
+    uint32_t* o = reinterpret_cast<uint32_t*>((uint16_t*)counts + base);
+    for (int i = threadIdx.x; i < total / 2; i += blockDim.x) o[i] = hist[2 * i] | (hist[2 * i + 1] << 16);
+  } else {
+    uint32_t* o = (uint32_t*)counts + base;
+    for (int i = threadIdx.x; i < total; i += blockDim.x) o[i] = hist[i];
+  }
+}
+
 static int make_geom(LbpGeom& g, int H, int W, int P, const int32_t* offs, const double* w, int oy, int ox, int by,
                      int bx) {
   if (P < 1 || P > MAXP) return fail(OFR_E_UNSUPPORTED, "ofr_elbp: neighbors must be in [1, 32]");
@@ -191,6 +278,21 @@ extern "C" int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H
   if (cell_px == 0) {  // empty cells: all counts zero (the reference's histogram is then NaN)
     hipError_t e = hipMemsetAsync(counts, 0, (size_t)n * gr * gc * nb * count_bytes, st);
     return e == hipSuccess ? OFR_OK : hip_status(e, "hipMemsetAsync");
+  }
+  const int64_t nbins_total = (int64_t)gr * gc * nb;
+  const size_t lds_whole = (size_t)nbins_total * 4 + round_up((int64_t)H * W, 16);
+  // whole-image LDS variant: counters + image fit the budget, and the packed stores stay aligned
+  if (lds_whole <= (size_t)LDS_IMG_BUDGET && nbins_total % 4 == 0 && n <= 0x7fffffffLL) {
+    static bool attr_done = false;
+    if (!attr_done) {
+      hipError_t e = hipFuncSetAttribute((const void*)elbp_hist_lds_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS_IMG_BUDGET);
+      if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(elbp_hist_lds)");
+      attr_done = true;
+    }
+    hipLaunchKernelGGL(elbp_hist_lds_kernel, dim3((unsigned)n), dim3(1024), lds_whole, st, imgs, g, a, counts);
+    OFR_LAUNCH_CHECK("elbp_hist_lds_kernel");
+    return OFR_OK;
   }
   const int64_t lds_cap = 64 * 1024;  // bytes of u32 counters per workgroup
   const int64_t row_bytes = (int64_t)gc * nb * 4;

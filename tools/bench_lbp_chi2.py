@@ -1,0 +1,144 @@
+"""BASELINE.json configs[3]: ExtendedLBP(1,8) + SpatialHistogram 8x8 + ChiSquare 1-NN, 65,536 gallery
+faces at 128x128 (bit-exact integer histograms), B = 4,096 query faces.  Prints one JSON line.
+
+    python tools/bench_lbp_chi2.py [--gallery 65536] [--batch 4096]
+
+Synthetic faces (opencv_facerecognizer_amd/synthetic.py at 128x128, 8 images per identity) are generated
+on the device.  Timed with HIP events: (1) LBP codes + per-cell histograms of the whole gallery
+(ofr_elbp_hist, the reference's SpatialHistogram.compute, feature.py:272-302 with lbp.py:80-130), (2) the
+chi-square 1-NN search of the query batch (ofr_chi2_knn, classifier.py:104-119 with distance.py:112-116).
+The CPU baseline times the oracle (the reference's numpy formulation, one thread) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from opencv_facerecognizer_amd import _lib  # noqa: E402
+from opencv_facerecognizer_amd._device import Chi2Gallery  # noqa: E402
+from opencv_facerecognizer_amd.facerec.feature import SpatialHistogram  # noqa: E402
+from opencv_facerecognizer_amd.facerec.lbp import ExtendedLBP  # noqa: E402
+from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
+
+PEAK_HBM = 8.0e12
+PEAK_F64_VALU = 78.6e12     # MI355X fp64 vector (spec)
+PEAK_F32_VALU = 157.3e12    # fp32 vector FMA (spec, 2 flop per FMA)
+
+
+def timed(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        out = fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, out
+
+
+def lbp_flops_per_code(geom):
+    (_, _), (_, _), offs, wts = geom
+    # per sample point: one multiply per non-zero weight and an add per extra term (lbp.py:123-126)
+    terms = [max(1, int(np.count_nonzero(np.asarray(w) > 0))) for w in wts]
+    return sum(2 * t - 1 for t in terms)
+
+
+def cpu_baseline(imgs_g, imgs_q, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import facerec_oracle as O  # the checker; timed here as the CPU baseline
+    t_h, nh = 0.0, 0
+    deadline = time.perf_counter() + seconds / 2
+    hists = []
+    while time.perf_counter() < deadline and nh < len(imgs_g):
+        t0 = time.perf_counter()
+        hists.append(O.spatial_histogram(imgs_g[nh], 1, 8, (8, 8)))
+        t_h += time.perf_counter() - t0
+        nh += 1
+    q = O.spatial_histogram(imgs_q[0], 1, 8, (8, 8))
+    t_c, nc = 0.0, 0
+    deadline = time.perf_counter() + seconds / 2
+    while time.perf_counter() < deadline:
+        t0 = time.perf_counter()
+        for h in hists:                                   # classifier.py:104-108, one call per item
+            O.chisquare(h, q)
+        t_c += time.perf_counter() - t0
+        nc += len(hists)
+    return t_h / nh, t_c / nc, nh
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gallery", type=int, default=65536)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--per-id", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+    device = _lib.device()
+    N, B, H = args.gallery, args.batch, 128
+    n_ids = (N + args.per_id - 1) // args.per_id
+    bank = IdentityBank(n_ids, H, H, device=device)
+    G_img = bank.images(torch.arange(N, device=device) // args.per_id, seed=SEED + 11).reshape(N, H, H)
+    gq = torch.Generator(device=device)
+    gq.manual_seed(SEED + 12)
+    ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
+    Q_img = bank.images(ids_q, seed=SEED + 13).reshape(B, H, H)
+
+    sh = SpatialHistogram(ExtendedLBP(1, 8), (8, 8))
+    ms_hist, (gc, cell, cb) = timed(lambda: sh.counts_device(G_img), args.reps)
+    qc, _, _ = sh.counts_device(Q_img)
+    nb = gc.shape[1] * gc.shape[2]
+    gal = Chi2Gallery(gc.reshape(N, nb), dtype=_lib.DT_U8, denom=float(cell), nbins=nb)
+    Qc = qc.reshape(B, nb).contiguous()
+    ms_search, (dd, ii) = timed(lambda: gal.search(Qc, 1), args.reps)
+    acc = float(((ii[:, 0] // args.per_id) == ids_q).double().mean().item())
+
+    ncode = (H - 2) * (H - 2)
+    flops_face = ncode * lbp_flops_per_code(sh.lbp_operator.geometry())
+    bytes_face = H * H + nb * cb                          # image in, uint8 counts out
+    pair_bins = float(B) * N * nb
+    t_h, t_c, nh = cpu_baseline(G_img[:64].cpu().numpy(), Q_img[:1].cpu().numpy(), args.cpu_seconds)
+    cpu_total = N * t_h + B * (t_h + N * t_c)             # histograms of gallery + queries, per-item chi2 loop
+    gpu_total = (ms_hist * (1 + B / N) + ms_search) * 1e-3
+    out = {
+        "metric": "faces/sec: ExtendedLBP + SpatialHistogram 8x8 + ChiSquare 1-NN (configs[3])",
+        "config": {"gallery": N, "batch": B, "side": H, "lbp": "ExtendedLBP(radius=1, neighbors=8)",
+                   "grid": [8, 8], "bins": nb, "k": 1},
+        "data": "synthetic",
+        "lbp_hist": {"ms": ms_hist, "faces_per_s": N / (ms_hist * 1e-3),
+                     "roofline": {"bound": "fp64 VALU / HBM", "fp64_tflops": flops_face * N / (ms_hist * 1e-3) / 1e12,
+                                  "fp64_peak": PEAK_F64_VALU / 1e12,
+                                  "fp64_frac": flops_face * N / (ms_hist * 1e-3) / PEAK_F64_VALU,
+                                  "hbm_gbs": bytes_face * N / (ms_hist * 1e-3) / 1e9,
+                                  "hbm_frac": bytes_face * N / (ms_hist * 1e-3) / PEAK_HBM,
+                                  "flops_per_face": flops_face, "bytes_per_face": bytes_face}},
+        "chi2_search": {"ms": ms_search, "queries_per_s": B / (ms_search * 1e-3),
+                        "pair_bins_per_s": pair_bins / (ms_search * 1e-3),
+                        "roofline": {"bound": "fp32 VALU", "note": "~6 VALU ops per (pair, bin): sub, add, add, "
+                                     "rcp, mul, fma; peak counted as 2 flop per lane-cycle",
+                                     "achieved_tflops": 6 * pair_bins / (ms_search * 1e-3) / 1e12,
+                                     "peak": PEAK_F32_VALU / 1e12,
+                                     "frac": 6 * pair_bins / (ms_search * 1e-3) / PEAK_F32_VALU}},
+        "top1_identity_acc": acc,
+        "end_to_end_queries_per_s": B / gpu_total,
+        "cpu_baseline": {"kind": "port", "cores": 1,
+                         "sample": f"{nh} gallery faces through the oracle's histogram, x{nh} chi2 calls per timing "
+                                   f"round; extrapolated to {N} gallery + {B} queries",
+                         "hist_ms_per_face": 1e3 * t_h, "chi2_us_per_pair": 1e6 * t_c,
+                         "queries_per_s": B / cpu_total},
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
