@@ -8,7 +8,7 @@
 // computes a 64-query x 64-gallery tile, 4x4 pairs per thread, histogram bins
 // streamed through LDS in [bin][row] panels of 64 bins (uint8/16/32 counts or
 // fp32 values widened once on the LDS write).  Coarse fp32 score per pair:
-//     S = sum_b (a-c)^2 * rcp(a+c+tiny)      (tiny makes empty bins exact 0)
+//     S = sum_b (a-c)^2 * rcp(a+c)   on values staged + 2^-100 (empty bins give exact 0)
 // The best KC rows per query per tile go to cand[tile][query][KC]; the merge
 // kernel then re-evaluates the reference formula EXACTLY in fp64 on the
 // survivors, with p = value/denom (denom = cell pixel count for counts, the
@@ -19,6 +19,7 @@ namespace ofr {
 
 enum { DT_U8 = 0, DT_U16 = 1, DT_U32 = 2, DT_F32 = 3 };
 constexpr int C2_TQ = 64, C2_TG = 64, C2_BB = 64;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int DT>
 __device__ __forceinline__ void load16(const void* base, int64_t ld, int64_t row, int64_t b0, float (&v)[16]) {
@@ -91,11 +92,9 @@ __global__ void __launch_bounds__(256) chi2_tile_kernel(Chi2Args p) {
   const int64_t qrow = min(q0 + lrow, p.B - 1);
   const int64_t grow = min(g0 + lrow, p.N - 1);
 
-  float acc[4][4];
+  f32x2 acc2[4][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int i = 0; i < 4; ++i) acc2[i][0] = acc2[i][1] = f32x2{0.f, 0.f};
 
   float vq[16], vg[16];
   const int nsteps = (int)(p.nbins / C2_BB);
@@ -105,30 +104,41 @@ __global__ void __launch_bounds__(256) chi2_tile_kernel(Chi2Args p) {
   }
   for (int s = 0; s < nsteps; ++s) {
     __syncthreads();
+    // values are staged biased by 2^-100: a + c > 0 for every pair (no per-pair "+ tiny"), while
+    // a - c and (a + c) for a, c >= 2^-76 round exactly as without the bias
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      Qs[lseg * 16 + i][lrow] = vq[i];
-      Gs[lseg * 16 + i][lrow] = vg[i];
+      Qs[lseg * 16 + i][lrow] = vq[i] + 0x1p-100f;
+      Gs[lseg * 16 + i][lrow] = vg[i] + 0x1p-100f;
     }
     __syncthreads();
     if (s + 1 < nsteps) {
       load16<DT>(p.Q, p.ldq, qrow, (int64_t)(s + 1) * C2_BB + lseg * 16, vq);
       load16<DT>(p.G, p.ldg, grow, (int64_t)(s + 1) * C2_BB + lseg * 16, vg);
     }
+    // packed fp32: per two (pair, bin) terms one v_pk_add for a - c, one for a + c, two v_rcp,
+    // v_pk_mul, v_pk_fma
 #pragma unroll 4
     for (int b = 0; b < C2_BB; ++b) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(&Qs[b][tq * 4]);
       const f32x4 c = *reinterpret_cast<const f32x4*>(&Gs[b][tg * 4]);
+      const f32x2 c01 = {c[0], c[1]}, c23 = {c[2], c[3]};
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float df = a[i] - c[j];
-          const float sm = (a[i] + c[j]) + 1e-30f;
-          acc[i][j] = __builtin_fmaf(df * df, __builtin_amdgcn_rcpf(sm), acc[i][j]);
-        }
+      for (int i = 0; i < 4; ++i) {
+        const f32x2 ai = {a[i], a[i]};
+        const f32x2 d0 = ai - c01, s0 = ai + c01, d1 = ai - c23, s1 = ai + c23;
+        const f32x2 r0 = {__builtin_amdgcn_rcpf(s0[0]), __builtin_amdgcn_rcpf(s0[1])};
+        const f32x2 r1 = {__builtin_amdgcn_rcpf(s1[0]), __builtin_amdgcn_rcpf(s1[1])};
+        acc2[i][0] = __builtin_elementwise_fma(d0 * d0, r0, acc2[i][0]);
+        acc2[i][1] = __builtin_elementwise_fma(d1 * d1, r1, acc2[i][1]);
+      }
     }
   }
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = acc2[i][j >> 1][j & 1];
   // tail bins (nbins % 64): plain loads
   for (int64_t b = (int64_t)nsteps * C2_BB; b < p.nbins; ++b) {
 #pragma unroll
