@@ -106,6 +106,7 @@ int main(int argc, char** argv) {
   a.gg = 4 < ntg ? 4 : ntg;
   if (run<1>(a, reps, "no-dma")) return 1;
   if (run<2>(a, reps, "no-mfma")) return 1;
+  if (run<4>(a, reps, "no-epilog")) return 1;
   if (run<0>(a, reps, "search")) return 1;
   return 0;
 }
