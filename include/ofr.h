@@ -161,10 +161,17 @@ int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, 
  * stats[3] = (||x~||, ||x - x~||, 0); maxima as ofr_q8_quantize_rows.
  * ofr_knn_f6: v_mfma_scale_f32_32x32x64_f8f6f4 (fp6 x fp6, unit block scales)
  * sums v_q.v_g with fp32 accumulation, whose error (<= (2 nst + 64) 2^-23
- * a_q A) is added to the certificate bound; otherwise exactly ofr_knn_q8
- * (best 16 per 256-row tile, exact fp64 re-rank, cert[q]).  Workspace:
- * ofr_knn_q8_workspace_bytes(B, N).                                          */
+ * a_q A) is added to the certificate bound; otherwise the ofr_knn_q8 contract
+ * (exact fp64 re-rank of the best 16 coarse rows, cert[q], bound[q]).
+ * B <= 32: one streaming pass, best 16 per 256-row tile.  B > 32: a sieve --
+ * a sample pass over every 64th tile sets a per-query keep threshold, the
+ * full pass keeps only rows at or below it (the certificate uses min(threshold,
+ * 16th kept)); a query whose bucket (8192 rows) overflows comes back with
+ * cert 0 and bound -inf.  Phase 1 state lives in the workspace:
+ * ofr_knn_f6_workspace_bytes(B, N) bytes, 16-byte aligned, kept between the
+ * phase-1 and phase-2 calls.                                                 */
 size_t ofr_f6_tiles_bytes(int64_t R, int64_t d);
+size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N);
 int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
                          size_t tiles_bytes, float* scale, double* stats, const float* aux, double* maxima);
 int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,

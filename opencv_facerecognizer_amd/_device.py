@@ -297,7 +297,9 @@ class FloatGallery:
         if out is None:
             out = (torch.empty((B, k), dtype=torch.float64, device=Qd.device),
                    torch.empty((B, k), dtype=torch.int64, device=Qd.device))
-        ws = self.ws.get(_lib.load().ofr_knn_q8_workspace_bytes(B, self.N), Qd.device)
+        lib = _lib.load()
+        nbytes = lib.ofr_knn_f6_workspace_bytes(B, self.N) if tier == "f6" else lib.ofr_knn_q8_workspace_bytes(B, self.N)
+        ws = self.ws.get(nbytes, Qd.device)
         if tier == "f6":
             call("ofr_knn_f6", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
                  ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),

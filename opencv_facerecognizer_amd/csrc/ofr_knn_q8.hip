@@ -56,6 +56,12 @@ struct TileArgs {
   Cand* cand;   // [B][T][KC] (query-major)
   int64_t ntq, ntg;
   int64_t gg;   // gallery tiles per tile group (see tile_coords)
+  // fp6 sieve (tile_kernel_f6 MODE 8, see below); gstride: tile t reads gallery panel t * gstride
+  int64_t gstride;
+  const uint32_t* theta;   // [B] keep threshold (a key with the low byte 0; KEY_NONE keeps every row)
+  int* count;              // [B] rows kept so far
+  Cand* bucket;            // [B][cap] the kept rows (truncated coarse score, row)
+  int64_t cap;
 };
 
 // ---- keys of the tile epilogue --------------------------------------------------------
@@ -75,6 +81,10 @@ __device__ __forceinline__ uint32_t score_key(float sc, int local) {
 __device__ __forceinline__ float key_score(uint32_t k) {
   const uint32_t t = k & ~0xffu;
   return __uint_as_float((t & 0x80000000u) ? (t ^ 0x80000000u) : ~t);
+}
+// the float whose order key is u (inverse of the map in score_key; 0xffffffff -> NaN)
+__device__ __forceinline__ float key_float(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u ^ 0x80000000u) : ~u);
 }
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a < b ? b : a; }
@@ -192,6 +202,77 @@ __device__ __forceinline__ void tile_epilogue(char* smem, const TileArgs& p, int
   }
 }
 
+// ---- fp6 sieve ------------------------------------------------------------------------
+// The list epilogue above costs ~10 us per tile (64 sorted inserts per lane and query block)
+// and writes 16 candidates per (query, tile): 2 GB per pass at B = 4096, N = 1M.  The sieve
+// replaces it for the fp6 tier at B > 32.  A sample pass (the list kernel over every
+// SIEVE_STRIDE-th gallery tile) gives per query theta = the 16th best truncated key of the
+// sample, an upper bound of the 16th best over the whole gallery.  The full pass then keeps
+// only rows whose truncated key is <= theta (one compare per (query, row); hits are staged in
+// LDS and appended to a per-query bucket), ~16 * SIEVE_STRIDE rows per query on gallery-like
+// data.  Certificate (merge_kernel): a row outside the final 16 either failed the test
+// (truncated key > theta) or was kept and lost to the 16th, so tau = min(theta, 16th kept)
+// bounds every excluded row exactly as before.  theta only steers the volume: a bucket that
+// overflows its cap makes the query uncertified (bound -inf), never wrong.
+constexpr int64_t SIEVE_STRIDE = 64;   // sample: gallery tiles 0, 64, 128, ...
+constexpr int64_t SIEVE_CAP = 8192;    // kept rows per query (64 KiB)
+constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
+
+// Hits of one 256 x 256 tile: (a, s) = (aux, gscale) of gallery row threadIdx.x (padding rows:
+// (+inf, 0), which never pass), sq2 / th per query block of this lane (th = key_float(theta | 0xff):
+// truncated key <= theta  <=>  !(score > th); NaN for KEY_NONE keeps everything).
+template <int CT, int TQ, int QW, int WQ, class CV>
+__device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, int64_t g0, int64_t q0, float ga,
+                                               float gs, const float (&sq2)[CT], const float (&th)[CT], CV&& cval) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
+  float* gtab = reinterpret_cast<float*>(smem);                                  // [TG][2]
+  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + TG * 8);
+  uint2* hits = reinterpret_cast<uint2*>(smem + TG * 8 + 16);                    // [SIEVE_HCAP]
+  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
+  if (threadIdx.x < TG) {
+    gtab[2 * threadIdx.x + 0] = ga;
+    gtab[2 * threadIdx.x + 1] = gs;
+  }
+  if (threadIdx.x == 0) *nhit = 0;
+  __syncthreads();
+  auto append = [&](int64_t q, int gl, uint32_t kb) {
+    if (q < p.B && gl < nvalid) {
+      const int slot = atomicAdd(p.count + q, 1);
+      if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(kb), (int)(g0 + gl)};
+    }
+  };
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int gl = wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float a = gtab[2 * gl], sg = gtab[2 * gl + 1];
+      auto one = [&](auto ctc) {
+        constexpr int ct = decltype(ctc)::value;
+        if constexpr (ct < CT) {
+          const float sc = a - sq2[ct] * sg * cval(rt, ctc, r);
+          if (!(sc > th[ct])) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
+            const int ql = wc * QW + ct * 32 + r32;
+            const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
+            const uint32_t slot = atomicAdd(nhit, 1u);
+            if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)gl);
+            else append(q0 + ql, gl, kb);
+          }
+        }
+      };
+      static_assert(CT <= 2, "sieve unroll");
+      one(std::integral_constant<int, 0>{});
+      one(std::integral_constant<int, 1>{});
+    }
+  __syncthreads();
+  const uint32_t n = *nhit < (uint32_t)SIEVE_HCAP ? *nhit : (uint32_t)SIEVE_HCAP;
+  for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+    const uint2 hv = hits[e];
+    append(q0 + (int)(hv.y >> 8), (int)(hv.y & 0xffu), hv.x);
+  }
+}
+
 // MODE 0 is the search; 1 (no k-loop DMA) and 2 (no MFMA) exist only for the
 // feed/compute probe in tools/ and are never instantiated by the library.
 template <int SL, int MODE>
@@ -214,33 +295,58 @@ __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
   });
 }
 
-// fp6 tier: p.G / p.Q are f6 tiled buffers (ofr_f6_tile.h), p.nk = stages.  MODE bits 1/2 go to
-// the main loop (probes); 4 skips the epilogue (probe).
+// fp6 tier: p.G / p.Q are f6 tiled buffers (ofr_f6_tile.h), p.nk = stages.  MODE 0: tile lists
+// (tile t = gallery panel t * gstride, the sieve's sample pass); 8: the sieve.  MODE bits 1/2 go
+// to the main loop (probes); 4 skips the epilogue (probe).
 template <int MODE>
 __global__ void __launch_bounds__(f6t::NT, 1) tile_kernel_f6(TileArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool SIEVE = (MODE & 8) != 0;
+  constexpr int CT = f6t::CT;
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   int64_t gt, qt;
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
-  const int64_t g0 = gt * TG, q0 = qt * f6t::TQ;
-  f6t::f32x16 acc[4][f6t::CT];
-  f6t::mainloop<MODE & 3>(smem, reinterpret_cast<const char*>(p.G), gt, reinterpret_cast<const char*>(p.Q), qt,
+  const int64_t gp = gt * p.gstride;
+  const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
+  // sieve operands, loaded under the main loop
+  float ga = __builtin_inff(), gs = 0.f, sq2[CT], th[CT];
+  if constexpr (SIEVE) {
+    const int64_t g = g0 + threadIdx.x;
+    if (threadIdx.x < TG && g < p.N) {
+      ga = p.aux[g];
+      gs = p.gscale[g];
+    }
+    const int wc = (threadIdx.x >> 6) % f6t::WQ, r32 = threadIdx.x & 31;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int64_t q = q0 + wc * f6t::QW + c * 32 + r32;
+      const bool ok = q < p.B;
+      sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
+      th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
+    }
+  }
+  f6t::f32x16 acc[4][CT];
+  f6t::mainloop<MODE & 3>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
                           p.nk, acc);
   if constexpr ((MODE & 4) != 0) {   // probe: no epilogue (the accumulators kept alive)
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int c = 0; c < f6t::CT; ++c)
+      for (int c = 0; c < CT; ++c)
 #pragma unroll
         for (int r = 0; r < 16; ++r) s += acc[i][c][r];
     if (s == 1.2345f) p.cand[0].d = s;
     return;
   }
-  tile_epilogue<f6t::CT, f6t::TQ, f6t::QW, f6t::WQ>(smem, p, gt, g0, q0, [&](int rt, auto ctc, int r) {
+  auto cval = [&](int rt, auto ctc, int r) {
     constexpr int ct = decltype(ctc)::value;
     return acc[rt][ct][r];
-  });
+  };
+  if constexpr (SIEVE)
+    sieve_epilogue<CT, f6t::TQ, f6t::QW, f6t::WQ>(smem, p, g0, q0, ga, gs, sq2, th, cval);
+  else
+    tile_epilogue<CT, f6t::TQ, f6t::QW, f6t::WQ>(smem, p, gt, g0, q0, cval);
 }
 
 // ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
@@ -345,7 +451,7 @@ __global__ void __launch_bounds__(512) stream_kernel_f6(TileArgs p) {
 // ---- pass 2 ----------------------------------------------------------------------------
 
 struct MergeArgs {
-  const Cand* cand;
+  const Cand* cand;       // tile lists [B][T][KC], or the sieve's buckets [B][cap]
   int64_t T, B;
   const float* Q;
   int64_t ldq;
@@ -360,11 +466,62 @@ struct MergeArgs {
   int64_t* out_i;
   int* cert;
   double* bound;   // optional: squared-distance lower bound of every row outside the candidates
+  const int* count;        // sieve: rows kept per query (null for tile lists)
+  const uint32_t* theta;   // sieve: the keep thresholds
+  int64_t cap;
 };
 
-// One block per query.  (1) best KC of the T tile lists, read as one contiguous stream
-// (candidate lists are query-major: cand[q][t][KC]; 16 B per lane and load, fully
-// coalesced) with a per-thread sorted list and a tree merge; (2) the exact fp64 distance
+// Best KC (distance, index) of the n candidates at src (16-byte aligned) into lists[0..KC),
+// ascending; one 256-thread block.  16 B per lane and load (two candidates), fully coalesced,
+// a per-thread sorted list, then a tree merge through lists[256 * KC].
+__device__ __forceinline__ void block_best(const Cand* src, int64_t n, Cand* lists) {
+  TopList<KC> L;
+  L.init();
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  for (int64_t e = threadIdx.x; e < n / 2; e += blockDim.x) {
+    const uint4 v = s4[e];
+    const float d0 = __uint_as_float(v.x), d1 = __uint_as_float(v.z);
+    if (better_f(d0, (int)v.y, L.d[KC - 1], L.i[KC - 1])) L.insert(d0, (int)v.y);
+    if (better_f(d1, (int)v.w, L.d[KC - 1], L.i[KC - 1])) L.insert(d1, (int)v.w);
+  }
+  if ((n & 1) && threadIdx.x == 0) L.insert(src[n - 1].d, src[n - 1].i);
+#pragma unroll
+  for (int j = 0; j < KC; ++j) lists[threadIdx.x * KC + j] = Cand{L.d[j], L.i[j]};
+  __syncthreads();
+  for (int active = (int)blockDim.x / 2; active > 0; active >>= 1) {
+    if ((int)threadIdx.x < active) {
+      float od[KC];
+      int oi[KC];
+      const Cand* o = lists + (threadIdx.x + active) * KC;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        od[j] = o[j].d;
+        oi[j] = o[j].i;
+      }
+      L.merge(od, oi);
+#pragma unroll
+      for (int j = 0; j < KC; ++j) lists[threadIdx.x * KC + j] = Cand{L.d[j], L.i[j]};
+    }
+    __syncthreads();
+  }
+}
+
+// Sieve thresholds from the sample pass's tile lists: theta[q] = the 16th best key (KEY_NONE
+// when the sample holds fewer than 16 rows); resets the bucket counts.
+__global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists, int64_t T, uint32_t* theta,
+                                                              int* count) {
+  __shared__ Cand best[256 * KC];
+  const int64_t q = blockIdx.x;
+  block_best(lists + (size_t)q * T * KC, T * KC, best);
+  if (threadIdx.x == 0) {
+    const Cand c = best[KC - 1];
+    theta[q] = c.i != CAND_EMPTY ? score_key(c.d, 0) : KEY_NONE;
+    count[q] = 0;
+  }
+}
+
+// One block per query.  (1) best KC of the tile lists (query-major: cand[q][t][KC], one
+// contiguous stream) or of the query's sieve bucket; (2) the exact fp64 distance
 // (distance.py:60) of the KC survivors, one wave per candidate (float4 loads, lane partial
 // sums, shuffle reduction); (3) sort by (distance, index) and the certificate.
 __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
@@ -373,36 +530,13 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   __shared__ double red[4];
   const int64_t q = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  {
-    TopList<KC> L;
-    L.init();
-    const uint4* src = reinterpret_cast<const uint4*>(p.cand + (size_t)q * p.T * KC);
-    const int64_t n4 = p.T * KC / 2;   // two candidates per 16 B
-    for (int64_t e = threadIdx.x; e < n4; e += blockDim.x) {
-      const uint4 v = src[e];
-      const float d0 = __uint_as_float(v.x), d1 = __uint_as_float(v.z);
-      if (better_f(d0, (int)v.y, L.d[KC - 1], L.i[KC - 1])) L.insert(d0, (int)v.y);
-      if (better_f(d1, (int)v.w, L.d[KC - 1], L.i[KC - 1])) L.insert(d1, (int)v.w);
-    }
-#pragma unroll
-    for (int j = 0; j < KC; ++j) lists[threadIdx.x * KC + j] = Cand{L.d[j], L.i[j]};
-    __syncthreads();
-    for (int active = (int)blockDim.x / 2; active > 0; active >>= 1) {
-      if ((int)threadIdx.x < active) {
-        float od[KC];
-        int oi[KC];
-        const Cand* o = lists + (threadIdx.x + active) * KC;
-#pragma unroll
-        for (int j = 0; j < KC; ++j) {
-          od[j] = o[j].d;
-          oi[j] = o[j].i;
-        }
-        L.merge(od, oi);
-#pragma unroll
-        for (int j = 0; j < KC; ++j) lists[threadIdx.x * KC + j] = Cand{L.d[j], L.i[j]};
-      }
-      __syncthreads();
-    }
+  bool overflow = false;
+  if (p.count) {
+    const int64_t c = p.count[q];
+    overflow = c > p.cap;
+    block_best(p.cand + (size_t)q * p.cap, overflow ? p.cap : c, lists);
+  } else {
+    block_best(p.cand + (size_t)q * p.T * KC, p.T * KC, lists);
   }
   const float* qr = p.Q + q * p.ldq;
   const int64_t d4 = p.d >> 2;
@@ -446,13 +580,16 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     sort_and_write<KC>(lists, exact, p.k, p.index_base, od, oi);
     // certificate.  Every row outside the KC candidates has coarse score >= tau, hence exact
     // score S = d^2 - |q|^2 >= tau - dS, i.e. d^2 >= bound = tau - dS + |q|^2 (less a relative
-    // 1e-12 for the fp64 evaluation); the local top-k is exact iff d_k^2 < bound.  A sharded
-    // search compares the GLOBAL k-th with every rank's bound instead (parallel.py).
-    int nvalid = 0;
-    for (int c = 0; c < KC; ++c) nvalid += lists[c].i != CAND_EMPTY;
-    double bnd = __builtin_inf();   // every gallery row was a candidate
-    if (nvalid == KC) {
-      const double tau = (double)lists[KC - 1].d;
+    // 1e-12 for the fp64 evaluation); the local top-k is exact iff d_k^2 < bound.  tau = the
+    // 16th key (none when every gallery row is a candidate), with the sieve min(theta, 16th).
+    // A sharded search compares the GLOBAL k-th with every rank's bound instead (parallel.py).
+    uint32_t tk = lists[KC - 1].i != CAND_EMPTY ? score_key(lists[KC - 1].d, 0) : KEY_NONE;
+    if (p.theta) tk = umin(tk, p.theta[q]);
+    double bnd = __builtin_inf();
+    if (overflow) {
+      bnd = -__builtin_inf();   // the bucket dropped kept rows: no bound
+    } else if (tk != KEY_NONE) {
+      const double tau = (double)key_score(tk);
       const double a = p.qstats[q * 3 + 0], e = p.qstats[q * 3 + 1], tq = p.qstats[q * 3 + 2];
       const double A = p.gmax[0], E = p.gmax[1], T = p.gmax[2], auxmax = p.gmax[3];
       double dS = 2.0 * (a * E + e * A + e * E + tq * T) + 0x1p-20 * (auxmax + 2.0 * a * A) +
@@ -731,7 +868,7 @@ extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, 
   OFR_CHECK_ARG(N < 0x7fffffffLL - q8s::TG, "ofr_knn_q8: N too large for one shard");
   OFR_CHECK_ARG(workspace_bytes >= ofr_knn_q8_workspace_bytes(B, N), "ofr_knn_q8: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  q8s::TileArgs a;
+  q8s::TileArgs a{};
   a.G = Gs; a.N = N; a.ld = ld; a.gscale = gscale; a.aux = aux;
   a.Q = Qs; a.B = B; a.qscale = qscale;
   a.nk = (int)cdiv(d, slices == 1 ? q8s::Shape<1>::BK : q8s::Shape<2>::BK);
@@ -784,6 +921,26 @@ extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int
   return OFR_OK;
 }
 
+// f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
+// thresholds, counts and buckets (each 256-byte aligned)
+struct SieveWs {
+  size_t lists, theta, count, bucket, bytes;
+};
+static SieveWs sieve_ws(int64_t B, int64_t N) {
+  const int64_t ts = cdiv(cdiv(N > 0 ? N : 1, q8s::TG), q8s::SIEVE_STRIDE);
+  SieveWs w;
+  w.lists = 0;
+  w.theta = round_up((int64_t)(B * ts * q8s::KC * sizeof(Cand)), 256);
+  w.count = w.theta + round_up(B * 4, 256);
+  w.bucket = w.count + round_up(B * 4, 256);
+  w.bytes = w.bucket + (size_t)B * q8s::SIEVE_CAP * sizeof(Cand);
+  return w;
+}
+
+extern "C" size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N) {
+  return B <= 32 ? ofr_knn_q8_workspace_bytes(B, N) : sieve_ws(B, N).bytes;
+}
+
 extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                           const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
                           int64_t d, const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
@@ -796,11 +953,13 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
   OFR_CHECK_ARG(ldq >= d && ldg >= d, "ofr_knn_f6: bad leading dimensions");
   OFR_CHECK_ARG(Q && Qt && qscale && qstats && G && Gt && gscale && aux && gmax && workspace,
                 "ofr_knn_f6: null pointer");
-  OFR_CHECK_ARG(((uintptr_t)Qt | (uintptr_t)Gt) % 16 == 0, "ofr_knn_f6: tiles must be 16-byte aligned");
+  OFR_CHECK_ARG(((uintptr_t)Qt | (uintptr_t)Gt | (uintptr_t)workspace) % 16 == 0,
+                "ofr_knn_f6: tiles and workspace must be 16-byte aligned");
   OFR_CHECK_ARG(N < 0x7fffffffLL - q8s::TG, "ofr_knn_f6: N too large for one shard");
-  OFR_CHECK_ARG(workspace_bytes >= ofr_knn_q8_workspace_bytes(B, N), "ofr_knn_f6: workspace too small");
+  OFR_CHECK_ARG(workspace_bytes >= ofr_knn_f6_workspace_bytes(B, N), "ofr_knn_f6: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  q8s::TileArgs a;
+  const bool sieve = B > 32;
+  q8s::TileArgs a{};
   a.G = (const int8_t*)Gt; a.N = N; a.ld = 0; a.gscale = gscale; a.aux = aux;
   a.Q = (const int8_t*)Qt; a.B = B; a.qscale = qscale;
   a.nk = (int)f6t::stages(d);
@@ -808,22 +967,44 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
   a.ntq = f6t::panels(B);
   a.ntg = f6t::panels(N);
   a.gg = a.ntg < q8s::GROUP_G ? a.ntg : q8s::GROUP_G;
+  a.gstride = 1;
+  const SieveWs w = sieve_ws(B, N);
+  char* wsb = reinterpret_cast<char*>(workspace);
+  uint32_t* theta = reinterpret_cast<uint32_t*>(wsb + w.theta);
+  int* count = reinterpret_cast<int*>(wsb + w.count);
+  Cand* bucket = reinterpret_cast<Cand*>(wsb + w.bucket);
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
   if (phases & 1) {
-    if (B <= 32) {   // HBM regime: one 32-query block, gallery streamed straight to VGPRs
+    if (!sieve) {   // HBM regime: one 32-query block, gallery streamed straight to VGPRs
       hipLaunchKernelGGL((q8s::stream_kernel_f6<q8s::SU, true>), dim3((unsigned)a.ntg), dim3(512), 0, st, a);
       OFR_LAUNCH_CHECK("f6 stream_kernel");
     } else {
       static bool attr_done = false;
       if (!attr_done) {
-        hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel_f6<0>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
-        if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
+        for (const void* f : {(const void*)q8s::tile_kernel_f6<0>, (const void*)q8s::tile_kernel_f6<8>}) {
+          hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
+          if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
+        }
         attr_done = true;
       }
-      hipLaunchKernelGGL((q8s::tile_kernel_f6<0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::NT), f6t::LDS, st,
+      // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel -> thresholds
+      q8s::TileArgs s = a;
+      s.gstride = q8s::SIEVE_STRIDE;
+      s.ntg = cdiv(a.ntg, q8s::SIEVE_STRIDE);
+      s.gg = s.ntg < q8s::GROUP_G ? s.ntg : q8s::GROUP_G;
+      s.cand = reinterpret_cast<Cand*>(wsb + w.lists);
+      hipLaunchKernelGGL((q8s::tile_kernel_f6<0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(f6t::NT), f6t::LDS, st, s);
+      OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
+      hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)B), dim3(256), 0, st, s.cand, s.ntg, theta,
+                         count);
+      OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
+      a.theta = theta;
+      a.count = count;
+      a.bucket = bucket;
+      a.cap = q8s::SIEVE_CAP;
+      hipLaunchKernelGGL((q8s::tile_kernel_f6<8>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::NT), f6t::LDS, st,
                          a);
-      OFR_LAUNCH_CHECK("f6 tile_kernel");
+      OFR_LAUNCH_CHECK("f6 tile_kernel (sieve)");
     }
   }
   if (phases & 2) {
@@ -832,6 +1013,12 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
     // sum|q~ g~| <= a_q a_g <= a_q A (tools/mx_probe.hip measures <= 3 * 2^-24 at n = 160)
     const double gamma = (double)(2 * a.nk + 64) * 0x1p-23;
     q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, gamma, k, index_base, out_d, out_i, cert, bound};
+    if (sieve) {
+      m.cand = bucket;
+      m.count = count;
+      m.theta = theta;
+      m.cap = q8s::SIEVE_CAP;
+    }
     hipLaunchKernelGGL(q8s::merge_kernel, dim3((unsigned)B), dim3(256), 0, st, m);
     OFR_LAUNCH_CHECK("f6 merge_kernel");
   }

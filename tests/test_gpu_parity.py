@@ -81,7 +81,7 @@ def test_knn_vs_oracle(metric, B, N, d, k):
 
 @pytest.mark.parametrize("B,N,d,k", [(1, 3000, 99, 1), (5, 257, 64, 8), (32, 20000, 200, 3), (33, 300, 3, 1),
                                      (300, 5000, 99, 5), (257, 3000, 300, 16), (600, 20000, 64, 3),
-                                     (1000, 70000, 130, 1)])
+                                     (1000, 70000, 130, 1), (64, 10, 16, 3), (48, 17, 40, 5)])
 @pytest.mark.parametrize("mode", ["auto", "q8", "q8x2", "fp32"])
 def test_knn_euclidean_paths_vs_oracle(monkeypatch, mode, B, N, d, k):
     """Euclidean searches with k <= 8 take the certified tiers (ofr_knn_f6 -- the streaming kernel for
@@ -122,6 +122,26 @@ def test_knn_q8_certificate_forces_fallback(monkeypatch):
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     dd, ii = g.search(g.query_rows(Q), 3)
     assert len(g.last_fallbacks) == 3 and min(g.last_fallbacks) > 0
+    _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
+
+
+def test_knn_f6_sieve_overflow_falls_back(monkeypatch):
+    """The fp6 sieve (B > 32) keeps the rows at or below a sampled threshold in a per-query bucket of
+    8192 rows.  10,000 exact copies of one row all tie with the threshold, every bucket overflows:
+    each query must come back uncertified from the fp6 tier and be resolved by the next tiers, with
+    ties to the lowest index (the oracle's order)."""
+    from opencv_facerecognizer_amd._device import FloatGallery
+    from opencv_facerecognizer_amd import _lib
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(1234)
+    d = 96
+    x = r.normal(0, 20, d)
+    G = np.concatenate([np.tile(x, (10000, 1)), r.normal(0, 20, (2000, d))]).astype(np.float32).astype(np.float64)
+    Q = (x + r.normal(0, 0.5, (40, d))).astype(np.float32).astype(np.float64)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    dd, ii = g.search(g.query_rows(Q), 3)
+    assert g.last_fallbacks[0] == 40
+    assert (ii.cpu().numpy() == np.array([0, 1, 2])).all()
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
 
 
