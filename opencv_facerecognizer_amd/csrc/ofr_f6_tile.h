@@ -35,16 +35,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int TA = 256, TQ = 256;            // gallery x query rows per tile
 constexpr int BK = 128;                      // features per stage
 constexpr int PANEL = 24576;                 // bytes per (panel, stage) block = 256 rows x 96 B
-constexpr int NW = 8, NT = NW * 64;          // 2 waves per SIMD
-constexpr int WQ = 4, QW = TQ / WQ;          // wave grid 2 (gallery) x 4 (queries); 128 x 64 per wave
-constexpr int CT = QW / 32;                  // 32-query blocks per wave (2)
 constexpr int NST = 3;                       // LDS stages
 constexpr int STAGE = 2 * PANEL;             // gallery block + query block
 constexpr int LDS = NST * STAGE;             // 144 KiB
-constexpr int IPW = STAGE / 1024 / NW;       // DMA wave-instructions per wave per stage (6)
-constexpr int YOUNG = (NST - 2) * IPW;       // DMAs allowed in flight at the stage wait
-constexpr int NFR = 2 * (4 + CT);            // ds_reads per MFMA step (b128 + b64 per fragment)
-constexpr int MF = 4 * CT;                   // MFMAs per MFMA step
+constexpr int DMA_INS = STAGE / 1024;        // 1-KiB DMA wave-instructions per stage (48)
 
 __host__ __device__ constexpr int64_t panels(int64_t rows) { return (rows + TA - 1) / TA; }
 __host__ __device__ constexpr int64_t stages(int64_t d) { return (d + BK - 1) / BK; }
@@ -52,28 +46,13 @@ __host__ __device__ constexpr int64_t tiles_bytes(int64_t rows, int64_t d) {
   return panels(rows) * stages(d) * (int64_t)PANEL;
 }
 
-// Stage kt of gallery panel gp and query panel qp -> LDS stage buffer st:
-// 48 wave-instructions of 1 KiB, waves 0-3 the gallery block, 4-7 the query block.
-__device__ __forceinline__ void dma(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst, int kt,
-                                    char* st) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool gal = wave < 4;
-  const char* blk = (gal ? G + (gp * nst + kt) * (int64_t)PANEL : Q + (qp * nst + kt) * (int64_t)PANEL);
-  const int w4 = wave & 3;
-  char* dst = st + (gal ? 0 : PANEL);
-#pragma unroll
-  for (int t = 0; t < IPW; ++t) {
-    const int ins = w4 * IPW + t;
-    __builtin_amdgcn_global_load_lds((const OFR_GLOBAL void*)(blk + ins * 1024 + lane * 16),
-                                     (OFR_LDS void*)(dst + ins * 1024), 16, 0, 0);
-  }
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else static_assert(N == 0 || N == 6, "vmcnt");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else static_assert(N == 0 || N == 6 || N == 12 || N == 24, "vmcnt");
 }
 
 __device__ __forceinline__ void barrier() {
@@ -96,79 +75,133 @@ __device__ __forceinline__ i32x8 frag(const char* blk, int j, int h, int row) {
   return f;
 }
 
-// Main loop.  Wave (wr, wc) owns gallery rows wr*128 + i*32 + (C/D row map) and query
-// rows wc*64 + j*32 + lane&31 (C/D: column = lane & 31, row = (reg & 3) + 8 (reg >> 2) +
-// 4 (lane >> 5)).  MODE 1/2: probe variants without k-loop DMA / without MFMA.
-template <int MODE>
-__device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
-                                         int nst, f32x16 (&acc)[4][CT]) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < CT; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+// The tile engine for NW waves: NW = 8 (2 per SIMD, 128 x 64 per wave, wave grid 2 x 4) or
+// NW = 4 (1 per SIMD, 128 x 128 per wave, grid 2 x 2: a third fewer fragment bytes per MFMA,
+// 256 accumulators per lane in AGPRs).  Wave (wr, wc) owns gallery rows wr*128 + i*32 + (C/D
+// row map) and query rows wc*QW + c*32 + lane&31 (C/D: column = lane & 31, row = (reg & 3) +
+// 8 (reg >> 2) + 4 (lane >> 5)).
+template <int NW_>
+struct Engine {
+  static constexpr int NW = NW_, NT = NW * 64;
+  static constexpr int WQ = NW / 2, QW = TQ / WQ;   // query columns per wave
+  static constexpr int CT = QW / 32;                // 32-query blocks per wave
+  static constexpr int IPW = DMA_INS / NW;          // DMA wave-instructions per wave per stage
+  static constexpr int NFR = 2 * (4 + CT);          // ds_reads per MFMA step (b128 + b64 per fragment)
+  static constexpr int MF = 4 * CT;                 // MFMAs per MFMA step
+  static_assert(NW == 4 || NW == 8, "engine");
 
-  auto issue = [&](int kt) { dma(G, gp, Q, qp, nst, kt, smem + (kt % NST) * STAGE); };
-  // Branch-free k loop: the stage issued at kt is min(kt + NST - 1, last); past the end it
-  // re-loads the last stage into the buffer nobody reads any more (constant vmcnt bookkeeping).
-  const int last = nst - 1;
+  // Stage kt of gallery panel gp and query panel qp -> LDS stage buffer st: DMA_INS
+  // wave-instructions of 1 KiB, the first half the gallery block, the second the query block.
+  // SKIP (probes only): 2 = no gallery block, 16 = no query block
+  template <int SKIP = 0>
+  static __device__ __forceinline__ void dma(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst,
+                                             int kt, char* st) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const char* gb = G + (gp * nst + kt) * (int64_t)PANEL;
+    const char* qb = Q + (qp * nst + kt) * (int64_t)PANEL;
 #pragma unroll
-  for (int s = 0; s < NST - 1; ++s) issue(s < last ? s : last);
-
-  i32x8 ga[2][4], qb[2][CT];
-  auto frags = [&](const char* st, int j) {
-#pragma unroll
-    for (int c = 0; c < CT; ++c) qb[j][c] = frag(st + PANEL, j, h, wc * QW + c * 32 + r32);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ga[j][i] = frag(st, j, h, wr * 128 + i * 32 + r32);
-  };
-  auto mfmas = [&](int j) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < CT; ++c)
-        acc[i][c] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ga[j][i], qb[j][c], acc[i][c], 2, 2, 0,
-                                                                    0x7f7f7f7f, 0, 0x7f7f7f7f);
-  };
-
-  for (int kt = 0; kt < nst; ++kt) {
-    if constexpr (MODE == 1) wait_vm<0>();
-    else wait_vm<YOUNG>();   // stage kt landed; the younger stage may stay in flight
-    barrier();
-    const char* st = smem + (kt % NST) * STAGE;
-    frags(st, 0);
-    if constexpr (MODE != 1) {
-      const int nx = kt + NST - 1;
-      issue(nx < last ? nx : last);
+    for (int t = 0; t < IPW; ++t) {
+      const int ins = wave * IPW + t;   // gallery: ins < 24 (a wave's instructions never straddle)
+      const bool gal = ins < DMA_INS / 2;
+      const int off = (gal ? ins : ins - DMA_INS / 2) * 1024;
+      if (((SKIP & 2) && gal) || ((SKIP & 16) && !gal)) continue;
+      __builtin_amdgcn_global_load_lds((const OFR_GLOBAL void*)((gal ? gb : qb) + off + lane * 16),
+                                       (OFR_LDS void*)(st + (gal ? 0 : PANEL) + off), 16, 0, 0);
     }
-    frags(st, 1);
-    if constexpr (MODE != 2) {
-      mfmas(0);
-      mfmas(1);
-    }
-    // schedule: step-0 reads, the DMAs, step-0 MFMAs with step-1 reads threaded between
-    // them (2 reads after each of the first 4, 1 after each of the last 4), step-1 MFMAs
-    __builtin_amdgcn_sched_group_barrier(0x100, NFR, 0);
-    __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
-    static_assert(NFR == 12 && MF == 8, "schedule below");
+  }
+
+  // reads threaded through MFMAs: NFR reads over MF MFMAs, front-loaded (2 after each MFMA while
+  // they last, then 1, then none)
+  static __device__ __forceinline__ void interleave() {
+    constexpr int two = NW == 8 ? 4 : 8;   // MFMAs followed by 2 reads
+    constexpr int one = NW == 8 ? 4 : 0;   // then by 1
+    static_assert(2 * two + one == NFR && two + one <= MF, "schedule");
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < two; ++r) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < one; ++r) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
+    if constexpr (MF - two - one > 0) __builtin_amdgcn_sched_group_barrier(0x008, MF - two - one, 0);
   }
-  wait_vm<0>();
-  barrier();
-}
+
+  // Main loop, stage hand-off in the middle of a stage.  Per stage kt:
+  //   A: fragments (kt, j=1) read between the MFMAs of (kt, j=0)
+  //   wait for stage kt+1 to land, barrier (every wave has read all of stage kt)
+  //   B: fragments (kt+1, j=0) read between the MFMAs of (kt, j=1); DMA of stage kt+3 into
+  //      kt's buffer after the first MFMA
+  // so every fragment read has a block of MFMAs to land behind and each barrier falls while
+  // the matrix pipe still drains the previous block (2 % faster than a hand-off at the stage
+  // boundary, which exposes the step-0 reads after every barrier: tools/f6_probe.hip).
+  // Fragments double-buffered by j; 3 LDS stages (kt+1 read next, kt+2 and kt+3 in flight).
+  // MODE (probes): 1 = no k-loop DMA, 2 / 16 = no gallery / query block in the DMA.
+  template <int MODE>
+  static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
+                                                  int nst, f32x16 (&acc)[4][CT]) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < CT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto issue = [&](int kt) { dma<MODE & 18>(G, gp, Q, qp, nst, kt, smem + (kt % NST) * STAGE); };
+    // branch-free: a stage past the end re-loads the last one onto itself (same bytes)
+    const int last = nst - 1;
+    static_assert(NST == 3, "hand-off below assumes 3 stages");
+#pragma unroll
+    for (int s = 0; s < NST; ++s) issue(s < last ? s : last);
+
+    i32x8 ga[2][4], qb[2][CT];
+    auto frags = [&](const char* st, int j) {
+#pragma unroll
+      for (int c = 0; c < CT; ++c) qb[j][c] = frag(st + PANEL, j, h, wc * QW + c * 32 + r32);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ga[j][i] = frag(st, j, h, wr * 128 + i * 32 + r32);
+    };
+    auto mfmas = [&](int j) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+          acc[i][c] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ga[j][i], qb[j][c], acc[i][c], 2, 2, 0,
+                                                                      0x7f7f7f7f, 0, 0x7f7f7f7f);
+    };
+
+    if constexpr (MODE == 1) wait_vm<0>();
+    else wait_vm<2 * IPW>();   // stage 0 landed; 1 and 2 may be in flight
+    barrier();
+    frags(smem, 0);
+    for (int kt = 0; kt < last; ++kt) {
+      frags(smem + (kt % NST) * STAGE, 1);
+      mfmas(0);
+      interleave();
+      if constexpr (MODE == 1) wait_vm<0>();
+      else wait_vm<IPW>();     // stage kt+1 landed; kt+2 may be in flight
+      barrier();
+      if constexpr (MODE != 1) {
+        const int nx = kt + NST;
+        issue(nx < last ? nx : last);
+      }
+      frags(smem + ((kt + 1) % NST) * STAGE, 0);
+      mfmas(1);
+      interleave();
+      __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
+    }
+    frags(smem + (last % NST) * STAGE, 1);
+    mfmas(0);
+    interleave();
+    mfmas(1);
+    wait_vm<0>();
+    barrier();
+  }
+};
 
 }  // namespace f6t
 }  // namespace ofr

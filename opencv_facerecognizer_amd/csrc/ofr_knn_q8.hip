@@ -261,9 +261,11 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
           }
         }
       };
-      static_assert(CT <= 2, "sieve unroll");
+      static_assert(CT <= 4, "sieve unroll");
       one(std::integral_constant<int, 0>{});
       one(std::integral_constant<int, 1>{});
+      one(std::integral_constant<int, 2>{});
+      one(std::integral_constant<int, 3>{});
     }
   __syncthreads();
   const uint32_t n = *nhit < (uint32_t)SIEVE_HCAP ? *nhit : (uint32_t)SIEVE_HCAP;
@@ -295,14 +297,16 @@ __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
   });
 }
 
-// fp6 tier: p.G / p.Q are f6 tiled buffers (ofr_f6_tile.h), p.nk = stages.  MODE 0: tile lists
-// (tile t = gallery panel t * gstride, the sieve's sample pass); 8: the sieve.  MODE bits 1/2 go
-// to the main loop (probes); 4 skips the epilogue (probe).
-template <int MODE>
-__global__ void __launch_bounds__(f6t::NT, 1) tile_kernel_f6(TileArgs p) {
+// fp6 tier: p.G / p.Q are f6 tiled buffers (ofr_f6_tile.h), p.nk = stages, NW waves
+// (f6t::Engine).  MODE 0: tile lists (tile t = gallery panel t * gstride, the sieve's sample
+// pass); 8: the sieve.  Probe bits: 1 / 2 / 16 = no k-loop DMA / gallery DMA / query DMA,
+// 4 = no epilogue.
+template <int NW, int MODE>
+__global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
+  using E = f6t::Engine<NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool SIEVE = (MODE & 8) != 0;
-  constexpr int CT = f6t::CT;
+  constexpr int CT = E::CT;
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   int64_t gt, qt;
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
@@ -311,23 +315,23 @@ __global__ void __launch_bounds__(f6t::NT, 1) tile_kernel_f6(TileArgs p) {
   // sieve operands, loaded under the main loop
   float ga = __builtin_inff(), gs = 0.f, sq2[CT], th[CT];
   if constexpr (SIEVE) {
-    const int64_t g = g0 + threadIdx.x;
-    if (threadIdx.x < TG && g < p.N) {
-      ga = p.aux[g];
-      gs = p.gscale[g];
+    static_assert(E::NT >= TG, "one gallery row per thread");
+    if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
+      ga = p.aux[g0 + threadIdx.x];
+      gs = p.gscale[g0 + threadIdx.x];
     }
-    const int wc = (threadIdx.x >> 6) % f6t::WQ, r32 = threadIdx.x & 31;
+    const int wc = (threadIdx.x >> 6) % E::WQ, r32 = threadIdx.x & 31;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
-      const int64_t q = q0 + wc * f6t::QW + c * 32 + r32;
+      const int64_t q = q0 + wc * E::QW + c * 32 + r32;
       const bool ok = q < p.B;
       sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
       th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
     }
   }
   f6t::f32x16 acc[4][CT];
-  f6t::mainloop<MODE & 3>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
-                          p.nk, acc);
+  E::template mainloop<MODE & 19>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q),
+                                 qt, p.nk, acc);
   if constexpr ((MODE & 4) != 0) {   // probe: no epilogue (the accumulators kept alive)
     float s = 0.f;
 #pragma unroll
@@ -344,9 +348,9 @@ __global__ void __launch_bounds__(f6t::NT, 1) tile_kernel_f6(TileArgs p) {
     return acc[rt][ct][r];
   };
   if constexpr (SIEVE)
-    sieve_epilogue<CT, f6t::TQ, f6t::QW, f6t::WQ>(smem, p, g0, q0, ga, gs, sq2, th, cval);
+    sieve_epilogue<CT, f6t::TQ, E::QW, E::WQ>(smem, p, g0, q0, ga, gs, sq2, th, cval);
   else
-    tile_epilogue<CT, f6t::TQ, f6t::QW, f6t::WQ>(smem, p, gt, g0, q0, cval);
+    tile_epilogue<CT, f6t::TQ, E::QW, E::WQ>(smem, p, gt, g0, q0, cval);
 }
 
 // ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
@@ -921,6 +925,9 @@ extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int
   return OFR_OK;
 }
 
+// waves of the fp6 tile engine (f6t::Engine; tools/f6_probe.hip times both)
+constexpr int F6_NW = 8;
+
 // f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
 // thresholds, counts and buckets (each 256-byte aligned)
 struct SieveWs {
@@ -981,7 +988,7 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
     } else {
       static bool attr_done = false;
       if (!attr_done) {
-        for (const void* f : {(const void*)q8s::tile_kernel_f6<0>, (const void*)q8s::tile_kernel_f6<8>}) {
+        for (const void* f : {(const void*)q8s::tile_kernel_f6<F6_NW, 0>, (const void*)q8s::tile_kernel_f6<F6_NW, 8>}) {
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
         }
@@ -993,7 +1000,8 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
       s.ntg = cdiv(a.ntg, q8s::SIEVE_STRIDE);
       s.gg = s.ntg < q8s::GROUP_G ? s.ntg : q8s::GROUP_G;
       s.cand = reinterpret_cast<Cand*>(wsb + w.lists);
-      hipLaunchKernelGGL((q8s::tile_kernel_f6<0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(f6t::NT), f6t::LDS, st, s);
+      hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64), f6t::LDS,
+                         st, s);
       OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
       hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)B), dim3(256), 0, st, s.cand, s.ntg, theta,
                          count);
@@ -1002,8 +1010,8 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
       a.count = count;
       a.bucket = bucket;
       a.cap = q8s::SIEVE_CAP;
-      hipLaunchKernelGGL((q8s::tile_kernel_f6<8>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::NT), f6t::LDS, st,
-                         a);
+      hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 8>), dim3((unsigned)(a.ntq * a.ntg)), dim3(F6_NW * 64), f6t::LDS,
+                         st, a);
       OFR_LAUNCH_CHECK("f6 tile_kernel (sieve)");
     }
   }

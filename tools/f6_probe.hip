@@ -1,6 +1,5 @@
 // Feed / compute probe for the fp6 tile kernel (diagnostic tool, not part of the library).
-// Times q8s::tile_kernel_f6<MODE> on random e2m3 tiles: MODE 0 = search, 1 = no k-loop DMA
-// (MFMA + LDS only), 2 = no MFMA (DMA feed only), for several tile-group sizes.
+// Times q8s::tile_kernel_f6<NW, MODE> on random e2m3 tiles (MODE bits: see main).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/f6_probe.hip \
 //         opencv_facerecognizer_amd/csrc/ofr_api.hip -o tools/f6_probe
 //   ./tools/f6_probe [N] [B] [d] [reps]
@@ -24,23 +23,23 @@ __global__ void fill_f(float* p, size_t n, float v) {
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
-template <int MODE>
+template <int NW, int MODE>
 static int run(q8s::TileArgs a, int reps, const char* tag) {
   const double ops = 2.0 * (double)a.ntg * f6t::TA * a.ntq * f6t::TQ * a.nk * f6t::BK;
-  CK(hipFuncSetAttribute((const void*)q8s::tile_kernel_f6<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS));
+  CK(hipFuncSetAttribute((const void*)q8s::tile_kernel_f6<NW, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const unsigned grid = (unsigned)(a.ntq * a.ntg);
-  hipLaunchKernelGGL((q8s::tile_kernel_f6<MODE>), dim3(grid), dim3(f6t::NT), f6t::LDS, 0, a);
+  hipLaunchKernelGGL((q8s::tile_kernel_f6<NW, MODE>), dim3(grid), dim3(NW * 64), f6t::LDS, 0, a);
   CK(hipGetLastError());
   CK(hipEventRecord(e0));
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((q8s::tile_kernel_f6<MODE>), dim3(grid), dim3(f6t::NT), f6t::LDS, 0, a);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((q8s::tile_kernel_f6<NW, MODE>), dim3(grid), dim3(NW * 64), f6t::LDS, 0, a);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= reps;
   const double bytes = (double)grid * a.nk * f6t::STAGE;
-  printf("f6 %-8s mode=%d gg=%-3ld ms=%8.2f  executed=%7.1f TOPS (%.1f%% of 10000)  LDS-fill=%6.2f TB/s\n", tag, MODE,
+  printf("f6 nw=%d %-12s mode=%-2d gg=%-3ld ms=%8.2f  executed=%7.1f TOPS (%.1f%% of 10000)  LDS-fill=%6.2f TB/s\n", NW, tag, MODE,
          (long)a.gg, ms, ops / ms / 1e9, ops / ms / 1e9 / 100.0, bytes / ms / 1e9);
   fflush(stdout);
   return 0;
@@ -85,11 +84,21 @@ int main(int argc, char** argv) {
   fill_u8<<<4096, 256>>>(Q, qb, 3);
   fill_f<<<1024, 256>>>(gs, N, 1.f); fill_f<<<1024, 256>>>(aux, N, 1.f); fill_f<<<64, 256>>>(qs, B, 1.f);
   CK(hipDeviceSynchronize());
-  q8s::TileArgs a;
+  q8s::TileArgs a{};
   a.G = (const int8_t*)G; a.N = N; a.ld = 0; a.gscale = gs; a.aux = aux;
   a.Q = (const int8_t*)Q; a.B = B; a.qscale = qs; a.cand = cand; a.ntg = ntg;
   a.ntq = f6t::panels(B);
   a.nk = (int)f6t::stages(d);
+  a.gstride = 1;
+  // sieve operands: a threshold below every score (-FLT_MAX): the pure cost of the test
+  uint32_t* theta;
+  int* count;
+  CK(hipMalloc(&theta, B * 4));
+  CK(hipMalloc(&count, B * 4));
+  std::vector<uint32_t> th(B, 0x00800000u);
+  CK(hipMemcpy(theta, th.data(), B * 4, hipMemcpyHostToDevice));
+  CK(hipMemset(count, 0, B * 4));
+  a.theta = theta; a.count = count; a.bucket = cand; a.cap = 16;
   printf("N=%ld B=%ld d=%ld\n", (long)N, (long)B, (long)d);
   if (getenv("STREAM_ONLY")) {
     for (int rep = 0; rep < 2; ++rep)
@@ -98,15 +107,13 @@ int main(int argc, char** argv) {
         return 1;
     return 0;
   }
-  const int ggs[] = {1, 2, 4, 8, 16};
-  for (int g : ggs) {
-    a.gg = g < ntg ? g : ntg;
-    if (run<0>(a, reps, "search")) return 1;
-  }
   a.gg = 4 < ntg ? 4 : ntg;
-  if (run<1>(a, reps, "no-dma")) return 1;
-  if (run<2>(a, reps, "no-mfma")) return 1;
-  if (run<4>(a, reps, "no-epilog")) return 1;
-  if (run<0>(a, reps, "search")) return 1;
+  // MODE bits: 8 = sieve epilogue (else tile lists); 4 = no epilogue; 1 = no k-loop DMA;
+  // 2 / 16 = no gallery / query block in the DMA
+  for (int rep = 0; rep < 2; ++rep) {
+    if (run<8, 8>(a, reps, "sieve") || run<8, 4>(a, reps, "noepi") || run<8, 5>(a, reps, "nodma") ||
+        run<8, 6>(a, reps, "no-gal-dma") || run<8, 20>(a, reps, "no-q-dma"))
+      return 1;
+  }
   return 0;
 }
