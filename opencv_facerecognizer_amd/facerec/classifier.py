@@ -41,9 +41,17 @@ class AbstractClassifier(object):
 
 
 def vote(sorted_y):
-    """classifier.py:121-123: most frequent label among the k nearest, ties -> smallest label."""
-    hist = dict((key, val) for key, val in enumerate(np.bincount(sorted_y)) if val)
-    return max(hist.items(), key=op.itemgetter(1))[0]
+    """classifier.py:121-123: most frequent label among the k nearest, ties -> smallest label.
+
+    The reference walks np.bincount(sorted_y), O(largest label) per query (1.8 s for 4096 queries
+    against 10k identities); np.unique gives the same answer in O(k log k).  Empty or negative
+    labels take the reference expression, which raises as it does there."""
+    sorted_y = np.asarray(sorted_y)
+    if sorted_y.size == 0 or sorted_y.min() < 0:
+        hist = dict((key, val) for key, val in enumerate(np.bincount(sorted_y)) if val)
+        return max(hist.items(), key=op.itemgetter(1))[0]
+    vals, counts = np.unique(sorted_y, return_counts=True)
+    return int(vals[np.argmax(counts)])
 
 
 class NearestNeighbor(AbstractClassifier):

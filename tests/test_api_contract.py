@@ -77,3 +77,24 @@ def test_compute_path_fails_loudly_without_gpu():
         ExtendedLBP()(np.zeros((5, 5), np.uint8))
     with pytest.raises(OfrError, match="no HIP device"):
         EuclideanDistance()(np.ones(3), np.zeros(3))
+
+
+def test_vote_matches_reference_expression():
+    """classifier.vote: the reference's bincount/dict/max (classifier.py:121-123) -- most frequent
+    label, ties to the smallest -- computed with np.unique; same value and type, same errors."""
+    import operator as op
+    from ocvfacerec.facerec.classifier import vote
+
+    def ref(sorted_y):
+        hist = dict((key, val) for key, val in enumerate(np.bincount(sorted_y)) if val)
+        return max(hist.items(), key=op.itemgetter(1))[0]
+
+    r = np.random.default_rng(7)
+    for _ in range(3000):
+        y = r.integers(0, r.integers(1, 40), r.integers(1, 17))
+        got = vote(y)
+        assert got == ref(y) and type(got) is int
+    with pytest.raises(ValueError):
+        vote(np.array([], dtype=np.int64))
+    with pytest.raises(ValueError):
+        vote(np.array([2, -1]))

@@ -453,6 +453,27 @@ def test_fisherfaces_compute_bundled(golden):
     assert (np.linalg.norm(feats - ref, axis=1) / np.linalg.norm(ref, axis=1)).max() < 1e-4
 
 
+def test_fisherfaces_eigh_solver_matches_eig(golden, monkeypatch):
+    """OFR_LDA_SOLVER=eigh (symmetric-definite LDA, feature.lda_eigen) trains the same model on the
+    bundled faces: W columns equal the reference-eig W up to sign, same resubstitution labels."""
+    from ocvfacerec.facerec.classifier import NearestNeighbor
+    from ocvfacerec.facerec.distance import EuclideanDistance
+    from ocvfacerec.facerec.feature import Fisherfaces
+    from ocvfacerec.facerec.model import PredictableModel
+    f = golden("individuals_faces.npz")
+    X, y = list(f["X"]), list(f["y"])
+    Ws = []
+    for solver in ("eig", "eigh"):
+        monkeypatch.setenv("OFR_LDA_SOLVER", solver)
+        m = PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=1))
+        m.compute(X, y)
+        Ws.append(np.asarray(m.feature.eigenvectors))
+        assert np.array_equal([p[0] for p in m.predict_batch(X)], f["resub_labels"])
+    W0, W1 = Ws
+    cos = np.abs(np.sum(W0 * W1, 0)) / (np.linalg.norm(W0, axis=0) * np.linalg.norm(W1, axis=0))
+    assert cos.min() > 1 - 1e-5, cos
+
+
 def test_gemm_f64_vs_numpy():
     from opencv_facerecognizer_amd._device import f64_dev, gemm_f64
     r = _rng(3)

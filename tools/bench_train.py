@@ -1,12 +1,14 @@
 """BASELINE.json configs[4] (Fisherfaces training) at a scale one box finishes in about a minute:
 n synthetic 100x100 faces of c identities, Fisherfaces().compute (PCA -> LDA, thetrainer.py:120 defaults).
 
-    python tools/bench_train.py [--n 4000] [--ids 400]
+    python tools/bench_train.py [--n 4000] [--ids 400] [--solver eig|eigh]
+    python tools/bench_train.py --n 100000 --ids 10000 --solver eigh     # configs[4] at full scale
 
 Splits the wall time into the host LAPACK eigensolves the reference itself calls (np.linalg.eigh for the
 PCA Gram / covariance, inv + eig for LDA, feature.py:94/170; timed by wrapping numpy) and the rest: the
 device work (centring, Gram, left vectors, class centring, Sw/Sb, W = P.L, feature projections on the
-fp64 / int8 MFMA) plus host transfers.  The CPU baseline runs the oracle's reference-faithful
+fp64 / int8 MFMA) plus host transfers.  --solver eigh times the symmetric-definite LDA eigensolve
+(feature.lda_eigen, sygvx/sygvd) instead of the reference's inv + eig.  The CPU baseline runs the oracle's reference-faithful
 Fisherfaces.compute (SVD, O(N^2) as_column_matrix) on a smaller sample and scales it by (n / n_cpu)^2
 (N^2 scaling measured).  Prints one JSON line.
 """
@@ -25,10 +27,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from opencv_facerecognizer_amd import _lib  # noqa: E402
+from opencv_facerecognizer_amd.facerec.classifier import NearestNeighbor  # noqa: E402
+from opencv_facerecognizer_amd.facerec.distance import EuclideanDistance  # noqa: E402
 from opencv_facerecognizer_amd.facerec.feature import Fisherfaces  # noqa: E402
+from opencv_facerecognizer_amd.facerec.model import PredictableModel  # noqa: E402
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 
-HOST = {"eigh": 0.0, "eig": 0.0, "inv": 0.0}
+HOST = {"eigh": 0.0, "eig": 0.0, "inv": 0.0, "sygv": 0.0}
 
 
 def _timed(name, fn):
@@ -53,25 +58,50 @@ def main():
     ap.add_argument("--ids", type=int, default=400)
     ap.add_argument("--side", type=int, default=100)
     ap.add_argument("--n-cpu", type=int, default=600)
+    ap.add_argument("--solver", choices=["eig", "eigh"], default="eig")
+    ap.add_argument("--predict", type=int, default=4096)
     args = ap.parse_args()
     device = _lib.device()
     X, y = faces(args.n, args.ids, args.side, device, SEED + 21)
     la = np.linalg
     la.eigh, la.eig, la.inv = _timed("eigh", la.eigh), _timed("eig", la.eig), _timed("inv", la.inv)
-    ff = Fisherfaces()
+    import scipy.linalg
+    scipy.linalg.eigh = _timed("sygv", scipy.linalg.eigh)
+    os.environ["OFR_LDA_SOLVER"] = args.solver
+    # the reference's training call: PredictableModel.compute = Fisherfaces.compute + NearestNeighbor.compute
+    # (model.py:49-51, thetrainer.py:176)
+    model = PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=1))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    feats = ff.compute(X, y)
+    model.compute(X, y)
     torch.cuda.synchronize()
     total = time.perf_counter() - t0
+    ff = model.feature
+    feats = model.classifier.X
+    # then predict (configs[4]): fresh faces of random identities, one batch; the first call also
+    # builds the device gallery from the training features
+    gq = torch.Generator(device=device)
+    gq.manual_seed(SEED + 23)
+    ids_q = torch.randint(0, args.ids, (args.predict,), generator=gq, device=device)
+    Xq = IdentityBank(args.ids, args.side, args.side, device=device).images(ids_q, seed=SEED + 24)
+    Xq = Xq.reshape(args.predict, args.side, args.side).cpu().numpy()
+    pred_s = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        labels = np.array([p[0] for p in model.predict_batch(Xq)])
+        torch.cuda.synchronize()
+        pred_s.append(time.perf_counter() - t1)
+    acc = float((labels == ids_q.cpu().numpy()).mean())
     host = sum(HOST.values())
     n, D, c = args.n, args.side * args.side, args.ids
-    k = min(n - c, n - 1)
+    k = min(n - c, n - 1, D)     # PCA components (feature.py:88-89, at most min(D, N) singular vectors)
     d = c - 1
     W = np.asarray(ff._eigenvectors)
-    # resubstitution 1-NN on the training features (sanity, host)
     F = np.stack([np.asarray(f).reshape(-1) for f in feats])
-    flops = {"pca_gram": 2.0 * n * n * D, "pca_left_vectors": 2.0 * D * n * n, "pca_features": 2.0 * n * D * k,
+    pca = ({"pca_gram": 2.0 * n * n * D, "pca_left_vectors": 2.0 * D * n * n} if n <= D else
+           {"pca_covariance": 2.0 * n * D * D})
+    flops = {**pca, "pca_features": 2.0 * n * D * k,
              "lda_sw": 2.0 * k * k * n, "lda_sb": 2.0 * k * k * c, "lda_features": 2.0 * n * k * d,
              "w_pl": 2.0 * D * k * d, "train_projection_int8x4": 4 * 2.0 * n * D * d}
 
@@ -82,10 +112,13 @@ def main():
     O.fisherfaces_compute([x.astype(np.uint8) for x in Xc], yc)
     t_cpu = time.perf_counter() - t1
     out = {
-        "metric": "Fisherfaces.compute wall time (configs[4] at reduced scale)",
-        "config": {"n": n, "identities": c, "D": D, "pca_components": k, "d": d},
+        "metric": "PredictableModel(Fisherfaces, NearestNeighbor).compute wall time, then predict (configs[4])",
+        "config": {"n": n, "identities": c, "D": D, "pca_components": k, "d": d, "lda_solver": args.solver},
         "data": "synthetic",
         "wall_s": total, "host_lapack_s": dict(HOST), "device_and_transfers_s": total - host,
+        "predict": {"batch": args.predict, "first_call_s": pred_s[0], "steady_s": min(pred_s[1:]),
+                    "queries_per_s": args.predict / min(pred_s[1:]), "top1_identity_acc": acc,
+                    "note": "first call builds the device gallery (upload + quantized tiers) from the training features"},
         "device_flops": flops, "device_flops_total": sum(flops.values()),
         "device_tflops_upper_bound": sum(flops.values()) / max(total - host, 1e-9) / 1e12,
         "W_shape": list(W.shape), "finite": bool(np.isfinite(W).all() and np.isfinite(F).all()),
