@@ -270,6 +270,9 @@ def main():
     ms_merge = np.mean([e[2].elapsed_time(e[3]) for e in ev])
     idx = res[1][:, 0]
     acc = float(((idx // args.per_id) == ids_q).double().mean().item())
+    kept = gallery.sieve_counts(B) if args.search == "f6" else None   # last step's fp6 sieve (this rank)
+    kept = None if kept is None else {"mean": float(kept.double().mean()), "max": int(kept.max()),
+                                      "cap": 32768, "expected": "~16 x OFR_SIEVE_STRIDE (64)"}
 
     # ---- small-batch regime (the recognizers send one face per call): HBM-bound streaming of the gallery ----
     small = []
@@ -325,7 +328,8 @@ def main():
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
     if args.search == "f6":
-        peak, kname = PEAK_F6_MFMA, "q8s::tile_kernel_f6 (ofr_knn_f6 phase 1, one fp6 e2m3 slice)"
+        peak, kname = PEAK_F6_MFMA, ("ofr_knn_f6 phase 1 (fp6 e2m3): q8s::tile_kernel_f6<8, 0> sample pass + "
+                                     "sieve_threshold_kernel + q8s::tile_kernel_f6<8, 8> sieve pass")
         alg_bytes_tiles = 0.75 * (nl * d + B * d)                    # 6 bits per feature, gallery + queries
         executed = flops_tiles
     elif use_q8:
@@ -367,6 +371,7 @@ def main():
                            "knn_merge_rerank" + ("+certificate+fallback" if use_q8 else ""): ms_merge},
             "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
             "uncertified_after_each_tier": (list(last_counts) if use_q8 else None),
+            "sieve_kept_rows_per_query": kept,
             "top1_identity_acc": acc,
             "small_batch": small,
         }

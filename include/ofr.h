@@ -166,12 +166,15 @@ int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, 
  * B <= 32: one streaming pass, best 16 per 256-row tile.  B > 32: a sieve --
  * a sample pass over every 64th tile sets a per-query keep threshold, the
  * full pass keeps only rows at or below it (the certificate uses min(threshold,
- * 16th kept)); a query whose bucket (8192 rows) overflows comes back with
+ * 16th kept)); a query whose bucket (32768 rows) overflows comes back with
  * cert 0 and bound -inf.  Phase 1 state lives in the workspace:
  * ofr_knn_f6_workspace_bytes(B, N) bytes, 16-byte aligned, kept between the
- * phase-1 and phase-2 calls.                                                 */
+ * phase-1 and phase-2 calls; after phase 1 the int32 kept-row counts [B] sit
+ * at byte ofr_knn_f6_sieve_counts_offset(B, N) of it (SIZE_MAX: no sieve,
+ * B <= 32).  Env OFR_SIEVE_STRIDE (default 64) sets the sample stride.       */
 size_t ofr_f6_tiles_bytes(int64_t R, int64_t d);
 size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N);
+size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N);
 int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
                          size_t tiles_bytes, float* scale, double* stats, const float* aux, double* maxima);
 int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,

@@ -11,6 +11,7 @@ Layouts:
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -311,6 +312,14 @@ class FloatGallery:
                  ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]),
                  ptr(qq["cert"]), ptr(qq["bound"]), ptr(ws), ws.numel())
         return out
+
+    def sieve_counts(self, B):
+        """Rows kept per query by the last fp6 sieve pass of a B-query batch (int32 device view of
+        the workspace, valid until the next search), or None when B <= 32 (no sieve)."""
+        off = _lib.load().ofr_knn_f6_sieve_counts_offset(B, self.N)
+        if off == ctypes.c_size_t(-1).value or self.ws.buf is None:
+            return None
+        return self.ws.buf[off:off + 4 * B].view(torch.int32)
 
     def fallback(self, Qd, qq, k, out, index_base=0):
         """Re-run the queries the first tier left uncertified down the tier chain (then fp32).

@@ -27,6 +27,7 @@
 //     S_k(exact) < tau - dS(q)
 // (strictly: no excluded row can reach or tie the k-th).  cert[q] = 1 then;
 // otherwise 0 and the caller re-runs that query on the fp32 path.
+#include <cstdlib>
 #include <type_traits>
 
 #include "ofr_f6_tile.h"
@@ -214,8 +215,8 @@ __device__ __forceinline__ void tile_epilogue(char* smem, const TileArgs& p, int
 // (truncated key > theta) or was kept and lost to the 16th, so tau = min(theta, 16th kept)
 // bounds every excluded row exactly as before.  theta only steers the volume: a bucket that
 // overflows its cap makes the query uncertified (bound -inf), never wrong.
-constexpr int64_t SIEVE_STRIDE = 64;   // sample: gallery tiles 0, 64, 128, ...
-constexpr int64_t SIEVE_CAP = 8192;    // kept rows per query (64 KiB)
+constexpr int64_t SIEVE_STRIDE = 64;   // sample: gallery tiles 0, 64, 128, ... (OFR_SIEVE_STRIDE overrides)
+constexpr int64_t SIEVE_CAP = 32768;   // kept rows per query (256 KiB; ~16 * SIEVE_STRIDE expected, heavy tail)
 constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
 
 // Hits of one 256 x 256 tile: (a, s) = (aux, gscale) of gallery row threadIdx.x (padding rows:
@@ -933,8 +934,17 @@ constexpr int F6_NW = 8;
 struct SieveWs {
   size_t lists, theta, count, bucket, bytes;
 };
+static int64_t sieve_stride() {
+  static const int64_t s = [] {
+    const char* e = getenv("OFR_SIEVE_STRIDE");
+    const long v = e ? atol(e) : 0;
+    return v >= 1 && v <= 4096 ? (int64_t)v : q8s::SIEVE_STRIDE;
+  }();
+  return s;
+}
+
 static SieveWs sieve_ws(int64_t B, int64_t N) {
-  const int64_t ts = cdiv(cdiv(N > 0 ? N : 1, q8s::TG), q8s::SIEVE_STRIDE);
+  const int64_t ts = cdiv(cdiv(N > 0 ? N : 1, q8s::TG), sieve_stride());
   SieveWs w;
   w.lists = 0;
   w.theta = round_up((int64_t)(B * ts * q8s::KC * sizeof(Cand)), 256);
@@ -946,6 +956,10 @@ static SieveWs sieve_ws(int64_t B, int64_t N) {
 
 extern "C" size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N) {
   return B <= 32 ? ofr_knn_q8_workspace_bytes(B, N) : sieve_ws(B, N).bytes;
+}
+
+extern "C" size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N) {
+  return B <= 32 ? (size_t)-1 : sieve_ws(B, N).count;
 }
 
 extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
@@ -996,8 +1010,8 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
       }
       // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel -> thresholds
       q8s::TileArgs s = a;
-      s.gstride = q8s::SIEVE_STRIDE;
-      s.ntg = cdiv(a.ntg, q8s::SIEVE_STRIDE);
+      s.gstride = sieve_stride();
+      s.ntg = cdiv(a.ntg, s.gstride);
       s.gg = s.ntg < q8s::GROUP_G ? s.ntg : q8s::GROUP_G;
       s.cand = reinterpret_cast<Cand*>(wsb + w.lists);
       hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64), f6t::LDS,

@@ -127,7 +127,7 @@ def test_knn_q8_certificate_forces_fallback(monkeypatch):
 
 def test_knn_f6_sieve_overflow_falls_back(monkeypatch):
     """The fp6 sieve (B > 32) keeps the rows at or below a sampled threshold in a per-query bucket of
-    8192 rows.  10,000 exact copies of one row all tie with the threshold, every bucket overflows:
+    32768 rows.  40,000 exact copies of one row all tie with the threshold, every bucket overflows:
     each query must come back uncertified from the fp6 tier and be resolved by the next tiers, with
     ties to the lowest index (the oracle's order)."""
     from opencv_facerecognizer_amd._device import FloatGallery
@@ -136,12 +136,17 @@ def test_knn_f6_sieve_overflow_falls_back(monkeypatch):
     r = _rng(1234)
     d = 96
     x = r.normal(0, 20, d)
-    G = np.concatenate([np.tile(x, (10000, 1)), r.normal(0, 20, (2000, d))]).astype(np.float32).astype(np.float64)
+    G = np.concatenate([np.tile(x, (40000, 1)), r.normal(0, 20, (2000, d))]).astype(np.float32).astype(np.float64)
     Q = (x + r.normal(0, 0.5, (40, d))).astype(np.float32).astype(np.float64)
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     dd, ii = g.search(g.query_rows(Q), 3)
     assert g.last_fallbacks[0] == 40
     assert (ii.cpu().numpy() == np.array([0, 1, 2])).all()
+    # the kept-row counts of the fp6 pass: every duplicate (and nothing less) passed the threshold
+    qq = g.quantize_queries(g.query_rows(Q), tier="f6")
+    g.search_q8_phase(1, g.query_rows(Q), qq, 3)
+    cnt = g.sieve_counts(40).cpu().numpy()
+    assert (cnt >= 40000).all(), cnt
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
 
 

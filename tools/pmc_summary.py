@@ -1,6 +1,9 @@
 """Summarise the rocprofv3 passes of tools/prof_search.sh (gpurun_out/prof) into profiles/.
 
-    python tools/pmc_summary.py <name> [kernel-substring]
+    python tools/pmc_summary.py <name> ["kernel-substring[;kernel-substring...]"]
+
+Several substrings (the kernels of one phase, e.g. the fp6 sieve's sample pass, thresholds and
+sieve pass) are summed: durations and counters per phase launch, with the per-kernel split.
 
 writes profiles/<name>_kernel_stats.csv (the --stats table) and profiles/<name>_pmc_summary.json
 (per-launch counters of the search tile kernel; traffic = FETCH_SIZE x 2 + WRITE_SIZE, the gfx950
@@ -32,14 +35,19 @@ def counters(kname):
 
 def main():
     name = sys.argv[1]
-    kname = sys.argv[2] if len(sys.argv) > 2 else "tile_kernel_f6<0>"
+    knames = (sys.argv[2] if len(sys.argv) > 2 else "tile_kernel_f6<8, 8>").split(";")
     stats = os.path.join(P, "kt", "kt_kernel_stats.csv")
     shutil.copy(stats, os.path.join(ROOT, "profiles", f"{name}_kernel_stats.csv"))
-    avg_ns = None
-    for r in csv.DictReader(open(stats)):
-        if kname in r["Name"]:
-            avg_ns = float(r["AverageNs"])
-    c, n = counters(kname)
+    rows = list(csv.DictReader(open(stats)))
+    per = {}
+    for kn in knames:
+        ns = [float(r["AverageNs"]) for r in rows if kn in r["Name"]]
+        c, n = counters(kn)
+        per[kn] = {"rocprof_avg_ns": ns[-1] if ns else None, "launches": n, "counters_per_launch": c}
+    c = collections.Counter()
+    for v in per.values():
+        c.update(v["counters_per_launch"])
+    avg_ns = sum(v["rocprof_avg_ns"] or 0.0 for v in per.values()) or None
     log = open(os.path.join(P, "kt.log")).read().strip().splitlines()
     bench = json.loads([ln for ln in log if ln.startswith("{")][-1])
     cfg = bench["config"]
@@ -47,8 +55,10 @@ def main():
         "config": {"gallery": cfg["gallery"], "batch": cfg["global_batch"], "d": cfg["d"], "D": cfg["D"],
                    "k": cfg["k"],
                    "search": "f6" if "fp6" in bench["dtype"] else ("q8" if "i8" in bench["dtype"] else "fp32")},
-        "kernel": kname, "launches": n, "rocprof_avg_ns": avg_ns,
-        "counters_per_launch": c,
+        "kernel": " + ".join(knames), "launches": min(v["launches"] for v in per.values()), "rocprof_avg_ns": avg_ns,
+        "bench_launch_ms": bench["roofline"].get("launch_ms"),
+        "counters_per_launch": dict(c),
+        "per_kernel": per if len(knames) > 1 else None,
         "correction": "gfx950: FETCH_SIZE reports half of the bytes of wide coalesced streaming reads "
                       "(MI355X_MICROARCH.md §HBM) -> x2; WRITE_SIZE exact for 16-B stores",
     }
