@@ -173,6 +173,13 @@ int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, 
  * at byte ofr_knn_f6_sieve_counts_offset(B, N) of it (SIZE_MAX: no sieve,
  * B <= 32).  Env OFR_SIEVE_STRIDE (default 64) sets the sample stride.       */
 size_t ofr_f6_tiles_bytes(int64_t R, int64_t d);
+/* Append support (NearestNeighbor.update, classifier.py:65-70): quantize X's R rows
+ * into rows row0 .. row0+R-1 of an existing tiled buffer (scale/stats indexed by
+ * the destination row), zeroing the rest of the last panel; then recompute the
+ * gallery maxima over all rows with ofr_q8_maxima.                           */
+int ofr_f6_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int64_t row0,
+                            void* tiles, size_t tiles_bytes, float* scale, double* stats);
+int ofr_q8_maxima(void* stream, const double* stats, const float* aux, int64_t R, double* maxima);
 size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N);
 size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N);
 int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,

@@ -194,12 +194,54 @@ class FloatGallery:
         return self
 
     def _finish(self, device):
-        self.aux = torch.empty(max(self.N, 1), dtype=torch.float32, device=device)
+        self._Gbuf = self.G                      # rows [capacity][ld]; self.G = the first N
+        self._auxbuf = torch.empty(max(self.N, 1), dtype=torch.float32, device=device)
+        self.aux = self._auxbuf
         if self.N > 0:
             call("ofr_row_aux", stream(), self.metric, ptr(self.G), self.N, self.d, self.ld, ptr(self.aux))
         self.ws = Workspace()
         self.q8 = None
         self.last_fallbacks = 0
+
+    def capacity(self):
+        return int(self._Gbuf.shape[0])
+
+    def append(self, feats):
+        """Append gallery rows in place (NearestNeighbor.update, classifier.py:65-70): the new rows are
+        centred on the EXISTING shift (any shift keeps distances exact; the first rows' mean keeps the
+        fp32 rounding small), their aux terms and every built quantized tier are extended, the tier
+        maxima recomputed.  Storage grows geometrically; a growth re-allocates and copies on the device
+        and drops the quantized tiers (rebuilt on the next search).  Returns the new row count."""
+        dev_ = self.G.device
+        F = feats.to(device=dev_, dtype=torch.float64).contiguous() if isinstance(feats, torch.Tensor) else \
+            f64_dev(np.asarray(feats, np.float64).reshape(-1, self.d), device=dev_)
+        if F.ndim != 2 or F.shape[1] != self.d:
+            raise ValueError(f"appended rows must have {self.d} features")
+        n = int(F.shape[0])
+        if n == 0:
+            return self.N
+        if self.N == 0:
+            raise ValueError("append to an empty gallery: build it from the rows instead")
+        N0, N1 = self.N, self.N + n
+        if N1 > self.capacity():
+            cap = max(N1, self.capacity() + self.capacity() // 2, 256)
+            G = torch.zeros((cap, self.ld), dtype=torch.float32, device=dev_)
+            G[:N0].copy_(self._Gbuf[:N0])
+            aux = torch.empty(cap, dtype=torch.float32, device=dev_)
+            aux[:N0].copy_(self._auxbuf[:N0])
+            self._Gbuf, self._auxbuf, self.q8 = G, aux, None
+        center_round(F, self.shift64, self.ld, out=self._Gbuf[N0:N1])
+        call("ofr_row_aux", stream(), self.metric, ptr(self._Gbuf[N0:]), n, self.d, self.ld, ptr(self._auxbuf[N0:]))
+        self.N, self.G, self.aux = N1, self._Gbuf[:N1], self._auxbuf[:N1]
+        for tier, g in (self.q8 or {}).items():
+            if tier == "f6":
+                call("ofr_f6_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, ptr(g["Gs"]),
+                     g["Gs"].numel(), ptr(g["scale"]), ptr(g["stats"]))
+            else:
+                call("ofr_q8_quantize_rows", stream(), tier, ptr(self.G[N0:]), n, self.d, self.ld, ptr(g["Gs"][N0:]),
+                     g["ld"], ptr(g["scale"][N0:]), ptr(g["stats"][N0:]), None, None)
+            call("ofr_q8_maxima", stream(), ptr(g["stats"]), ptr(self.aux), N1, ptr(g["gmax"]))
+        return self.N
 
     # -- certified quantized coarse passes (Euclidean, B > 32) -------------------------------------
     # Tier "f6": one fp6 (e2m3) slice per row with an fp32 row scale (x~ = s v), fp6 MFMA at twice
@@ -236,18 +278,19 @@ class FloatGallery:
             self.q8 = {}
         if tier not in self.q8:
             dev_ = self.G.device
-            gs = torch.empty(self.N, dtype=torch.float32, device=dev_)
-            st = torch.empty((self.N, 3), dtype=torch.float64, device=dev_)
+            cap = self.capacity()                 # sized for the row storage (append fills in place)
+            gs = torch.empty(cap, dtype=torch.float32, device=dev_)
+            st = torch.empty((cap, 3), dtype=torch.float64, device=dev_)
             gmax = torch.empty(4, dtype=torch.float64, device=dev_)
             if tier == "f6":
-                nbytes = _lib.load().ofr_f6_tiles_bytes(self.N, self.d)
+                nbytes = _lib.load().ofr_f6_tiles_bytes(cap, self.d)
                 Gs = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
                 call("ofr_f6_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, ptr(Gs), nbytes,
                      ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
                 ld = 0
             else:
                 ld = self._q8_ld(self.d, tier)
-                Gs = torch.empty((self.N, ld), dtype=torch.int8, device=dev_)
+                Gs = torch.empty((cap, ld), dtype=torch.int8, device=dev_)
                 call("ofr_q8_quantize_rows", stream(), tier, ptr(self.G), self.N, self.d, self.ld, ptr(Gs), ld,
                      ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
             self.q8[tier] = dict(Gs=Gs, scale=gs, stats=st, gmax=gmax, ld=ld)
@@ -404,7 +447,30 @@ class Chi2Gallery:
             self.nbins = int(arr.shape[1])
             self.G = f32_rows(arr, ld=max(4, round_up(self.nbins, 4)), device=device)
         self.N = int(self.G.shape[0])
+        self._Gbuf = self.G
         self.ws = Workspace()
+
+    def append(self, rows):
+        """Append rows in place (NearestNeighbor.update): host float rows for fp32 galleries, or a
+        device tensor of the gallery's element type; geometric growth.  Returns the new row count."""
+        if isinstance(rows, torch.Tensor) and rows.dtype == self._Gbuf.dtype:
+            new = torch.zeros((rows.shape[0], self._Gbuf.shape[1]), dtype=rows.dtype, device=self._Gbuf.device)
+            new[:, :rows.shape[1]] = rows.to(self._Gbuf.device)
+        elif self.dtype == _lib.DT_F32:
+            new = f32_rows(np.asarray(rows, np.float64).reshape(-1, self.nbins), ld=self._Gbuf.shape[1],
+                           device=self._Gbuf.device)
+        else:
+            raise TypeError("append to a count gallery takes a device tensor of its element type")
+        n = int(new.shape[0])
+        N0, N1 = self.N, self.N + n
+        if N1 > self._Gbuf.shape[0]:
+            cap = max(N1, self._Gbuf.shape[0] + self._Gbuf.shape[0] // 2, 256)
+            G = torch.zeros((cap, self._Gbuf.shape[1]), dtype=self._Gbuf.dtype, device=self._Gbuf.device)
+            G[:N0].copy_(self._Gbuf[:N0])
+            self._Gbuf = G
+        self._Gbuf[N0:N1].copy_(new)
+        self.N, self.G = N1, self._Gbuf[:N1]
+        return self.N
 
     def search(self, Qd, k, index_base=0):
         B = Qd.shape[0]

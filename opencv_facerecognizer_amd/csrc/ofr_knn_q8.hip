@@ -705,11 +705,11 @@ __device__ __forceinline__ uint32_t e2m3_code(double r, double& q) {
 }
 
 __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_t ldx, int64_t d, int64_t nst,
-                                                          char* tiles, float* scale, double* stats) {
+                                                          int64_t row0, char* tiles, float* scale, double* stats) {
   __shared__ float redf[4];
   __shared__ double red[4][2];
-  const int64_t row = blockIdx.x;
-  const float* x = X + row * ldx;
+  const int64_t row = row0 + blockIdx.x;   // destination row (X row blockIdx.x)
+  const float* x = X + (int64_t)blockIdx.x * ldx;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float mx = 0.f;
   for (int64_t i = threadIdx.x; i < d; i += blockDim.x) mx = fmaxf(mx, fabsf(x[i]));
@@ -901,29 +901,40 @@ extern "C" size_t ofr_f6_tiles_bytes(int64_t R, int64_t d) {
   return R <= 0 || d <= 0 ? 0 : (size_t)f6t::tiles_bytes(R, d);
 }
 
+extern "C" int ofr_f6_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx,
+                                       int64_t row0, void* tiles, size_t tiles_bytes, float* scale, double* stats) {
+  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d && row0 >= 0, "ofr_f6_quantize_rows_at: bad sizes");
+  if (R == 0) return OFR_OK;
+  OFR_CHECK_ARG(X && tiles && scale && stats, "ofr_f6_quantize_rows_at: null pointer");
+  OFR_CHECK_ARG(row0 + R < 0x7fffffffLL, "ofr_f6_quantize_rows_at: too many rows");
+  OFR_CHECK_ARG(tiles_bytes >= ofr_f6_tiles_bytes(row0 + R, d), "ofr_f6_quantize_rows_at: tile buffer too small");
+  OFR_CHECK_ARG((uintptr_t)tiles % 16 == 0, "ofr_f6_quantize_rows_at: tiles must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nst = f6t::stages(d);
+  hipLaunchKernelGGL(q8s::quantize_f6_kernel, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
+                     (char*)tiles, scale, stats);
+  OFR_LAUNCH_CHECK("f6 quantize_kernel");
+  const int64_t end = row0 + R;
+  if (end % 256) {
+    hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)tiles, end, nst);
+    OFR_LAUNCH_CHECK("f6 zero_tail");
+  }
+  return OFR_OK;
+}
+
+extern "C" int ofr_q8_maxima(void* stream, const double* stats, const float* aux, int64_t R, double* maxima) {
+  OFR_CHECK_ARG(R >= 0 && stats && maxima, "ofr_q8_maxima: bad arguments");
+  hipLaunchKernelGGL(q8s::maxima_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, stats, aux, R, maxima);
+  OFR_LAUNCH_CHECK("q8 maxima_kernel");
+  return OFR_OK;
+}
+
 extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
                                     size_t tiles_bytes, float* scale, double* stats, const float* aux,
                                     double* maxima) {
-  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d, "ofr_f6_quantize_rows: bad sizes");
-  if (R == 0) return OFR_OK;
-  OFR_CHECK_ARG(X && tiles && scale && stats, "ofr_f6_quantize_rows: null pointer");
-  OFR_CHECK_ARG(R < 0x7fffffffLL, "ofr_f6_quantize_rows: too many rows");
-  OFR_CHECK_ARG(tiles_bytes >= ofr_f6_tiles_bytes(R, d), "ofr_f6_quantize_rows: tile buffer too small");
-  OFR_CHECK_ARG((uintptr_t)tiles % 16 == 0, "ofr_f6_quantize_rows: tiles must be 16-byte aligned");
-  hipStream_t st = (hipStream_t)stream;
-  const int64_t nst = f6t::stages(d);
-  hipLaunchKernelGGL(q8s::quantize_f6_kernel, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, (char*)tiles,
-                     scale, stats);
-  OFR_LAUNCH_CHECK("f6 quantize_kernel");
-  if (R % 256) {
-    hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)tiles, R, nst);
-    OFR_LAUNCH_CHECK("f6 zero_tail");
-  }
-  if (maxima) {
-    hipLaunchKernelGGL(q8s::maxima_kernel, dim3(1), dim3(256), 0, st, stats, aux, R, maxima);
-    OFR_LAUNCH_CHECK("q8 maxima_kernel");
-  }
-  return OFR_OK;
+  const int rc = ofr_f6_quantize_rows_at(stream, X, R, d, ldx, 0, tiles, tiles_bytes, scale, stats);
+  if (rc || R == 0 || !maxima) return rc;
+  return ofr_q8_maxima(stream, stats, aux, R, maxima);
 }
 
 // waves of the fp6 tile engine (f6t::Engine; tools/f6_probe.hip times both)

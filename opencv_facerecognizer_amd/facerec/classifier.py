@@ -114,21 +114,30 @@ class NearestNeighbor(AbstractClassifier):
         self.__dict__.pop("_dev", None)
 
     def _gallery(self):
+        """Device gallery of self.X, built once and extended in place when items were appended
+        (update, or X grown by the caller): an update costs the new rows, not a re-upload."""
         mid = self._metric()
-        key = (mid, len(self.X), id(self.X), _lib.device())
+        key = (mid, id(self.X), _lib.device())
+        n = len(self.X)
+        if n > len(self.y):
+            raise Exception("More distances than classes. Is your distance metric correct?")  # classifier.py:109-110
         cache = self.__dict__.get("_dev")
         if cache is not None and cache[0] == key:
-            return cache[1]
-        if len(self.X) > len(self.y):
-            raise Exception("More distances than classes. Is your distance metric correct?")  # classifier.py:109-110
-        feats = np.stack([np.asarray(x, dtype=np.float64).reshape(-1) for x in self.X]) if len(self.X) else \
-            np.zeros((0, 1))
-        if mid == _lib.METRIC_CHISQUARE:
-            g = Chi2Gallery(feats)
-        else:
-            g = FloatGallery(feats, mid)
-        self.__dict__["_dev"] = (key, g)
+            n0, g = cache[1], cache[2]
+            if n0 == n:
+                return g
+            if 0 < n0 < n and g.N == n0:
+                g.append(self._stack(self.X[n0:]))
+                self.__dict__["_dev"] = (key, n, g)
+                return g
+        feats = self._stack(self.X) if n else np.zeros((0, 1))
+        g = Chi2Gallery(feats) if mid == _lib.METRIC_CHISQUARE else FloatGallery(feats, mid)
+        self.__dict__["_dev"] = (key, n, g)
         return g
+
+    @staticmethod
+    def _stack(items):
+        return np.stack([np.asarray(x, dtype=np.float64).reshape(-1) for x in items])
 
     def _queries(self, Q):
         g = self._gallery()

@@ -246,6 +246,76 @@ def test_knn_exact_duplicates_tie_to_lowest_index():
     assert np.all(dd.cpu().numpy() == 0)
 
 
+@pytest.mark.parametrize("mode", ["auto", "fp32"])
+def test_gallery_append_in_place_vs_oracle(monkeypatch, mode):
+    """FloatGallery.append (NearestNeighbor.update without a re-upload): rows appended in chunks that
+    cross 256-row panels, with the fp6 / int8 tiers already built (extended in place) and across a
+    storage growth (tiers dropped, rebuilt); every search matches the oracle on the full set."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", mode)
+    r = _rng(77)
+    d = 130
+    protos = r.normal(0, 30, (900, d))
+    G = (protos[np.arange(9000) % 900] + r.normal(0, 5, (9000, d))).astype(np.float32).astype(np.float64)
+    Q = (protos[r.integers(0, 900, 300)] + r.normal(0, 5, (300, d))).astype(np.float32).astype(np.float64)
+    g = FloatGallery(G[:1000], _lib.METRIC_EUCLIDEAN)
+    n = 1000
+    for step, m in enumerate([1, 255, 200, 2444, 5000]):   # steps 1-2 in place (capacity 1500), then growth
+        if step == 1:
+            g.search(g.query_rows(Q[:64]), 1)       # build the first tier before the next appends
+            if mode == "auto":
+                g._tier_gallery(1)                  # and the int8 tier
+        g.append(G[n:n + m])
+        n += m
+        assert g.N == n and g.G.shape[0] == n
+        for B, k in [(300, 1), (5, 3)]:
+            dd, ii = g.search(g.query_rows(Q[:B]), k)
+            _check_search("EuclideanDistance", Q[:B], G[:n], dd.cpu().numpy(), ii.cpu().numpy(), k)
+        if mode == "auto":
+            assert g.last_fallbacks[0] <= 30
+
+
+def test_nearest_neighbor_update_extends_device_gallery():
+    """NearestNeighbor.update (classifier.py:65-70) appends to the cached device gallery instead of
+    rebuilding it; predictions equal the oracle's on the grown set; a new X list rebuilds."""
+    from ocvfacerec.facerec.classifier import NearestNeighbor
+    from ocvfacerec.facerec.distance import EuclideanDistance
+    r = _rng(78)
+    d = 40
+    G = r.normal(0, 10, (700, d)).astype(np.float32).astype(np.float64)
+    y = np.arange(700) % 70
+    nn = NearestNeighbor(EuclideanDistance(), k=1)
+    nn.compute([np.asmatrix(x.reshape(-1, 1)) for x in G[:500]], y[:500])
+    Q = (G[r.integers(0, 700, 50)] + r.normal(0, 0.1, (50, d))).astype(np.float32).astype(np.float64)
+    nn.predict_batch(list(Q))
+    g0 = nn._gallery()
+    for i in range(500, 700):
+        nn.update(np.asmatrix(G[i].reshape(-1, 1)), y[i])
+        if i % 50 == 0:
+            nn.predict(Q[0])
+    assert nn._gallery() is g0 and g0.N == 700
+    dd, ii = nn.search(list(Q))
+    _check_search("EuclideanDistance", Q, G, dd, ii, 1)
+    labels = [p[0] for p in nn.predict_batch(list(Q))]
+    assert labels == [int(y[i]) for i in ii[:, 0]]
+    nn.compute(list(G[:10].reshape(10, d, 1)), y[:10])
+    assert nn._gallery() is not g0 and nn._gallery().N == 10
+
+
+def test_chi2_gallery_append_vs_oracle():
+    from opencv_facerecognizer_amd._device import Chi2Gallery
+    r = _rng(79)
+    G = (r.random((700, 200)) ** 3).astype(np.float32).astype(np.float64)
+    Q = (r.random((20, 200)) ** 3).astype(np.float32).astype(np.float64)
+    g = Chi2Gallery(G[:300])
+    g.append(G[300:301])
+    g.append(G[301:700])
+    assert g.N == 700
+    dd, ii = g.search(g.query_rows(Q), 3)
+    _check_search("ChiSquareDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
+
+
 def test_knn_golden_reference_predictions(golden):
     """NearestNeighbor.predict vs the reference's own outputs (tests/golden/dist_golden.npz)."""
     from ocvfacerec.facerec.classifier import NearestNeighbor

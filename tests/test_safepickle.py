@@ -69,3 +69,35 @@ def test_parse_numpy_payloads_all_protocols():
         assert np.array_equal(r["a"], obj["a"]) and r["a"].dtype == np.float32
         assert isinstance(r["b"], np.matrix)
         assert r["c"] == obj["c"] and list(r["e"]) == [1, 2]
+
+
+def _globals(raw):
+    import pickletools
+    return {tuple(a.split(" ", 1)) for op, a, _ in pickletools.genops(raw) if op.name == "GLOBAL"}
+
+
+@pytest.mark.parametrize("proto", [0, 2])
+def test_save_writes_numpy1_globals(tmp_path, proto):
+    """A saved model names numpy the way the reference's individuals.pkl does (numpy 1.x / Python 2
+    consumers cannot import numpy 2's numpy._core) and still loads here, safely and with pickle."""
+    m = load_model(os.path.join(GOLDEN, "individuals.pkl"))
+    p = tmp_path / "m.pkl"
+    save_model(str(p), m, protocol=proto)
+    raw = p.read_bytes()
+    assert b"numpy._core" not in raw
+    g = _globals(raw)
+    assert ("numpy.core.multiarray", "_reconstruct") in g and ("numpy.matrixlib.defmatrix", "matrix") in g
+    ref = open(os.path.join(GOLDEN, "individuals.pkl"), "rb").read()
+    for mod, name in [("numpy.core.multiarray", "_reconstruct"), ("numpy.matrixlib.defmatrix", "matrix"),
+                      ("ocvfacerec.facerec.feature", "Fisherfaces")]:
+        assert f"c{mod}\n{name}\n".encode() in ref
+    assert all(mod.split(".")[0] in ("numpy", "ocvfacerec", "copy_reg", "__builtin__", "_codecs") for mod, _ in g), g
+    m2 = load_model(str(p))
+    assert np.array_equal(np.asarray(m2.feature._eigenvectors), np.asarray(m.feature._eigenvectors))
+    assert np.array_equal(np.stack([np.asarray(x).ravel() for x in m2.classifier.X]),
+                          np.stack([np.asarray(x).ravel() for x in m.classifier.X]))
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", DeprecationWarning)
+        m3 = pickle.loads(raw)
+    assert isinstance(m3.classifier.X[0], np.matrix)
