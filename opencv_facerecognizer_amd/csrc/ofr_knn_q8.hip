@@ -527,12 +527,14 @@ __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists,
 
 // One block per query.  (1) best KC of the tile lists (query-major: cand[q][t][KC], one
 // contiguous stream) or of the query's sieve bucket; (2) the exact fp64 distance
-// (distance.py:60) of the KC survivors, one wave per candidate (float4 loads, lane partial
-// sums, shuffle reduction); (3) sort by (distance, index) and the certificate.
+// (distance.py:60) of the survivors in coarse order, one wave per candidate (float4 loads, lane
+// partial sums, shuffle reduction), until the coarse bound proves the rest cannot reach the
+// k-th; (3) sort by (distance, index) and the certificate.
 __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   __shared__ Cand lists[256 * KC];
   __shared__ double exact[KC];
   __shared__ double red[4];
+  __shared__ int stop_flag;
   const int64_t q = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   bool overflow = false;
@@ -552,7 +554,20 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     qq += x * x;
   }
   qq = block_sum_f64(qq, red);
-  for (int c = wave; c < KC; c += 4) {
+  // dS(q): |S - S~| <= dS for every row, S = d^2 - |q|^2
+  const double qa = p.qstats[q * 3 + 0], qe = p.qstats[q * 3 + 1], qt = p.qstats[q * 3 + 2];
+  const double A = p.gmax[0], E = p.gmax[1], T = p.gmax[2], auxmax = p.gmax[3];
+  double dS = 2.0 * (qa * E + qe * A + qe * E + qt * T) + 0x1p-20 * (auxmax + 2.0 * qa * A) + 2.0 * p.gamma * qa * A;
+  dS = dS * (1.0 + 1e-6) + 1e-300;
+  // lower bound of d^2 of any row whose (truncated) coarse score is >= s, less a relative 1e-12
+  // for the fp64 evaluation
+  auto d2_lower = [&](double s) { return (s - dS + qq) - 1e-12 * (fabs(s) + dS + 2.0 * qq); };
+  const int kk = p.k < KC ? p.k : KC;
+  // exact fp64 distance (distance.py:60) of the candidates in coarse order, 4 per round (one per
+  // wave); stop once the next candidate's lower bound exceeds the k-th exact distance so far:
+  // it and every later one (and every row outside the list) are strictly farther
+  for (int r = 0; r < KC / 4; ++r) {
+    const int c = 4 * r + wave;
     const Cand cc = lists[c];
     double a = 0;
     if (cc.i != CAND_EMPTY) {
@@ -577,6 +592,34 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
       for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
     }
     if (lane == 0) exact[c] = cc.i != CAND_EMPTY ? sqrt(a) : __builtin_inf();
+    __syncthreads();
+    const int done = 4 * r + 4;
+    if (threadIdx.x == 0) {
+      int st = 0;
+      if (done < KC && done >= kk) {
+        if (lists[done].i == CAND_EMPTY) {
+          st = 1;
+        } else {
+          double kth = __builtin_inf();   // kk-th smallest of exact[0..done)
+          for (int t = 0; t < done; ++t) {
+            const double v = exact[t];
+            int lt = 0, le = 0;
+            for (int u = 0; u < done; ++u) {
+              lt += exact[u] < v;
+              le += exact[u] <= v;
+            }
+            if (lt < kk && kk <= le) kth = v;
+          }
+          st = d2_lower((double)lists[done].d) > kth * kth;
+        }
+      }
+      stop_flag = st;
+    }
+    __syncthreads();
+    if (stop_flag) {
+      if ((int)threadIdx.x >= done && (int)threadIdx.x < KC) exact[threadIdx.x] = __builtin_inf();
+      break;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -591,18 +634,8 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     uint32_t tk = lists[KC - 1].i != CAND_EMPTY ? score_key(lists[KC - 1].d, 0) : KEY_NONE;
     if (p.theta) tk = umin(tk, p.theta[q]);
     double bnd = __builtin_inf();
-    if (overflow) {
-      bnd = -__builtin_inf();   // the bucket dropped kept rows: no bound
-    } else if (tk != KEY_NONE) {
-      const double tau = (double)key_score(tk);
-      const double a = p.qstats[q * 3 + 0], e = p.qstats[q * 3 + 1], tq = p.qstats[q * 3 + 2];
-      const double A = p.gmax[0], E = p.gmax[1], T = p.gmax[2], auxmax = p.gmax[3];
-      double dS = 2.0 * (a * E + e * A + e * E + tq * T) + 0x1p-20 * (auxmax + 2.0 * a * A) +
-                  2.0 * p.gamma * a * A;
-      dS = dS * (1.0 + 1e-6) + 1e-300;
-      bnd = (tau - dS + qq) - 1e-12 * (fabs(tau) + dS + 2.0 * qq);
-    }
-    const int kk = p.k < KC ? p.k : KC;
+    if (overflow) bnd = -__builtin_inf();   // the bucket dropped kept rows: no bound
+    else if (tk != KEY_NONE) bnd = d2_lower((double)key_score(tk));
     const double dk = od[kk - 1];
     p.cert[q] = (dk == dk) && (dk * dk < bnd);
     if (p.bound) p.bound[q] = bnd;
