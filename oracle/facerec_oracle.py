@@ -298,3 +298,36 @@ def near_tie_mask(metric, Q, G, rel=1e-4):
     d1, d2 = part[:, 0], part[:, 1]
     scale = np.maximum(np.abs(d1), 1e-300)
     return (d2 - d1) / scale <= rel
+
+
+# ---------------------------------------------------------------------------
+# validation.py: KFoldCrossValidation with Fisherfaces + NearestNeighbor
+# ---------------------------------------------------------------------------
+def kfold_fisherfaces_faithful(X, y, k=10, seed=0, metric="EuclideanDistance"):
+    """validation.py:202-258 (shuffle :54-70 from random.seed(seed)), the model of
+    thetrainer.py:120-124 (Fisherfaces + NearestNeighbor k=1), one predict per test face
+    (:251-256).  Returns (true_positives, false_positives, k_used)."""
+    import math
+    import random
+    random.seed(seed)
+    idx = np.argsort([random.random() for _ in range(len(y))])
+    y = np.asarray(y)[idx]
+    X = [X[i] for i in idx]
+    c = len(np.unique(y))
+    folds = [np.where(y == i)[0].tolist() for i in range(c)]
+    n = min(len(f) for f in folds)
+    k = min(k, n)
+    size = int(math.floor(n / k))
+    tp = fp = 0
+    for i in range(k):
+        lo, hi = i * size, (i + 1) * size
+        test = [folds[r][j] for j in range(lo, hi) for r in range(c)]
+        train = [folds[r][j] for j in range(0, lo) for r in range(c)]
+        train += [folds[r][j] for j in range(hi, n) for r in range(c)]
+        m = fisherfaces_compute([X[t] for t in train], y[train])
+        for j in test:
+            q = fisherfaces_project(m["W"], X[j])
+            pred = nn_predict_faithful(m["features"], y[train], q, metric, 1)[0][0]
+            tp, fp = (tp + 1, fp) if pred == y[j] else (tp, fp + 1)
+    return tp, fp, k
+

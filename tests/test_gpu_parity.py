@@ -549,6 +549,32 @@ def test_fisherfaces_eigh_solver_matches_eig(golden, monkeypatch):
     assert cos.min() > 1 - 1e-5, cos
 
 
+def test_kfold_validation_matches_reference_loop():
+    """KFoldCrossValidation (validation.py:202-258) of the trainer's model (Fisherfaces +
+    NearestNeighbor, thetrainer.py:120-124): one device batch per fold gives the reference loop's
+    counts (oracle: per-face predicts, same random.seed shuffle).  Synthetic 32x32 faces of 12
+    identities: the bundled set's folds (16 training faces, 4 classes) make LDA ill-conditioned
+    (W parity is judged on scatter matrices and well-posed labels there)."""
+    import random
+    from opencv_facerecognizer_amd.synthetic import IdentityBank
+    from ocvfacerec.facerec.classifier import NearestNeighbor
+    from ocvfacerec.facerec.distance import EuclideanDistance
+    from ocvfacerec.facerec.feature import Fisherfaces
+    from ocvfacerec.facerec.model import PredictableModel
+    from ocvfacerec.facerec.validation import KFoldCrossValidation
+    ids = torch.arange(12 * 9, device="cuda") % 12
+    imgs = IdentityBank(12, 32, 32, device="cuda").images(ids, seed=5).reshape(-1, 32, 32).cpu().numpy()
+    X, y = list(imgs), ids.cpu().numpy()
+    for k, seed in [(3, 1), (9, 7)]:
+        random.seed(seed)
+        v = KFoldCrossValidation(PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=1)), k=k)
+        v.validate(X, y)
+        r = v.validation_results[0]
+        tp, fp, k_used = O.kfold_fisherfaces_faithful(X, y, k=k, seed=seed)
+        assert v.k == k_used and (r.true_positives, r.false_positives) == (tp, fp), (r, tp, fp)
+        assert tp >= 0.9 * (tp + fp)
+
+
 def test_gemm_f64_vs_numpy():
     from opencv_facerecognizer_amd._device import f64_dev, gemm_f64
     r = _rng(3)
