@@ -220,8 +220,10 @@ constexpr int64_t SIEVE_CAP = 32768;   // kept rows per query (256 KiB; ~16 * SI
 constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
 
 // Hits of one 256 x 256 tile: (a, s) = (aux, gscale) of gallery row threadIdx.x (padding rows:
-// (+inf, 0), which never pass), sq2 / th per query block of this lane (th = key_float(theta | 0xff):
-// truncated key <= theta  <=>  !(score > th); NaN for KEY_NONE keeps everything).
+// (+inf, 0); they are also excluded explicitly, since a NaN th passes everything), sq2 / th per
+// query block of this lane (th = key_float(theta | 0xff): truncated key <= theta  <=>
+// !(score > th); NaN for KEY_NONE keeps every row).  More than SIEVE_HCAP hits in one tile push
+// every query of the tile past its bucket cap (uncertified, no candidates read by the merge).
 template <int CT, int TQ, int QW, int WQ, class CV>
 __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, int64_t g0, int64_t q0, float ga,
                                                float gs, const float (&sq2)[CT], const float (&th)[CT], CV&& cval) {
@@ -237,12 +239,7 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
   }
   if (threadIdx.x == 0) *nhit = 0;
   __syncthreads();
-  auto append = [&](int64_t q, int gl, uint32_t kb) {
-    if (q < p.B && gl < nvalid) {
-      const int slot = atomicAdd(p.count + q, 1);
-      if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(kb), (int)(g0 + gl)};
-    }
-  };
+
 #pragma unroll
   for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
@@ -253,12 +250,11 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
         constexpr int ct = decltype(ctc)::value;
         if constexpr (ct < CT) {
           const float sc = a - sq2[ct] * sg * cval(rt, ctc, r);
-          if (!(sc > th[ct])) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
+          if (!(sc > th[ct]) && gl < nvalid) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
             const int ql = wc * QW + ct * 32 + r32;
             const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
             const uint32_t slot = atomicAdd(nhit, 1u);
             if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)gl);
-            else append(q0 + ql, gl, kb);
           }
         }
       };
@@ -269,10 +265,19 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
       one(std::integral_constant<int, 3>{});
     }
   __syncthreads();
-  const uint32_t n = *nhit < (uint32_t)SIEVE_HCAP ? *nhit : (uint32_t)SIEVE_HCAP;
-  for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+  const uint32_t nh = *nhit;
+  if (nh > (uint32_t)SIEVE_HCAP) {   // hits lost: push every query of the tile past its cap (uncertified)
+    if ((int)threadIdx.x < TQ && q0 + threadIdx.x < p.B) atomicAdd(p.count + q0 + threadIdx.x, (int)p.cap + 1);
+    return;
+  }
+  for (uint32_t e = threadIdx.x; e < nh; e += blockDim.x) {
     const uint2 hv = hits[e];
-    append(q0 + (int)(hv.y >> 8), (int)(hv.y & 0xffu), hv.x);
+    const int64_t q = q0 + (int)(hv.y >> 8);
+    const int gl = (int)(hv.y & 0xffu);
+    if (q < p.B) {
+      const int slot = atomicAdd(p.count + q, 1);
+      if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(hv.x), (int)(g0 + gl)};
+    }
   }
 }
 
@@ -540,8 +545,8 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   bool overflow = false;
   if (p.count) {
     const int64_t c = p.count[q];
-    overflow = c > p.cap;
-    block_best(p.cand + (size_t)q * p.cap, overflow ? p.cap : c, lists);
+    overflow = c > p.cap;   // rows were dropped (and a tile-level overflow writes none): no candidates
+    block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
   } else {
     block_best(p.cand + (size_t)q * p.T * KC, p.T * KC, lists);
   }
