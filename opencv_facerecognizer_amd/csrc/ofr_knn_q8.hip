@@ -241,11 +241,17 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
   __syncthreads();
 
 #pragma unroll
-  for (int rt = 0; rt < 4; ++rt)
+  for (int rt = 0; rt < 4; ++rt) {
+    // the 16 rows of this row block first (one LDS wait), then the compares: a read per element
+    // would expose the LDS latency 64 times
+    float2 ag[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      ag[r] = reinterpret_cast<const float2*>(gtab)[wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int gl = wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float a = gtab[2 * gl], sg = gtab[2 * gl + 1];
+      const float a = ag[r].x, sg = ag[r].y;
       auto one = [&](auto ctc) {
         constexpr int ct = decltype(ctc)::value;
         if constexpr (ct < CT) {
@@ -264,6 +270,7 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
       one(std::integral_constant<int, 2>{});
       one(std::integral_constant<int, 3>{});
     }
+  }
   __syncthreads();
   const uint32_t nh = *nhit;
   if (nh > (uint32_t)SIEVE_HCAP) {   // hits lost: push every query of the tile past its cap (uncertified)
