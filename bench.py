@@ -35,8 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from opencv_facerecognizer_amd import _lib  # noqa: E402
-from opencv_facerecognizer_amd._device import (FloatGallery, Projection, SmallBatchGraph, col_mean_u8, round_up,  # noqa: E402
-                                               u8_rows)
+from opencv_facerecognizer_amd._device import FloatGallery, Projection, col_mean_u8, round_up  # noqa: E402
 from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, merge_topk,  # noqa: E402
                                                 shard_range)
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
@@ -313,18 +312,6 @@ def main():
                 gallery.search_phase("merge", Qs, k, index_base=n0)
         torch.cuda.synchronize()
         ms_step = (time.perf_counter() - t1) * 1e3 / reps
-        ms_graph = None
-        if f6_small:                          # the same step as one captured graph (SmallBatchGraph)
-            xr = u8_rows(Xq[:bs])
-            sg = SmallBatchGraph(gallery, P, gallery.shift64, bs, k, xr.shape[1])
-            for _ in range(2):
-                sg(xr)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(reps):
-                sg(xr)
-            torch.cuda.synchronize()
-            ms_graph = (time.perf_counter() - t1) * 1e3 / reps
         if f6_small:
             kern = "q8s::stream_kernel_f6 (ofr_knn_f6 phase 1, B<=32)"
             bytes_t = 0.75 * (nl * d + bs * d)                       # fp6 tiles streamed once per batch
@@ -332,8 +319,6 @@ def main():
             kern = "knn_tile_kernel<Cfg<32,4,1,4>> (ofr_knn_tiles_f32, B<=32)"
             bytes_t = nl * d * 4 + bs * d * 4                        # fp32 rows streamed once per batch
         small.append({"batch": bs, "queries_per_s": bs / (ms_step * 1e-3), "ms_per_batch": ms_step,
-                      "ms_per_batch_graph": ms_graph,
-                      "queries_per_s_graph": (bs / (ms_graph * 1e-3) if ms_graph else None),
                       "uncertified": (list(gallery.last_fallbacks) if f6_small else None),
                       "roofline": {"kernel": kern, "bound": "hbm", "achieved": bytes_t / (ms_t * 1e-3) / 1e9,
                                    "peak": PEAK_HBM / 1e9, "unit": "GB/s",

@@ -335,7 +335,7 @@ class FloatGallery:
 
     def search_q8_phase(self, phases, Qd, qq, k, index_base=0, out=None, workspace=None):
         """phases 1 = quantized tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"]), 3 = both.
-        workspace: a Workspace of the caller's (a captured graph keeps its own) instead of the gallery's."""
+        workspace: a Workspace of the caller's instead of the gallery's."""
         tier = qq["tier"]
         g = self._tier_gallery(tier)
         B = Qd.shape[0]
@@ -431,52 +431,6 @@ class FloatGallery:
         call("ofr_knn_f32", stream(), self.metric, ptr(Qd), B, Qd.shape[1], ptr(self.G), self.N, self.ld, self.d,
              ptr(self.aux), k, index_base, ptr(out_d), ptr(out_i), ptr(ws), ws.numel())
         return out_d, out_i
-
-
-class SmallBatchGraph:
-    """The recognizers' call (one face, or a few: B <= SMALL_BATCH) as one HIP graph: exact
-    projection of the uint8 faces with the gallery centring, fp6 quantization, the streaming fp6
-    pass and the merge / exact re-rank / certificate, captured once per (gallery state, B, k) and
-    replayed per call, so a call costs one H2D copy, one replay and the certificate readback
-    instead of a dozen launches and their Python.  Uncertified queries take the eager tier chain
-    (FloatGallery.fallback).  Static buffers and its own workspace: the captured pointers stay valid
-    while the gallery's storage does (``valid()``: same rows, row count and fp6 tier buffer)."""
-
-    def __init__(self, gallery, P, shift64, B, k, ldx):
-        self.g, self.P, self.B, self.k = gallery, P, int(B), int(k)
-        dev_ = gallery.G.device
-        self.x = torch.zeros((self.B, ldx), dtype=torch.uint8, device=dev_)
-        self.Qd = torch.zeros((self.B, gallery.ld), dtype=torch.float32, device=dev_)
-        self.shift = shift64
-        self.qq = gallery.quantize_queries(self.Qd, tier="f6")
-        self.out = (torch.empty((self.B, self.k), dtype=torch.float64, device=dev_),
-                    torch.empty((self.B, self.k), dtype=torch.int64, device=dev_))
-        self.ws = Workspace()
-        self._run()                          # eager warm-up: kernel attributes, workspace size
-        torch.cuda.synchronize()
-        self.key = self._key()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self._run()
-
-    def _key(self):
-        return (self.g.N, self.g.G.data_ptr(), self.g._tier_gallery("f6")["Gs"].data_ptr())
-
-    def valid(self):
-        return self.g.q8 is not None and "f6" in self.g.q8 and self._key() == self.key
-
-    def _run(self):
-        self.P.project(self.x, shift64=self.shift, out=self.Qd)
-        self.g.quantize_queries(self.Qd, self.qq, tier="f6")
-        self.g.search_q8_phase(3, self.Qd, self.qq, self.k, out=self.out, workspace=self.ws)
-
-    def __call__(self, xrows):
-        """xrows: uint8 [B][ldx] device rows -> (distances fp64 [B,k], indices int64 [B,k])."""
-        self.x.copy_(xrows)
-        self.graph.replay()
-        out = (self.out[0].clone(), self.out[1].clone())
-        self.g.fallback(self.Qd, self.qq, self.k, out)
-        return out
 
 
 class Chi2Gallery:

@@ -495,11 +495,24 @@ __device__ __forceinline__ void block_best(const Cand* src, int64_t n, Cand* lis
   TopList<KC> L;
   L.init();
   const uint4* s4 = reinterpret_cast<const uint4*>(src);
-  for (int64_t e = threadIdx.x; e < n / 2; e += blockDim.x) {
-    const uint4 v = s4[e];
-    const float d0 = __uint_as_float(v.x), d1 = __uint_as_float(v.z);
-    if (better_f(d0, (int)v.y, L.d[KC - 1], L.i[KC - 1])) L.insert(d0, (int)v.y);
-    if (better_f(d1, (int)v.w, L.d[KC - 1], L.i[KC - 1])) L.insert(d1, (int)v.w);
+  const int64_t n4 = n / 2;
+  // BU loads in flight per thread: with few queries (B <= 32, one block each) the stream of
+  // T * 16 candidates is latency-bound otherwise (285 us for one query at N = 1M)
+  constexpr int BU = 8;
+  for (int64_t e0 = threadIdx.x; e0 < n4; e0 += (int64_t)BU * blockDim.x) {
+    uint4 v[BU];
+#pragma unroll
+    for (int u = 0; u < BU; ++u) {
+      const int64_t e = e0 + (int64_t)u * blockDim.x;
+      v[u] = e < n4 ? s4[e] : make_uint4(__float_as_uint(__builtin_inff()), CAND_EMPTY,
+                                         __float_as_uint(__builtin_inff()), CAND_EMPTY);
+    }
+#pragma unroll
+    for (int u = 0; u < BU; ++u) {
+      const float d0 = __uint_as_float(v[u].x), d1 = __uint_as_float(v[u].z);
+      if (better_f(d0, (int)v[u].y, L.d[KC - 1], L.i[KC - 1])) L.insert(d0, (int)v[u].y);
+      if (better_f(d1, (int)v[u].w, L.d[KC - 1], L.i[KC - 1])) L.insert(d1, (int)v[u].w);
+    }
   }
   if ((n & 1) && threadIdx.x == 0) L.insert(src[n - 1].d, src[n - 1].i);
 #pragma unroll
@@ -521,6 +534,21 @@ __device__ __forceinline__ void block_best(const Cand* src, int64_t n, Cand* lis
     }
     __syncthreads();
   }
+}
+
+// Small batches: the streaming pass leaves T * KC candidates per query (62.5k at N = 1M), and one
+// merge block per query inserting them into per-thread sorted lists is divergent and serial
+// (240 us per query).  PM blocks per query first reduce contiguous chunks to their best KC.
+constexpr int PM = 64;
+__global__ void __launch_bounds__(256) premerge_kernel(const Cand* cand, int64_t T, Cand* out) {
+  __shared__ Cand lists[256 * KC];
+  const int64_t q = blockIdx.y;
+  const int64_t n = T * KC;
+  const int64_t chunk = ((n + PM - 1) / PM + 1) & ~(int64_t)1;   // even: chunks start 16-B aligned
+  const int64_t b = (int64_t)blockIdx.x * chunk;
+  const int64_t e = b + chunk < n ? b + chunk : n;
+  block_best(cand + q * n + (b < n ? b : 0), e > b ? e - b : 0, lists);
+  if ((int)threadIdx.x < KC) out[(q * PM + blockIdx.x) * KC + threadIdx.x] = lists[threadIdx.x];
 }
 
 // Sieve thresholds from the sample pass's tile lists: theta[q] = the 16th best key (KEY_NONE
@@ -560,10 +588,19 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   const float* qr = p.Q + q * p.ldq;
   const int64_t d4 = p.d >> 2;
   const bool vec = ((p.ldq | p.ldg) & 3) == 0 && (((uintptr_t)p.Q | (uintptr_t)p.G) & 15) == 0;
+  // loads batched 8 deep: with few queries (one block each) a loop with one load per iteration is
+  // bound by the memory latency, not the bytes
+  constexpr int RU = 8;
   double qq = 0;
-  for (int64_t j = threadIdx.x; j < p.d; j += blockDim.x) {
-    const double x = qr[j];
-    qq += x * x;
+  for (int64_t j0 = threadIdx.x; j0 < p.d; j0 += (int64_t)RU * blockDim.x) {
+    float x[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int64_t j = j0 + (int64_t)u * blockDim.x;
+      x[u] = j < p.d ? qr[j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) qq += (double)x[u] * (double)x[u];
   }
   qq = block_sum_f64(qq, red);
   // dS(q): |S - S~| <= dS for every row, S = d^2 - |q|^2
@@ -1010,8 +1047,13 @@ static SieveWs sieve_ws(int64_t B, int64_t N) {
   return w;
 }
 
+// B <= 32: tile lists [B][T][KC], then the premerge lists [B][PM][KC]
+static size_t stream_ws_lists(int64_t B, int64_t N) {
+  return (size_t)round_up((int64_t)cdiv(N > 0 ? N : 1, q8s::TG) * B * q8s::KC * (int64_t)sizeof(Cand), 256);
+}
+
 extern "C" size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N) {
-  return B <= 32 ? ofr_knn_q8_workspace_bytes(B, N) : sieve_ws(B, N).bytes;
+  return B <= 32 ? stream_ws_lists(B, N) + (size_t)B * q8s::PM * q8s::KC * sizeof(Cand) : sieve_ws(B, N).bytes;
 }
 
 extern "C" size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N) {
@@ -1096,6 +1138,12 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
       m.count = count;
       m.theta = theta;
       m.cap = q8s::SIEVE_CAP;
+    } else if (a.ntg > q8s::PM) {
+      Cand* pm = reinterpret_cast<Cand*>(wsb + stream_ws_lists(B, N));
+      hipLaunchKernelGGL(q8s::premerge_kernel, dim3(q8s::PM, (unsigned)B), dim3(256), 0, st, a.cand, a.ntg, pm);
+      OFR_LAUNCH_CHECK("f6 premerge_kernel");
+      m.cand = pm;
+      m.T = q8s::PM;
     }
     hipLaunchKernelGGL(q8s::merge_kernel, dim3((unsigned)B), dim3(256), 0, st, m);
     OFR_LAUNCH_CHECK("f6 merge_kernel");

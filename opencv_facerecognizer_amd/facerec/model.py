@@ -8,13 +8,9 @@ the features ever leaving the GPU.
 """
 from __future__ import annotations
 
-import os
-import warnings
-
 import numpy as np
 
-from .. import _device, _lib
-from .classifier import _DEVICE_LOCK, AbstractClassifier, NearestNeighbor, vote
+from .classifier import AbstractClassifier, NearestNeighbor, vote
 from .feature import AbstractFeature, Fisherfaces
 
 
@@ -51,46 +47,9 @@ class PredictableModel(object):
         g = clf._gallery()
         if g.N and g.d != self.feature._proj().d:
             raise ValueError("feature dimension does not match the classifier gallery")
-        graph = self._small_batch_graph(X, k, g)
-        if graph is not None:
-            with _DEVICE_LOCK:
-                return graph(_device.u8_rows(X if isinstance(X, np.ndarray) else np.stack([np.asarray(x) for x in X])))
         # Euclidean: the gallery centring is folded into the projection (W^T x - c, fp64, rounded once)
         Qd = self.feature.project_device(X, shift64=g.shift64)
         return clf._search_prepared(Qd, k)
-
-    def _small_batch_graph(self, X, k, g):
-        """The captured small-batch step (SmallBatchGraph) for uint8 faces, B <= 32, Euclidean, the
-        fp6 first tier; None otherwise (OFR_GRAPHS=0 disables)."""
-        B = len(X)
-        if (os.environ.get("OFR_GRAPHS", "1") == "0" or self.__dict__.get("_graphs_off")
-                or not 0 < B <= _device.SMALL_BATCH or not g.use_q8(B, k) or g.first_tier() != "f6"
-                or g.metric != _lib.METRIC_EUCLIDEAN or np.asarray(X[0]).dtype != np.uint8):
-            return None
-        P = self.feature._proj()
-        cache = self.__dict__.setdefault("_graphs", {})
-        if any(gr.g is not g or gr.P is not P for gr in cache.values()):
-            cache.clear()                                   # new gallery or projection: drop old captures
-        gr = cache.get((B, k))
-        if gr is None or not gr.valid():
-            cache.pop((B, k), None)
-            sh = self.feature._shift(P, g.shift64)
-            ldx = _device.round_up(max(int(np.asarray(X[0]).size), 1), 16)
-            try:
-                with _DEVICE_LOCK:
-                    gr = _device.SmallBatchGraph(g, P, sh, B, k, ldx)
-            except RuntimeError as e:                       # capture refused: stay on the eager launches
-                warnings.warn("small-batch graph capture failed (%s); using eager launches" % e)
-                self.__dict__["_graphs_off"] = True
-                return None
-            cache[(B, k)] = gr
-        return gr
-
-    def __getstate__(self):
-        st = dict(self.__dict__)
-        st.pop("_graphs", None)
-        st.pop("_graphs_off", None)
-        return st
 
     def predict_batch(self, X):
         """Predict a batch of faces (list of 2-D arrays or an array [B, H, W])."""

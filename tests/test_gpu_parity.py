@@ -575,43 +575,6 @@ def test_kfold_validation_matches_reference_loop():
         assert tp >= 0.9 * (tp + fp)
 
 
-def test_small_batch_graph_matches_eager(monkeypatch):
-    """PredictableModel.predict through the captured small-batch graph (projection + fp6 quantization +
-    streaming pass + merge as one replay) equals the eager launches, across repeated calls, batch
-    sizes and a gallery update (the capture is invalidated and rebuilt)."""
-    from opencv_facerecognizer_amd.synthetic import IdentityBank
-    from ocvfacerec.facerec.classifier import NearestNeighbor
-    from ocvfacerec.facerec.distance import EuclideanDistance
-    from ocvfacerec.facerec.feature import Fisherfaces
-    from ocvfacerec.facerec.model import PredictableModel
-    ids = torch.arange(40 * 6, device="cuda") % 40
-    bank = IdentityBank(40, 24, 24, device="cuda")
-    X = list(bank.images(ids, seed=11).reshape(-1, 24, 24).cpu().numpy())
-    y = ids.cpu().numpy()
-    qid = torch.arange(40, device="cuda")
-    Q = bank.images(qid, seed=12).reshape(-1, 24, 24).cpu().numpy()
-    m = PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=3))
-    m.compute(X, y)
-    monkeypatch.setenv("OFR_GRAPHS", "0")
-    ref = {B: m.search_batch(Q[:B]) for B in (1, 5, 32)}
-    monkeypatch.setenv("OFR_GRAPHS", "1")
-    for rep in range(3):
-        for B in (1, 5, 32):
-            d, i = m.search_batch(Q[:B])
-            np.testing.assert_array_equal(i, ref[B][1])
-            np.testing.assert_array_equal(d, ref[B][0])
-    assert set(m.__dict__["_graphs"]) == {(1, 3), (5, 3), (32, 3)}
-    assert m.predict(Q[0])[0] == m.predict_batch(Q[:1])[0][0]
-    # an update appends to the gallery: the captures are rebuilt and see the new row
-    feat = m.feature.extract(Q[3])
-    m.classifier.update(feat, 3)
-    d, i = m.search_batch(Q[3:4])
-    assert i[0, 0] == len(X) and d[0, 0] < 1e-6 * max(1.0, float(np.linalg.norm(np.asarray(feat))))
-    monkeypatch.setenv("OFR_GRAPHS", "0")
-    d0, i0 = m.search_batch(Q[3:4])
-    np.testing.assert_array_equal(i, i0)
-
-
 def test_gemm_f64_vs_numpy():
     from opencv_facerecognizer_amd._device import f64_dev, gemm_f64
     r = _rng(3)
