@@ -780,7 +780,8 @@ __device__ __forceinline__ uint32_t e2m3_code(double r, double& q) {
   if (v < 1.0) code = (uint32_t)(v * 8.0);
   else {
     const int e = v < 2.0 ? 1 : (v < 4.0 ? 2 : 3);
-    code = ((uint32_t)e << 3) | (uint32_t)((v / (double)(1 << (e - 1)) - 1.0) * 8.0);
+    const double inv = e == 1 ? 1.0 : (e == 2 ? 0.5 : 0.25);   // 2^-(e-1), exact
+    code = ((uint32_t)e << 3) | (uint32_t)((v * inv - 1.0) * 8.0);
   }
   q = r < 0 ? -v : v;
   return (r < 0 && v != 0.0) ? (code | 32u) : code;
@@ -806,19 +807,33 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
     while ((double)mx / (double)s > 7.5) s = __uint_as_float(__float_as_uint(s) + 1u);
   }
   const double sd = (double)s;
+  const double inv_sd = 1.0 / sd;   // x * (1/s) instead of x / s: any rounding of x/s is fine (the
+                                    // stats below are of the values actually stored)
+  const bool vec4 = ((ldx & 3) == 0) && (((uintptr_t)X & 15) == 0);
   double sa = 0, se = 0;
   const int64_t ngroups = nst * 4;
   char* pbase = tiles + (row >> 8) * nst * (int64_t)f6t::PANEL;
   const int rl = (int)(row & 255);
   for (int64_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
     uint32_t w[6] = {0, 0, 0, 0, 0, 0};
+    float xg[32];
+    if (vec4 && g * 32 + 32 <= d) {
+#pragma unroll
+      for (int e = 0; e < 32; e += 4) {
+        const float4 v4 = *reinterpret_cast<const float4*>(x + g * 32 + e);
+        xg[e] = v4.x; xg[e + 1] = v4.y; xg[e + 2] = v4.z; xg[e + 3] = v4.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 32; ++e) xg[e] = g * 32 + e < d ? x[g * 32 + e] : 0.f;
+    }
 #pragma unroll
     for (int e = 0; e < 32; ++e) {
       const int64_t k = g * 32 + e;
       if (k < d) {
-        const double xv = (double)x[k];
+        const double xv = (double)xg[e];
         double qv;
-        const uint32_t c = e2m3_code(xv / sd, qv);
+        const uint32_t c = e2m3_code(xv * inv_sd, qv);
         const double xt = sd * qv;   // exact: 24-bit s times a 4-bit significand
         sa += xt * xt;
         se += (xv - xt) * (xv - xt);
