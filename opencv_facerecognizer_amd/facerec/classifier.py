@@ -122,18 +122,22 @@ class NearestNeighbor(AbstractClassifier):
         if n > len(self.y):
             raise Exception("More distances than classes. Is your distance metric correct?")  # classifier.py:109-110
         cache = self.__dict__.get("_dev")
-        if cache is not None and cache[0] == key:
-            n0, g = cache[1], cache[2]
-            if n0 == n:
-                return g
-            if 0 < n0 < n and g.N == n0:
-                g.append(self._stack(self.X[n0:]))
-                self.__dict__["_dev"] = (key, n, g)
-                return g
-        feats = self._stack(self.X) if n else np.zeros((0, 1))
-        g = Chi2Gallery(feats) if mid == _lib.METRIC_CHISQUARE else FloatGallery(feats, mid)
-        self.__dict__["_dev"] = (key, n, g)
-        return g
+        if cache is not None and cache[0] == key and cache[1] == n:
+            return cache[2]
+        with _DEVICE_LOCK:   # a search on another thread must not see a half-grown gallery
+            cache = self.__dict__.get("_dev")
+            if cache is not None and cache[0] == key:
+                n0, g = cache[1], cache[2]
+                if n0 == n:
+                    return g
+                if 0 < n0 < n and g.N == n0:
+                    g.append(self._stack(self.X[n0:]))
+                    self.__dict__["_dev"] = (key, n, g)
+                    return g
+            feats = self._stack(self.X) if n else np.zeros((0, 1))
+            g = Chi2Gallery(feats) if mid == _lib.METRIC_CHISQUARE else FloatGallery(feats, mid)
+            self.__dict__["_dev"] = (key, n, g)
+            return g
 
     @staticmethod
     def _stack(items):
