@@ -86,6 +86,18 @@ int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, i
  * computed in fp64 and stored fp32.  G [N][ldg] fp32.                       */
 int ofr_row_aux(void* stream, int metric, const float* G, int64_t N, int64_t d, int64_t ldg,
                 float* aux);
+/* Certified Cosine search (CosineDistance, distance.py:74-77): the Cosine
+ * ranking is the Euclidean ranking of unit vectors, so the certified Euclidean
+ * tiers run on out = fp32(g / ||g|| - shift) (fp64, rounded once; shift
+ * nullable, e.g. the mean unit row, which keeps the quantization relative to
+ * the rows' spread rather than their common direction; zero rows stay zero,
+ * pad columns [d, ldo) zeroed) and ofr_cosine_pairs then evaluates the reference
+ * formula -p.q / sqrt(p.p q.q) in fp64 for the found (query, row) pairs
+ * (out_i [B][k] in: local rows, -1 = none; out: sorted by (distance, row)).  */
+int ofr_normalize_rows_f32(void* stream, const float* G, int64_t N, int64_t d, int64_t ldg, const double* shift,
+                           float* out, int64_t ldo);
+int ofr_cosine_pairs(void* stream, const float* Q, int64_t B, int64_t ldq, const float* G, int64_t N,
+                     int64_t ldg, int64_t d, int k, double* out_d, int64_t* out_i);
 /* out[n][j] = (float)(F[n][j] - shift[j]) for j < d: fp64 features -> the
  * fp32 search layout, centred BEFORE the rounding (shift may be NULL).       */
 int ofr_center_round_f64(void* stream, const double* F, int64_t N, int64_t d, int64_t ldf,

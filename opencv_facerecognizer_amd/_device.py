@@ -201,6 +201,7 @@ class FloatGallery:
             call("ofr_row_aux", stream(), self.metric, ptr(self.G), self.N, self.d, self.ld, ptr(self.aux))
         self.ws = Workspace()
         self.q8 = None
+        self._twin = None
         self.last_fallbacks = 0
 
     def capacity(self):
@@ -233,6 +234,8 @@ class FloatGallery:
         center_round(F, self.shift64, self.ld, out=self._Gbuf[N0:N1])
         call("ofr_row_aux", stream(), self.metric, ptr(self._Gbuf[N0:]), n, self.d, self.ld, ptr(self._auxbuf[N0:]))
         self.N, self.G, self.aux = N1, self._Gbuf[:N1], self._auxbuf[:N1]
+        if self._twin is not None:                 # Cosine: the unit-row twin grows with it
+            self._twin.append(self.unit_rows(self.G[N0:N1])[:, :self.d])
         for tier, g in (self.q8 or {}).items():
             if tier == "f6":
                 call("ofr_f6_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, ptr(g["Gs"]),
@@ -251,6 +254,49 @@ class FloatGallery:
     # proves the result exact.  OFR_SEARCH picks the first tier: auto (= f6), q8
     # (tier 1), q8x2 (tier 2) or fp32.
     TIER_CHAIN = ("f6", 1, 2, "fp32")
+
+    # -- certified Cosine search: Euclidean tiers on the unit rows, then the reference formula ----------
+    def unit_rows(self, X, shift64=None, out=None):
+        """fp32 rows [n][>= d] -> fp32(x / ||x|| - shift) [n][ld] (fp64, rounded once)."""
+        if out is None:
+            out = torch.empty((X.shape[0], self.ld), dtype=torch.float32, device=X.device)
+        call("ofr_normalize_rows_f32", stream(), ptr(X), X.shape[0], self.d, X.shape[1], ptr(shift64), ptr(out),
+             self.ld)
+        return out
+
+    def _cos_twin(self):
+        """Euclidean gallery of the unit rows, centred on their mean (Euclidean distances are translation
+        invariant; features share a large common direction, and centring keeps the fp6 / int8
+        quantization relative to the spread of the unit rows instead).  Built once, grown by append."""
+        if self._twin is None:
+            U = self.unit_rows(self.G)
+            shift = torch.empty(self.d, dtype=torch.float64, device=U.device)
+            call("ofr_col_mean", stream(), ptr(U), self.N, self.d, self.ld, ptr(shift))
+            self.unit_rows(self.G, shift, out=U)     # centred, one rounding
+            self._twin = FloatGallery.from_device_rows(U, self.d, _lib.METRIC_EUCLIDEAN, shift64=shift)
+        return self._twin
+
+    def use_cos_cert(self, B, k):
+        """Certified Cosine path: not for galleries with a zero row (its distance is NaN, which the fp32
+        path ranks last like the reference; a unit-row twin cannot represent it)."""
+        if (os.environ.get("OFR_SEARCH", "auto") == "fp32" or self.metric != _lib.METRIC_COSINE or self.N == 0
+                or B == 0 or k > Q8_MAX_K):
+            return False
+        if getattr(self, "_cos_ok", None) is None or self._cos_ok[0] != self.N:
+            self._cos_ok = (self.N, not bool(torch.isinf(self.aux[:self.N]).any()))
+        return self._cos_ok[1]
+
+    def _search_cosine(self, Qd, k, index_base=0):
+        """Cosine top-k = Euclidean top-k of the unit vectors (certified chain on the twin; ranks agree
+        up to the fp32 rounding of the unit rows, ~1e-7 relative), distances by the reference formula."""
+        tw = self._cos_twin()
+        d_, i_ = tw.search(self.unit_rows(Qd, tw.shift64), k)
+        self.last_fallbacks = tw.last_fallbacks
+        call("ofr_cosine_pairs", stream(), ptr(Qd), Qd.shape[0], Qd.shape[1], ptr(self.G), self.N, self.ld, self.d,
+             k, ptr(d_), ptr(i_))
+        if index_base:
+            i_ = torch.where(i_ >= 0, i_ + index_base, i_)
+        return d_, i_
 
     def use_q8(self, B, k):
         mode = os.environ.get("OFR_SEARCH", "auto")
@@ -414,6 +460,8 @@ class FloatGallery:
         if Qd.shape[1] != self.ld:
             raise ValueError(f"query row stride {Qd.shape[1]} != gallery stride {self.ld}")
         B = Qd.shape[0]
+        if self.use_cos_cert(B, k):
+            return self._search_cosine(Qd, k, index_base)
         if self.use_q8(B, k):
             qq = self.quantize_queries(Qd, tier=self.first_tier())
             out = self.search_q8_phase(3, Qd, qq, k, index_base)

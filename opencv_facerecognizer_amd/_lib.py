@@ -54,6 +54,8 @@ SIGNATURES = {
     "ofr_knn_q8_workspace_bytes": (c_sz, [c_i64, c_i64]),
     "ofr_knn_q8": (c_int, [c_vp, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
                            c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz]),
+    "ofr_normalize_rows_f32": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
+    "ofr_cosine_pairs": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp]),
     "ofr_f6_tiles_bytes": (c_sz, [c_i64, c_i64]),
     "ofr_f6_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp]),
     "ofr_q8_maxima": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),

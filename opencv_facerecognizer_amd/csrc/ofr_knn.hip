@@ -207,6 +207,79 @@ __global__ void row_aux_kernel(int metric, const float* G, int64_t N, int64_t d,
   if (lane == 0) aux[row] = metric == OFR_METRIC_COSINE ? (float)(1.0 / sqrt(s)) : (float)s;
 }
 
+// unit rows for the certified Cosine search: out = fp32(g / ||g|| - shift), in fp64 and rounded once
+// (shift nullable), zero rows stay zero; one wave per row
+__global__ void normalize_rows_kernel(const float* G, int64_t N, int64_t d, int64_t ldg, const double* shift,
+                                      float* out, int64_t ldo) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= N) return;
+  const float* g = G + row * ldg;
+  double s = 0;
+  for (int64_t j = lane; j < d; j += 64) {
+    const double x = g[j];
+    s += x * x;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const double inv = s > 0 ? 1.0 / sqrt(s) : 0.0;
+  float* o = out + row * ldo;
+  for (int64_t j = lane; j < ldo; j += 64)
+    o[j] = j < d ? (float)((double)g[j] * inv - (shift ? shift[j] : 0.0)) : 0.f;
+}
+
+// CosineDistance (distance.py:74-77) of given (query, row) pairs in fp64 on the stored fp32 rows,
+// then each query's k sorted by (distance, row); one wave per query, k <= 16
+__global__ void cosine_pairs_kernel(const float* Q, int64_t ldq, const float* G, int64_t ldg, int64_t d,
+                                    int64_t B, int k, double* out_d, int64_t* out_i) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= B) return;
+  const float* qr = Q + q * ldq;
+  double qq = 0;
+  for (int64_t j = lane; j < d; j += 64) qq += (double)qr[j] * (double)qr[j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) qq += __shfl_xor(qq, o);
+  double dist[16];
+  int64_t idx[16];
+  for (int c = 0; c < k; ++c) {
+    const int64_t i = out_i[q * k + c];
+    double val = __builtin_inf();
+    if (i >= 0) {
+      const float* gr = G + i * ldg;
+      double a = 0, gg = 0;
+      for (int64_t j = lane; j < d; j += 64) {
+        const double x = qr[j], y = gr[j];
+        a += x * y;
+        gg += y * y;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o);
+        gg += __shfl_xor(gg, o);
+      }
+      val = -a / sqrt(gg * qq);
+    }
+    dist[c] = val;
+    idx[c] = i;
+  }
+  if (lane == 0) {
+    for (int c = 1; c < k; ++c)   // insertion sort by (distance, row), empty (-1) rows last
+      for (int u = c; u > 0; --u) {
+        // empty (-1) rows last, then NaN distances (as the reference's argsort), then (distance, row)
+        const bool sw = idx[u - 1] < 0 ? idx[u] >= 0
+                                       : (idx[u] >= 0 && nan_last_before(dist[u], idx[u], dist[u - 1], idx[u - 1]));
+        if (!sw) break;
+        const double td = dist[u]; dist[u] = dist[u - 1]; dist[u - 1] = td;
+        const int64_t ti = idx[u]; idx[u] = idx[u - 1]; idx[u - 1] = ti;
+      }
+    for (int c = 0; c < k; ++c) {
+      out_d[q * k + c] = dist[c];
+      out_i[q * k + c] = idx[c];
+    }
+  }
+}
+
 // column means in two deterministic passes: fixed row chunks, then an ordered sum of the chunks
 constexpr int COLMEAN_CHUNKS = 256;
 __global__ void col_mean_partial_kernel(const float* G, int64_t N, int64_t d, int64_t ldg, double* part) {
@@ -363,6 +436,29 @@ extern "C" int ofr_row_aux(void* stream, int metric, const float* G, int64_t N, 
   if (N == 0) return OFR_OK;
   hipLaunchKernelGGL(row_aux_kernel, dim3((unsigned)cdiv(N, 4)), dim3(256), 0, (hipStream_t)stream, metric, G, N, d, ldg, aux);
   OFR_LAUNCH_CHECK("row_aux_kernel");
+  return OFR_OK;
+}
+
+extern "C" int ofr_normalize_rows_f32(void* stream, const float* G, int64_t N, int64_t d, int64_t ldg,
+                                      const double* shift, float* out, int64_t ldo) {
+  OFR_CHECK_ARG(N >= 0 && d >= 1 && ldg >= d && ldo >= d, "ofr_normalize_rows_f32: bad sizes");
+  if (N == 0) return OFR_OK;
+  OFR_CHECK_ARG(G && out, "ofr_normalize_rows_f32: null pointer");
+  hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)cdiv(N, 4)), dim3(256), 0, (hipStream_t)stream, G, N, d,
+                     ldg, shift, out, ldo);
+  OFR_LAUNCH_CHECK("normalize_rows_kernel");
+  return OFR_OK;
+}
+
+extern "C" int ofr_cosine_pairs(void* stream, const float* Q, int64_t B, int64_t ldq, const float* G, int64_t N,
+                                int64_t ldg, int64_t d, int k, double* out_d, int64_t* out_i) {
+  OFR_CHECK_ARG(B >= 0 && N >= 0 && d >= 1 && ldq >= d && ldg >= d && k >= 1 && k <= 16,
+                "ofr_cosine_pairs: bad sizes (k <= 16)");
+  if (B == 0) return OFR_OK;
+  OFR_CHECK_ARG(Q && G && out_d && out_i, "ofr_cosine_pairs: null pointer");
+  hipLaunchKernelGGL(cosine_pairs_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, (hipStream_t)stream, Q, ldq, G,
+                     ldg, d, B, k, out_d, out_i);
+  OFR_LAUNCH_CHECK("cosine_pairs_kernel");
   return OFR_OK;
 }
 

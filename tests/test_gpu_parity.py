@@ -316,6 +316,36 @@ def test_chi2_gallery_append_vs_oracle():
     _check_search("ChiSquareDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
 
 
+@pytest.mark.parametrize("B,N,d,k", [(300, 20000, 64, 1), (40, 9000, 130, 5), (5, 3000, 99, 3)])
+def test_knn_cosine_certified_vs_oracle(monkeypatch, B, N, d, k):
+    """CosineDistance with k <= 8 runs the certified Euclidean tiers on the unit rows (the Cosine
+    ranking) and evaluates distance.py:77 in fp64 for the result; matches the oracle and the fp32
+    path, including after an append (the unit-row twin grows with the gallery)."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(B + N + d)
+    protos = r.normal(0, 1, (max(N // 10, 1), d))
+    G = (protos[np.arange(N) % len(protos)] * r.uniform(0.5, 3, (N, 1)) + r.normal(0, 0.15, (N, d)))
+    G = G.astype(np.float32).astype(np.float64)
+    Q = (protos[r.integers(0, len(protos), B)] * 2 + r.normal(0, 0.15, (B, d))).astype(np.float32).astype(np.float64)
+    g = FloatGallery(G[:N - 500], _lib.METRIC_COSINE)
+    assert g.use_cos_cert(B, k)
+    dd, ii = g.search(g.query_rows(Q), k)
+    _check_search("CosineDistance", Q, G[:N - 500], dd.cpu().numpy(), ii.cpu().numpy(), k)
+    assert g.last_fallbacks[0] <= max(1, B // 10)
+    g.append(G[N - 500:])
+    dd, ii = g.search(g.query_rows(Q), k)
+    _check_search("CosineDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
+    monkeypatch.setenv("OFR_SEARCH", "fp32")
+    d2, i2 = g.search(g.query_rows(Q), k)
+    np.testing.assert_allclose(d2.cpu().numpy(), dd.cpu().numpy(), rtol=0, atol=1e-12)
+    # a zero row makes the Cosine distance NaN: such galleries stay on the fp32 path
+    Z = G[:100].copy()
+    Z[7] = 0
+    assert not FloatGallery(Z, _lib.METRIC_COSINE).use_cos_cert(40, 1)
+
+
 def test_knn_golden_reference_predictions(golden):
     """NearestNeighbor.predict vs the reference's own outputs (tests/golden/dist_golden.npz)."""
     from ocvfacerec.facerec.classifier import NearestNeighbor
