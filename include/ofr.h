@@ -279,6 +279,20 @@ int ofr_class_center_f64(void* stream, const double* F, int64_t N, int64_t D, in
                          const double* total_mean, double* means, double* Fc, double* Mc,
                          double* Mc_n);
 
+/* Face-tensor ingestion ------------------------------------
+ * Replaces cv2.imread(IMREAD_GRAYSCALE) + cv2.resize(im, size) [INTER_LINEAR] of
+ * TheTrainer.read_images trainer/thetrainer.py:99-103 and the recognizers'
+ * img[y0:y1, x0:x1] -> cv2.cvtColor(BGR2GRAY) -> cv2.resize(size, INTER_CUBIC)
+ * (../bin/ocvf_recognizer.py:64-66), for a ragged batch in ONE launch.
+ * src: device bytes holding every source image; jobs: device int64 [n][7] =
+ * (byte offset of the image, row pitch in bytes, crop x0, y0, width, height,
+ * channels 1 = grey | 3 = BGR | 4 = BGRA); crops must lie inside their image.
+ * out: uint8 [n][dh][dw].  interp 1 = INTER_LINEAR, 2 = INTER_CUBIC, in
+ * OpenCV's 8-bit fixed point (11-bit coefficients; grey = (1868 B + 9617 G +
+ * 4899 R + 2^13) >> 14); a crop of the output size is copied (grey only).       */
+int ofr_ingest_faces(void* stream, const uint8_t* src, const int64_t* jobs, int64_t n, int dh, int dw,
+                     int interp, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -296,6 +296,13 @@ class FloatGallery:
              k, ptr(d_), ptr(i_))
         if index_base:
             i_ = torch.where(i_ >= 0, i_ + index_base, i_)
+        # a zero query has no unit vector (every reference distance is NaN, distance.py:77): the fp32
+        # path ranks it exactly as for any other NaN row set
+        zero = torch.nonzero(Qd[:, :self.d].abs().amax(1) == 0).reshape(-1)
+        if zero.numel():
+            d2, i2 = self._search_f32(Qd.index_select(0, zero).contiguous(), k, index_base)
+            d_.index_copy_(0, zero, d2)
+            i_.index_copy_(0, zero, i2)
         return d_, i_
 
     def use_q8(self, B, k):
@@ -341,9 +348,6 @@ class FloatGallery:
                      ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
             self.q8[tier] = dict(Gs=Gs, scale=gs, stats=st, gmax=gmax, ld=ld)
         return self.q8[tier]
-
-    def _q8_gallery(self, slices=1):   # kept for callers of the int8 tiers
-        return self._tier_gallery(slices)
 
     def quantize_queries(self, Qd, out=None, tier="f6"):
         """Centred fp32 query rows -> the tier's quantized rows, scales and stats (device)."""

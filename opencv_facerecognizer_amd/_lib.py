@@ -79,6 +79,7 @@ SIGNATURES = {
     "ofr_col_mean_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "ofr_sub_mean_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
     "ofr_normalize_cols_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64]),
+    "ofr_ingest_faces": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
     "ofr_class_center_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                      c_vp]),
 }

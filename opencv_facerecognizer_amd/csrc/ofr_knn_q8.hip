@@ -274,7 +274,9 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
   __syncthreads();
   const uint32_t nh = *nhit;
   if (nh > (uint32_t)SIEVE_HCAP) {   // hits lost: push every query of the tile past its cap (uncertified)
-    if ((int)threadIdx.x < TQ && q0 + threadIdx.x < p.B) atomicAdd(p.count + q0 + threadIdx.x, (int)p.cap + 1);
+    // saturating (max, not add): any number of overflowing tiles leaves the count at cap + 1 plus
+    // at most one increment per gallery row, which the host bounds below 2^31 (ofr_knn_f6)
+    if ((int)threadIdx.x < TQ && q0 + threadIdx.x < p.B) atomicMax(p.count + q0 + threadIdx.x, (int)p.cap + 1);
     return;
   }
   for (uint32_t e = threadIdx.x; e < nh; e += blockDim.x) {
@@ -580,7 +582,7 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   bool overflow = false;
   if (p.count) {
     const int64_t c = p.count[q];
-    overflow = c > p.cap;   // rows were dropped (and a tile-level overflow writes none): no candidates
+    overflow = c > p.cap || c < 0;   // rows were dropped (and a tile-level overflow writes none): no candidates
     block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
   } else {
     block_best(p.cand + (size_t)q * p.T * KC, p.T * KC, lists);
@@ -1089,7 +1091,8 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
                 "ofr_knn_f6: null pointer");
   OFR_CHECK_ARG(((uintptr_t)Qt | (uintptr_t)Gt | (uintptr_t)workspace) % 16 == 0,
                 "ofr_knn_f6: tiles and workspace must be 16-byte aligned");
-  OFR_CHECK_ARG(N < 0x7fffffffLL - q8s::TG, "ofr_knn_f6: N too large for one shard");
+  // the sieve's per-query count reaches at most cap + 1 + N (saturating overflow + one per row)
+  OFR_CHECK_ARG(N < 0x7fffffffLL - 2 * q8s::SIEVE_CAP, "ofr_knn_f6: N too large for one shard");
   OFR_CHECK_ARG(workspace_bytes >= ofr_knn_f6_workspace_bytes(B, N), "ofr_knn_f6: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const bool sieve = B > 32;

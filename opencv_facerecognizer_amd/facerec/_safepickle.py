@@ -346,6 +346,19 @@ def _as_text(x):
     return x
 
 
+# Derived device state (classifier ``_dev``, feature ``_dev_proj``, PCA ``_shift_cache``) is never
+# pickled by this package (``__getstate__`` drops it); a file that carries such keys must not
+# pre-seed the caches, whose identity checks would then be bypassed.
+def _is_cache_key(k):
+    return isinstance(k, str) and (k.startswith("_dev") or k == "_shift_cache")
+
+
+def _drop_caches(st):
+    if not isinstance(st, dict):
+        raise UnpicklingError("instance state must be a dict")
+    return {k: v for k, v in st.items() if not _is_cache_key(k)}
+
+
 class _Materializer:
     def __init__(self, classes):
         self.classes = classes   # qualname -> python class
@@ -453,6 +466,7 @@ class _Materializer:
         raise UnpicklingError(f"global {q} is not whitelisted")
 
     def _instance(self, cls_node, node):
+        """Build a whitelisted facerec instance; device-cache slots in the file are ignored."""
         if not isinstance(cls_node, _Global):
             raise UnpicklingError("class must be a global")
         cls = self.classes.get(cls_node.qualname)
@@ -468,12 +482,13 @@ class _Materializer:
             st = self(state) if state is not None else {}
             if not isinstance(st, dict):
                 raise UnpicklingError("instance state must be a dict")
+            st = _drop_caches(st)
             if hasattr(obj, "__setstate__") and getattr(cls, "_facerec_setstate", False):
                 obj.__setstate__(st)
             else:
                 obj.__dict__.update(st)
             if slotstate:
-                for k, v in self(slotstate).items():
+                for k, v in _drop_caches(self(slotstate)).items():
                     setattr(obj, k, v)
         return obj
 

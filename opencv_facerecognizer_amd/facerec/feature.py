@@ -30,6 +30,7 @@ import os
 import warnings
 
 import numpy as np
+import torch
 
 from .. import _device
 
@@ -117,8 +118,12 @@ class _DeviceProjMixin:
     def project_device(self, X, shift64=None, f64=False, ld=None):
         """Batch of items -> (W^T x - own shift - shift64): fp32 search rows [B][ldy] or fp64 [B][d]."""
         P = self._proj()
-        A = X if isinstance(X, np.ndarray) and X.ndim == 2 and not isinstance(X, np.matrix) else _stack_rows(X)
         sh = self._shift(P, shift64)
+        if hasattr(X, "data_ptr"):      # device uint8 faces [B][H][W] / [B][D] (e.g. ingest.faces): no host trip
+            if X.dtype != torch.uint8:
+                raise TypeError("device face batches must be uint8")
+            return P.project(_device.u8_rows(X), shift64=sh, f64=f64)
+        A = X if isinstance(X, np.ndarray) and X.ndim == 2 and not isinstance(X, np.matrix) else _stack_rows(X)
         if A.dtype == np.uint8:
             return P.project(_device.u8_rows(A), shift64=sh, f64=f64)
         Y = _device.gemm_f64(_device.f64_dev(A.astype(np.float64)), P.W64)

@@ -52,8 +52,11 @@ class PredictableModel(object):
         return clf._search_prepared(Qd, k)
 
     def predict_batch(self, X):
-        """Predict a batch of faces (list of 2-D arrays or an array [B, H, W])."""
+        """Predict a batch of faces (list of 2-D arrays, an array [B, H, W], or a uint8 device
+        tensor [B, H, W] such as ``ingest.faces`` returns)."""
         if not self._fused():
+            if hasattr(X, "data_ptr"):   # a device face batch: the generic path works on host items
+                X = list(X.cpu().numpy())
             qs = [self.feature.extract(x) for x in X]
             return self.classifier.predict_batch(qs) if hasattr(self.classifier, "predict_batch") else \
                 [self.classifier.predict(q) for q in qs]

@@ -46,14 +46,8 @@ def gather_rows(x, group=None):
 
 def exchange_topk(d, i, group=None):
     """All-gather per-rank (B x k) lists -> (B x world*k) tensors, rank-major (list p = rank p)."""
-    _, ws = world()
-    if ws == 1:
-        return d, i
-    gd = [torch.empty_like(d) for _ in range(ws)]
-    gi = [torch.empty_like(i) for _ in range(ws)]
-    dist.all_gather(gd, d.contiguous(), group=group)
-    dist.all_gather(gi, i.contiguous(), group=group)
-    return torch.cat(gd, dim=1).contiguous(), torch.cat(gi, dim=1).contiguous()
+    gd, gi, _ = exchange_lists(d, i, None, group)
+    return gd, gi
 
 
 def merge_topk(gd, gi, nlists, kin, k):
@@ -72,31 +66,60 @@ def sharded_search(local_search, k, group=None):
     return merge_topk(gd, gi, ws, k, k)
 
 
+def exchange_lists(d, i, bound=None, group=None):
+    """ONE all-gather of every rank's (B x k) lists and per-query bound -> (gd, gi, min bound).
+
+    The fp64 distances, the int64 indices (bit-copied as fp64 words: a collective only moves
+    bytes) and the bound travel as one [B][2k+1] fp64 block per rank, so a tier of the sharded
+    search costs one collective instead of three.  gd/gi are [B][world*k], rank-major."""
+    _, ws = world(group)
+    B, k = d.shape
+    if ws == 1:
+        return d, i, bound
+    cols = [d.to(torch.float64), i.to(torch.int64).contiguous().view(torch.float64)]
+    if bound is not None:
+        cols.append(bound.to(torch.float64).reshape(B, 1))
+    g = gather_rows(torch.cat(cols, 1).contiguous(), group).reshape(ws, B, -1)
+    gd = g[:, :, :k].permute(1, 0, 2).reshape(B, ws * k).contiguous()
+    gi = g[:, :, k:2 * k].contiguous().view(torch.int64).permute(1, 0, 2).reshape(B, ws * k).contiguous()
+    minb = g[:, :, 2 * k].min(0).values if bound is not None else None
+    return gd, gi, minb
+
+
+def global_certificate(kth, minb):
+    """Query certified iff its GLOBAL k-th squared distance is below every rank's bound.
+
+    A rank whose sieve bucket overflowed reports bound = -inf (no bound: its candidates were
+    dropped) and never certifies; +inf (every local row was a candidate) always does, even when
+    the gallery holds fewer than k rows (kth = inf)."""
+    return (kth * kth < minb) | torch.isposinf(minb)
+
+
 def certify_sharded(gallery, Qd, qq, k, out, index_base, group=None):
     """Global certificate + collective fallback of the certified tiers on a sharded gallery.
 
     ``out`` is this rank's local top-k (exact fp64 distances, global row indices) of the whole
     batch from the tier of ``qq``; the merge kernel left in ``qq["bound"]`` a lower bound of the
-    squared distance of every local row outside its candidates.  After the all-gather + merge,
-    query q is certified iff its GLOBAL k-th squared distance is below every rank's bound: a row
-    that is not among its rank's candidates is then farther than the global k-th, and one that is
-    a candidate but not in its rank's top-k has k better rows on that rank, so the merged list is
-    the exact global top-k.  (A per-rank certificate would fail for every query whose identity
-    lives on another rank: its local neighbours are not separated from its 16th candidate.)
-    Uncertified queries -- the same set on every rank, it is computed from gathered data -- go
-    down the tier chain on every rank, each stage with its own exchange; the fp32 stage is exact.
+    squared distance of every local row outside its candidates (-inf when the rank could not
+    bound them).  After the all-gather + merge, query q is certified iff its GLOBAL k-th squared
+    distance is below every rank's bound: a row that is not among its rank's candidates is then
+    farther than the global k-th, and one that is a candidate but not in its rank's top-k has k
+    better rows on that rank, so the merged list is the exact global top-k.  (A per-rank
+    certificate would fail for every query whose identity lives on another rank: its local
+    neighbours are not separated from its 16th candidate.)  Uncertified queries -- the same set on
+    every rank, it is computed from gathered data -- go down the tier chain on every rank, each
+    stage with its own exchange; the fp32 stage is exact.  Reference semantics:
+    classifier.py:104-119 (the k nearest of the whole gallery).
     Returns ((d, i) global top-k, [uncertified after each quantized tier]).
     """
     _, ws = world(group)
 
     def merged(d, i, bound):
-        gd, gi = exchange_topk(d, i, group)
+        gd, gi, minb = exchange_lists(d, i, bound, group)
         md, mi = merge_topk(gd, gi, ws, k, k)
         if bound is None:
             return md, mi, None
-        minb = gather_rows(bound.reshape(1, -1), group).min(0).values
-        kth = md[:, k - 1]
-        return md, mi, (kth * kth < minb) | torch.isinf(minb)
+        return md, mi, global_certificate(md[:, k - 1], minb)
 
     md, mi, cert = merged(out[0], out[1], qq["bound"])
     rows = torch.nonzero(~cert).reshape(-1)

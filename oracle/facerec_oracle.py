@@ -331,3 +331,85 @@ def kfold_fisherfaces_faithful(X, y, k=10, seed=0, metric="EuclideanDistance"):
             tp, fp = (tp + 1, fp) if pred == y[j] else (tp, fp + 1)
     return tp, fp, k
 
+
+
+# ---------------------------------------------------------------------------
+# Face-tensor ingestion: cv2.imread(GRAYSCALE) + cv2.resize
+# (INTER_LINEAR) in TheTrainer.read_images (trainer/thetrainer.py:99-103), and
+# the recognizers' crop + cv2.cvtColor(BGR2GRAY) + cv2.resize(INTER_CUBIC)
+# (bin/ocvf_recognizer.py:64-66, ocvf_recognizer_ros.py:113-115).
+#
+# The arithmetic lives in OpenCV, a third-party dependency ABSENT from
+# /root/reference and from this image (README.md:44-48 names Ubuntu 14.04's
+# python-opencv, i.e. OpenCV 2.4.8).  Restated from OpenCV's published 8-bit
+# fixed-point algorithm (imgproc resize.cpp resizeGeneric_ with
+# INTER_RESIZE_COEF_BITS = 11; color.cpp RGB2Gray with yuv_shift = 14), scalar
+# (non-SIMD) form.  Parity against cv2 itself is UNPINNED: OpenCV's SSE paths of
+# the vertical pass round differently in the last bit on some pixels.  What
+# pins it: the reference's pickled gallery (data/individuals.pkl) is reproduced
+# from the bundled JPEGs to ~1e-3 (tests/test_gpu_ingest.py).
+# ---------------------------------------------------------------------------
+CV_COEF_BITS = 11
+CV_COEF_SCALE = 1 << CV_COEF_BITS
+
+
+def _cv_axis(dsize, ssize, interp):
+    """Source taps [dsize][ksize] (clamped to the image) and int16 weights of one axis.
+
+    resizeGeneric_: scale = 1 / (dsize / ssize); f = (float)((i + 0.5) * scale - 0.5); s = floor(f);
+    f -= s; weights = saturate_cast<short>(rint(cbuf * 2048)) with cbuf = (1 - f, f) for
+    INTER_LINEAR and interpolateCubic(f) (A = -0.75, float arithmetic) for INTER_CUBIC.  Linear
+    columns past the edges use f = 0 (x only; rows keep their weights and clamp the row index)."""
+    scale = 1.0 / (dsize / ssize)
+    f = ((np.arange(dsize) + 0.5) * scale - 0.5).astype(np.float32)
+    s = np.floor(f).astype(np.int64)
+    f = (f - s.astype(np.float32)).astype(np.float32)
+    one = np.float32(1.0)
+    if interp == "linear":
+        cbuf = np.stack([one - f, f], 1)
+        first = s
+    else:
+        A = np.float32(-0.75)
+        x = f
+        c0 = ((A * (x + one) - np.float32(5) * A) * (x + one) + np.float32(8) * A) * (x + one) - np.float32(4) * A
+        c1 = ((A + np.float32(2)) * x - (A + np.float32(3))) * x * x + one
+        c2 = ((A + np.float32(2)) * (one - x) - (A + np.float32(3))) * (one - x) * (one - x) + one
+        c3 = one - c0 - c1 - c2
+        cbuf = np.stack([c0, c1, c2, c3], 1).astype(np.float32)
+        first = s - 1
+    w = np.clip(np.rint(cbuf * np.float32(CV_COEF_SCALE)), -32768, 32767).astype(np.int64)
+    taps = np.clip(first[:, None] + np.arange(cbuf.shape[1])[None, :], 0, ssize - 1)
+    return taps, w, s, f
+
+
+def cv_resize_u8(img, size, interp="linear"):
+    """cv2.resize(img, size=(width, height), interpolation) of a 2-D uint8 image, fixed point:
+    H pass D[x] = sum_k S[tap_k] * alpha_k (int), V pass (sum_k D_k * beta_k + 2^21) >> 22,
+    saturated to uint8; a resize to the same size is a copy (cv::resize shortcut)."""
+    img = np.asarray(img, np.uint8)
+    H, W = img.shape
+    dw, dh = int(size[0]), int(size[1])
+    if (dw, dh) == (W, H):
+        return img.copy()
+    xt, xw, xs, xf = _cv_axis(dw, W, interp)
+    if interp == "linear":                       # x only: columns past either edge take (1, 0) at the edge pixel
+        edge = (xs < 0) | (xs >= W - 1)
+        xt[edge] = np.clip(xs[edge], 0, W - 1)[:, None]
+        xw[edge] = np.array([CV_COEF_SCALE, 0])
+    yt, yw, _, _ = _cv_axis(dh, H, interp)
+    S = img.astype(np.int64)
+    Dh = np.einsum("rxk,xk->rx", S[:, xt], xw)                 # [H][dw]
+    V = np.einsum("ykx,yk->yx", Dh[yt], yw)                    # [dh][dw]
+    return np.clip((V + (1 << (2 * CV_COEF_BITS - 1))) >> (2 * CV_COEF_BITS), 0, 255).astype(np.uint8)
+
+
+def cv_bgr2gray(img):
+    """cv2.cvtColor(img, COLOR_BGR2GRAY) for uint8 BGR (or BGRA): (1868 B + 9617 G + 4899 R + 2^13) >> 14."""
+    a = np.asarray(img, np.uint8).astype(np.int64)
+    return ((a[..., 0] * 1868 + a[..., 1] * 9617 + a[..., 2] * 4899 + (1 << 13)) >> 14).astype(np.uint8)
+
+
+def recognizer_face(frame_bgr, box, size):
+    """ocvf_recognizer.py:64-66: crop img[y0:y1, x0:x1], BGR2GRAY, resize(size, INTER_CUBIC)."""
+    x0, y0, x1, y1 = box
+    return cv_resize_u8(cv_bgr2gray(frame_bgr[y0:y1, x0:x1]), size, "cubic")

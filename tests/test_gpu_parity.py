@@ -638,3 +638,25 @@ def test_topk_merge_kernel():
         ref = cand[:k]
         assert [x[1] for x in ref] == list(oi[b, :len(ref)])
         assert np.array_equal([x[0] for x in ref], od[b, :len(ref)])
+
+
+def test_knn_cosine_zero_query_takes_fp32_path(monkeypatch):
+    """A zero query has no unit vector: every reference distance is NaN (distance.py:77).  It must
+    not be answered by the certified unit-row twin (whose row for it would be -shift); it gets the
+    fp32 path's answer, NaN distances ranked by index like any all-NaN row set."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(404)
+    G = r.normal(50, 10, (3000, 40)).astype(np.float32).astype(np.float64)
+    Q = r.normal(50, 10, (64, 40)).astype(np.float32).astype(np.float64)
+    Q[5] = 0.0
+    g = FloatGallery(G, _lib.METRIC_COSINE)
+    assert g.use_cos_cert(64, 3)
+    dd, ii = g.search(g.query_rows(Q), 3)
+    dd, ii = dd.cpu().numpy(), ii.cpu().numpy()
+    monkeypatch.setenv("OFR_SEARCH", "fp32")
+    d32, i32 = g.search(g.query_rows(Q[5:6]), 3)
+    assert np.array_equal(ii[5], i32.cpu().numpy()[0]) and np.isnan(dd[5]).all()
+    keep = np.arange(64) != 5
+    _check_search("CosineDistance", Q[keep], G, dd[keep], ii[keep], 3)

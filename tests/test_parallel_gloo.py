@@ -114,8 +114,9 @@ class _MockShardGallery:
     TIER_CHAIN = ("f6", 1, 2, "fp32")
     SLACK = {"f6": 0.5, 1: 0.97, 2: 0.999}
 
-    def __init__(self, G, n0):
+    def __init__(self, G, n0, overflow=()):
         self.G, self.n0 = G, n0
+        self.overflow = np.asarray(overflow, dtype=np.int64)   # first-tier queries whose sieve bucket overflows
 
     def next_tier(self, tier, nrows):
         return self.TIER_CHAIN[self.TIER_CHAIN.index(tier) + 1]
@@ -130,15 +131,19 @@ class _MockShardGallery:
     def search_q8_phase(self, phases, sub, q2, k, index_base):
         d, i = self._local(q2["Q"], k)
         b = d[:, -1] ** 2 * self.SLACK[q2["tier"]] if d.shape[1] == 16 else np.full(len(d), np.inf)
+        d, i = d[:, :k].copy(), i[:, :k].copy()
+        if q2["tier"] == "f6" and len(self.overflow):
+            # merge_kernel on an overflowed bucket: no candidates (inf, -1) and bound -inf
+            d[self.overflow], i[self.overflow], b[self.overflow] = np.inf, -1, -np.inf
         q2["bound"] = torch.from_numpy(b)
-        return torch.from_numpy(d[:, :k].copy()), torch.from_numpy(i[:, :k].copy())
+        return torch.from_numpy(d), torch.from_numpy(i)
 
     def _search_f32(self, sub, k, index_base):
         d, i = self._local(sub.numpy(), k)
         return torch.from_numpy(d[:, :k].copy()), torch.from_numpy(i[:, :k].copy())
 
 
-def _cert_worker(rank, ws, port, k, out):
+def _cert_worker(rank, ws, port, k, out, overflow=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
@@ -146,7 +151,10 @@ def _cert_worker(rank, ws, port, k, out):
         par.merge_topk = _host_merge                      # the device merge kernel needs a GPU
         Q, G = _data()
         n0, n1 = shard_range(len(G), rank, ws)
-        g = _MockShardGallery(G[n0:n1], n0)
+        # rank 1 overflows on the queries that are copies of its own rows (their true neighbours)
+        g = _MockShardGallery(G[n0:n1], n0, overflow=_OVERFLOW_Q if (overflow and rank == 1) else ())
+        if overflow:
+            Q = _overflow_queries(Q, G)
         Qt = torch.from_numpy(Q)
         qq = g.quantize_queries(Qt, "f6")
         d, i = g.search_q8_phase(3, Qt, qq, k, n0)
@@ -155,6 +163,15 @@ def _cert_worker(rank, ws, port, k, out):
             out.put((md.numpy(), mi.numpy(), counts))
     finally:
         dist.destroy_process_group()
+
+
+_OVERFLOW_Q = np.arange(4, 12)
+
+
+def _overflow_queries(Q, G):
+    Q = Q.copy()
+    Q[_OVERFLOW_Q] = G[700:708]          # rows of rank 1's shard [500, 1001)
+    return Q
 
 
 def _host_merge(gd, gi, nlists, kin, k):
@@ -184,3 +201,33 @@ def test_sharded_global_certificate_and_collective_fallback(k):
     ref_d, ref_i = O.nn_search_vectorized("EuclideanDistance", Q, G, k)
     assert np.array_equal(mi, ref_i) and np.allclose(md, ref_d, rtol=0, atol=0)
     assert counts[0] > 0 and len(counts) >= 2            # the loose first-tier bound forced fallbacks
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_sharded_overflowed_rank_is_never_certified(k):
+    """A rank whose fp6 sieve bucket overflows returns no candidates and bound -inf for that query.
+    The global certificate must send the query down the chain (the bound proves nothing), so the
+    merged result still holds the overflowed rank's rows -- the exact global top-k."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cert_worker, args=(r, 2, port, k, q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    md, mi, counts = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    Q, G = _data()
+    Q = _overflow_queries(Q, G)
+    ref_d, ref_i = O.nn_search_vectorized("EuclideanDistance", Q, G, k)
+    assert np.array_equal(mi, ref_i) and np.allclose(md, ref_d, rtol=0, atol=0)
+    assert np.array_equal(mi[_OVERFLOW_Q, 0], np.arange(700, 708))
+    assert counts[0] >= len(_OVERFLOW_Q)
+
+
+def test_global_certificate_bounds():
+    from opencv_facerecognizer_amd.parallel import global_certificate
+    kth = torch.tensor([1.0, 1.0, float("inf"), 1.0, 3.0])
+    minb = torch.tensor([2.0, -float("inf"), float("inf"), float("inf"), 4.0])
+    assert global_certificate(kth, minb).tolist() == [True, False, True, True, False]
