@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--small-batches", default="32,1", help="extra HBM-regime measurements (B <= 32); '' to skip")
+    ap.add_argument("--stress", default="48,96,192",
+                    help="pixel-noise levels of the crowded-neighbour stress runs (same shape, 1 GPU); '' to skip")
+    ap.add_argument("--stress-steps", type=int, default=3)
     ap.add_argument("--search", choices=["f6", "q8", "fp32"], default="f6",
                     help="f6: certified fp6 coarse pass (uncertified queries go down the int8 tiers, then fp32); "
                          "q8: start at the certified int8 tier; fp32: fp32-MFMA pass")
@@ -137,6 +140,86 @@ def committed_traffic(cfg):
     return best
 
 
+def build_gallery(P, bank, per_id, n0, nl, N, d, ld, device, noise=12.0):
+    """Gallery rows [n0, n0 + nl) of the N-image synthetic gallery, projected exactly and centred on
+    c = W^T round(mean image of the gallery's first chunk) (fp64, the same on every rank)."""
+    chunk = 8192
+    G = torch.zeros((nl, ld), dtype=torch.float32, device=device)
+    rows = torch.arange(0, min(N, chunk), device=device)
+    m = col_mean_u8(bank.images(rows // per_id, seed=SEED + 1000, noise=noise), P.D)
+    m_img = torch.clamp(torch.round(m), 0, 255).to(torch.uint8).reshape(1, -1).contiguous()
+    centre = P.project(m_img, f64=True)[0].contiguous()
+    for c0 in range(0, nl, chunk):
+        c1 = min(nl, c0 + chunk)
+        rows = torch.arange(n0 + c0, n0 + c1, device=device)
+        imgs = bank.images(rows // per_id, seed=SEED + 1000 + (n0 + c0) // chunk, noise=noise)
+        P.project(imgs, shift64=centre, out=G[c0:c1])
+    return FloatGallery.from_device_rows(G, d, _lib.METRIC_EUCLIDEAN, shift64=centre)
+
+
+def certificate_margin(gallery, Qd, qq, nsample=64):
+    """(d_16^2 - d_1^2) / dS of the fp6 tier for a sample of queries: the certificate needs about 2
+    (the 16th coarse candidate must clear the k-th exact distance by the bound on both sides).
+    d from the exact fp32 path, dS = the bound merge_kernel uses."""
+    s = torch.arange(0, Qd.shape[0], max(1, Qd.shape[0] // nsample), device=Qd.device)[:nsample]
+    dd, _ = gallery._search_f32(Qd.index_select(0, s).contiguous(), 16)
+    dd = dd.cpu().numpy()
+    st = qq["stats"].index_select(0, s).cpu().numpy()
+    gmax = gallery._tier_gallery("f6")["gmax"].cpu().numpy()
+    A, E, aux = gmax[0], gmax[1], gmax[3]
+    a, e = st[:, 0], st[:, 1]
+    gamma = (2 * -(-gallery.d // 128) + 64) * 2.0 ** -23
+    dS = 2 * (a * E + e * A + e * E) + 2.0 ** -20 * (aux + 2 * a * A) + 2 * gamma * a * A
+    r = (dd[:, 15] ** 2 - dd[:, 0] ** 2) / dS
+    return {"median": float(np.median(r)), "min": float(r.min()), "sample": int(len(r))}
+
+
+def stress_run(P, bank, args, noise, device):
+    """Crowded neighbours: the headline shape (1M gallery, B = 4096, d = 9999) with the pixel noise
+    raised so that identities crowd together and the fp6 certificate fails; the uncertified queries
+    then run down the int8 / fp32 tiers inside the timed step.  One GPU."""
+    N, B, d, k = args.gallery, args.batch, args.dim, args.k
+    ld = max(32, round_up(d, 32))
+    n_ids = (N + args.per_id - 1) // args.per_id
+    gallery = build_gallery(P, bank, args.per_id, 0, N, N, d, ld, device, noise=noise)
+    for t in FloatGallery.TIER_CHAIN[:-1]:
+        gallery._tier_gallery(t)
+    gq = torch.Generator(device=device)
+    gq.manual_seed(SEED + 7)
+    ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
+    Xq = bank.images(ids_q, seed=SEED + 99, noise=noise)
+    Qd = torch.zeros((B, ld), dtype=torch.float32, device=device)
+    out = (torch.empty((B, k), dtype=torch.float64, device=device), torch.empty((B, k), dtype=torch.int64, device=device))
+    qq, tiers, counts = None, [], None
+
+    def step(timings=None):
+        nonlocal qq
+        P.project(Xq, shift64=gallery.shift64, out=Qd)
+        qq = gallery.quantize_queries(Qd, qq, tier="f6")
+        gallery.search_q8_phase(3, Qd, qq, k, out=out)
+        gallery.fallback(Qd, qq, k, out, timings=timings)
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.stress_steps):
+        step(tiers)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / args.stress_steps
+    counts = list(gallery.last_fallbacks)
+    per_tier = {}
+    for t, n, m in tiers:
+        e = per_tier.setdefault(t, {"queries": n, "ms": 0.0})
+        e["ms"] += m / args.stress_steps
+    acc = float(((out[1][:, 0] // args.per_id) == ids_q).double().mean().item())
+    res = {"pixel_noise": noise, "queries_per_s": B / (ms * 1e-3), "ms_per_step": ms,
+           "uncertified_after_each_tier": counts, "fallback_ms_per_step": per_tier,
+           "certificate_margin_fp6": certificate_margin(gallery, Qd, qq), "top1_identity_acc": acc}
+    del gallery
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -164,21 +247,7 @@ def main():
     P, Wt = build_projection(D, d, device)
     bank = IdentityBank(n_ids, H, W, device=device)
     ld = max(32, round_up(d, 32))
-    G = torch.zeros((nl, ld), dtype=torch.float32, device=device)
-    chunk = 8192
-    # centring vector c = W^T round(mean image of the gallery's first chunk), exact fp64, the same on
-    # every rank (the query rows are centred once and shared): rows are stored as fp32(W^T x - c),
-    # rounded after centring (FloatGallery docstring)
-    rows = torch.arange(0, min(N, chunk), device=device)
-    m = col_mean_u8(bank.images(rows // args.per_id, seed=SEED + 1000), D)
-    m_img = torch.clamp(torch.round(m), 0, 255).to(torch.uint8).reshape(1, -1).contiguous()
-    centre = P.project(m_img, f64=True)[0].contiguous()
-    for c0 in range(0, nl, chunk):
-        c1 = min(nl, c0 + chunk)
-        rows = torch.arange(n0 + c0, n0 + c1, device=device)
-        imgs = bank.images(rows // args.per_id, seed=SEED + 1000 + (n0 + c0) // chunk)
-        P.project(imgs, shift64=centre, out=G[c0:c1])
-    gallery = FloatGallery.from_device_rows(G, d, _lib.METRIC_EUCLIDEAN, shift64=centre)
+    gallery = build_gallery(P, bank, args.per_id, n0, nl, N, d, ld, device)
     gq = torch.Generator(device=device)
     gq.manual_seed(SEED + 7)
     ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
@@ -325,6 +394,7 @@ def main():
                                    "frac": bytes_t / (ms_t * 1e-3) / PEAK_HBM, "launch_ms": ms_t,
                                    "algorithmic_bytes_per_launch": bytes_t}})
 
+    margin = certificate_margin(gallery, Qd, qq) if args.search == "f6" and world == 1 else None
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
     if args.search == "f6":
@@ -373,11 +443,19 @@ def main():
             "uncertified_after_each_tier": (list(last_counts) if use_q8 else None),
             "sieve_kept_rows_per_query": kept,
             "top1_identity_acc": acc,
+            "certificate_margin_fp6": margin,
             "small_batch": small,
         }
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(Wt, gallery, Xq, N, args.cpu_seconds)
             result["speedup_vs_cpu"] = value / result["cpu_baseline"]["value"]
+        if world == 1 and args.search == "f6" and args.stress.strip():
+            gallery.q8, gallery.G, gallery._Gbuf = None, None, None      # free the headline gallery first
+            torch.cuda.empty_cache()
+            result["stress"] = [stress_run(P, bank, args, float(x), device) for x in args.stress.split(",") if x.strip()]
+            for r in result["stress"]:
+                log(rank, f"stress noise {r['pixel_noise']}: {r['queries_per_s']:.0f} q/s, uncertified "
+                          f"{r['uncertified_after_each_tier']}, margin {r['certificate_margin_fp6']}")
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

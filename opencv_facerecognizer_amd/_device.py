@@ -415,28 +415,37 @@ class FloatGallery:
             return None
         return self.ws.buf[off:off + 4 * B].view(torch.int32)
 
-    def fallback(self, Qd, qq, k, out, index_base=0):
+    def fallback(self, Qd, qq, k, out, index_base=0, timings=None):
         """Re-run the queries the first tier left uncertified down the tier chain (then fp32).
         Returns the number of first-tier failures (host sync); self.last_fallbacks = the number of
-        uncertified queries after each quantized tier that ran."""
+        uncertified queries after each quantized tier that ran.  timings (a list, optional)
+        receives (tier, queries, ms) per stage that ran (HIP events on the current stream)."""
         bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
         counts = [int(bad.numel())]
         rows = bad                      # indices into the original batch still unresolved
         tier = qq["tier"]
         while rows.numel():
             tier = self.next_tier(tier, int(rows.numel()))
+            if timings is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             sub = Qd.index_select(0, rows).contiguous()
             if tier == "fp32":
                 d2, i2 = self._search_f32(sub, k, index_base)
                 out[0].index_copy_(0, rows, d2)
                 out[1].index_copy_(0, rows, i2)
-                break
-            q2 = self.quantize_queries(sub, tier=tier)
-            d2, i2 = self.search_q8_phase(3, sub, q2, k, index_base)
-            out[0].index_copy_(0, rows, d2)
-            out[1].index_copy_(0, rows, i2)
-            still = torch.nonzero(q2["cert"] == 0).reshape(-1)
-            counts.append(int(still.numel()))
+                still = rows[:0]
+            else:
+                q2 = self.quantize_queries(sub, tier=tier)
+                d2, i2 = self.search_q8_phase(3, sub, q2, k, index_base)
+                out[0].index_copy_(0, rows, d2)
+                out[1].index_copy_(0, rows, i2)
+                still = torch.nonzero(q2["cert"] == 0).reshape(-1)
+                counts.append(int(still.numel()))
+            if timings is not None:
+                ev[1].record()
+                ev[1].synchronize()
+                timings.append((str(tier), int(rows.numel()), ev[0].elapsed_time(ev[1])))
             rows = rows.index_select(0, still)
         self.last_fallbacks = tuple(counts)
         return counts[0]

@@ -29,11 +29,12 @@ class IdentityBank:
         g = _gen(seed, device)
         self.grids = torch.randn((n_ids, 1, 13, 13), generator=g, device=device, dtype=torch.float32)
 
-    def images(self, ids, seed):
-        """ids: int64 device tensor -> uint8 [len(ids)][H*W] images."""
+    def images(self, ids, seed, noise=12.0):
+        """ids: int64 device tensor -> uint8 [len(ids)][H*W] images (pixel noise N(0, noise^2); the
+        bench's stress runs raise it to crowd the identities together)."""
         g = _gen(seed, self.device)
         up = F.interpolate(self.grids[ids], size=(self.H, self.W), mode="bilinear", align_corners=False)[:, 0]
-        noise = torch.randn(up.shape, generator=g, device=self.device) * 12.0
+        noise = torch.randn(up.shape, generator=g, device=self.device) * float(noise)
         bright = (torch.rand((len(ids), 1, 1), generator=g, device=self.device) * 20.0 - 10.0)
         img = torch.clamp(torch.round(up * 40.0 + 128.0 + noise + bright), 0, 255).to(torch.uint8)
         return img.reshape(len(ids), -1)

@@ -200,7 +200,7 @@ def test_config4_training_4k_vs_oracle():
     # LDA scatter at this size vs the oracle (feature.py:160-168)
     F = np.stack([np.asarray(f).reshape(-1) for f in pf])
     Sw, Sb, _ = LDA.scatter(list(F), y)
-    oSw, oSb = O.lda_scatter(F, y)
+    _, oSw, oSb = O.lda_scatter(F.T, y)
     assert np.abs(Sw - oSw).max() <= 1e-10 * np.abs(oSw).max()
     assert np.abs(Sb - oSb).max() <= 1e-10 * np.abs(oSb).max()
     # the full training call and resubstitution
