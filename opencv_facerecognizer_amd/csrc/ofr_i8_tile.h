@@ -96,10 +96,10 @@ __device__ __forceinline__ void barrier() {
 // row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)).
 //   SL = 1: acc0 += A1 . B1
 //   SL = 2: acc0 += A1 . B1,  acc1 += A2 . B1 + A1 . B2   (slices interleaved per 128-B line)
-// XB: B holds uint8 (images); fragments are turned into x - 128 by an XOR with 0x80.
+// XB / XA: B / A hold uint8 (images); fragments are turned into x - 128 by an XOR with 0x80.
 // bcols: readable bytes per B row (DMA columns past it are clamped into the row; the
 // matching A columns are zero).  MODE 1/2: probe variants without k-loop DMA / MFMA.
-template <int SL, int MODE, bool XB>
+template <int SL, int MODE, bool XB, bool XA = false>
 __device__ __forceinline__ void mainloop(char* smem, const int8_t* A, int64_t lda, int64_t arows, int64_t a0,
                                          const int8_t* Bm, int64_t ldb, int64_t brows, int64_t b0, int64_t bcols,
                                          int nk, i32x16 (&acc0)[4][Shape<SL>::CT],
@@ -145,6 +145,7 @@ __device__ __forceinline__ void mainloop(char* smem, const int8_t* A, int64_t ld
     for (int i = 0; i < 4; ++i) {
       const int row = wr * 128 + i * 32 + r32;
       g1[b][i] = *reinterpret_cast<const i32x4*>(st + off(row, c));
+      if constexpr (XA) g1[b][i] ^= (int)0x80808080;
       if constexpr (SL == 2) g2[b][i] = *reinterpret_cast<const i32x4*>(st + off(row, c + 4));
     }
     if constexpr (SL == 2) {
