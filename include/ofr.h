@@ -287,17 +287,19 @@ int ofr_class_center_f64(void* stream, const double* F, int64_t N, int64_t D, in
  *   ofr_gram_u8        C[R][R] = X' X'^T over K columns, EXACT (int8 MFMA, int32
  *                      per chunk of < 2^17 columns, chunks summed in fp64), X the
  *                      padded uint8 [R][ld] (ld % 128 == 0), both triangles written;
- *   ofr_class_sums_u8  sums[c][D] = per-class column sums (exact, fp64 storage);
+ *   ofr_class_sums_u8  sums[c][D] = per-class column sums of x - shift (shift 0 or
+ *                      128; exact, fp64 storage), means (nullable) = sums / n_class;
  *   ofr_row_dot_u8     r[n] = sum_j (X[n][j] - 128) s[j] (exact int64, fp64 out);
  *   ofr_center_gram_f64   C[a][b] += alpha (u[a] + u[b]) + beta (R < 65536);
  *   ofr_scatter_combine_f64  Sw = G - T (skipped when Sw is NULL), Sb = T - s s^T / N
  *                      (all [D][ld]);
- *   ofr_rank1_f64      C[a][b] += alpha u[a] v[b].                                    */
+ *   ofr_rank1_f64      C[a][b] += alpha u[a] v[b];
+ *   ofr_row_div_f64    out[r][j] = A[r][j] / n[r] (class means from class sums).       */
 int ofr_pad_u8(void* stream, const uint8_t* X, int64_t rows, int64_t cols, int64_t ldx, int transpose,
                uint8_t* out, int64_t ldo);
 int ofr_gram_u8(void* stream, const uint8_t* X, int64_t R, int64_t K, int64_t ld, double* C, int64_t ldc);
 int ofr_class_sums_u8(void* stream, const uint8_t* X, int64_t D, int64_t ldx, const int64_t* perm,
-                      const int64_t* offsets, int64_t c, double* sums);
+                      const int64_t* offsets, int64_t c, int shift, double* sums, double* means);
 int ofr_row_dot_u8(void* stream, const uint8_t* X, int64_t N, int64_t D, int64_t ldx, const double* s,
                    double* r);
 int ofr_center_gram_f64(void* stream, double* C, int64_t R, int64_t ldc, const double* u, double alpha,
@@ -306,6 +308,8 @@ int ofr_scatter_combine_f64(void* stream, const double* G, const double* T, cons
                             int64_t D, int64_t ld, double* Sw, double* Sb);
 int ofr_rank1_f64(void* stream, double* C, int64_t rows, int64_t cols, int64_t ldc, const double* u,
                   const double* v, double alpha);
+int ofr_row_div_f64(void* stream, const double* A, int64_t rows, int64_t cols, int64_t lda, const double* n,
+                    double* out, int64_t ldo);
 
 /* Face-tensor ingestion ------------------------------------
  * Replaces cv2.imread(IMREAD_GRAYSCALE) + cv2.resize(im, size) [INTER_LINEAR] of

@@ -81,11 +81,12 @@ SIGNATURES = {
     "ofr_normalize_cols_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64]),
     "ofr_pad_u8": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_i64]),
     "ofr_gram_u8": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64]),
-    "ofr_class_sums_u8": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "ofr_class_sums_u8": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
     "ofr_row_dot_u8": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "ofr_center_gram_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_dbl, c_dbl]),
     "ofr_scatter_combine_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_dbl, c_i64, c_i64, c_vp, c_vp]),
     "ofr_rank1_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_dbl]),
+    "ofr_row_div_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
     "ofr_ingest_faces": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
     "ofr_class_center_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                      c_vp]),

@@ -124,15 +124,20 @@ __global__ void __launch_bounds__(256) sym_lower_kernel(double* C, int64_t R, in
   }
 }
 
-// exact per-class column sums of uint8 rows (classes given by perm / offsets), fp64 (integers)
+// exact per-class column sums of x - shift (shift 0 or 128) over uint8 rows (classes given by
+// perm / offsets), fp64 storage of the integers; means (nullable) = sums / n_class, rounded once
 __global__ void __launch_bounds__(256) class_sums_u8_kernel(const uint8_t* X, int64_t D, int64_t ldx,
-                                                            const int64_t* perm, const int64_t* offsets, double* sums) {
+                                                            const int64_t* perm, const int64_t* offsets, int shift,
+                                                            double* sums, double* means) {
   const int64_t c = blockIdx.y;
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= D) return;
+  const int64_t r0 = offsets[c], r1 = offsets[c + 1];
   int64_t s = 0;
-  for (int64_t r = offsets[c]; r < offsets[c + 1]; ++r) s += X[perm[r] * ldx + j];
+  for (int64_t r = r0; r < r1; ++r) s += X[perm[r] * ldx + j];
+  s -= (int64_t)shift * (r1 - r0);
   sums[c * D + j] = (double)s;
+  if (means) means[c * D + j] = r1 > r0 ? (double)s / (double)(r1 - r0) : 0.0;
 }
 
 // r[n] = sum_j (X[n][j] - 128) s[j]: exact int64 (|s| <= 2^53 / (128 D) is the caller's bound)
@@ -177,6 +182,15 @@ __global__ void __launch_bounds__(256) rank1_kernel(double* C, int64_t cols, int
   const double ua = alpha * u[a];
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < cols; b += (int64_t)gridDim.x * blockDim.x)
     C[a * ldc + b] += ua * v[b];
+}
+
+// out[r][j] = A[r][j] / n[r]  (class means from class sums; n[r] = 0 -> 0)
+__global__ void __launch_bounds__(256) row_div_kernel(const double* A, int64_t cols, int64_t lda, const double* n,
+                                                      double* out, int64_t ldo) {
+  const int64_t r = blockIdx.y;
+  const double nr = n[r];
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < cols; j += (int64_t)gridDim.x * blockDim.x)
+    out[r * ldo + j] = nr != 0.0 ? A[r * lda + j] / nr : 0.0;
 }
 
 }  // namespace gram
@@ -240,11 +254,12 @@ extern "C" int ofr_gram_u8(void* stream, const uint8_t* X, int64_t R, int64_t K,
 }
 
 extern "C" int ofr_class_sums_u8(void* stream, const uint8_t* X, int64_t D, int64_t ldx, const int64_t* perm,
-                                 const int64_t* offsets, int64_t c, double* sums) {
+                                 const int64_t* offsets, int64_t c, int shift, double* sums, double* means) {
   OFR_CHECK_ARG(D >= 1 && ldx >= D && c >= 1 && c < 65536, "ofr_class_sums_u8: bad sizes");
+  OFR_CHECK_ARG(shift == 0 || shift == 128, "ofr_class_sums_u8: shift must be 0 or 128");
   OFR_CHECK_ARG(X && perm && offsets && sums, "ofr_class_sums_u8: null pointer");
   hipLaunchKernelGGL(gram::class_sums_u8_kernel, dim3((unsigned)cdiv(D, 256), (unsigned)c), dim3(256), 0,
-                     (hipStream_t)stream, X, D, ldx, perm, offsets, sums);
+                     (hipStream_t)stream, X, D, ldx, perm, offsets, shift, sums, means);
   OFR_LAUNCH_CHECK("class_sums_u8_kernel");
   return OFR_OK;
 }
@@ -290,6 +305,20 @@ extern "C" int ofr_rank1_f64(void* stream, double* C, int64_t rows, int64_t cols
     hipLaunchKernelGGL(gram::rank1_kernel, dim3((unsigned)std::min<int64_t>(cdiv(cols, 256), 64), (unsigned)nr),
                        dim3(256), 0, (hipStream_t)stream, C + r0 * ldc, cols, ldc, u + r0, v, alpha);
     OFR_LAUNCH_CHECK("rank1_kernel");
+  }
+  return OFR_OK;
+}
+
+extern "C" int ofr_row_div_f64(void* stream, const double* A, int64_t rows, int64_t cols, int64_t lda,
+                               const double* n, double* out, int64_t ldo) {
+  OFR_CHECK_ARG(rows >= 0 && cols >= 0 && lda >= cols && ldo >= cols, "ofr_row_div_f64: bad sizes");
+  if (rows == 0 || cols == 0) return OFR_OK;
+  OFR_CHECK_ARG(A && n && out, "ofr_row_div_f64: null pointer");
+  for (int64_t r0 = 0; r0 < rows; r0 += 65535) {
+    const int64_t nr = std::min<int64_t>(65535, rows - r0);
+    hipLaunchKernelGGL(gram::row_div_kernel, dim3((unsigned)std::min<int64_t>(cdiv(cols, 256), 64), (unsigned)nr),
+                       dim3(256), 0, (hipStream_t)stream, A + r0 * lda, cols, lda, n + r0, out + r0 * ldo, ldo);
+    OFR_LAUNCH_CHECK("row_div_kernel");
   }
   return OFR_OK;
 }

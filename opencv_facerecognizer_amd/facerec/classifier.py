@@ -139,6 +139,16 @@ class NearestNeighbor(AbstractClassifier):
             self.__dict__["_dev"] = (key, n, g)
             return g
 
+    def adopt_device_rows(self, F):
+        """Seed the device gallery from fp64 device rows F [N][d] equal to self.X (e.g. the training
+        features a Fisherfaces.compute just produced on the device)."""
+        mid = self._metric()
+        if mid == _lib.METRIC_CHISQUARE or int(F.shape[0]) != len(self.X):
+            return
+        with _DEVICE_LOCK:
+            g = FloatGallery(F, mid)
+            self.__dict__["_dev"] = ((mid, id(self.X), _lib.device()), len(self.X), g)
+
     @staticmethod
     def _stack(items):
         return np.stack([np.asarray(x, dtype=np.float64).reshape(-1) for x in items])

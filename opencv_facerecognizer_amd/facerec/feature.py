@@ -138,7 +138,8 @@ class _DeviceProjMixin:
 
     def __getstate__(self):
         st = dict(self.__dict__)
-        st.pop("_dev_proj", None)
+        for key in ("_dev_proj", "_dev_features", "_regime"):   # derived state, never pickled
+            st.pop(key, None)
         return st
 
 
@@ -339,7 +340,69 @@ class Fisherfaces(_DeviceProjMixin, AbstractFeature):
         self._num_components = num_components
 
     def compute(self, X, y):
+        """feature.py:211-235.  uint8 faces take the exact device pipeline (training.py): PCA(n - c)
+        then LDA(num_components), W = P . L, features W^T x; any other input dtype takes the
+        ChainOperator(PCA, LDA) path on fp64 device GEMMs."""
         y = np.asarray(y)
+        Xd, D, kind = _device_rows(X)
+        if kind != "u8":
+            return self._compute_chain(X, y)
+        from .. import training
+        lay = training.Layout(y, Xd.device)
+        n, c = lay.n, lay.c
+        k = n - c                                              # PCA(n - c), feature.py:219 / :88-89
+        if k <= 0 or k > n - 1:
+            k = n - 1
+        k = min(k, D, n)                                       # columns of the economy SVD
+        m = self._num_components                               # LDA(num_components), feature.py:155-158
+        if m <= 0 or m > c - 1:
+            m = c - 1
+        if k >= D:
+            # PCA keeps every pixel dimension (a rotation): LDA in pixel space, W = V directly
+            self._regime = "pixel"
+            Sw, Sb = training.pixel_scatter(training.pixel_pieces(Xd, D, lay), lay.counts, n)
+            evals, W = lda_eigen(Sw.cpu().numpy(), Sb.cpu().numpy(), m)
+            del Sw, Sb
+            Wd = None
+        elif n <= D:
+            # n x n Gram of the centred faces: U_k = XC^T V_k / sigma_k, features V_k sigma_k
+            self._regime = "gram"
+            lam, V = training.host_eigh_desc(training.centred_gram(Xd, D, lay))
+            sig = np.sqrt(np.maximum(lam[:k], 0.0))
+            F = V[:, :k] * sig
+            Sw, Sb = training.feature_scatter(_device.f64_dev(F), y)
+            evals, L = lda_eigen(Sw.cpu().numpy(), Sb.cpu().numpy(), m)
+            L32 = np.asarray(L, dtype=np.float32).astype(np.float64)          # feature.py:176
+            inv = np.divide(1.0, sig, out=np.zeros_like(sig), where=sig > 0)
+            M = _device.gemm_f64(_device.f64_dev(V[:, :k] * inv), _device.f64_dev(L32))   # V_k Sigma^-1 L
+            Wd = training.xct_times(Xd, D, lay, M, training.mean_image(Xd, D, lay))
+        else:
+            # D x D covariance: P = leading k eigenvectors, features XC P, W = P L
+            self._regime = "cov"
+            pieces = training.pixel_pieces(Xd, D, lay)
+            lam, V = training.host_eigh_desc(training.covariance(pieces, n))
+            del pieces
+            Pd = _device.f64_dev(V[:, :k])
+            mu = training.mean_image(Xd, D, lay)
+            shift = _device.gemm_f64(mu.reshape(1, -1).contiguous(), Pd).reshape(-1)
+            Fd = _device.Projection(Wt_device=Pd.t().contiguous(), D=D).project(Xd, shift64=shift, f64=True)
+            Sw, Sb = training.feature_scatter(Fd, y)
+            del Fd
+            evals, L = lda_eigen(Sw.cpu().numpy(), Sb.cpu().numpy(), m)
+            L32 = np.asarray(L, dtype=np.float32).astype(np.float64)          # feature.py:176
+            Wd = _device.gemm_f64(Pd, _device.f64_dev(L32))                      # feature.py:229
+        self._eigenvalues = np.array(evals, dtype=np.float32, copy=True)      # :226-227 (LDA's, float32)
+        self._num_components = m
+        self._eigenvectors = np.asmatrix(Wd.cpu().numpy() if Wd is not None else np.asarray(W, np.float64))
+        self.__dict__.pop("_dev_proj", None)
+        # features of the training set (:231-235): one batched exact projection of the resident faces
+        Fd = self.project_device(Xd, f64=True)
+        feats = [np.asmatrix(r.reshape(-1, 1)) for r in Fd.cpu().numpy()]
+        self.__dict__["_dev_features"] = (id(feats), Fd)      # handed to the classifier's gallery
+        return feats
+
+    def _compute_chain(self, X, y):
+        """feature.py:211-235 for non-uint8 inputs: ChainOperator(PCA, LDA) on fp64 device GEMMs."""
         n = len(y)                                             # feature.py:216-217
         c = len(np.unique(y))
         pca = PCA(num_components=(n - c))                      # :219-224

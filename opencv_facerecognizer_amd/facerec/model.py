@@ -24,9 +24,13 @@ class PredictableModel(object):
         self.classifier = classifier
 
     def compute(self, X, y):
-        """model.py:49-51."""
+        """model.py:49-51.  When the feature left its training features on the device, the classifier
+        builds its device gallery from them (no host round trip of the gallery)."""
         features = self.feature.compute(X, y)
         self.classifier.compute(features, y)
+        dev = self.feature.__dict__.pop("_dev_features", None)
+        if dev is not None and dev[0] == id(features) and hasattr(self.classifier, "adopt_device_rows"):
+            self.classifier.adopt_device_rows(dev[1])
 
     def predict(self, X):
         """model.py:53-55 (one face)."""

@@ -14,6 +14,7 @@ projection costs 1/G instead of being replicated.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -143,3 +144,71 @@ def certify_sharded(gallery, Qd, qq, k, out, index_base, group=None):
         counts.append(int(still.numel()))
         rows = rows.index_select(0, still)
     return (md, mi), counts
+
+
+# ---------------------------------------------------------------------------
+# training: the one exchange step of SURVEY §8e
+# ---------------------------------------------------------------------------
+def allreduce_exact(tensors, group=None):
+    """Sum integer-valued fp64 tensors (partial Grams / class sums) over the ranks.  Every partial
+    value and every sum is an integer below 2^53, so the floating-point additions are exact and the
+    result does not depend on the reduction order or the number of ranks."""
+    _, ws = world(group)
+    if ws == 1:
+        return tensors
+    for t in tensors:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return tensors
+
+
+def train_fisherfaces_sharded(feature, X_local, y_local, num_classes, group=None):
+    """Fisherfaces.compute (feature.py:211-235) with the training faces sharded over the ranks.
+
+    Each rank holds its own faces (uint8) and their labels (global 0..c-1).  In the pixel regime
+    (PCA keeps every dimension: n - c >= D and n >= D, e.g. BASELINE configs[4]) the statistics are
+    sums over faces: rank r forms its exact pieces (X'^T X', class sums, column sums; int8 MFMA) and
+    ONE all-reduce (RCCL over xGMI; gloo in tests) combines them exactly; every rank then has the
+    same Sw, Sb.  Rank 0 solves the eigenproblem (host LAPACK, as the reference) and broadcasts W,
+    and each rank projects its own faces: the features come back as this rank's gallery shard.
+    Returns this rank's features (list of (d,1) matrices, the reference's return type)."""
+    from . import _device, training
+    from .facerec.feature import lda_eigen
+    rank, ws = world(group)
+    Xd, D, kind = _device_rows_u8(X_local)
+    lay = training.Layout(y_local, Xd.device, c=num_classes)
+    counts = torch.from_numpy(lay.counts.astype(np.float64)).to(Xd.device)
+    pieces = training.pixel_pieces(Xd, D, lay)
+    allreduce_exact([pieces["G"], pieces["S"], pieces["s"], counts], group)
+    cnt = counts.cpu().numpy()
+    n, c = int(cnt.sum()), int(num_classes)
+    if n - c < D or n < D:
+        raise NotImplementedError("sharded training needs the pixel regime (n - c >= D and n >= D)")
+    m = feature._num_components
+    if m <= 0 or m > c - 1:
+        m = c - 1
+    Sw, Sb = training.pixel_scatter(pieces, cnt, n)
+    del pieces
+    W = torch.empty((D, m), dtype=torch.float64, device=Xd.device)
+    ev = torch.empty(m, dtype=torch.float64, device=Xd.device)
+    if rank == 0:
+        evals, V = lda_eigen(Sw.cpu().numpy(), Sb.cpu().numpy(), m)
+        W.copy_(torch.from_numpy(np.ascontiguousarray(V, dtype=np.float64)))
+        ev.copy_(torch.from_numpy(np.asarray(evals, dtype=np.float64)))
+    del Sw, Sb
+    if ws > 1:
+        dist.broadcast(W, 0, group=group)
+        dist.broadcast(ev, 0, group=group)
+    feature._eigenvalues = ev.cpu().numpy().astype(np.float32)
+    feature._num_components = m
+    feature._eigenvectors = np.asmatrix(W.cpu().numpy())
+    feature.__dict__.pop("_dev_proj", None)
+    Fd = feature.project_device(Xd, f64=True)
+    return [np.asmatrix(r.reshape(-1, 1)) for r in Fd.cpu().numpy()]
+
+
+def _device_rows_u8(X):
+    from .facerec.feature import _device_rows
+    Xd, D, kind = _device_rows(X)
+    if kind != "u8":
+        raise TypeError("sharded training takes uint8 faces")
+    return Xd, D, kind

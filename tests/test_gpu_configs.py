@@ -234,3 +234,90 @@ def test_config4_training_full_100k(monkeypatch):
     Xq, yq = _faces(4096, c, side, 20261015 + 24)
     labels = np.array([p[0] for p in model.predict_batch(Xq)])
     assert np.mean(labels == yq) >= 0.99
+
+
+# ---------------------------------------------------------------------------
+# Fisherfaces training regimes (training.py) against the oracle
+# ---------------------------------------------------------------------------
+def _small_faces(n, c, side, seed, noise=12.0):
+    from opencv_facerecognizer_amd.synthetic import IdentityBank
+    dev = torch.device("cuda", 0)
+    y = torch.arange(n, device=dev) % c
+    X = IdentityBank(c, side, side, device=dev, seed=seed).images(y, seed=seed + 1, noise=noise)
+    return X.reshape(n, side, side).cpu().numpy(), y.cpu().numpy()
+
+
+@pytest.mark.parametrize("regime,n,c,side", [("pixel", 400, 20, 12), ("cov", 200, 100, 12), ("gram", 120, 12, 12)])
+def test_fisherfaces_regimes_vs_oracle(regime, n, c, side):
+    """Fisherfaces.compute (feature.py:211-235) in each regime of the exact device pipeline against the
+    oracle's PCA (SVD) -> LDA (inv + eig) chain: LDA eigenvalues, W columns up to sign (for distinct
+    eigenvalues), and the training features."""
+    from ocvfacerec.facerec.feature import Fisherfaces
+    X, y = _small_faces(n, c, side, 900 + n)
+    ff = Fisherfaces()
+    feats = ff.compute(list(X), y)
+    assert ff._regime == regime
+    ref = O.fisherfaces_compute(list(X), y)
+    W, Wr = np.asarray(ff._eigenvectors), np.asarray(ref["eigenvectors"])
+    assert W.shape == Wr.shape
+    ev, evr = np.asarray(ff._eigenvalues, np.float64), np.asarray(ref["eigenvalues"], np.float64)
+    assert np.allclose(ev, evr, rtol=2e-5, atol=1e-6 * evr.max())
+    gap = np.minimum(np.abs(np.diff(np.r_[np.inf, evr])), np.abs(np.diff(np.r_[evr, -np.inf])))
+    ok = gap > 1e-3 * evr.max()
+    cos = np.abs(np.sum(W * Wr, 0)) / (np.linalg.norm(W, axis=0) * np.linalg.norm(Wr, axis=0))
+    assert ok.sum() >= len(ok) // 2 and np.all(cos[ok] > 1 - 1e-6), (cos[ok].min(), ok.sum())
+    # features are W^T x of the training faces (feature.py:231-235), column signs aside
+    F = np.stack([np.asarray(f).reshape(-1) for f in feats])
+    Fr = X.reshape(n, -1).astype(np.float64) @ W
+    assert np.allclose(F, Fr, rtol=0, atol=1e-9 * np.abs(Fr).max())
+
+
+def _sharded_train_worker(rank, ws, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from ocvfacerec.facerec.feature import Fisherfaces
+        from opencv_facerecognizer_amd.parallel import shard_range, train_fisherfaces_sharded
+        X, y = _small_faces(400, 20, 12, 1300)
+        n0, n1 = shard_range(len(y), rank, ws)
+        ff = Fisherfaces()
+        feats = train_fisherfaces_sharded(ff, list(X[n0:n1]), y[n0:n1], 20)
+        out.put((rank, np.asarray(ff._eigenvectors), np.asarray(ff._eigenvalues),
+                 np.stack([np.asarray(f).reshape(-1) for f in feats])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_training_equals_single_process():
+    """SURVEY §8e training exchange on 2 gloo ranks sharing the device: the exact pieces all-reduce
+    bit for bit, so W equals the single-process Fisherfaces.compute; each rank returns the features
+    of its own faces (its gallery shard)."""
+    import torch.multiprocessing as mp
+    from ocvfacerec.facerec.feature import Fisherfaces
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        item = q.get(timeout=240)
+        res[item[0]] = item[1:]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    X, y = _small_faces(400, 20, 12, 1300)
+    ff = Fisherfaces()
+    feats = ff.compute(list(X), y)
+    assert ff._regime == "pixel"
+    W = np.asarray(ff._eigenvectors)
+    for r in (0, 1):
+        assert np.array_equal(res[r][0], res[0][0])                       # the same model on every rank
+    assert np.allclose(res[0][0], W, rtol=0, atol=1e-12)
+    assert np.array_equal(res[0][1], np.asarray(ff._eigenvalues))
+    F = np.stack([np.asarray(f).reshape(-1) for f in feats])
+    assert np.allclose(np.concatenate([res[0][2], res[1][2]]), F, rtol=0, atol=1e-9 * np.abs(F).max())

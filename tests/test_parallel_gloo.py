@@ -231,3 +231,60 @@ def test_global_certificate_bounds():
     kth = torch.tensor([1.0, 1.0, float("inf"), 1.0, 3.0])
     minb = torch.tensor([2.0, -float("inf"), float("inf"), float("inf"), 4.0])
     assert global_certificate(kth, minb).tolist() == [True, False, True, True, False]
+
+
+def _train_pieces_worker(rank, ws, port, out):
+    """Each rank: the exact pixel-space pieces of its shard (X'^T X', class sums, counts as integer-
+    valued fp64, the layout training.pixel_pieces produces on the device), then allreduce_exact."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from opencv_facerecognizer_amd.parallel import allreduce_exact
+        X, y, c = _train_data()
+        n0, n1 = shard_range(len(y), rank, ws)
+        Xs = X[n0:n1].astype(np.int64) - 128
+        G = torch.from_numpy((Xs.T @ Xs).astype(np.float64))
+        S = torch.from_numpy(np.stack([Xs[y[n0:n1] == i].sum(0) for i in range(c)]).astype(np.float64))
+        cnt = torch.from_numpy(np.bincount(y[n0:n1], minlength=c).astype(np.float64))
+        allreduce_exact([G, S, cnt])
+        if rank == 0:
+            out.put((G.numpy(), S.numpy(), cnt.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _train_data():
+    r = np.random.default_rng(77)
+    c, n, D = 7, 301, 36
+    y = np.arange(n) % c
+    protos = r.integers(40, 216, (c, D))
+    X = np.clip(protos[y] + r.integers(-30, 31, (n, D)), 0, 255).astype(np.uint8)
+    return X, y, c
+
+
+def test_sharded_training_pieces_allreduce_exactly():
+    """SURVEY §8e's training exchange: per-rank X'^T X' and class sums, one all-reduce; the sums are
+    integer-valued, so they equal the single-process pieces BIT FOR BIT, and the pixel-space
+    Sw / Sb formed from them (training.pixel_scatter's formula) equal the reference's scatter
+    (feature.py:160-168, the oracle) over pixels."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_pieces_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    G, S, cnt = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    X, y, c = _train_data()
+    Xs = X.astype(np.int64) - 128
+    assert np.array_equal(G, (Xs.T @ Xs).astype(np.float64))
+    assert np.array_equal(S, np.stack([Xs[y == i].sum(0) for i in range(c)]).astype(np.float64))
+    n = len(y)
+    s = S.sum(0)
+    T = (S / cnt[:, None]).T @ S
+    Sw, Sb = G - T, T - np.outer(s, s) / n
+    _, oSw, oSb = O.lda_scatter(X.T.astype(np.float64), y)
+    assert np.allclose(Sw, oSw, rtol=0, atol=1e-9 * np.abs(oSw).max())
+    assert np.allclose(Sb, oSb, rtol=0, atol=1e-9 * np.abs(oSb).max())
