@@ -258,7 +258,7 @@ def test_fisherfaces_regimes_vs_oracle(regime, n, c, side):
     feats = ff.compute(list(X), y)
     assert ff._regime == regime
     ref = O.fisherfaces_compute(list(X), y)
-    W, Wr = np.asarray(ff._eigenvectors), np.asarray(ref["eigenvectors"])
+    W, Wr = np.asarray(ff._eigenvectors), np.asarray(ref["W"])
     assert W.shape == Wr.shape
     ev, evr = np.asarray(ff._eigenvalues, np.float64), np.asarray(ref["eigenvalues"], np.float64)
     assert np.allclose(ev, evr, rtol=2e-5, atol=1e-6 * evr.max())

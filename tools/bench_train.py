@@ -95,16 +95,25 @@ def main():
     acc = float((labels == ids_q.cpu().numpy()).mean())
     host = sum(HOST.values())
     n, D, c = args.n, args.side * args.side, args.ids
-    k = min(n - c, n - 1, D)     # PCA components (feature.py:88-89, at most min(D, N) singular vectors)
+    k = min(n - c if 0 < n - c <= n - 1 else n - 1, D, n)   # PCA components (feature.py:88-89)
     d = c - 1
     W = np.asarray(ff._eigenvectors)
     F = np.stack([np.asarray(f).reshape(-1) for f in feats])
-    pca = ({"pca_gram": 2.0 * n * n * D, "pca_left_vectors": 2.0 * D * n * n} if n <= D else
-           {"pca_covariance": 2.0 * n * D * D})
-    flops = {**pca, "pca_features": 2.0 * n * D * k,
-             "lda_sw": 2.0 * k * k * n, "lda_sb": 2.0 * k * k * c, "lda_features": 2.0 * n * k * d,
-             "w_pl": 2.0 * D * k * d, "train_projection_int8x4": 4 * 2.0 * n * D * d}
-
+    regime = getattr(ff, "_regime", "?")
+    # algorithmic work of the device products per regime (training.py); int8 ops are exact Gram
+    # products on the int8 MFMA, fp64 flops on the fp64 MFMA
+    t = lambda R: -(-R // 256)                                             # noqa: E731
+    gram_ops = lambda R, K: 2.0 * (t(R) * (t(R) + 1) // 2) * 256 * 256 * (-(-K // 128) * 128)   # noqa: E731
+    if regime == "pixel":
+        work = {"gram_u8_XtX_int8": gram_ops(D, n), "class_means_T_fp64": 2.0 * c * D * D}
+    elif regime == "gram":
+        work = {"gram_u8_XXt_int8": gram_ops(n, D), "lda_sw_sb_fp64": 2.0 * k * k * (n + c),
+                "xct_M_int8x4": 4 * 2.0 * D * n * d}
+    else:
+        work = {"gram_u8_XtX_int8": gram_ops(D, n), "pca_features_int8x4": 4 * 2.0 * n * D * k,
+                "lda_sw_sb_fp64": 2.0 * k * k * (n + c), "w_pl_fp64": 2.0 * D * k * d}
+    work["train_projection_int8x4"] = 4 * 2.0 * n * D * d
+    flops = work
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import facerec_oracle as O  # the checker; timed here as the CPU baseline
     Xc, yc = faces(args.n_cpu, max(2, args.ids * args.n_cpu // args.n), args.side, device, SEED + 22)
@@ -113,14 +122,14 @@ def main():
     t_cpu = time.perf_counter() - t1
     out = {
         "metric": "PredictableModel(Fisherfaces, NearestNeighbor).compute wall time, then predict (configs[4])",
-        "config": {"n": n, "identities": c, "D": D, "pca_components": k, "d": d, "lda_solver": args.solver},
+        "config": {"n": n, "identities": c, "D": D, "pca_components": k, "d": d, "lda_solver": args.solver,
+                   "regime": regime},
         "data": "synthetic",
         "wall_s": total, "host_lapack_s": dict(HOST), "device_and_transfers_s": total - host,
         "predict": {"batch": args.predict, "first_call_s": pred_s[0], "steady_s": min(pred_s[1:]),
                     "queries_per_s": args.predict / min(pred_s[1:]), "top1_identity_acc": acc,
                     "note": "first call builds the device gallery (upload + quantized tiers) from the training features"},
-        "device_flops": flops, "device_flops_total": sum(flops.values()),
-        "device_tflops_upper_bound": sum(flops.values()) / max(total - host, 1e-9) / 1e12,
+        "device_ops": flops, "device_ops_total": sum(flops.values()),
         "W_shape": list(W.shape), "finite": bool(np.isfinite(W).all() and np.isfinite(F).all()),
         "cpu_baseline": {"kind": "port", "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
                          "sample": f"oracle fisherfaces_compute (reference-faithful: SVD, as_column_matrix) on "
