@@ -265,11 +265,12 @@ def test_fisherfaces_regimes_vs_oracle(regime, n, c, side):
     gap = np.minimum(np.abs(np.diff(np.r_[np.inf, evr])), np.abs(np.diff(np.r_[evr, -np.inf])))
     ok = gap > 1e-3 * evr.max()
     cos = np.abs(np.sum(W * Wr, 0)) / (np.linalg.norm(W, axis=0) * np.linalg.norm(Wr, axis=0))
-    assert ok.sum() >= len(ok) // 2 and np.all(cos[ok] > 1 - 1e-6), (cos[ok].min(), ok.sum())
-    # features are W^T x of the training faces (feature.py:231-235), column signs aside
+    assert ok.sum() >= 3 and np.all(cos[ok] > 1 - 1e-6), (cos[ok].min(), ok.sum())
+    # features are W^T x of the training faces (feature.py:231-235), on the int8-slice projection
+    # engine (W cut at 2^-28 of its column maxima: ~1e-8 relative)
     F = np.stack([np.asarray(f).reshape(-1) for f in feats])
     Fr = X.reshape(n, -1).astype(np.float64) @ W
-    assert np.allclose(F, Fr, rtol=0, atol=1e-9 * np.abs(Fr).max())
+    assert np.allclose(F, Fr, rtol=0, atol=1e-7 * np.abs(Fr).max())
 
 
 def _sharded_train_worker(rank, ws, port, out):
