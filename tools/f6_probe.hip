@@ -107,6 +107,13 @@ int main(int argc, char** argv) {
         return 1;
     return 0;
   }
+  if (getenv("GG_SWEEP")) {   // tile-group width (gallery panels per group) vs the sieve pass time
+    for (int g : {1, 2, 4, 8, 16, 32}) {
+      a.gg = g < ntg ? g : ntg;
+      if (run<8, 8>(a, reps, "sieve-gg")) return 1;
+    }
+    return 0;
+  }
   a.gg = 4 < ntg ? 4 : ntg;
   // MODE bits: 8 = sieve epilogue (else tile lists); 4 = no epilogue; 1 = no k-loop DMA;
   // 2 / 16 = no gallery / query block in the DMA
