@@ -14,13 +14,16 @@
 //     block(p, s) = base + (p * nst + s) * 24576
 //     sub-block (j, h) at + (2j + h) * 6144       j = 64-feature MFMA step, h = 32-feature half
 //         part0: 16 B per row at + row * 16       (4 KiB)
-//         part1:  8 B per row at + 4096 + row * 8 (2 KiB)
+//         part1:  8 B per row at + 4096 + slot * 8 (2 KiB), slot = row ^ 16 h (p1_slot)
 // Features k = 128 s + 64 j + 32 h + e (e < 32) of a row form a 192-bit little-endian
 // stream (part0 then part1), element e at bits 6e..6e+5 -- exactly the register image
 // lane (h, r) of the MFMA takes for row r (tools/mx_probe.hip verified the map).  The
 // LDS image of a stage is the same bytes: each DMA wave-instruction copies 1 KiB
-// contiguous, and the fragment reads (ds_read_b128 of part0, ds_read_b64 of part1, 32
-// consecutive rows per half-wave) are bank-conflict free without a swizzle.
+// contiguous.  Fragment reads are bank-conflict free for both MFMA shapes: 32x32x64 (a
+// half-wave reads 32 consecutive rows of one sub-block: part0 ds_read_b128 and part1
+// ds_read_b64, whose slot swizzle only permutes inside the 32 rows) and 16x16x128 (lanes
+// 16q..16q+15 read 16 rows of sub-block q: the odd sub-blocks' part1 rows sit 16 slots away,
+// in the other half of the 64 banks the b64 lane group {0-31} / {32-63} spans).
 #pragma once
 #include "ofr_common.h"
 
@@ -30,7 +33,9 @@ namespace f6t {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x6 __attribute__((ext_vector_type(6)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int TA = 256, TQ = 256;            // gallery x query rows per tile
 constexpr int BK = 128;                      // features per stage
@@ -40,6 +45,7 @@ constexpr int STAGE = 2 * PANEL;             // gallery block + query block
 constexpr int LDS = NST * STAGE;             // 144 KiB
 constexpr int DMA_INS = STAGE / 1024;        // 1-KiB DMA wave-instructions per stage (48)
 
+__host__ __device__ constexpr int p1_slot(int jh, int row) { return row ^ ((jh & 1) << 4); }
 __host__ __device__ constexpr int64_t panels(int64_t rows) { return (rows + TA - 1) / TA; }
 __host__ __device__ constexpr int64_t stages(int64_t d) { return (d + BK - 1) / BK; }
 __host__ __device__ constexpr int64_t tiles_bytes(int64_t rows, int64_t d) {
@@ -65,7 +71,7 @@ __device__ __forceinline__ i32x8 frag(const char* blk, int j, int h, int row) {
   const char* sb = blk + (2 * j + h) * 6144;
   // opaque part1 address: keeps the compiler from pairing part1 reads of different
   // fragments into ds_read2_b64 (which lands them apart from part0 and costs v_movs)
-  const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + row * 8);
+  const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + p1_slot(h, row) * 8);
   asm volatile("" : "+v"(p1a));
   const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
   const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
@@ -198,6 +204,107 @@ struct Engine {
     mfmas(0);
     interleave();
     mfmas(1);
+    wait_vm<0>();
+    barrier();
+  }
+};
+
+// ---- 16x16x128 engine (the sieve pass) -------------------------------------------------------
+// Same stages, LDS image and DMA as Engine<8>; the MFMA is v_mfma_scale_f32_16x16x128_f8f6f4: on
+// random fp6 operands the chip holds a higher clock for it than for the 32x32x64 form, +14 %
+// sustained rate at equal work (tools/f6_shape_probe.hip).  One MFMA k-step = one 128-feature
+// stage.  Lane l holds rows (l % 16) of a 16-row block and the 32 features of sub-block
+// q = l / 16 (the f6 tiled sub-blocks are exactly these 32-feature groups).  C/D: query column
+// l % 16 of the 16-query block, gallery rows 4 (l / 16) + reg.
+// 8 waves (2 per SIMD), wave grid 2 x 4 as Engine<8>: wave (wr, wc) owns gallery rows
+// wr*128 + 16 i + .. (i < 8) and queries wc*64 + 16 c + l % 16 (c < 4): 32 accumulators of 4.
+struct Engine16 {
+  static constexpr int NW = 8, NT = 512, WQ = 4, QW = 64, NA = 8, NB = 4;
+  static constexpr int IPW = DMA_INS / NW;   // 6
+
+  // fragments live as 6 registers (the fp6 MFMA reads v[0:5] of its 8-register operand slot)
+  static __device__ __forceinline__ i32x6 frag16(const char* st, int row) {
+    const int q = (threadIdx.x & 63) >> 4;
+    const char* sb = st + q * 6144;
+    const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + p1_slot(q, row) * 8);
+    asm volatile("" : "+v"(p1a));
+    const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
+    const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
+    i32x6 f;
+    f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
+    return f;
+  }
+  static __device__ __forceinline__ f32x4 mfma(const i32x6& a, const i32x6& b, const f32x4& c) {
+    const i32x8 a8 = __builtin_shufflevector(a, a, 0, 1, 2, 3, 4, 5, -1, -1);
+    const i32x8 b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, 4, 5, -1, -1);
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 2, 2, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+  }
+
+  // MODE (probes): 1 = no k-loop DMA
+  template <int MODE>
+  static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
+                                                  int nst, f32x4 (&acc)[NA][NB]) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr = wave / WQ, wc = wave % WQ, r16 = lane & 15;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto issue = [&](int kt) { Engine<8>::dma<0>(G, gp, Q, qp, nst, kt, smem + (kt % NST) * STAGE); };
+    const int last = nst - 1;
+#pragma unroll
+    for (int s = 0; s < NST; ++s) issue(s < last ? s : last);
+    i32x6 a[NA], b[NB];
+    auto readA = [&](const char* st, int i) { a[i] = frag16(st, wr * 128 + i * 16 + r16); };
+    auto readB = [&](const char* st, int c) { b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16); };
+    if constexpr (MODE == 1) wait_vm<0>();
+    else wait_vm<2 * IPW>();
+    barrier();
+#pragma unroll
+    for (int i = 0; i < NA; ++i) readA(smem, i);
+#pragma unroll
+    for (int c = 0; c < NB; ++c) readB(smem, c);
+    // Per stage kt: MFMAs of stage kt, each fragment replaced by stage kt+1's as soon as its last
+    // MFMA is issued (A-major: A[i] after row i's 4 MFMAs, B[c] after row 7's MFMA c), so the
+    // fragments need no second register set (acc 128 + fragments 72 registers).
+    for (int kt = 0; kt < last; ++kt) {
+      if constexpr (MODE == 1) wait_vm<0>();
+      else wait_vm<IPW>();       // stage kt+1 landed; kt+2 may be in flight
+      barrier();                 // every wave has read stage kt: its buffer takes stage kt+3
+      if constexpr (MODE != 1) {
+        const int nx = kt + NST;
+        issue(nx < last ? nx : last);
+      }
+      const char* nxt = smem + ((kt + 1) % NST) * STAGE;
+#pragma unroll
+      for (int i = 0; i < NA - 1; ++i) {
+#pragma unroll
+        for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i], b[c], acc[i][c]);
+        readA(nxt, i);
+      }
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        acc[NA - 1][c] = mfma(a[NA - 1], b[c], acc[NA - 1][c]);
+        readB(nxt, c);
+      }
+      readA(nxt, NA - 1);
+      __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
+#pragma unroll
+      for (int i = 0; i < NA - 1; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i], b[c], acc[i][c]);
     wait_vm<0>();
     barrier();
   }

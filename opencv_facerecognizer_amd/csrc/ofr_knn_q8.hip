@@ -224,6 +224,9 @@ constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
 // query block of this lane (th = key_float(theta | 0xff): truncated key <= theta  <=>
 // !(score > th); NaN for KEY_NONE keeps every row).  More than SIEVE_HCAP hits in one tile push
 // every query of the tile past its bucket cap (uncertified, no candidates read by the merge).
+template <int TQ>
+__device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64_t g0, int64_t q0);
+
 template <int CT, int TQ, int QW, int WQ, class CV>
 __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, int64_t g0, int64_t q0, float ga,
                                                float gs, const float (&sq2)[CT], const float (&th)[CT], CV&& cval) {
@@ -272,6 +275,14 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
     }
   }
   __syncthreads();
+  sieve_flush<TQ>(smem, p, g0, q0);
+}
+
+// The tile's staged hits -> per-query buckets (after the compares and a barrier)
+template <int TQ>
+__device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
+  const uint32_t* nhit = reinterpret_cast<const uint32_t*>(smem + TG * 8);
+  const uint2* hits = reinterpret_cast<const uint2*>(smem + TG * 8 + 16);
   const uint32_t nh = *nhit;
   if (nh > (uint32_t)SIEVE_HCAP) {   // hits lost: push every query of the tile past its cap (uncertified)
     // saturating (max, not add): any number of overflowing tiles leaves the count at cap + 1 plus
@@ -368,6 +379,90 @@ __global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
     tile_epilogue<CT, f6t::TQ, E::QW, E::WQ>(smem, p, gt, g0, q0, cval);
 }
 
+// Sieve epilogue of the 16x16x128 engine (f6t::Engine16): element reg r of accumulator (i, c) of
+// lane l is gallery row wr*128 + 16 i + 4 (l / 16) + r, query wc*64 + 16 c + l % 16.
+__device__ __forceinline__ void sieve_epilogue16(char* smem, const TileArgs& p, int64_t g0, int64_t q0, float ga,
+                                                 float gs, const float (&sq2)[4], const float (&th)[4],
+                                                 const f6t::f32x4 (&acc)[8][4]) {
+  using E = f6t::Engine16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave / E::WQ, wc = wave % E::WQ, g4 = (lane >> 4) * 4, r16 = lane & 15;
+  float* gtab = reinterpret_cast<float*>(smem);                                  // [TG][2]
+  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + TG * 8);
+  uint2* hits = reinterpret_cast<uint2*>(smem + TG * 8 + 16);                    // [SIEVE_HCAP]
+  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
+  if (threadIdx.x < TG) {
+    gtab[2 * threadIdx.x + 0] = ga;
+    gtab[2 * threadIdx.x + 1] = gs;
+  }
+  if (threadIdx.x == 0) *nhit = 0;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int gl0 = wr * 128 + i * 16 + g4;        // this lane's 4 consecutive gallery rows
+    const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
+    const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
+    const float av[4] = {t0.x, t0.z, t1.x, t1.z}, sv[4] = {t0.y, t0.w, t1.y, t1.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gl = gl0 + r;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float sc = av[r] - sq2[c] * sv[r] * acc[i][c][r];
+        if (!(sc > th[c]) && gl < nvalid) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
+          const int ql = wc * E::QW + c * 16 + r16;
+          const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
+          const uint32_t slot = atomicAdd(nhit, 1u);
+          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)gl);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  sieve_flush<f6t::TQ>(smem, p, g0, q0);
+}
+
+// fp6 sieve pass on the 16x16x128 engine.  MODE probe bits: 1 = no k-loop DMA, 4 = no epilogue.
+template <int MODE>
+__global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
+  using E = f6t::Engine16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t gt, qt;
+  i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
+  const int64_t gp = gt * p.gstride;
+  const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
+  f6t::f32x4 acc[8][4];
+  E::mainloop<MODE & 1>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt, p.nk,
+                        acc);
+  // sieve operands after the main loop (the 16x16 engine needs every register in it)
+  float ga = __builtin_inff(), gs = 0.f, sq2[4], th[4];
+  if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
+    ga = p.aux[g0 + threadIdx.x];
+    gs = p.gscale[g0 + threadIdx.x];
+  }
+  const int wc = (threadIdx.x >> 6) % E::WQ, r16 = threadIdx.x & 15;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int64_t q = q0 + wc * E::QW + c * 16 + r16;
+    const bool ok = q < p.B;
+    sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
+    th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
+  }
+  if constexpr ((MODE & 4) != 0) {   // probe: no epilogue (the accumulators kept alive)
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += acc[i][c][r];
+    if (s == 1.2345f) p.cand[0].d = s;
+    return;
+  }
+  sieve_epilogue16(smem, p, g0, q0, ga, gs, sq2, th, acc);
+}
+
 // ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
 // One workgroup per 256-row gallery panel, wave w owns rows 32w..32w+31 against the (single)
 // 32-row query block, loading its fragments straight to VGPRs from the f6 tiled layout (each
@@ -385,10 +480,10 @@ __device__ __forceinline__ f6t::i32x8 stream_frag(const char* stage, int j, int 
   f6t::i32x2 p1;
   if constexpr (NT) {   // streamed once: non-temporal, keeps L2 for the query fragments
     p0 = __builtin_nontemporal_load(reinterpret_cast<const f6t::i32x4*>(sb + row * 16));
-    p1 = __builtin_nontemporal_load(reinterpret_cast<const f6t::i32x2*>(sb + 4096 + row * 8));
+    p1 = __builtin_nontemporal_load(reinterpret_cast<const f6t::i32x2*>(sb + 4096 + f6t::p1_slot(h, row) * 8));
   } else {
     p0 = *reinterpret_cast<const f6t::i32x4*>(sb + row * 16);
-    p1 = *reinterpret_cast<const f6t::i32x2*>(sb + 4096 + row * 8);
+    p1 = *reinterpret_cast<const f6t::i32x2*>(sb + 4096 + f6t::p1_slot(h, row) * 8);
   }
   f6t::i32x8 f;
   f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3];
@@ -848,7 +943,7 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
     const int jh = (int)(g & 3);   // 2 j + h
     char* sb = pbase + st * f6t::PANEL + jh * 6144;
     *reinterpret_cast<uint4*>(sb + rl * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-    *reinterpret_cast<uint2*>(sb + 4096 + rl * 8) = make_uint2(w[4], w[5]);
+    *reinterpret_cast<uint2*>(sb + 4096 + f6t::p1_slot(jh, rl) * 8) = make_uint2(w[4], w[5]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -881,7 +976,7 @@ __global__ void f6_zero_tail(char* tiles, int64_t R, int64_t nst) {
     const int rl = r0 + (int)(i % (256 - r0));
     char* sb = pbase + (sjh >> 2) * f6t::PANEL + (sjh & 3) * 6144;
     *reinterpret_cast<uint4*>(sb + rl * 16) = make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint2*>(sb + 4096 + rl * 8) = make_uint2(0, 0);
+    *reinterpret_cast<uint2*>(sb + 4096 + f6t::p1_slot((int)(sjh & 3), rl) * 8) = make_uint2(0, 0);
   }
 }
 
@@ -1039,6 +1134,16 @@ extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int
 // waves of the fp6 tile engine (f6t::Engine; tools/f6_probe.hip times both)
 constexpr int F6_NW = 8;
 
+// MFMA shape of the sieve pass: 16 = v_mfma_scale_f32_16x16x128 (f6t::Engine16, default),
+// 32 = the 32x32x64 engine (OFR_F6_SHAPE=32)
+static int f6_shape() {
+  static const int s = [] {
+    const char* e = getenv("OFR_F6_SHAPE");
+    return e && atoi(e) == 32 ? 32 : 16;
+  }();
+  return s;
+}
+
 // f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
 // thresholds, counts and buckets (each 256-byte aligned)
 struct SieveWs {
@@ -1118,7 +1223,8 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
     } else {
       static bool attr_done = false;
       if (!attr_done) {
-        for (const void* f : {(const void*)q8s::tile_kernel_f6<F6_NW, 0>, (const void*)q8s::tile_kernel_f6<F6_NW, 8>}) {
+        for (const void* f : {(const void*)q8s::tile_kernel_f6<F6_NW, 0>, (const void*)q8s::tile_kernel_f6<F6_NW, 8>,
+                              (const void*)q8s::tile_kernel_f6s<0>}) {
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
         }
@@ -1140,8 +1246,12 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
       a.count = count;
       a.bucket = bucket;
       a.cap = q8s::SIEVE_CAP;
-      hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 8>), dim3((unsigned)(a.ntq * a.ntg)), dim3(F6_NW * 64), f6t::LDS,
-                         st, a);
+      if (f6_shape() == 16)
+        hipLaunchKernelGGL((q8s::tile_kernel_f6s<0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
+                           f6t::LDS, st, a);
+      else
+        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 8>), dim3((unsigned)(a.ntq * a.ntg)), dim3(F6_NW * 64),
+                           f6t::LDS, st, a);
       OFR_LAUNCH_CHECK("f6 tile_kernel (sieve)");
     }
   }

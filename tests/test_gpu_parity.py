@@ -162,6 +162,8 @@ def _decode_f6_tiles(tiles, R, d):
     t = tiles.reshape(P, nst, 4, 6144)                       # (panel, stage, 2j+h, sub-block)
     p0 = t[..., :4096].reshape(P, nst, 4, 256, 16)
     p1 = t[..., 4096:].reshape(P, nst, 4, 256, 8)
+    # part1 row slots are swizzled: row r of sub-block 2j+h sits at slot r ^ 16h (ofr_f6_tile.h p1_slot)
+    p1 = np.stack([p1[:, :, jh, np.arange(256) ^ (16 * (jh & 1))] for jh in range(4)], axis=2)
     grp = np.concatenate([p0, p1], axis=-1)                  # 24 bytes = 32 x 6 bits per row and group
     bits = np.unpackbits(grp, axis=-1, bitorder="little").reshape(P, nst, 4, 256, 32, 6)
     code = (bits * (1 << np.arange(6))).sum(-1)

@@ -45,6 +45,27 @@ static int run(q8s::TileArgs a, int reps, const char* tag) {
   return 0;
 }
 
+template <int MODE>
+static int run16(q8s::TileArgs a, int reps, const char* tag) {
+  const double ops = 2.0 * (double)a.ntg * f6t::TA * a.ntq * f6t::TQ * a.nk * f6t::BK;
+  CK(hipFuncSetAttribute((const void*)q8s::tile_kernel_f6s<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const unsigned grid = (unsigned)(a.ntq * a.ntg);
+  hipLaunchKernelGGL((q8s::tile_kernel_f6s<MODE>), dim3(grid), dim3(512), f6t::LDS, 0, a);
+  CK(hipGetLastError());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((q8s::tile_kernel_f6s<MODE>), dim3(grid), dim3(512), f6t::LDS, 0, a);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  printf("f6 16x16 %-12s mode=%-2d gg=%-3ld ms=%8.2f  executed=%7.1f TOPS (%.1f%% of 10000)\n", tag, MODE, (long)a.gg, ms,
+         ops / ms / 1e9, ops / ms / 1e9 / 100.0);
+  fflush(stdout);
+  return 0;
+}
+
 template <int U, bool NT>
 static int run_stream(q8s::TileArgs a, int reps, const char* tag) {
   a.ntq = 1;
@@ -104,6 +125,14 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; ++rep)
       if (run_stream<4, false>(a, 20, "base") || run_stream<8, false>(a, 20, "u8") || run_stream<2, false>(a, 20, "u2") ||
           run_stream<4, true>(a, 20, "nt") || run_stream<8, true>(a, 20, "u8+nt"))
+        return 1;
+    return 0;
+  }
+  if (getenv("SHAPE16")) {   // the 16x16x128 sieve engine next to the 32x32x64 one
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (run<8, 8>(a, reps, "sieve32") || run16<0>(a, reps, "sieve16") || run16<4>(a, reps, "noepi16") ||
+          run16<5>(a, reps, "nodma-noepi16") || run<8, 5>(a, reps, "nodma-noepi32"))
         return 1;
     return 0;
   }
