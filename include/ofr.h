@@ -237,12 +237,20 @@ int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H, int W, in
  * of ofr_elbp_hist, whose float histogram is count/(py*px); 1.0 for fp32).
  * Rows must be 16-byte aligned.  Coarse fp32 VALU pass + exact fp64
  * re-evaluation of the reference formula on the best candidates; outputs as
- * ofr_knn_f32.                                                                */
+ * ofr_knn_f32.  cert (nullable, [B]): 1 iff the result is provably the exact
+ * fp64 top-k -- the k-th exact distance lies below every excluded row's
+ * coarse score / (1 + gamma), gamma the coarse pass's relative error bound
+ * ((ceil(nbins/2) + 4) 2^-24 + 2 ulp per term).  Queries with cert 0 are
+ * re-run by ofr_chi2_knn_exact: the same search with fp64 per-term arithmetic
+ * (the reference formula in every tile; its cert covers the fp32 tile keys).   */
 
 size_t ofr_chi2_workspace_bytes(int64_t B, int64_t N, int k);
 int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
                  int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
-                 int64_t* out_i, void* workspace, size_t workspace_bytes);
+                 int64_t* out_i, void* workspace, size_t workspace_bytes, int* cert);
+int ofr_chi2_knn_exact(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
+                       int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
+                       int64_t* out_i, void* workspace, size_t workspace_bytes, int* cert);
 
 /* Training (PCA Gram / LDA scatter) ----------------------------------------
  * C[M][N] = alpha * op(A) op(B) + beta * C in fp64 on the fp64 MFMA

@@ -511,6 +511,7 @@ class Chi2Gallery:
         self.N = int(self.G.shape[0])
         self._Gbuf = self.G
         self.ws = Workspace()
+        self.last_fallbacks = ()
 
     def append(self, rows):
         """Append rows in place (NearestNeighbor.update): host float rows for fp32 galleries, or a
@@ -535,13 +536,34 @@ class Chi2Gallery:
         return self.N
 
     def search(self, Qd, k, index_base=0):
+        """Certified ChiSquare top-k: the fp32 VALU pass with its error bound; the queries it cannot
+        certify are re-run with fp64 per-term arithmetic (ofr_chi2_knn_exact).  self.last_fallbacks
+        = (uncertified after the fp32 pass, uncertified after the exact pass: near-ties at fp32 key
+        resolution, 2^-23 relative)."""
         B = Qd.shape[0]
         out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
         out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)
+        cert = torch.empty(B, dtype=torch.int32, device=Qd.device)
         lib = _lib.load()
         ws = self.ws.get(lib.ofr_chi2_workspace_bytes(B, self.N, k), Qd.device)
         call("ofr_chi2_knn", stream(), self.dtype, ptr(Qd), B, Qd.shape[1], ptr(self.G), self.N, self.G.shape[1],
-             self.nbins, self.denom, k, index_base, ptr(out_d), ptr(out_i), ptr(ws), ws.numel())
+             self.nbins, self.denom, k, index_base, ptr(out_d), ptr(out_i), ptr(ws), ws.numel(), ptr(cert))
+        rows = torch.nonzero(cert == 0).reshape(-1)
+        counts = [int(rows.numel())]
+        if rows.numel():
+            sub = Qd.index_select(0, rows).contiguous()
+            n = sub.shape[0]
+            d2 = torch.empty((n, k), dtype=torch.float64, device=Qd.device)
+            i2 = torch.empty((n, k), dtype=torch.int64, device=Qd.device)
+            c2 = torch.empty(n, dtype=torch.int32, device=Qd.device)
+            ws2 = self.ws.get(lib.ofr_chi2_workspace_bytes(n, self.N, k), Qd.device)
+            call("ofr_chi2_knn_exact", stream(), self.dtype, ptr(sub), n, sub.shape[1], ptr(self.G), self.N,
+                 self.G.shape[1], self.nbins, self.denom, k, index_base, ptr(d2), ptr(i2), ptr(ws2), ws2.numel(),
+                 ptr(c2))
+            out_d.index_copy_(0, rows, d2)
+            out_i.index_copy_(0, rows, i2)
+            counts.append(int((c2 == 0).sum()))
+        self.last_fallbacks = tuple(counts)
         return out_d, out_i
 
     def query_rows(self, arr):

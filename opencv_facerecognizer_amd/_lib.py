@@ -71,7 +71,9 @@ SIGNATURES = {
                               c_int, c_int, c_vp, c_int]),
     "ofr_chi2_workspace_bytes": (c_sz, [c_i64, c_i64, c_int]),
     "ofr_chi2_knn": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_dbl, c_int, c_i64, c_vp,
-                             c_vp, c_vp, c_sz]),
+                             c_vp, c_vp, c_sz, c_vp]),
+    "ofr_chi2_knn_exact": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_dbl, c_int, c_i64,
+                                   c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ofr_gemm_f64": (c_int, [c_vp, c_int, c_int, c_i64, c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp, c_i64, c_dbl, c_vp,
                              c_i64]),
     "ofr_center_u8_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),

@@ -76,7 +76,68 @@ struct Chi2Args {
   int64_t nbins;
   Cand* cand;  // [T][B][KC]
   int64_t ntq, ntg;
+  double denom;   // exact pass: reference values are element / denom
 };
+
+// Exact pass (the certificate's fallback, few queries): the reference formula distance.py:115-116
+// in fp64 per (pair, bin) -- p = value / denom, (p - q)^2 / (p + q + eps) -- on 16 x 16 pairs
+// per workgroup, values staged once as fp64 p = v / denom in LDS.  The tile lists carry the sum
+// rounded to fp32 (a 2^-24 relative key; the merge re-evaluates the survivors in fp64 again).
+constexpr int C2X_T = 32;
+template <int DT, int KC>
+__global__ void __launch_bounds__(256) chi2_exact_tile_kernel(Chi2Args p) {
+  __shared__ double Qs[C2_BB][C2X_T];
+  __shared__ double Gs[C2_BB][C2X_T + 1];
+  __shared__ float S[C2X_T][C2X_T + 1];
+  const int64_t t = blockIdx.x;
+  const int64_t gt = t / p.ntq, qt = t % p.ntq;
+  const int64_t q0 = qt * C2X_T, g0 = gt * C2X_T;
+  const int tid = threadIdx.x;
+  const int tq = tid >> 4, tg = tid & 15;      // queries tq*2.., gallery tg*2..
+  const double eps = 2.220446049250313e-16;    // np.finfo('float').eps, distance.py:115
+  double acc[2][2] = {{0, 0}, {0, 0}};
+  for (int64_t b0 = 0; b0 < p.nbins; b0 += C2_BB) {
+    __syncthreads();
+    for (int e = tid; e < C2_BB * C2X_T; e += 256) {
+      const int r = e / C2_BB, b = e % C2_BB;
+      const int64_t bb = b0 + b;
+      const int64_t qr = min(q0 + r, p.B - 1), gr = min(g0 + r, p.N - 1);
+      Qs[b][r] = bb < p.nbins ? load1<DT>(p.Q, qr * p.ldq + bb) / p.denom : 0.0;
+      Gs[b][r] = bb < p.nbins ? load1<DT>(p.G, gr * p.ldg + bb) / p.denom : 0.0;
+    }
+    __syncthreads();
+    const int nb = (int)min((int64_t)C2_BB, p.nbins - b0);
+    for (int b = 0; b < nb; ++b) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const double x = Qs[b][tq * 2 + i], y = Gs[b][tg * 2 + j];
+          const double df = x - y;
+          acc[i][j] += (df * df) / (x + y + eps);
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) S[tq * 2 + i][tg * 2 + j] = (float)acc[i][j];
+  __syncthreads();
+  if (tid < C2X_T) {
+    const int64_t q = q0 + tid;
+    TopList<KC> L;
+    L.init();
+    for (int j = 0; j < C2X_T; ++j) {
+      const int64_t g = g0 + j;
+      if (g < p.N) L.insert(S[tid][j], (int)g);
+    }
+    if (q < p.B) {
+      Cand* out = p.cand + ((size_t)gt * p.B + q) * KC;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) out[j] = Cand{L.d[j], L.i[j]};
+    }
+  }
+}
 
 template <int DT, int KC>
 __global__ void __launch_bounds__(256) chi2_tile_kernel(Chi2Args p) {
@@ -185,6 +246,9 @@ struct Chi2MergeArgs {
   int64_t index_base;
   double* out_d;
   int64_t* out_i;
+  int* cert;      // nullable: 1 iff the result is provably the exact fp64 top-k
+  double gamma;   // relative error bound of the coarse scores (and their keys)
+  double scale;   // coarse score -> reference units (1 / denom for the fp32 pass, 1 for the exact pass)
 };
 
 template <int DT, int KC>
@@ -211,13 +275,31 @@ __global__ void __launch_bounds__(256) chi2_merge_rerank_kernel(Chi2MergeArgs p)
     if (threadIdx.x == 0) exact[c] = val;
   }
   __syncthreads();
-  if (threadIdx.x == 0) sort_and_write<KC>(lists, exact, p.k, p.index_base, p.out_d + q * p.k, p.out_i + q * p.k);
+  if (threadIdx.x == 0) {
+    double* od = p.out_d + q * p.k;
+    sort_and_write<KC>(lists, exact, p.k, p.index_base, od, p.out_i + q * p.k);
+    if (p.cert) {
+      // certificate: every row outside the KC candidates has coarse score >= tau (the KC-th
+      // candidate; a tile's excluded rows are >= its own KC-th, which is >= tau), so its exact
+      // distance is >= tau * scale / (1 + gamma).  The top-k is exact iff the k-th exact distance
+      // lies strictly below that (a relative 1e-12 for the fp64 evaluation order).
+      const int kk = p.k < KC ? p.k : KC;
+      const Cand last = lists[KC - 1];
+      const double dk = od[kk - 1];
+      double bnd = __builtin_inf();
+      if (last.i != CAND_EMPTY) bnd = (double)last.d * p.scale / (1.0 + p.gamma) * (1.0 - 1e-12);
+      p.cert[q] = (dk == dk) && (dk < bnd);
+    }
+  }
 }
 
 template <int DT, int KC>
-static int launch_chi2(hipStream_t st, const Chi2Args& a, const Chi2MergeArgs& m) {
+static int launch_chi2(hipStream_t st, const Chi2Args& a, const Chi2MergeArgs& m, bool exact) {
   if (a.N > 0) {
-    hipLaunchKernelGGL((chi2_tile_kernel<DT, KC>), dim3((unsigned)(a.ntq * a.ntg)), dim3(256), 0, st, a);
+    if (exact)
+      hipLaunchKernelGGL((chi2_exact_tile_kernel<DT, KC>), dim3((unsigned)(a.ntq * a.ntg)), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((chi2_tile_kernel<DT, KC>), dim3((unsigned)(a.ntq * a.ntg)), dim3(256), 0, st, a);
     OFR_LAUNCH_CHECK("chi2_tile_kernel");
   }
   hipLaunchKernelGGL((chi2_merge_rerank_kernel<DT, KC>), dim3((unsigned)m.B), dim3(256), 0, st, m);
@@ -226,8 +308,8 @@ static int launch_chi2(hipStream_t st, const Chi2Args& a, const Chi2MergeArgs& m
 }
 
 template <int DT>
-static int chi2_dispatch(hipStream_t st, int kc, const Chi2Args& a, const Chi2MergeArgs& m) {
-  return kc == 8 ? launch_chi2<DT, 8>(st, a, m) : launch_chi2<DT, 16>(st, a, m);
+static int chi2_dispatch(hipStream_t st, int kc, const Chi2Args& a, const Chi2MergeArgs& m, bool exact) {
+  return kc == 8 ? launch_chi2<DT, 8>(st, a, m, exact) : launch_chi2<DT, 16>(st, a, m, exact);
 }
 
 }  // namespace ofr
@@ -236,13 +318,13 @@ using namespace ofr;
 
 extern "C" size_t ofr_chi2_workspace_bytes(int64_t B, int64_t N, int k) {
   const int kc = pick_kc(k);
-  const int64_t T = cdiv(N > 0 ? N : 1, C2_TG);
+  const int64_t T = cdiv(N > 0 ? N : 1, C2X_T);   // the exact pass's 32-row tiles (>= the 64-row ones)
   return (size_t)T * (size_t)B * kc * sizeof(Cand) + 256;
 }
 
-extern "C" int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
-                            int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
-                            int64_t* out_i, void* workspace, size_t workspace_bytes) {
+static int chi2_run(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
+                    int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
+                    int64_t* out_i, void* workspace, size_t workspace_bytes, int* cert, bool exact) {
   OFR_CHECK_ARG(dtype >= DT_U8 && dtype <= DT_F32, "ofr_chi2_knn: dtype must be 0 (u8), 1 (u16), 2 (u32) or 3 (f32)");
   OFR_CHECK_ARG(B >= 0 && N >= 0 && nbins >= 1 && denom > 0, "ofr_chi2_knn: bad sizes");
   if (k < 1 || k > OFR_MAX_K) return fail(OFR_E_UNSUPPORTED, "ofr_chi2_knn: k must be in [1, 16]");
@@ -260,17 +342,39 @@ extern "C" int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, i
   const int kc = pick_kc(k);
   OFR_CHECK_ARG(workspace_bytes >= ofr_chi2_workspace_bytes(B, N, k), "ofr_chi2_knn: workspace too small");
   Chi2Args a;
-  a.Q = Q; a.B = B; a.ldq = ldq; a.G = G; a.N = N; a.ldg = ldg; a.nbins = nbins;
+  a.Q = Q; a.B = B; a.ldq = ldq; a.G = G; a.N = N; a.ldg = ldg; a.nbins = nbins; a.denom = denom;
   a.cand = reinterpret_cast<Cand*>(workspace);
-  a.ntq = cdiv(B, C2_TQ);
-  a.ntg = N > 0 ? cdiv(N, C2_TG) : 0;
+  const int tq = exact ? C2X_T : C2_TQ, tg = exact ? C2X_T : C2_TG;
+  a.ntq = cdiv(B, tq);
+  a.ntg = N > 0 ? cdiv(N, tg) : 0;
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_chi2_knn: grid too large");
-  Chi2MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, nbins, denom, k, index_base, out_d, out_i};
+  // error bound of the coarse scores (relative): the fp32 pass sums ceil(nbins / 2) terms per
+  // accumulator sequentially (two packed halves) and each term d^2 * rcp(s) carries <= 2 ulp
+  // (d, s exact for integer counts < 2^24; <= 2 more ulp from their roundings for fp32 values);
+  // the exact pass's key is its fp64 sum rounded to fp32 (1/2 ulp) plus the fp64 summation.
+  const double gamma = exact ? 0x1p-23 + (double)nbins * 0x1p-52
+                             : ((double)((nbins + 1) / 2) + 4.0) * 0x1p-24 + (dtype == DT_F32 ? 4.0 : 2.0) * 0x1p-23;
+  Chi2MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, nbins, denom, k, index_base, out_d, out_i, cert, gamma,
+                  exact ? 1.0 : 1.0 / denom};
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
-    case DT_U8: return chi2_dispatch<DT_U8>(st, kc, a, m);
-    case DT_U16: return chi2_dispatch<DT_U16>(st, kc, a, m);
-    case DT_U32: return chi2_dispatch<DT_U32>(st, kc, a, m);
-    default: return chi2_dispatch<DT_F32>(st, kc, a, m);
+    case DT_U8: return chi2_dispatch<DT_U8>(st, kc, a, m, exact);
+    case DT_U16: return chi2_dispatch<DT_U16>(st, kc, a, m, exact);
+    case DT_U32: return chi2_dispatch<DT_U32>(st, kc, a, m, exact);
+    default: return chi2_dispatch<DT_F32>(st, kc, a, m, exact);
   }
+}
+
+extern "C" int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
+                            int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
+                            int64_t* out_i, void* workspace, size_t workspace_bytes, int* cert) {
+  return chi2_run(stream, dtype, Q, B, ldq, G, N, ldg, nbins, denom, k, index_base, out_d, out_i, workspace,
+                  workspace_bytes, cert, false);
+}
+
+extern "C" int ofr_chi2_knn_exact(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G,
+                                  int64_t N, int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base,
+                                  double* out_d, int64_t* out_i, void* workspace, size_t workspace_bytes, int* cert) {
+  return chi2_run(stream, dtype, Q, B, ldq, G, N, ldg, nbins, denom, k, index_base, out_d, out_i, workspace,
+                  workspace_bytes, cert, true);
 }

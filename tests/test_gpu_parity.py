@@ -507,6 +507,26 @@ def test_chi2_counts_search_vs_oracle():
     Gh = counts_numpy(gc, cb).reshape(n, nb).astype(np.float64) / cell
     Qh = counts_numpy(qc, cb).reshape(-1, nb).astype(np.float64) / cell
     _check_search("ChiSquareDistance", Qh, Gh, dd.cpu().numpy(), ii.cpu().numpy(), 5)
+    assert g.last_fallbacks[0] <= len(qry) // 10     # separated identities: the fp32 pass certifies
+
+
+def test_chi2_certificate_forces_exact_pass():
+    """Near-identical gallery rows: the 8 candidates of the fp32 pass lie within its error bound of each
+    other, so no query can be certified there; every query is re-run by the exact fp64 pass
+    (ofr_chi2_knn_exact) and the result matches the oracle."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import Chi2Gallery
+    r = _rng(14)
+    base = r.integers(0, 20, (1, 4096))
+    G = np.repeat(base, 600, axis=0)
+    flip = r.integers(0, 4096, 600)
+    G[np.arange(600), flip] += 1                       # rows differ from each other in one bin by one count
+    Q = np.repeat(base, 12, axis=0)
+    Q[np.arange(12), r.integers(0, 4096, 12)] += 1
+    g = Chi2Gallery(torch.from_numpy(G.astype(np.uint8)).cuda(), dtype=_lib.DT_U8, denom=225.0, nbins=4096)
+    dd, ii = g.search(torch.from_numpy(Q.astype(np.uint8)).cuda().contiguous(), 3)
+    assert g.last_fallbacks[0] == 12, g.last_fallbacks
+    _check_search("ChiSquareDistance", Q / 225.0, G / 225.0, dd.cpu().numpy(), ii.cpu().numpy(), 3)
 
 
 def test_chi2_float_search_vs_oracle():
