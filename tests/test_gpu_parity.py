@@ -517,12 +517,10 @@ def test_chi2_certificate_forces_exact_pass():
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import Chi2Gallery
     r = _rng(14)
-    base = r.integers(0, 20, (1, 4096))
-    G = np.repeat(base, 600, axis=0)
-    flip = r.integers(0, 4096, 600)
-    G[np.arange(600), flip] += 1                       # rows differ from each other in one bin by one count
-    Q = np.repeat(base, 12, axis=0)
-    Q[np.arange(12), r.integers(0, 4096, 12)] += 1
+    G = np.full((600, 4096), 10)
+    for i in range(600):                               # every row: 50 bins one count above the base
+        G[i, r.choice(4096, 50, replace=False)] += 1
+    Q = np.full((12, 4096), 10)                        # every query is the base: all 600 rows tie
     g = Chi2Gallery(torch.from_numpy(G.astype(np.uint8)).cuda(), dtype=_lib.DT_U8, denom=225.0, nbins=4096)
     dd, ii = g.search(torch.from_numpy(Q.astype(np.uint8)).cuda().contiguous(), 3)
     assert g.last_fallbacks[0] == 12, g.last_fallbacks
