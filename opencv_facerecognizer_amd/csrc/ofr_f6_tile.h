@@ -240,8 +240,8 @@ struct Engine16 {
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 2, 2, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
   }
 
-  // MODE (probes): 1 = no k-loop DMA; STAG: staggered DMA issue (below)
-  template <int MODE, bool STAG = true>
+  // MODE (probes): 1 = no k-loop DMA
+  template <int MODE>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
                                                   int nst, f32x4 (&acc)[NA][NB]) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -267,75 +267,42 @@ struct Engine16 {
     // Per stage kt: MFMAs of stage kt, each fragment replaced by stage kt+1's as soon as its last
     // MFMA is issued (A-major: A[i] after row i's 4 MFMAs, B[c] after row 7's MFMA c), so the
     // fragments need no second register set (acc 128 + fragments 72 registers).
-    // STAG (MODE bit 32 in the probes, default on): waves 4-7 -- the second wave of each SIMD --
-    // issue their stage DMA after rows 0-3 instead of right after the barrier, so that the two
-    // waves of a SIMD do not both stall on LDS-DMA issue while its matrix pipe idles.
-    const bool late = STAG && wave >= 4;
-    auto rowA = [&](const char* nxt, int i) {
+    for (int kt = 0; kt < last; ++kt) {
+      if constexpr (MODE == 1) wait_vm<0>();
+      else wait_vm<IPW>();       // stage kt+1 landed; kt+2 may be in flight
+      barrier();                 // every wave has read stage kt: its buffer takes stage kt+3
+      if constexpr (MODE != 1) {
+        const int nx = kt + NST;
+        issue(nx < last ? nx : last);
+      }
+      const char* nxt = smem + ((kt + 1) % NST) * STAGE;
 #pragma unroll
-      for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i], b[c], acc[i][c]);
-      readA(nxt, i);
-    };
-    auto row_last = [&](const char* nxt) {
+      for (int i = 0; i < NA - 1; ++i) {
+#pragma unroll
+        for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i], b[c], acc[i][c]);
+        readA(nxt, i);
+      }
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
         acc[NA - 1][c] = mfma(a[NA - 1], b[c], acc[NA - 1][c]);
         readB(nxt, c);
       }
       readA(nxt, NA - 1);
-    };
-    auto sched_rows = [&](int lo, int hi) {   // rows [lo, hi) of 4 MFMAs + 2 reads (hi <= NA - 1)
-      for (int i = lo; i < hi; ++i) {
+      // the stage's DMAs first (issuing them later in the stage, staggered between the two waves of
+      // a SIMD, measured 8 % slower: tools/f6_probe.hip SHAPE16), then per row i its 4 MFMAs and
+      // the 2 reads of its successor; row 7 refills B as each of its MFMAs retires its operand
+      __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
+#pragma unroll
+      for (int i = 0; i < NA - 1; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
-    };
-    auto sched_last = [&]() {
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    };
-    for (int kt = 0; kt < last; ++kt) {
-      if constexpr (MODE == 1) wait_vm<0>();
-      else wait_vm<IPW>();       // stage kt+1 landed; kt+2 may be in flight
-      barrier();                 // every wave has read stage kt: its buffer takes stage kt+3
-      const int nx = kt + NST < last ? kt + NST : last;
-      const char* nxt = smem + ((kt + 1) % NST) * STAGE;
-      if (late) {
-#pragma unroll
-        for (int i = 0; i < NA / 2; ++i) rowA(nxt, i);
-        if constexpr (MODE != 1) issue(nx);
-#pragma unroll
-        for (int i = NA / 2; i < NA - 1; ++i) rowA(nxt, i);
-        row_last(nxt);
-#pragma unroll
-        for (int i = 0; i < NA / 2; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
-#pragma unroll
-        for (int i = NA / 2; i < NA - 1; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        sched_last();
-      } else {
-        if constexpr (MODE != 1) issue(nx);
-#pragma unroll
-        for (int i = 0; i < NA - 1; ++i) rowA(nxt, i);
-        row_last(nxt);
-        __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
-#pragma unroll
-        for (int i = 0; i < NA - 1; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        sched_last();
-      }
     }
 #pragma unroll
     for (int i = 0; i < NA; ++i)

@@ -131,8 +131,8 @@ int main(int argc, char** argv) {
   if (getenv("SHAPE16")) {   // the 16x16x128 sieve engine next to the 32x32x64 one
     a.gg = 4 < ntg ? 4 : ntg;
     for (int rep = 0; rep < 2; ++rep)
-      if (run<8, 8>(a, reps, "sieve32") || run16<0>(a, reps, "sieve16") || run16<32>(a, reps, "sieve16-nostag") ||
-          run16<4>(a, reps, "noepi16") || run16<36>(a, reps, "noepi16-nostag") || run16<5>(a, reps, "nodma-noepi16"))
+      if (run<8, 8>(a, reps, "sieve32") || run16<0>(a, reps, "sieve16") || run16<4>(a, reps, "noepi16") ||
+          run16<5>(a, reps, "nodma-noepi16") || run<8, 5>(a, reps, "nodma-noepi32"))
         return 1;
     return 0;
   }
