@@ -5,16 +5,19 @@
 // MFMA (v_mfma_f64_16x16x4_f64, 78.6 TF peak); the eigensolves stay on host
 // LAPACK as the reference calls them.
 //
-// ofr_gemm_f64: 64x64 output tile per 256-thread workgroup (4 waves, 2x2,
-// each 32x32 = 2x2 MFMA blocks of 16x16), K panels of 16 staged in LDS
-// as [k][m] with an 80-double row pitch (conflict-free ds_read_b64 for the
-// 16-lane x 4-k fragment reads).  f64 MFMA C/D map: col = lane&15,
-// row = (lane>>4) + 4*reg;  A/B: lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15].
+// ofr_gemm_f64: 128 x 128 output tile per 256-thread workgroup (4 waves, 2 x 2, each 64 x 64 =
+// 4 x 4 blocks of v_mfma_f64_16x16x4_f64, 128 accumulator VGPRs), K panels of 16 double-buffered
+// in LDS as [k][m] / [k][n] with a 144-double pitch (rows k and k+1 in opposite bank halves: the
+// 16-lane fragment reads are conflict free): the next panel's global loads (8 doubles per thread
+// and operand, 16-B vector loads along the stored matrix's contiguous dimension) are in flight
+// while the current panel's 4 k-steps run (64 MFMAs per wave, 64 cycles each).
+// f64 MFMA maps (cdna_hip_programming.md): A/B lane l holds A[l&15][k=l>>4] / B[k=l>>4][l&15];
+// C/D col = lane&15, row = (lane>>4) + 4*reg.  Two workgroups per CU (2 x 72 KiB LDS).
 #include "ofr_common.h"
 
 namespace ofr {
 
-constexpr int G64_T = 64, G64_BK = 16, G64_PITCH = 80;
+constexpr int G64_T = 128, G64_BK = 16, G64_PITCH = 144;
 
 struct Gemm64Args {
   int transA, transB;
@@ -28,66 +31,109 @@ struct Gemm64Args {
   int64_t ldc;
 };
 
-// element (m, k) of op(A) where op(A) is M x K
-__device__ __forceinline__ double opA(const Gemm64Args& p, int64_t m, int64_t k) {
-  if (m >= p.M || k >= p.K) return 0.0;
-  return p.transA ? p.A[k * p.lda + m] : p.A[m * p.lda + k];
-}
-// element (k, n) of op(B) where op(B) is K x N
-__device__ __forceinline__ double opB(const Gemm64Args& p, int64_t k, int64_t n) {
-  if (n >= p.N || k >= p.K) return 0.0;
-  return p.transB ? p.B[n * p.ldb + k] : p.B[k * p.ldb + n];
-}
-
-__global__ void __launch_bounds__(256) gemm_f64_kernel(Gemm64Args p) {
-  __shared__ double As[G64_BK][G64_PITCH];
-  __shared__ double Bs[G64_BK][G64_PITCH];
-  const int64_t m0 = (int64_t)blockIdx.y * G64_T, n0 = (int64_t)blockIdx.x * G64_T;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave >> 1, wc = wave & 1;
-  f64x4 acc[2][2];
+// 8 consecutive elements of op(X) (a 128 x 16 panel slab) -> registers, zero outside the matrix.
+// trans = 0: X is stored [rows][K] (op(X) = X, K contiguous): thread t takes row t/2, k 8(t&1)..+7.
+// trans = 1: X is stored [K][rows] (rows contiguous): thread t takes k t/16, rows 8(t&15)..+7.
+__device__ __forceinline__ void load_slab(const double* X, int64_t ld, int64_t rows, int64_t K, int trans, int64_t r0,
+                                          int64_t k0, double (&v)[8]) {
+  const int t = threadIdx.x;
+  if (!trans) {
+    const int64_t r = r0 + (t >> 1), k = k0 + 8 * (t & 1);
+    const bool rok = r < rows;
+    const double* src = X + (rok ? r : 0) * ld + k;
+    const bool vec = rok && k + 8 <= K && (((uintptr_t)src) & 15) == 0;
+    if (vec) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+      for (int e = 0; e < 8; e += 2) {
+        const double2 x = *reinterpret_cast<const double2*>(src + e);
+        v[e] = x.x;
+        v[e + 1] = x.y;
+      }
+    } else {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f64x4{0, 0, 0, 0};
-
-  for (int64_t k0 = 0; k0 < p.K; k0 += G64_BK) {
-    // stage 64 x 16 of op(A) and 16 x 64 of op(B); the index order follows the
-    // contiguous dimension of the stored matrix for coalescing
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = tid + 256 * r;
-      int mm, kk;
-      if (p.transA) { mm = e & 63; kk = e >> 6; } else { kk = e & 15; mm = e >> 4; }
-      As[kk][mm] = opA(p, m0 + mm, k0 + kk);
-      int nn, kb;
-      if (p.transB) { kb = e & 15; nn = e >> 4; } else { nn = e & 63; kb = e >> 6; }
-      Bs[kb][nn] = opB(p, k0 + kb, n0 + nn);
+      for (int e = 0; e < 8; ++e) v[e] = (rok && k + e < K) ? src[e] : 0.0;
     }
+  } else {
+    const int64_t k = k0 + (t >> 4), r = r0 + 8 * (t & 15);
+    const bool kok = k < K;
+    const double* src = X + (kok ? k : 0) * ld + r;
+    const bool vec = kok && r + 8 <= rows && (((uintptr_t)src) & 15) == 0;
+    if (vec) {
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const double2 x = *reinterpret_cast<const double2*>(src + e);
+        v[e] = x.x;
+        v[e + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (kok && r + e < rows) ? src[e] : 0.0;
+    }
+  }
+}
+
+// registers -> LDS panel [k][row] (the layout the fragments read)
+__device__ __forceinline__ void store_slab(double (*P)[G64_PITCH], int trans, const double (&v)[8]) {
+  const int t = threadIdx.x;
+  if (!trans) {
+    const int r = t >> 1, k = 8 * (t & 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) P[k + e][r] = v[e];
+  } else {
+    const int k = t >> 4, r = 8 * (t & 15);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) P[k][r + e] = v[e];
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) gemm_f64_kernel(Gemm64Args p) {
+  __shared__ double As[2][G64_BK][G64_PITCH];
+  __shared__ double Bs[2][G64_BK][G64_PITCH];
+  const int64_t m0 = (int64_t)blockIdx.y * G64_T, n0 = (int64_t)blockIdx.x * G64_T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f64x4{0, 0, 0, 0};
+  // op(A) is M x K: stored [M][K] (transA = 0) or [K][M]; op(B) is K x N: stored [K][N] (transB = 0)
+  // or [N][K] -- i.e. B's panel is a slab of B^T with the opposite storage flag
+  double va[8], vb[8];
+  const int npanel = (int)cdiv(p.K, G64_BK);
+  load_slab(p.A, p.lda, p.M, p.K, p.transA, m0, 0, va);
+  load_slab(p.B, p.ldb, p.N, p.K, !p.transB, n0, 0, vb);
+  for (int kp = 0; kp < npanel; ++kp) {
+    const int buf = kp & 1;
+    store_slab(As[buf], p.transA, va);
+    store_slab(Bs[buf], !p.transB, vb);
     __syncthreads();
+    if (kp + 1 < npanel) {   // the next panel's loads fly under this panel's MFMAs
+      load_slab(p.A, p.lda, p.M, p.K, p.transA, m0, (int64_t)(kp + 1) * G64_BK, va);
+      load_slab(p.B, p.ldb, p.N, p.K, !p.transB, n0, (int64_t)(kp + 1) * G64_BK, vb);
+    }
 #pragma unroll
     for (int ks = 0; ks < G64_BK; ks += 4) {
       const int kk = ks + (lane >> 4);
-      double a[2], b[2];
+      double a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = As[kk][wr * 32 + i * 16 + (lane & 15)];
+      for (int i = 0; i < 4; ++i) a[i] = As[buf][kk][wr * 64 + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = Bs[kk][wc * 32 + j * 16 + (lane & 15)];
+      for (int j = 0; j < 4; ++j) b[j] = Bs[buf][kk][wc * 64 + j * 16 + (lane & 15)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) + 4 * r;
-        const int64_t n = n0 + wc * 32 + j * 16 + (lane & 15);
+        const int64_t m = m0 + wr * 64 + i * 16 + (lane >> 4) + 4 * r;
+        const int64_t n = n0 + wc * 64 + j * 16 + (lane & 15);
         if (m < p.M && n < p.N) {
           double* c = p.C + m * p.ldc + n;
           const double v = p.alpha * acc[i][j][r];

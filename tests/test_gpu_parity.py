@@ -629,13 +629,16 @@ def test_kfold_validation_matches_reference_loop():
 def test_gemm_f64_vs_numpy():
     from opencv_facerecognizer_amd._device import f64_dev, gemm_f64
     r = _rng(3)
-    for (M, N, K) in [(31, 31, 4900), (100, 7, 33), (130, 257, 64)]:
+    for (M, N, K) in [(31, 31, 4900), (100, 7, 33), (130, 257, 64), (257, 129, 17), (1, 300, 5), (513, 64, 1000)]:
         A = r.normal(size=(M, K))
         Bm = r.normal(size=(K, N))
-        C = gemm_f64(f64_dev(A), f64_dev(Bm)).cpu().numpy()
-        np.testing.assert_allclose(C, A @ Bm, rtol=1e-12, atol=1e-12 * np.abs(A @ Bm).max())
-        Ct = gemm_f64(f64_dev(A.T.copy()), f64_dev(Bm.T.copy()), transA=True, transB=True).cpu().numpy()
-        np.testing.assert_allclose(Ct, A @ Bm, rtol=1e-12, atol=1e-12 * np.abs(A @ Bm).max())
+        ref = A @ Bm
+        for ta in (False, True):
+            for tb in (False, True):
+                Ad = f64_dev(A.T.copy() if ta else A)
+                Bd = f64_dev(Bm.T.copy() if tb else Bm)
+                C = gemm_f64(Ad, Bd, transA=ta, transB=tb).cpu().numpy()
+                np.testing.assert_allclose(C, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
 
 
 def test_topk_merge_kernel():
