@@ -132,6 +132,7 @@ def main():
                                      "peak": PEAK_PAIR_BINS / 1e12, "unit": "T (pair, bin)/s",
                                      "frac": pair_bins / (ms_search * 1e-3) / PEAK_PAIR_BINS}},
         "top1_identity_acc": acc,
+        "chi2_uncertified_after_each_pass": list(gal.last_fallbacks),
         "end_to_end_queries_per_s": B / gpu_total,
         "cpu_baseline": {"kind": "port", "cores": 1,
                          "sample": f"{nh} gallery faces through the oracle's histogram, x{nh} chi2 calls per timing "
