@@ -319,6 +319,53 @@ int ofr_rank1_f64(void* stream, double* C, int64_t rows, int64_t cols, int64_t l
 int ofr_row_div_f64(void* stream, const double* A, int64_t rows, int64_t cols, int64_t lda, const double* n,
                     double* out, int64_t ldo);
 
+/* Multi-GPU search in one process ---------------------------
+ * ofr_comm_init_all: one RCCL rank per device (ncclCommInitAll over xGMI; RCCL is
+ * bound at run time, OFR_E_UNSUPPORTED when librccl.so.1 is absent); devices NULL
+ * = 0 .. ndev-1.  ofr_knn_sharded: shard r (on devices[r], its own stream) holds
+ * the gallery rows [index_base, index_base + N) of a row-sharded gallery with its
+ * fp6 tier (ofr_f6_quantize_rows) and the replicated query batch (centred fp32
+ * rows + fp6 tiles, as for ofr_knn_f6).  Every shard runs the certified fp6 tier,
+ * ONE ncclAllGather exchanges the (distance, index, bound) lists, every device
+ * merges them (ofr_topk_merge_certify) and certifies a query iff the global k-th
+ * squared distance is below every rank's bound; uncertified queries are re-run
+ * exactly (ofr_knn_f32) on every shard and exchanged once more.  Output on
+ * EVERY device: out_d / out_i [B][k] = the exact top-k of the whole gallery
+ * (classifier.py:104-119), cert [B] = 1 if the fp6 tier certified the query.
+ * Euclidean, k <= 16.  workspace: ofr_knn_sharded_workspace_bytes per shard.   */
+typedef struct ofr_comm ofr_comm;
+typedef struct ofr_knn_shard {
+  void* stream;
+  const float* Q;
+  int64_t ldq;
+  const void* Qt;
+  const float* qscale;
+  const double* qstats;
+  const float* G;
+  int64_t N;
+  int64_t ldg;
+  const void* Gt;
+  const float* gscale;
+  const float* aux;
+  const double* gmax;
+  int64_t index_base;
+  void* workspace;
+  size_t workspace_bytes;
+  double* out_d;
+  int64_t* out_i;
+  int* cert;
+} ofr_knn_shard;
+int ofr_comm_init_all(int ndev, const int* devices, ofr_comm** comm);
+int ofr_comm_destroy(ofr_comm* comm);
+int ofr_comm_size(const ofr_comm* comm);
+size_t ofr_knn_sharded_workspace_bytes(int64_t B, int64_t N, int64_t ldq, int k, int ndev);
+int ofr_knn_sharded(ofr_comm* comm, const ofr_knn_shard* shards, int64_t B, int64_t d, int k);
+/* lists [P][B][2k+1] fp64: per rank and query k distances, k indices (int64
+ * bit patterns), the rank's bound -> the best k per query and the global
+ * certificate (bound -inf / NaN never certifies; +inf always does).             */
+int ofr_topk_merge_certify(void* stream, const double* lists, int P, int64_t B, int k, double* out_d,
+                           int64_t* out_i, int* cert);
+
 /* Face-tensor ingestion ------------------------------------
  * Replaces cv2.imread(IMREAD_GRAYSCALE) + cv2.resize(im, size) [INTER_LINEAR] of
  * TheTrainer.read_images trainer/thetrainer.py:99-103 and the recognizers'

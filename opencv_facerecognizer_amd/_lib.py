@@ -89,10 +89,24 @@ SIGNATURES = {
     "ofr_scatter_combine_f64": (c_int, [c_vp, c_vp, c_vp, c_vp, c_dbl, c_i64, c_i64, c_vp, c_vp]),
     "ofr_rank1_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_dbl]),
     "ofr_row_div_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
+    "ofr_comm_init_all": (c_int, [c_int, c_vp, c_vp]),
+    "ofr_comm_destroy": (c_int, [c_vp]),
+    "ofr_comm_size": (c_int, [c_vp]),
+    "ofr_knn_sharded_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_int, c_int]),
+    "ofr_knn_sharded": (c_int, [c_vp, c_vp, c_i64, c_i64, c_int]),
+    "ofr_topk_merge_certify": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp]),
     "ofr_ingest_faces": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
     "ofr_class_center_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                      c_vp]),
 }
+
+
+class KnnShard(ctypes.Structure):
+    """struct ofr_knn_shard (include/ofr.h): one device's part of ofr_knn_sharded."""
+    _fields_ = [("stream", c_vp), ("Q", c_vp), ("ldq", c_i64), ("Qt", c_vp), ("qscale", c_vp), ("qstats", c_vp),
+                ("G", c_vp), ("N", c_i64), ("ldg", c_i64), ("Gt", c_vp), ("gscale", c_vp), ("aux", c_vp),
+                ("gmax", c_vp), ("index_base", c_i64), ("workspace", c_vp), ("workspace_bytes", c_sz),
+                ("out_d", c_vp), ("out_i", c_vp), ("cert", c_vp)]
 
 
 class OfrError(RuntimeError):

@@ -212,3 +212,65 @@ def _device_rows_u8(X):
     if kind != "u8":
         raise TypeError("sharded training takes uint8 faces")
     return Xd, D, kind
+
+
+# ---------------------------------------------------------------------------
+# single-process multi-GPU search through the C ABI (ofr_comm_init_all / ofr_knn_sharded)
+# ---------------------------------------------------------------------------
+class DeviceComm:
+    """RCCL communicator over the given devices of this process (ofr_comm_init_all), for C / C++
+    style callers that drive every GPU from one process; the package's own multi-GPU path is one
+    process per GPU over torch.distributed (functions above)."""
+
+    def __init__(self, devices):
+        import ctypes
+        from . import _lib
+        self.devices = list(devices)
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        _lib.call("ofr_comm_init_all", len(self.devices), ctypes.cast(arr, ctypes.c_void_p), ctypes.byref(h))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            from . import _lib
+            _lib.call("ofr_comm_destroy", self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def knn(self, galleries, queries, k):
+        """galleries[r]: the FloatGallery of shard r (on devices[r], global row offset in
+        .index_base, default 0 for one shard); queries[r]: the centred fp32 query rows [B][ld] on
+        devices[r] (the same batch on every device).  Returns per device (out_d, out_i, cert)."""
+        import ctypes
+        from . import _lib
+        lib = _lib.load()
+        B, d = int(queries[0].shape[0]), galleries[0].d
+        shards = (_lib.KnnShard * len(galleries))()
+        keep = []
+        for r, (g, Qd) in enumerate(zip(galleries, queries)):
+            with torch.cuda.device(Qd.device):
+                qq = g.quantize_queries(Qd, tier="f6")
+                t = g._tier_gallery("f6")
+                nbytes = lib.ofr_knn_sharded_workspace_bytes(B, g.N, Qd.shape[1], k, len(galleries))
+                ws = torch.empty(nbytes, dtype=torch.uint8, device=Qd.device)
+                out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
+                out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)
+                cert = torch.empty(B, dtype=torch.int32, device=Qd.device)
+                s = shards[r]
+                s.stream = torch.cuda.current_stream(Qd.device).cuda_stream
+                s.Q, s.ldq, s.Qt = Qd.data_ptr(), Qd.shape[1], qq["Qs"].data_ptr()
+                s.qscale, s.qstats = qq["scale"].data_ptr(), qq["stats"].data_ptr()
+                s.G, s.N, s.ldg, s.Gt = g.G.data_ptr(), g.N, g.ld, t["Gs"].data_ptr()
+                s.gscale, s.aux, s.gmax = t["scale"].data_ptr(), g.aux.data_ptr(), t["gmax"].data_ptr()
+                s.index_base = int(getattr(g, "index_base", 0))
+                s.workspace, s.workspace_bytes = ws.data_ptr(), nbytes
+                s.out_d, s.out_i, s.cert = out_d.data_ptr(), out_i.data_ptr(), cert.data_ptr()
+                keep.append((qq, ws, out_d, out_i, cert))
+        _lib.call("ofr_knn_sharded", self.handle, ctypes.cast(shards, ctypes.c_void_p), B, d, k)
+        return [(o[2], o[3], o[4]) for o in keep]

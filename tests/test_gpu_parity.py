@@ -684,3 +684,74 @@ def test_knn_cosine_zero_query_takes_fp32_path(monkeypatch):
     assert np.array_equal(ii[5], i32.cpu().numpy()[0]) and np.isnan(dd[5]).all()
     keep = np.arange(64) != 5
     _check_search("CosineDistance", Q[keep], G, dd[keep], ii[keep], 3)
+
+
+def _merge_certify_ref(lists, P, B, k):
+    """numpy restatement of ofr_topk_merge_certify (the global certificate of parallel.certify_sharded)."""
+    L = lists.reshape(P, B, 2 * k + 1)
+    od, oi, cert = np.empty((B, k)), np.empty((B, k), np.int64), np.empty(B, np.int32)
+    for b in range(B):
+        d = L[:, b, :k].reshape(-1)
+        i = L[:, b, k:2 * k].copy().view(np.int64).reshape(-1)
+        ok = i >= 0
+        o = np.lexsort((i[ok], d[ok]))[:k]
+        dd, ii = np.full(k, np.inf), np.full(k, -1, np.int64)
+        dd[:len(o)], ii[:len(o)] = d[ok][o], i[ok][o]
+        bnd = L[:, b, 2 * k]
+        minb = -np.inf if np.isnan(bnd).any() else bnd.min()
+        od[b], oi[b] = dd, ii
+        cert[b] = np.isposinf(minb) or dd[-1] ** 2 < minb
+    return od, oi, cert
+
+
+def test_topk_merge_certify_kernel():
+    """In-library global certificate (ofr_topk_merge_certify): P = 3 ranks' lists with ties across
+    ranks, empty slots, and bounds -inf (an overflowed rank: never certifies), +inf, NaN, finite."""
+    from opencv_facerecognizer_amd._lib import call, ptr, stream
+    r = _rng(31)
+    P, B, k = 3, 64, 4
+    L = np.empty((P, B, 2 * k + 1))
+    for p in range(P):
+        d = np.sort(np.round(r.random((B, k)) * 8) / 4, axis=1)          # coarse values: ties across ranks
+        idx = (np.arange(k)[None, :] + 1000 * p + 10 * np.arange(B)[:, None]).astype(np.int64)
+        idx[r.random((B, k)) < 0.05] = -1
+        d[idx < 0] = np.inf
+        L[p, :, :k], L[p, :, k:2 * k] = d, idx.view(np.float64)
+        L[p, :, 2 * k] = r.choice([-np.inf, np.inf, np.nan, 0.5, 3.0, 100.0], B)
+    lt = torch.from_numpy(L.reshape(-1).copy()).cuda()
+    od = torch.empty((B, k), dtype=torch.float64, device="cuda")
+    oi = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    ce = torch.empty(B, dtype=torch.int32, device="cuda")
+    call("ofr_topk_merge_certify", stream(), ptr(lt), P, B, k, ptr(od), ptr(oi), ptr(ce))
+    rd, ri, rc = _merge_certify_ref(L, P, B, k)
+    assert np.array_equal(oi.cpu().numpy(), ri) and np.array_equal(od.cpu().numpy(), rd)
+    assert np.array_equal(ce.cpu().numpy(), rc)
+    assert rc.min() == 0 and rc.max() == 1
+
+
+@pytest.mark.parametrize("data", ["separated", "sphere"])
+def test_knn_sharded_c_abi_one_device(monkeypatch, data):
+    """ofr_comm_init_all + ofr_knn_sharded (single process, RCCL) on this box's one device: the fp6
+    tier, the all-gather, the global certificate and the exact fallback of uncertified queries, against
+    the oracle.  'sphere' (equidistant rows) leaves every query uncertified, forcing the fallback."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    from opencv_facerecognizer_amd.parallel import DeviceComm
+    r = _rng(41)
+    if data == "separated":
+        protos = r.normal(0, 30, (300, 96))
+        G = (protos[np.arange(3000) % 300] + r.normal(0, 5, (3000, 96)))
+        Q = (protos[r.integers(0, 300, 100)] + r.normal(0, 5, (100, 96)))
+    else:
+        c = r.normal(0, 50, 64)
+        U = r.normal(0, 1, (2000, 64))
+        G = c + 100.0 * U / np.linalg.norm(U, axis=1, keepdims=True)
+        Q = c + r.normal(0, 1e-6, (100, 64))
+    G = G.astype(np.float32).astype(np.float64)
+    Q = Q.astype(np.float32).astype(np.float64)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    with DeviceComm([0]) as comm:
+        (dd, ii, cert), = comm.knn([g], [g.query_rows(Q)], 3)
+    _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
+    c = cert.cpu().numpy()
+    assert (c.min() == 1) if data == "separated" else (c.max() == 0)
