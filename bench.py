@@ -398,8 +398,10 @@ def main():
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
     if args.search == "f6":
+        sieve = ("q8s::tile_kernel_f6s<0> sieve pass (16x16x128 engine)"
+                 if os.environ.get("OFR_F6_SHAPE", "16") == "16" else "q8s::tile_kernel_f6<8, 8> sieve pass (32x32x64 engine)")
         peak, kname = PEAK_F6_MFMA, ("ofr_knn_f6 phase 1 (fp6 e2m3): q8s::tile_kernel_f6<8, 0> sample pass + "
-                                     "sieve_threshold_kernel + q8s::tile_kernel_f6<8, 8> sieve pass")
+                                     "sieve_threshold_kernel + " + sieve)
         alg_bytes_tiles = 0.75 * (nl * d + B * d)                    # 6 bits per feature, gallery + queries
         executed = flops_tiles
     elif use_q8:

@@ -3,7 +3,7 @@
 # kernel trace + stats, then one PMC pass per counter group (no trace domains mixed with --pmc).
 set -e
 R=$GRAFT_REPO_ROOT
-K=${1:-tile_kernel_f6}
+K=${1:-tile_kernel_f6|sieve_threshold}
 shift || true
 ARGS=${*:---steps 2 --warmup 1 --small-batches= --no-cpu}
 mkdir -p $R/gpurun_out/prof
