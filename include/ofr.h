@@ -39,6 +39,7 @@ enum ofr_status {
   OFR_E_INVALID = -1,     /* bad argument (shape, stride, alignment, null) */
   OFR_E_UNSUPPORTED = -2, /* valid but not implemented (e.g. k > OFR_MAX_K) */
   OFR_E_DEVICE = -3,      /* no usable gfx950 device */
+  OFR_E_NUMERIC = -4,     /* numerical failure: matrix not positive definite, no convergence */
 };
 
 enum ofr_metric {
@@ -379,6 +380,24 @@ int ofr_topk_merge_certify(void* stream, const double* lists, int P, int64_t B, 
  * 4899 R + 2^13) >> 14); a crop of the output size is copied (grey only).       */
 int ofr_ingest_faces(void* stream, const uint8_t* src, const int64_t* jobs, int64_t n, int dh, int dw,
                      int interp, uint8_t* out);
+
+/* Training eigensolves on the device -------------------------
+ * Replace the host LAPACK of PCA (feature.py:94 svd -> eigh of the Gram /
+ * covariance, training.py) and LDA (feature.py:170 eig(inv(Sw) Sb) -> the
+ * symmetric-definite pencil Sb v = lambda Sw v, feature.lda_eigen): rocSOLVER
+ * divide and conquer (dsyevd / dsygvd, bound at run time: OFR_E_UNSUPPORTED
+ * without librocsolver.so.0).  A, Sb, Sw: contiguous symmetric [n][n] fp64,
+ * OVERWRITTEN.  Out: the m largest eigenvalues, descending, evals[m]; their
+ * eigenvectors as the columns of row-major evecs [n][ldv] (ofr_eigh_f64:
+ * orthonormal; ofr_sygv_f64: each scaled to unit 2-norm, as lda_eigen).
+ * OFR_E_NUMERIC when Sw is not positive definite (the caller falls back to the
+ * reference's general eig) or the solver did not converge.  Synchronises the
+ * stream (reads the solver's info).                                              */
+size_t ofr_eig_workspace_bytes(int64_t n, int64_t m);
+int ofr_eigh_f64(void* stream, int64_t n, double* A, int64_t m, double* evals, double* evecs, int64_t ldv,
+                 void* workspace, size_t workspace_bytes);
+int ofr_sygv_f64(void* stream, int64_t n, double* Sb, double* Sw, int64_t m, double* evals, double* evecs,
+                 int64_t ldv, void* workspace, size_t workspace_bytes);
 
 #ifdef __cplusplus
 }

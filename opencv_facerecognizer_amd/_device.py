@@ -632,6 +632,34 @@ def gemm_f64(A, B, transA=False, transB=False, alpha=1.0):
     return C
 
 
+def _eig_call(name, mats, m):
+    n = int(mats[0].shape[0])
+    m = max(0, min(int(m), n))
+    for A in mats:
+        if A.dtype != torch.float64 or tuple(A.shape) != (n, n) or not A.is_contiguous():
+            raise ValueError(f"{name}: needs contiguous square fp64 device matrices")
+    lib = _lib.load()
+    nbytes = lib.ofr_eig_workspace_bytes(n, m)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=mats[0].device)
+    evals = torch.empty(max(m, 1), dtype=torch.float64, device=mats[0].device)
+    evecs = torch.empty((n, max(m, 1)), dtype=torch.float64, device=mats[0].device)
+    call(name, stream(), n, *[ptr(A) for A in mats], m, ptr(evals), ptr(evecs), evecs.shape[1], ptr(ws), nbytes)
+    return evals[:m], evecs[:, :m]
+
+
+def eigh_desc_f64(A, m, overwrite=False):
+    """The m largest eigenpairs of a symmetric fp64 device matrix, descending, eigenvectors as the
+    columns of a device [n][m] (rocSOLVER dsyevd, ofr_eigh_f64)."""
+    return _eig_call("ofr_eigh_f64", [A if overwrite else A.clone()], m)
+
+
+def sygv_desc_f64(Sb, Sw, m, overwrite=False):
+    """The m largest eigenpairs of Sb v = lambda Sw v (Sw positive definite), descending, columns at
+    unit 2-norm (rocSOLVER dsygvd, ofr_sygv_f64).  OfrError(code E_NUMERIC) when Sw is not
+    positive definite."""
+    return _eig_call("ofr_sygv_f64", [Sb if overwrite else Sb.clone(), Sw if overwrite else Sw.clone()], m)
+
+
 def col_mean_u8(Xd, D):
     mean = torch.empty(D, dtype=torch.float64, device=Xd.device)
     call("ofr_col_mean_u8", stream(), ptr(Xd), Xd.shape[0], D, Xd.shape[1], ptr(mean))

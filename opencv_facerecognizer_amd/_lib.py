@@ -95,6 +95,9 @@ SIGNATURES = {
     "ofr_knn_sharded_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_int, c_int]),
     "ofr_knn_sharded": (c_int, [c_vp, c_vp, c_i64, c_i64, c_int]),
     "ofr_topk_merge_certify": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp]),
+    "ofr_eig_workspace_bytes": (c_sz, [c_i64, c_i64]),
+    "ofr_eigh_f64": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_sz]),
+    "ofr_sygv_f64": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_sz]),
     "ofr_ingest_faces": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
     "ofr_class_center_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                      c_vp]),
@@ -110,7 +113,14 @@ class KnnShard(ctypes.Structure):
 
 
 class OfrError(RuntimeError):
-    """A libocvf_hip call failed (message from ofr_last_error())."""
+    """A libocvf_hip call failed (message from ofr_last_error()); .code = the ofr_status."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
+
+
+E_UNSUPPORTED, E_NUMERIC = -2, -4
 
 
 _lib = None
@@ -139,7 +149,7 @@ def load():
 def check(rc, what=""):
     if rc != 0:
         msg = load().ofr_last_error().decode(errors="replace")
-        raise OfrError(f"{what or 'ofr'} failed ({rc}): {msg}")
+        raise OfrError(f"{what or 'ofr'} failed ({rc}): {msg}", rc)
 
 
 def device():

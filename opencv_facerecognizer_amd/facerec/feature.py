@@ -12,13 +12,14 @@ and errors as the reference:
 * ``SpatialHistogram`` (feature.py:266-305).
 
 What moves to the GPU: the centring and Gram/covariance products of PCA
-(the SVD of the centred data, feature.py:91-94, becomes an fp64-MFMA Gram
-matrix + host ``np.linalg.eigh``), the scatter matrices of LDA (feature.py:
-160-168 as fp64-MFMA GEMMs; ``inv`` and ``eig`` stay on host LAPACK exactly
-as the reference calls them, :170 -- or, with OFR_LDA_SOLVER=eigh, the same
-eigenpairs from the symmetric-definite problem, see ``lda_eigen``), W = P.L (:229), every projection loop
-(:104-108, :178-182, :231-235 and ``extract``) as the fp32-MFMA projection
-kernel, and the LBP + per-cell histograms (:286-302).
+(the SVD of the centred data, feature.py:91-94, becomes an exact int8-MFMA
+Gram matrix of the uint8 faces + a device ``eigh``, see training.py), the
+scatter matrices of LDA (feature.py:160-168), the LDA eigenproblem (:170: the
+reference's host ``inv`` + ``eig`` for small orders, the symmetric-definite
+pencil on the device above ``AUTO_DEVICE_MIN``, see ``lda_eigen``), W = P.L
+(:229), every projection loop (:104-108, :178-182, :231-235 and ``extract``)
+on the exact int8-slice projection engine, and the LBP + per-cell histograms
+(:286-302).
 
 Eigenvector signs: an eigensolver may return any column sign; distances and
 the Fisherfaces W are invariant to PCA column signs, and the LDA/Fisherfaces
@@ -233,21 +234,46 @@ class PCA(_DeviceProjMixin, AbstractFeature):
         return "PCA (num_components=%d)" % (self._num_components)
 
 
+# "auto": matrices up to this order keep the reference's own host inv + eig (well under a second);
+# larger ones go to the device pencil solver (configs[4], d = 10,000: 2.1 s against minutes of eig)
+AUTO_DEVICE_MIN = 1024
+
+
 def lda_eigen(Sw, Sb, num_components, solver=None):
     """Leading eigenpairs of inv(Sw) Sb, sorted by eigenvalue (feature.py:170-176).
 
-    solver "eig" (default): exactly the reference's ``np.linalg.eig(np.linalg.inv(Sw) * Sb)``,
-    real parts, descending.  solver "eigh" (or OFR_LDA_SOLVER=eigh): the symmetric-definite
-    pencil Sb v = lambda Sw v (LAPACK sygvx for the num_components largest, sygvd when they are most), columns scaled to
-    unit 2-norm like eig's -- the same eigenpairs up to column sign for distinct eigenvalues, in
-    O(d^3 / 3) work instead of a general eig of a d x d matrix (minutes at d = 10000).  Falls
-    back to "eig" when Sw is not positive definite.  Returns (float64 (m,), float64 (d, m)).
+    Sw, Sb: float64 host arrays or device tensors.  solver (or OFR_LDA_SOLVER):
+    * "eig": exactly the reference's ``np.linalg.eig(np.linalg.inv(Sw) * Sb)``, real parts, descending;
+    * "eigh": the symmetric-definite pencil Sb v = lambda Sw v on host LAPACK (sygvx for a few of
+      the largest, sygvd when most are kept);
+    * "device": the same pencil on the device (rocSOLVER dsygvd, ``ofr_sygv_f64``);
+    * "auto" (default): "eig" up to order AUTO_DEVICE_MIN, "device" above.
+    The pencil solvers scale columns to unit 2-norm like eig's -- the same eigenpairs up to
+    column sign for distinct eigenvalues, in O(d^3) symmetric work instead of a general eig of a
+    d x d matrix (minutes at d = 10000) -- and fall back to "eig" when Sw is not positive
+    definite.  Returns (float64 (m,), float64 (d, m)) host arrays.
     """
-    solver = solver or os.environ.get("OFR_LDA_SOLVER", "eig")
-    if solver not in ("eig", "eigh"):
-        raise ValueError("OFR_LDA_SOLVER must be 'eig' or 'eigh'")
+    solver = solver or os.environ.get("OFR_LDA_SOLVER", "auto")
+    if solver not in ("eig", "eigh", "device", "auto"):
+        raise ValueError("OFR_LDA_SOLVER must be 'eig', 'eigh', 'device' or 'auto'")
     n = Sw.shape[0]
     m = max(0, min(int(num_components), n))
+    if solver == "auto":
+        solver = "device" if n > AUTO_DEVICE_MIN else "eig"
+    if solver == "device" and m > 0:
+        from .._lib import E_NUMERIC, OfrError
+        Swd = Sw if isinstance(Sw, torch.Tensor) else _device.f64_dev(np.ascontiguousarray(Sw, np.float64))
+        Sbd = Sb if isinstance(Sb, torch.Tensor) else _device.f64_dev(np.ascontiguousarray(Sb, np.float64))
+        try:
+            lam, V = _device.sygv_desc_f64(Sbd.contiguous(), Swd.contiguous(), m)
+        except OfrError as e:
+            if e.code != E_NUMERIC:
+                raise
+            warnings.warn("LDA: Sw is not positive definite (%s); using the general eig" % e)
+        else:
+            return lam.cpu().numpy(), V.cpu().numpy()
+    if isinstance(Sw, torch.Tensor):
+        Sw, Sb = Sw.cpu().numpy(), Sb.cpu().numpy()
     if solver == "eigh" and m > 0:
         import scipy.linalg
         try:
@@ -361,34 +387,33 @@ class Fisherfaces(_DeviceProjMixin, AbstractFeature):
             # PCA keeps every pixel dimension (a rotation): LDA in pixel space, W = V directly
             self._regime = "pixel"
             Sw, Sb = training.pixel_scatter(training.pixel_pieces(Xd, D, lay), lay.counts, n)
-            evals, W = lda_eigen(Sw.cpu().numpy(), Sb.cpu().numpy(), m)
+            evals, W = lda_eigen(Sw, Sb, m)
             del Sw, Sb
             Wd = None
         elif n <= D:
             # n x n Gram of the centred faces: U_k = XC^T V_k / sigma_k, features V_k sigma_k
             self._regime = "gram"
-            lam, V = training.host_eigh_desc(training.centred_gram(Xd, D, lay))
-            sig = np.sqrt(np.maximum(lam[:k], 0.0))
-            F = V[:, :k] * sig
-            Sw, Sb = training.feature_scatter(_device.f64_dev(F), y)
-            evals, L = lda_eigen(Sw.cpu().numpy(), Sb.cpu().numpy(), m)
-            L32 = np.asarray(L, dtype=np.float32).astype(np.float64)          # feature.py:176
-            inv = np.divide(1.0, sig, out=np.zeros_like(sig), where=sig > 0)
-            M = _device.gemm_f64(_device.f64_dev(V[:, :k] * inv), _device.f64_dev(L32))   # V_k Sigma^-1 L
+            lam, V = training.eigh_desc(training.centred_gram(Xd, D, lay), k)
+            sig = lam.clamp_min(0.0).sqrt()
+            Sw, Sb = training.feature_scatter((V * sig).contiguous(), y)
+            evals, L = lda_eigen(Sw, Sb, m)
+            L32 = _device.f64_dev(np.asarray(L, dtype=np.float32).astype(np.float64))   # feature.py:176
+            inv = torch.where(sig > 0, 1.0 / sig, torch.zeros_like(sig))
+            M = _device.gemm_f64((V * inv).contiguous(), L32)                       # V_k Sigma^-1 L
             Wd = training.xct_times(Xd, D, lay, M, training.mean_image(Xd, D, lay))
         else:
             # D x D covariance: P = leading k eigenvectors, features XC P, W = P L
             self._regime = "cov"
             pieces = training.pixel_pieces(Xd, D, lay)
-            lam, V = training.host_eigh_desc(training.covariance(pieces, n))
+            lam, Pd = training.eigh_desc(training.covariance(pieces, n), k)
             del pieces
-            Pd = _device.f64_dev(V[:, :k])
+            Pd = Pd.contiguous()
             mu = training.mean_image(Xd, D, lay)
             shift = _device.gemm_f64(mu.reshape(1, -1).contiguous(), Pd).reshape(-1)
             Fd = _device.Projection(Wt_device=Pd.t().contiguous(), D=D).project(Xd, shift64=shift, f64=True)
             Sw, Sb = training.feature_scatter(Fd, y)
             del Fd
-            evals, L = lda_eigen(Sw.cpu().numpy(), Sb.cpu().numpy(), m)
+            evals, L = lda_eigen(Sw, Sb, m)
             L32 = np.asarray(L, dtype=np.float32).astype(np.float64)          # feature.py:176
             Wd = _device.gemm_f64(Pd, _device.f64_dev(L32))                      # feature.py:229
         self._eigenvalues = np.array(evals, dtype=np.float32, copy=True)      # :226-227 (LDA's, float32)

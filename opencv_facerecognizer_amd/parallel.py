@@ -191,7 +191,7 @@ def train_fisherfaces_sharded(feature, X_local, y_local, num_classes, group=None
     W = torch.empty((D, m), dtype=torch.float64, device=Xd.device)
     ev = torch.empty(m, dtype=torch.float64, device=Xd.device)
     if rank == 0:
-        evals, V = lda_eigen(Sw.cpu().numpy(), Sb.cpu().numpy(), m)
+        evals, V = lda_eigen(Sw, Sb, m)
         W.copy_(torch.from_numpy(np.ascontiguousarray(V, dtype=np.float64)))
         ev.copy_(torch.from_numpy(np.asarray(evals, dtype=np.float64)))
     del Sw, Sb

@@ -19,11 +19,11 @@ D pixels, c classes):
   (The reference rounds L to float32 in PCA coordinates, which has no pixel-space equivalent: W
   differs from it by that rounding, <= 2^-24 relative per element of L.)
 * ``gram``   n <= D (the bundled model, small training sets): the n x n Gram of the centred
-  images, G = X' X'^T - (r 1^T + 1 r^T) / n + (s.s) / n^2 (r = X' s), host ``eigh`` (as the
+  images, G = X' X'^T - (r 1^T + 1 r^T) / n + (s.s) / n^2 (r = X' s), device ``eigh`` (as the
   reference's ``svd``: sigma^2 = eigenvalues); PCA features are V_k Sigma_k (= U_k^T (x - mean)
   exactly), LDA runs on them, and W = U_k L = XC^T (V_k Sigma_k^-1 L) -- one exact uint8 x fp64
   product on the int8-slice projection engine, minus the rank-one mean term.
-* ``cov``    n > D and k < D: the D x D covariance X'^T X' - s s^T / n, host ``eigh``, P = its
+* ``cov``    n > D and k < D: the D x D covariance X'^T X' - s s^T / n, device ``eigh``, P = its
   leading k eigenvectors; features XC P on the projection engine (shift mean^T P); LDA on them;
   W = P L on the fp64 MFMA.
 
@@ -152,11 +152,11 @@ def centred_gram(Xd, D, lay):
     return G
 
 
-def host_eigh_desc(C):
-    """Eigenpairs of a symmetric device matrix on host LAPACK, descending (the reference's svd order)."""
-    lam, V = np.linalg.eigh(C.cpu().numpy())
-    order = np.argsort(-lam, kind="stable")
-    return lam[order], V[:, order]
+def eigh_desc(C, m):
+    """The m largest eigenpairs of a symmetric device matrix, descending (the reference's svd order),
+    on the device (``ofr_eigh_f64``, rocSOLVER dsyevd; C is overwritten).  Returns device tensors
+    (evals [m], V [n][m])."""
+    return _device.eigh_desc_f64(C, m, overwrite=True)
 
 
 def mean_image(Xd, D, lay):

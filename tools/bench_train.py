@@ -1,14 +1,16 @@
 """BASELINE.json configs[4] (Fisherfaces training) at a scale one box finishes in about a minute:
 n synthetic 100x100 faces of c identities, Fisherfaces().compute (PCA -> LDA, thetrainer.py:120 defaults).
 
-    python tools/bench_train.py [--n 4000] [--ids 400] [--solver eig|eigh]
-    python tools/bench_train.py --n 100000 --ids 10000 --solver eigh     # configs[4] at full scale
+    python tools/bench_train.py [--n 4000] [--ids 400] [--solver auto|eig|eigh|device]
+    python tools/bench_train.py --n 100000 --ids 10000                   # configs[4] at full scale
 
 Splits the wall time into the host LAPACK eigensolves the reference itself calls (np.linalg.eigh for the
 PCA Gram / covariance, inv + eig for LDA, feature.py:94/170; timed by wrapping numpy) and the rest: the
 device work (centring, Gram, left vectors, class centring, Sw/Sb, W = P.L, feature projections on the
-fp64 / int8 MFMA) plus host transfers.  --solver eigh times the symmetric-definite LDA eigensolve
-(feature.lda_eigen, sygvx/sygvd) instead of the reference's inv + eig.  The CPU baseline runs the oracle's reference-faithful
+fp64 / int8 MFMA) plus host transfers; the device eigensolves (rocSOLVER dsyevd / dsygvd, ofr_eig.hip)
+are reported apart.  --solver picks the LDA eigensolve (feature.lda_eigen): auto (default: the
+reference's inv + eig up to order 1024, the device pencil solver above), eig, eigh (host sygvx/sygvd),
+device.  The CPU baseline runs the oracle's reference-faithful
 Fisherfaces.compute (SVD, O(N^2) as_column_matrix) on a smaller sample and scales it by (n / n_cpu)^2
 (N^2 scaling measured).  Prints one JSON line.
 """
@@ -34,6 +36,18 @@ from opencv_facerecognizer_amd.facerec.model import PredictableModel  # noqa: E4
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 
 HOST = {"eigh": 0.0, "eig": 0.0, "inv": 0.0, "sygv": 0.0}
+DEV_EIG = {"eigh_dsyevd": 0.0, "sygv_dsygvd": 0.0}
+
+
+def _dev_timed(name, fn):
+    def w(*a, **k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = fn(*a, **k)
+        torch.cuda.synchronize()
+        DEV_EIG[name] += time.perf_counter() - t0
+        return r
+    return w
 
 
 def _timed(name, fn):
@@ -58,7 +72,7 @@ def main():
     ap.add_argument("--ids", type=int, default=400)
     ap.add_argument("--side", type=int, default=100)
     ap.add_argument("--n-cpu", type=int, default=600)
-    ap.add_argument("--solver", choices=["eig", "eigh"], default="eig")
+    ap.add_argument("--solver", choices=["eig", "eigh", "device", "auto"], default="auto")
     ap.add_argument("--predict", type=int, default=4096)
     args = ap.parse_args()
     device = _lib.device()
@@ -67,6 +81,9 @@ def main():
     la.eigh, la.eig, la.inv = _timed("eigh", la.eigh), _timed("eig", la.eig), _timed("inv", la.inv)
     import scipy.linalg
     scipy.linalg.eigh = _timed("sygv", scipy.linalg.eigh)
+    from opencv_facerecognizer_amd import _device
+    _device.eigh_desc_f64 = _dev_timed("eigh_dsyevd", _device.eigh_desc_f64)
+    _device.sygv_desc_f64 = _dev_timed("sygv_dsygvd", _device.sygv_desc_f64)
     os.environ["OFR_LDA_SOLVER"] = args.solver
     # the reference's training call: PredictableModel.compute = Fisherfaces.compute + NearestNeighbor.compute
     # (model.py:49-51, thetrainer.py:176)
@@ -125,7 +142,8 @@ def main():
         "config": {"n": n, "identities": c, "D": D, "pca_components": k, "d": d, "lda_solver": args.solver,
                    "regime": regime},
         "data": "synthetic",
-        "wall_s": total, "host_lapack_s": dict(HOST), "device_and_transfers_s": total - host,
+        "wall_s": total, "host_lapack_s": dict(HOST), "device_eigensolve_s": dict(DEV_EIG),
+        "device_and_transfers_s": total - host,
         "predict": {"batch": args.predict, "first_call_s": pred_s[0], "steady_s": min(pred_s[1:]),
                     "queries_per_s": args.predict / min(pred_s[1:]), "top1_identity_acc": acc,
                     "note": "first call builds the device gallery (upload + quantized tiers) from the training features"},
