@@ -25,6 +25,8 @@
 // 16q..16q+15 read 16 rows of sub-block q: the odd sub-blocks' part1 rows sit 16 slots away,
 // in the other half of the 64 banks the b64 lane group {0-31} / {32-63} spans).
 #pragma once
+#include <type_traits>
+
 #include "ofr_common.h"
 
 namespace ofr {
@@ -56,9 +58,17 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (N == 21) asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else static_assert(N == 0 || N == 6 || N == 12 || N == 24, "vmcnt");
+  else static_assert(N == 0 || N == 3 || N == 4 || N == 10 || N == 6 || N == 7 || N == 8 || N == 12 || N == 14 || N == 21 || N == 24,
+                     "vmcnt");
 }
 
 __device__ __forceinline__ void barrier() {

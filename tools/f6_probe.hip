@@ -10,6 +10,195 @@
 
 using namespace ofr;
 
+namespace ofr {
+namespace f6t {
+// ---- 16x16x128 engine, query operand straight to registers (experimental sieve pass) ----------
+// The LDS carries only the gallery block (24 KiB per stage, NSQ stages, one 1-KiB LDS-DMA
+// wave-instruction per 3 of the stage's 24 per wave); each wave owns 32 queries (2 fragments,
+// loaded from the query tiles in global memory -- L2-resident across the tile group -- D = NSQ - 2
+// stages ahead into NSQ - 1 register sets) against all 256 gallery rows, whose 16 fragments per
+// stage stream through a ring of R registers sets read R - 1 steps ahead (2 MFMAs per step).
+// Half the LDS-DMA bytes and LDS writes of Engine16 and no query fragment reads from LDS, for
+// a third more gallery fragment reads.  C/D of acc[i][c]: gallery rows 16 i + 4 (l / 16) + reg,
+// query 32 wave + 16 c + l % 16.
+template <int NSQ, int R, int D = NSQ - 2>
+struct EngineQ {
+  static constexpr int NW = 8, NT = 512, NA = 16, NB = 2;
+  static constexpr int NQS = D + 1;                      // query register sets
+  static constexpr int GINS = PANEL / 1024 / NW;         // 3 DMA wave-instructions per wave per stage
+  static constexpr int VM_PER_IT = GINS + 2 * NB;        // VMEM instructions per wave per stage (7)
+  static constexpr int LDS_BYTES = NSQ * PANEL;
+  static_assert(NSQ >= 4 && NSQ <= 6 && R >= 2 && R <= 8 && D >= 1 && D <= NSQ - 2, "EngineQ");
+  // per stage the query loads are issued first, then the DMA: at the start of stage kt the wave
+  // needs Q(kt) (issued D stages before) and DMA(kt+1) (NSQ-2 stages before) complete
+  static constexpr int VM_WAIT = D < NSQ - 2 ? GINS + (D - 1) * VM_PER_IT : (D - 1) * VM_PER_IT;
+  static constexpr int VM_WAIT_NODMA = (D - 1) * 2 * NB;
+
+  static __device__ __forceinline__ void dma(const char* G, int64_t gp, int64_t nst, int kt, char* st) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const char* gb = G + (gp * nst + kt) * (int64_t)PANEL;
+#pragma unroll
+    for (int t = 0; t < GINS; ++t) {
+      const int off = (wave * GINS + t) * 1024;
+      __builtin_amdgcn_global_load_lds((const OFR_GLOBAL void*)(gb + off + lane * 16), (OFR_LDS void*)(st + off), 16,
+                                       0, 0);
+    }
+  }
+  // the lane's query fragment c of stage kt straight from the tiled layout; zero past the last stage
+  static __device__ __forceinline__ i32x6 qfrag(const char* Q, int64_t qp, int64_t nst, int kt, int c) {
+    const int lane = threadIdx.x & 63, q = lane >> 4, row = (threadIdx.x >> 6) * 32 + c * 16 + (lane & 15);
+    const bool past = kt >= nst;   // uniform
+    const char* sb = Q + (qp * nst + (past ? nst - 1 : kt)) * (int64_t)PANEL + q * 6144;
+    const i32x4 p0 = *(const OFR_GLOBAL i32x4*)(sb + row * 16);
+    const i32x2 p1 = *(const OFR_GLOBAL i32x2*)(sb + 4096 + p1_slot(q, row) * 8);
+    const int z = past ? 0 : -1;
+    i32x6 f;
+    f[0] = p0[0] & z; f[1] = p0[1] & z; f[2] = p0[2] & z; f[3] = p0[3] & z; f[4] = p1[0] & z; f[5] = p1[1] & z;
+    return f;
+  }
+
+  template <int MODE>
+  static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
+                                                  int nst, f32x4 (&acc)[NA][NB]) {
+    const int r16 = threadIdx.x & 15;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int last = nst - 1;
+    auto clampk = [&](int k) { return k < last ? k : last; };
+    auto buf = [&](int k) { return smem + (k % NSQ) * PANEL; };
+    i32x6 qs[NQS][NB];
+    i32x6 g[R];
+    // prologue: DMA of stages 0 .. NSQ-2 and the query fragments of stages 0 .. D-1, in the
+    // per-iteration order (stage s's DMA then the queries of stage s - (NSQ-1) + D = s - 1)
+#pragma unroll
+    for (int s = 0; s < NSQ - 1; ++s) {
+      if constexpr ((MODE & 1) == 0) dma(G, gp, nst, clampk(s), buf(s));
+      if (s >= 1 && s - 1 < D) {
+#pragma unroll
+        for (int c = 0; c < NB; ++c) qs[s - 1][c] = qfrag(Q, qp, nst, s - 1, c);
+      }
+    }
+    wait_vm<0>();
+    barrier();
+#pragma unroll
+    for (int j = 0; j < R - 1; ++j) g[j] = Engine16::frag16(smem, j * 16 + r16);
+
+    auto iter = [&](int kt, auto setc) {
+      constexpr int S = decltype(setc)::value;               // register set of stage kt
+      if constexpr ((MODE & 1) == 0) wait_vm<VM_WAIT>();
+      else wait_vm<VM_WAIT_NODMA>();
+      barrier();   // stage kt+1 landed everywhere; the buffer of stage kt-1 is free
+#pragma unroll
+      for (int c = 0; c < NB; ++c) qs[(S + D) % NQS][c] = qfrag(Q, qp, nst, kt + D, c);
+      if constexpr ((MODE & 1) == 0) dma(G, gp, nst, clampk(kt + NSQ - 1), buf(kt + NSQ - 1));
+      const char* cur = buf(kt);
+      const char* nxt = buf(kt + 1);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int j = i + R - 1;
+        g[j % R] = Engine16::frag16(j < NA ? cur : nxt, (j % NA) * 16 + r16);
+#pragma unroll
+        for (int c = 0; c < NB; ++c) acc[i][c] = Engine16::mfma(g[i % R], qs[S][c], acc[i][c]);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x020, VM_PER_IT, 0);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NB, 0);
+      }
+    };
+    // stages past the end (kt >= nst, up to the next multiple of NQS) keep the schedule with
+    // zero query fragments (0 x finite = +0 exactly): one instance of each register-set
+    // iteration, no tail copy
+    for (int kt = 0; kt < nst; kt += NQS) {
+      iter(kt, std::integral_constant<int, 0>{});
+      if constexpr (NQS > 1) iter(kt + 1, std::integral_constant<int, 1>{});
+      if constexpr (NQS > 2) iter(kt + 2, std::integral_constant<int, 2>{});
+      if constexpr (NQS > 3) iter(kt + 3, std::integral_constant<int, 3>{});
+      if constexpr (NQS > 4) iter(kt + 4, std::integral_constant<int, 4>{});
+    }
+    wait_vm<0>();
+    barrier();
+  }
+};
+
+}  // namespace f6t
+namespace q8s {
+// fp6 sieve pass on the query-direct 16x16x128 engine (f6t::EngineQ, experimental: selected by
+// OFR_F6_SHAPE=17).  MODE probe bits: 1 = no k-loop DMA, 4 = no epilogue.
+template <int MODE, int NSQ, int R, int D = NSQ - 2>
+__global__ void __launch_bounds__(512, 1) tile_kernel_f6q(TileArgs p) {
+  using E = f6t::EngineQ<NSQ, R, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t gt, qt;
+  i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
+  const int64_t gp = gt * p.gstride;
+  const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
+  f6t::f32x4 acc[E::NA][E::NB];
+  E::template mainloop<MODE & 1>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+                                 p.nk, acc);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, g4 = (lane >> 4) * 4;
+  float sq2[E::NB], th[E::NB];
+#pragma unroll
+  for (int c = 0; c < E::NB; ++c) {
+    const int64_t q = q0 + wave * 32 + c * 16 + r16;
+    const bool ok = q < p.B;
+    sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
+    th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
+  }
+  if constexpr ((MODE & 4) != 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < E::NA; ++i)
+#pragma unroll
+      for (int c = 0; c < E::NB; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += acc[i][c][r];
+    if (s == 1.2345f) p.cand[0].d = s;
+    return;
+  }
+  float* gtab = reinterpret_cast<float*>(smem);                                  // [TG][2]
+  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + TG * 8);
+  uint2* hits = reinterpret_cast<uint2*>(smem + TG * 8 + 16);                    // [SIEVE_HCAP]
+  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
+  if (threadIdx.x < TG) {
+    const bool ok = g0 + threadIdx.x < p.N;
+    gtab[2 * threadIdx.x + 0] = ok ? p.aux[g0 + threadIdx.x] : __builtin_inff();
+    gtab[2 * threadIdx.x + 1] = ok ? p.gscale[g0 + threadIdx.x] : 0.f;
+  }
+  if (threadIdx.x == 0) *nhit = 0;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < E::NA; ++i) {
+    const int gl0 = i * 16 + g4;                   // this lane's 4 consecutive gallery rows
+    const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
+    const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
+    const float av[4] = {t0.x, t0.z, t1.x, t1.z}, sv[4] = {t0.y, t0.w, t1.y, t1.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gl = gl0 + r;
+#pragma unroll
+      for (int c = 0; c < E::NB; ++c) {
+        const float sc = av[r] - sq2[c] * sv[r] * acc[i][c][r];
+        if (!(sc > th[c]) && gl < nvalid) {
+          const int ql = wave * 32 + c * 16 + r16;
+          const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
+          const uint32_t slot = atomicAdd(nhit, 1u);
+          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)gl);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  sieve_flush<f6t::TQ>(smem, p, g0, q0);
+}
+
+}  // namespace q8s
+}  // namespace ofr
+
 __global__ void fill_u8(uint8_t* p, size_t n, uint32_t seed) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     uint32_t x = (uint32_t)i * 2654435761u ^ seed;
@@ -62,6 +251,28 @@ static int run16(q8s::TileArgs a, int reps, const char* tag) {
   ms /= reps;
   printf("f6 16x16 %-12s mode=%-2d gg=%-3ld ms=%8.2f  executed=%7.1f TOPS (%.1f%% of 10000)\n", tag, MODE, (long)a.gg, ms,
          ops / ms / 1e9, ops / ms / 1e9 / 100.0);
+  fflush(stdout);
+  return 0;
+}
+
+template <int MODE, int NSQ, int R, int D>
+static int runq(q8s::TileArgs a, int reps, const char* tag) {
+  const double ops = 2.0 * (double)a.ntg * f6t::TA * a.ntq * f6t::TQ * a.nk * f6t::BK;
+  const int lds = f6t::EngineQ<NSQ, R, D>::LDS_BYTES;
+  CK(hipFuncSetAttribute((const void*)q8s::tile_kernel_f6q<MODE, NSQ, R, D>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const unsigned grid = (unsigned)(a.ntq * a.ntg);
+  hipLaunchKernelGGL((q8s::tile_kernel_f6q<MODE, NSQ, R, D>), dim3(grid), dim3(512), lds, 0, a);
+  CK(hipGetLastError());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((q8s::tile_kernel_f6q<MODE, NSQ, R, D>), dim3(grid), dim3(512), lds, 0, a);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  printf("f6 qdirect nsq=%d r=%d d=%d %-12s mode=%-2d gg=%-3ld ms=%8.2f  executed=%7.1f TOPS (%.1f%% of 10000)\n", NSQ, R,
+         D, tag, MODE, (long)a.gg, ms, ops / ms / 1e9, ops / ms / 1e9 / 100.0);
   fflush(stdout);
   return 0;
 }
@@ -133,6 +344,16 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; ++rep)
       if (run<8, 8>(a, reps, "sieve32") || run16<0>(a, reps, "sieve16") || run16<4>(a, reps, "noepi16") ||
           run16<5>(a, reps, "nodma-noepi16") || run<8, 5>(a, reps, "nodma-noepi32"))
+        return 1;
+    return 0;
+  }
+  if (getenv("QDIRECT")) {   // query operand straight to registers (f6t::EngineQ) vs Engine16
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (run16<0>(a, reps, "sieve16") || run16<5>(a, reps, "nodma-noepi16") || runq<0, 4, 2, 1>(a, reps, "sieve") ||
+          runq<4, 4, 2, 1>(a, reps, "noepi") || runq<5, 4, 2, 1>(a, reps, "nodma-noepi") ||
+          runq<0, 5, 2, 1>(a, reps, "sieve") || runq<0, 6, 2, 1>(a, reps, "sieve") || runq<0, 4, 3, 1>(a, reps, "sieve") ||
+          runq<0, 5, 2, 2>(a, reps, "sieve"))
         return 1;
     return 0;
   }
