@@ -415,78 +415,38 @@ class FloatGallery:
             return None
         return self.ws.buf[off:off + 4 * B].view(torch.int32)
 
-    def _tier_dS(self, tier, stats):
-        """dS(q) of `tier` for query stats [R][3] (merge_kernel's bound: |S - S~| <= dS)."""
-        A, E, T, auxmax = (float(v) for v in self._tier_gallery(tier)["gmax"].cpu())
-        a, e, t = stats[:, 0], stats[:, 1], stats[:, 2]
-        gamma = (2 * -(-self.d // 128) + 64) * 2.0 ** -23 if tier == "f6" else 0.0
-        return 2.0 * (a * E + e * A + e * E + t * T) + 2.0 ** -20 * (auxmax + 2.0 * a * A) + 2.0 * gamma * a * A
-
     def fallback(self, Qd, qq, k, out, index_base=0, timings=None):
         """Re-run the queries the first tier left uncertified down the tier chain (then fp32).
-
-        Routing: a query the tier t could not certify missed by need = d_k^2 - bound_t, where
-        bound_t = tau - dS_t + |q|^2.  The next tier's bound is about tau - dS_t' + |q|^2 (tau, the
-        16th coarse score, moves by less than the two bounds), so it can only certify the query if
-        need < dS_t - dS_t'; queries with no such room skip it (crowded galleries: int8 x1 rescues
-        a band of margins only, int8 x2 the rest -- bench.py --stress).  Routing changes which
-        exact tier answers, never the answer: every stage still certifies or falls through.
         Returns the number of first-tier failures (host sync); self.last_fallbacks = the number of
-        uncertified queries after each quantized tier (queries routed past a tier count as
-        uncertified after it).
-        timings (a list, optional) receives (tier, queries, ms) per stage that ran (HIP events on
-        the current stream)."""
+        uncertified queries after each quantized tier that ran.  timings (a list, optional)
+        receives (tier, queries, ms) per stage that ran (HIP events on the current stream)."""
         bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
         counts = [int(bad.numel())]
         rows = bad                      # indices into the original batch still unresolved
         tier = qq["tier"]
-        if rows.numel():                # per row: the miss at the tier that measured it, and its dS
-            dk = out[0].index_select(0, rows)[:, k - 1]
-            need = dk * dk - qq["bound"].index_select(0, rows)
-            dS = self._tier_dS(tier, qq["stats"].index_select(0, rows))
         while rows.numel():
             tier = self.next_tier(tier, int(rows.numel()))
             if timings is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            nrun = int(rows.numel())
+            sub = Qd.index_select(0, rows).contiguous()
             if tier == "fp32":
-                sub = Qd.index_select(0, rows).contiguous()
                 d2, i2 = self._search_f32(sub, k, index_base)
                 out[0].index_copy_(0, rows, d2)
                 out[1].index_copy_(0, rows, i2)
-                rows = rows[:0]
+                still = rows[:0]
             else:
-                sub = Qd.index_select(0, rows).contiguous()
                 q2 = self.quantize_queries(sub, tier=tier)
-                dS2 = self._tier_dS(tier, q2["stats"])
-                hope = need < 0.9 * (dS - dS2)
-                run = torch.nonzero(hope).reshape(-1)
-                skip = torch.nonzero(~hope).reshape(-1)
-                nrun = int(run.numel())
-                if nrun == 0:           # nothing this tier could certify: straight on
-                    counts.append(int(rows.numel()))
-                    if timings is not None:
-                        ev[1].record()
-                    continue
-                if int(skip.numel()):
-                    sub = sub.index_select(0, run).contiguous()
-                    q2 = self.quantize_queries(sub, tier=tier)
-                    dS2 = dS2.index_select(0, run)
-                rrows = rows.index_select(0, run)
                 d2, i2 = self.search_q8_phase(3, sub, q2, k, index_base)
-                out[0].index_copy_(0, rrows, d2)
-                out[1].index_copy_(0, rrows, i2)
-                fail = torch.nonzero(q2["cert"] == 0).reshape(-1)
-                dkf = d2.index_select(0, fail)[:, k - 1]
-                rows = torch.cat([rrows.index_select(0, fail), rows.index_select(0, skip)])
-                need = torch.cat([dkf * dkf - q2["bound"].index_select(0, fail), need.index_select(0, skip)])
-                dS = torch.cat([dS2.index_select(0, fail), dS.index_select(0, skip)])
-                counts.append(int(rows.numel()))
+                out[0].index_copy_(0, rows, d2)
+                out[1].index_copy_(0, rows, i2)
+                still = torch.nonzero(q2["cert"] == 0).reshape(-1)
+                counts.append(int(still.numel()))
             if timings is not None:
                 ev[1].record()
                 ev[1].synchronize()
-                timings.append((str(tier), nrun, ev[0].elapsed_time(ev[1])))
+                timings.append((str(tier), int(rows.numel()), ev[0].elapsed_time(ev[1])))
+            rows = rows.index_select(0, still)
         self.last_fallbacks = tuple(counts)
         return counts[0]
 
