@@ -189,6 +189,119 @@ __global__ void __launch_bounds__(1024) elbp_hist_lds_kernel(const uint8_t* __re
   }
 }
 
+// ExtendedLBP(radius=1, neighbors=8) -- the reference's default operator and configs[3] -- with
+// its 3x3 sampling block held in registers.  Thread (tx, ty) walks code column x = tx down a strip
+// of rows; per code pixel it converts the 3 new pixels of the block's bottom row once and
+// shifts the block, instead of re-reading and converting the 21 terms' pixels from LDS.  The
+// arithmetic per point is lbp_code's (same products, same order, no contraction): the geometry
+// is fixed at compile time -- which block cell each term reads and which weights are zero --
+// and the host selects this kernel only when the caller's offsets and zero pattern are exactly
+// these (R1P8_OFFS below; the weights themselves are the caller's, e.g. bits 4 and 6 carry
+// the 2^-53 / 2^-52 terms of np.sin / np.cos).
+struct R1P8 {
+  double w[8][4];
+};
+constexpr int R1P8_OFFS[8][4] = {{1, 2, 1, 2}, {0, 1, 1, 2}, {0, 1, 0, 1}, {0, 0, 1, 1},
+                                 {0, 0, 1, 0}, {1, 0, 2, 1}, {2, 0, 2, 1}, {1, 1, 2, 2}};
+// non-zero terms per point: bit t set = weight t non-zero (points 0 and 2: weight 1.0 alone)
+constexpr int R1P8_TERMS[8] = {0x1, 0xf, 0x1, 0xf, 0x5, 0xf, 0x3, 0xf};
+
+__global__ void __launch_bounds__(1024) elbp_hist_r1p8_kernel(const uint8_t* __restrict__ imgs, LbpGeom g,
+                                                              HistArgs a, R1P8 k, void* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+  const int64_t img = blockIdx.x;
+  constexpr int nb = 256;
+  const int ncell = a.gr * a.gc;
+  uint8_t* im = reinterpret_cast<uint8_t*>(hist + ncell * nb);
+  const int W = g.W, npix = g.H * W;
+  for (int i = threadIdx.x; i < ncell * nb; i += blockDim.x) hist[i] = 0;
+  const uint8_t* src = imgs + img * (int64_t)npix;
+  if ((npix & 15) == 0 && ((uintptr_t)src & 15) == 0) {
+    for (int i = threadIdx.x; i < npix / 16; i += blockDim.x)
+      reinterpret_cast<uint4*>(im)[i] = reinterpret_cast<const uint4*>(src)[i];
+  } else {
+    for (int i = threadIdx.x; i < npix; i += blockDim.x) im[i] = src[i];
+  }
+  __syncthreads();
+  const int wpx = a.gc * a.px, hpx = a.gr * a.py;
+  const int tx = threadIdx.x & 127, ty = threadIdx.x >> 7;
+  const int rows = (hpx + 7) >> 3;
+  const int ya = ty * rows, yb = min(hpx, ya + rows);
+  for (int x = tx; x < wpx && ya < yb; x += 128) {
+    const uint8_t* col = im + x;
+    double b00 = col[ya * W], b01 = col[ya * W + 1], b02 = col[ya * W + 2];
+    double b10 = col[(ya + 1) * W], b11 = col[(ya + 1) * W + 1], b12 = col[(ya + 1) * W + 2];
+    const int cxo = x / a.px;
+    int cyc = ya / a.py, ry = ya - cyc * a.py;
+    for (int y = ya; y < yb; ++y) {
+      const uint8_t* r2 = col + (y + 2) * W;
+      const double b20 = r2[0], b21 = r2[1], b22 = r2[2];
+      const double C = b11;
+      uint32_t code = 0;
+      double N;
+      N = k.w[0][0] * b12;
+      code |= (N >= C ? 1u : 0u) << 0;
+      N = k.w[1][0] * b01; N = N + k.w[1][1] * b02; N = N + k.w[1][2] * b11; N = N + k.w[1][3] * b12;
+      code |= (N >= C ? 1u : 0u) << 1;
+      N = k.w[2][0] * b01;
+      code |= (N >= C ? 1u : 0u) << 2;
+      N = k.w[3][0] * b00; N = N + k.w[3][1] * b01; N = N + k.w[3][2] * b10; N = N + k.w[3][3] * b11;
+      code |= (N >= C ? 1u : 0u) << 3;
+      N = k.w[4][0] * b00; N = N + k.w[4][2] * b10;
+      code |= (N >= C ? 1u : 0u) << 4;
+      N = k.w[5][0] * b10; N = N + k.w[5][1] * b11; N = N + k.w[5][2] * b20; N = N + k.w[5][3] * b21;
+      code |= (N >= C ? 1u : 0u) << 5;
+      N = k.w[6][0] * b20; N = N + k.w[6][1] * b21;
+      code |= (N >= C ? 1u : 0u) << 6;
+      N = k.w[7][0] * b11; N = N + k.w[7][1] * b12; N = N + k.w[7][2] * b21; N = N + k.w[7][3] * b22;
+      code |= (N >= C ? 1u : 0u) << 7;
+      atomicAdd(&hist[(cyc * a.gc + cxo) * nb + (int)code], 1u);
+      if (++ry == a.py) {
+        ry = 0;
+        ++cyc;
+      }
+      b00 = b10; b01 = b11; b02 = b12;
+      b10 = b20; b11 = b21; b12 = b22;
+    }
+  }
+  __syncthreads();
+  const int total = ncell * nb;
+  const int64_t base = img * (int64_t)total;
+  if (a.count_bytes == 1) {
+    uint32_t* o = reinterpret_cast<uint32_t*>((uint8_t*)counts + base);
+    for (int i = threadIdx.x; i < total / 4; i += blockDim.x)
+      o[i] = hist[4 * i] | (hist[4 * i + 1] << 8) | (hist[4 * i + 2] << 16) | (hist[4 * i + 3] << 24);
+  } else if (a.count_bytes == 2) {
+    uint32_t* o = reinterpret_cast<uint32_t*>((uint16_t*)counts + base);
+    for (int i = threadIdx.x; i < total / 2; i += blockDim.x) o[i] = hist[2 * i] | (hist[2 * i + 1] << 16);
+  } else {
+    uint32_t* o = (uint32_t*)counts + base;
+    for (int i = threadIdx.x; i < total; i += blockDim.x) o[i] = hist[i];
+  }
+}
+
+// the caller's geometry is the compiled r1p8 one: same offsets, same zero pattern, weight 1.0 alone
+// for points 0 and 2
+static bool r1p8_match(int P, const int32_t* offs, const double* w, int oy, int ox, int by, int bx, R1P8& k) {
+  if (P != 8 || oy != 1 || ox != 1 || by != 3 || bx != 3) return false;
+  for (int i = 0; i < 8; ++i)
+    for (int t = 0; t < 4; ++t) {
+      if (offs[4 * i + t] != R1P8_OFFS[i][t]) return false;
+      const double wt = w[4 * i + t];
+      if (((R1P8_TERMS[i] >> t) & 1) != (wt != 0.0 ? 1 : 0)) return false;
+      k.w[i][t] = wt;
+    }
+  return w[0] == 1.0 && w[8] == 1.0;
+}
+
+static bool lbp_generic_forced() {
+  static const bool f = [] {
+    const char* e = getenv("OFR_LBP_GENERIC");
+    return e && atoi(e) != 0;
+  }();
+  return f;
+}
+
 static int make_geom(LbpGeom& g, int H, int W, int P, const int32_t* offs, const double* w, int oy, int ox, int by,
                      int bx) {
   if (P < 1 || P > MAXP) return fail(OFR_E_UNSUPPORTED, "ofr_elbp: neighbors must be in [1, 32]");
@@ -282,6 +395,20 @@ extern "C" int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H
   const int64_t nbins_total = (int64_t)gr * gc * nb;
   const size_t lds_whole = (size_t)nbins_total * 4 + round_up((int64_t)H * W, 16);
   // whole-image LDS variant: counters + image fit the budget, and the packed stores stay aligned
+  R1P8 k8;
+  if (lds_whole <= (size_t)LDS_IMG_BUDGET && nbins_total % 4 == 0 && n <= 0x7fffffffLL && !lbp_generic_forced() &&
+      r1p8_match(P, offs_host, w_host, oy, ox, by, bx, k8)) {
+    static bool attr8 = false;
+    if (!attr8) {
+      hipError_t e = hipFuncSetAttribute((const void*)elbp_hist_r1p8_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS_IMG_BUDGET);
+      if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(elbp_hist_r1p8)");
+      attr8 = true;
+    }
+    hipLaunchKernelGGL(elbp_hist_r1p8_kernel, dim3((unsigned)n), dim3(1024), lds_whole, st, imgs, g, a, k8, counts);
+    OFR_LAUNCH_CHECK("elbp_hist_r1p8_kernel");
+    return OFR_OK;
+  }
   if (lds_whole <= (size_t)LDS_IMG_BUDGET && nbins_total % 4 == 0 && n <= 0x7fffffffLL) {
     static bool attr_done = false;
     if (!attr_done) {

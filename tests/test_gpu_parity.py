@@ -486,6 +486,24 @@ def test_lbp_hist_counts_batch_vs_oracle():
         assert np.array_equal(c[i], ref), i
 
 
+@pytest.mark.parametrize("shape,grid", [((70, 70), (7, 7)), ((61, 93), (5, 4)), ((130, 128), (8, 8))])
+def test_lbp_hist_r1p8_ragged_vs_oracle(shape, grid):
+    """The register-window ExtendedLBP(1, 8) histogram kernel on sizes whose cells leave code rows /
+    columns uncovered and whose pixel counts are not multiples of 16 (unaligned image staging)."""
+    from ocvfacerec.facerec.feature import SpatialHistogram
+    from ocvfacerec.facerec.lbp import ExtendedLBP
+    from opencv_facerecognizer_amd._device import counts_numpy
+    r = _rng(12)
+    imgs = r.integers(0, 256, (24,) + shape, dtype=np.uint8)
+    imgs[:8] = (imgs[:8] // 128) * 128 + 60            # tie-heavy
+    sh = SpatialHistogram(ExtendedLBP(1, 8), grid)
+    counts, cell, cb = sh.counts_device(imgs)
+    c = counts_numpy(counts, cb).astype(np.int64)
+    for i in range(24):
+        ref, _ = O.spatial_histogram_counts(O.elbp(imgs[i]), 8, grid)
+        assert np.array_equal(c[i], ref), i
+
+
 # ---------------------------------------------------------------------------
 # chi-square search
 # ---------------------------------------------------------------------------
