@@ -399,6 +399,42 @@ int ofr_eigh_f64(void* stream, int64_t n, double* A, int64_t m, double* evals, d
 int ofr_sygv_f64(void* stream, int64_t n, double* Sb, double* Sw, int64_t m, double* evals, double* evecs,
                  int64_t ldv, void* workspace, size_t workspace_bytes);
 
+/* Context-based entry points (SURVEY §8b contract) ---------------------------
+ * For FFI callers holding the reference's plain row-major numpy layouts; each
+ * call lays its operands out for the kernels above in a workspace the context
+ * owns (grown on demand; a call may synchronise the stream when it grows).  A
+ * context belongs to one device and one thread at a time.
+ * ofr_project_u8: Y [B][d] fp32 = W^T (x - mu) for uint8 faces X [B][D] and
+ *   W [D][d] fp32 row-major (Fisherfaces.project feature.py:241-242 with mu
+ *   NULL; PCA.project :114-116 with mu [D] fp64) on the exact int8-slice engine
+ *   (exact products and sums, one rounding; OFR_FP64_ACC is accepted and always
+ *   in effect).  OFR_PROJ_REUSE_W: W is unchanged since the context's last
+ *   call with the same pointer and shape -> its prepared slices are reused.
+ * ofr_gram: G = A^T A [cols][cols] (OFR_GRAM_ATA) or A A^T [rows][rows]
+ *   (OFR_GRAM_AAT) of fp32 A [rows][cols] (feature.py:91-94): products exact
+ *   in fp64, fp64 accumulation on the fp64 MFMA; G fp32 or fp64 (prec =
+ *   OFR_DT_F32 / OFR_DT_F64).
+ * ofr_scatter: fp64 Sw, Sb [d][d] and class means [c][d] (nullable) of fp32
+ *   features F [N][d] with int32 device labels y in 0..c-1 (feature.py:160-168).
+ * ofr_knn: top-k of fp32 queries Q [B][d] against G [N][d] (Euclidean /
+ *   Cosine: exact fp64 re-rank of the fp32-MFMA candidates; ChiSquare: the
+ *   certified fp32 pass + exact fp64 pass for the rest, values used as given);
+ *   g_norms nullable (EUCLIDEAN: ||g||^2, COSINE: 1/||g||, as ofr_row_aux);
+ *   out_d fp32 [B][k] (distance.py values), out_i int64 [B][k] (+ index_base). */
+typedef struct ofr_ctx ofr_ctx;
+enum { OFR_FP64_ACC = 1, OFR_PROJ_REUSE_W = 2 };
+enum { OFR_GRAM_ATA = 0, OFR_GRAM_AAT = 1 };
+int ofr_ctx_create(int device, ofr_ctx** ctx);
+int ofr_ctx_destroy(ofr_ctx* ctx);
+int ofr_project_u8(ofr_ctx* ctx, void* stream, const uint8_t* X, int64_t B, int64_t D, const float* W, int64_t d,
+                   const double* mu_or_null, float* Y, int flags);
+int ofr_gram(ofr_ctx* ctx, void* stream, const float* A, int64_t rows, int64_t cols, int side, int prec, void* G);
+int ofr_scatter(ofr_ctx* ctx, void* stream, const float* F, const int32_t* y, int64_t N, int64_t d, int32_t c,
+                void* Sw, void* Sb, void* means);
+int ofr_knn(ofr_ctx* ctx, void* stream, int metric, const float* Q, int64_t B, const float* G,
+            const float* g_norms_or_null, int64_t N, int64_t d, int k, int64_t index_base, float* out_d,
+            int64_t* out_i);
+
 #ifdef __cplusplus
 }
 #endif

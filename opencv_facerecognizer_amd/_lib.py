@@ -96,6 +96,12 @@ SIGNATURES = {
     "ofr_knn_sharded": (c_int, [c_vp, c_vp, c_i64, c_i64, c_int]),
     "ofr_topk_merge_certify": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp]),
     "ofr_eig_workspace_bytes": (c_sz, [c_i64, c_i64]),
+    "ofr_ctx_create": (c_int, [c_int, c_vp]),
+    "ofr_ctx_destroy": (c_int, [c_vp]),
+    "ofr_project_u8": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_int]),
+    "ofr_gram": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_vp]),
+    "ofr_scatter": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp]),
+    "ofr_knn": (c_int, [c_vp, c_vp, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_int, c_i64, c_vp, c_vp]),
     "ofr_eigh_f64": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_sz]),
     "ofr_sygv_f64": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_sz]),
     "ofr_ingest_faces": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
@@ -121,6 +127,7 @@ class OfrError(RuntimeError):
 
 
 E_UNSUPPORTED, E_NUMERIC = -2, -4
+OFR_FP64_ACC, OFR_PROJ_REUSE_W = 1, 2          # ofr_project_u8 flags
 
 
 _lib = None
