@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--stress", default="48,96,192",
                     help="pixel-noise levels of the crowded-neighbour stress runs (same shape, 1 GPU); '' to skip")
     ap.add_argument("--stress-steps", type=int, default=3)
+    ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (100k-row gallery), 1 GPU")
     ap.add_argument("--search", choices=["f6", "q8", "fp32"], default="f6",
                     help="f6: certified fp6 coarse pass (uncertified queries go down the int8 tiers, then fp32); "
                          "q8: start at the certified int8 tier; fp32: fp32-MFMA pass")
@@ -174,11 +175,13 @@ def certificate_margin(gallery, Qd, qq, nsample=64):
     return {"median": float(np.median(r)), "min": float(r.min()), "sample": int(len(r))}
 
 
-def stress_run(P, bank, args, noise, device):
+def stress_run(P, bank, args, noise, device, N=None):
     """Crowded neighbours: the headline shape (1M gallery, B = 4096, d = 9999) with the pixel noise
     raised so that identities crowd together and the fp6 certificate fails; the uncertified queries
-    then run down the int8 / fp32 tiers inside the timed step.  One GPU."""
-    N, B, d, k = args.gallery, args.batch, args.dim, args.k
+    then run down the int8 / fp32 tiers inside the timed step.  One GPU.  With N (and the
+    headline noise) the same full step on another gallery size: configs[1] = 100k rows."""
+    N = N or args.gallery
+    B, d, k = args.batch, args.dim, args.k
     ld = max(32, round_up(d, 32))
     n_ids = (N + args.per_id - 1) // args.per_id
     gallery = build_gallery(P, bank, args.per_id, 0, N, N, d, ld, device, noise=noise)
@@ -451,9 +454,16 @@ def main():
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(Wt, gallery, Xq, N, args.cpu_seconds)
             result["speedup_vs_cpu"] = value / result["cpu_baseline"]["value"]
-        if world == 1 and args.search == "f6" and args.stress.strip():
+        if world == 1 and args.search == "f6" and (args.stress.strip() or args.config1):
             gallery.q8, gallery.G, gallery._Gbuf = None, None, None      # free the headline gallery first
             torch.cuda.empty_cache()
+        if world == 1 and args.search == "f6" and args.config1:
+            c1 = stress_run(P, bank, args, 12.0, device, N=100_000)
+            c1.pop("pixel_noise")
+            result["config1"] = dict(workload="configs[1]: 10k identities x 10 = 100k-row gallery, B=4096, d=9999, "
+                                              "the same full step (projection + fp6 tier + merge + fallback)", **c1)
+            log(rank, f"configs[1]: {c1['queries_per_s']:.0f} q/s, uncertified {c1['uncertified_after_each_tier']}")
+        if world == 1 and args.search == "f6" and args.stress.strip():
             result["stress"] = [stress_run(P, bank, args, float(x), device) for x in args.stress.split(",") if x.strip()]
             for r in result["stress"]:
                 log(rank, f"stress noise {r['pixel_noise']}: {r['queries_per_s']:.0f} q/s, uncertified "

@@ -60,7 +60,8 @@ def test_gram(ctx, side, prec):
     n = ref.shape[0]
     dt = torch.float64 if prec == "f64" else torch.float32
     G = torch.empty((n, n), dtype=dt, device="cuda")
-    call("ofr_gram", ctx, stream(), ptr(_dev(A)), 300, 129, side, _lib.DT_F64 if prec == "f64" else _lib.DT_F32, ptr(G))
+    Ad = _dev(A)                       # held: a temporary's memory could be reused before the kernels run
+    call("ofr_gram", ctx, stream(), ptr(Ad), 300, 129, side, _lib.DT_F64 if prec == "f64" else _lib.DT_F32, ptr(G))
     got = G.cpu().numpy().astype(np.float64)
     tol = 1e-12 if prec == "f64" else 2 ** -23
     assert np.abs(got - ref).max() <= tol * np.abs(ref).max() * 4
@@ -75,7 +76,8 @@ def test_scatter(ctx):
     Sw = torch.empty((d, d), dtype=torch.float64, device="cuda")
     Sb = torch.empty_like(Sw)
     M = torch.empty((c, d), dtype=torch.float64, device="cuda")
-    call("ofr_scatter", ctx, stream(), ptr(_dev(F)), ptr(_dev(y)), N, d, c, ptr(Sw), ptr(Sb), ptr(M))
+    Fd, yd, y1 = _dev(F), _dev(y), _dev((y + 1).astype(np.int32))
+    call("ofr_scatter", ctx, stream(), ptr(Fd), ptr(yd), N, d, c, ptr(Sw), ptr(Sb), ptr(M))
     _, Sw0, Sb0 = O.lda_scatter(F.astype(np.float64).T, y)
     assert np.allclose(Sw.cpu().numpy(), Sw0, rtol=1e-10, atol=1e-10 * np.abs(Sw0).max())
     assert np.allclose(Sb.cpu().numpy(), Sb0, rtol=1e-10, atol=1e-10 * np.abs(Sb0).max())
@@ -84,8 +86,7 @@ def test_scatter(ctx):
     # labels outside 0..c-1 are rejected like the reference's range(c) loop would mis-handle them
     from opencv_facerecognizer_amd._lib import OfrError
     with pytest.raises(OfrError):
-        call("ofr_scatter", ctx, stream(), ptr(_dev(F)), ptr(_dev((y + 1).astype(np.int32))), N, d, c, ptr(Sw),
-             ptr(Sb), None)
+        call("ofr_scatter", ctx, stream(), ptr(Fd), ptr(y1), N, d, c, ptr(Sw), ptr(Sb), None)
 
 
 @pytest.mark.parametrize("metric", ["EuclideanDistance", "CosineDistance", "ChiSquareDistance"])
@@ -108,6 +109,6 @@ def test_knn(ctx, metric):
          "ChiSquareDistance": _lib.METRIC_CHISQUARE}[metric]
     od = torch.empty((B, k), dtype=torch.float32, device="cuda")
     oi = torch.empty((B, k), dtype=torch.int64, device="cuda")
-    call("ofr_knn", ctx, stream(), m, ptr(_dev(Q.astype(np.float32))), B, ptr(_dev(G.astype(np.float32))), None, N, d,
-         k, 0, ptr(od), ptr(oi))
+    Qd, Gd = _dev(Q.astype(np.float32)), _dev(G.astype(np.float32))
+    call("ofr_knn", ctx, stream(), m, ptr(Qd), B, ptr(Gd), None, N, d, k, 0, ptr(od), ptr(oi))
     _check_search(metric, Q, G, od.cpu().numpy().astype(np.float64), oi.cpu().numpy(), k, near_rel=2e-4)
