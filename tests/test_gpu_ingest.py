@@ -45,8 +45,10 @@ def test_ingest_bit_exact_vs_oracle(interp):
             np.full((70, 70), 93, np.uint8),                              # same size: copy
             r.integers(0, 256, (480, 640, 3), dtype=np.uint8)]            # a camera frame (crops below)
     boxes = [(0, 0, 0, 53, 37), (1, 0, 0, 161, 200), (2, 0, 0, 14, 9), (3, 0, 0, 70, 70),
-             (4, 100, 50, 260, 230), (4, 0, 0, 3, 2), (4, 637, 470, 640, 480), (1, 10, 20, 90, 21)]
-    for size in [(70, 70), (23, 31), (100, 100)]:
+             (4, 100, 50, 260, 230), (4, 0, 0, 3, 2), (4, 637, 470, 640, 480), (1, 10, 20, 90, 21),
+             (4, 0, 0, 640, 480)]                                          # whole frame: > 64 KiB of grey
+    # (1100, 7): wider than the per-face kernel's tables -> the per-pixel kernel
+    for size in [(70, 70), (23, 31), (100, 100), (1100, 7)]:
         got = ingest.faces(imgs, size, interp, boxes=boxes, host=True)
         for j, (i, x0, y0, x1, y1) in enumerate(boxes):
             crop = imgs[i][y0:y1, x0:x1]
