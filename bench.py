@@ -43,6 +43,10 @@ from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
 PEAK_I8_MFMA = 5.0e15       # int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, matrix cores)
 PEAK_F6_MFMA = 10.0e15      # fp6 (block-scaled f8f6f4 MFMA): ~10 PF dense, the FP4 rate (MI355X_MICROARCH.md)
+# what the chip sustains on v_mfma_scale_f32_16x16x128_f8f6f4 (fp6 x fp6) with every CU busy and the
+# operands in registers, at the clock it holds under that load (tools/f6_shape_probe.hip,
+# profiles/r02_f6_shape_probe.log): the ceiling of any fp6 kernel on this part
+SUSTAINED_F6_MFMA = 6.28e15
 PEAK_HBM = 8.0e12           # HBM3E 8 TB/s (spec)
 
 
@@ -440,7 +444,10 @@ def main():
                          "executed_ops_per_launch": executed, "executed_frac": executed / (ms_tiles * 1e-3) / peak,
                          "traffic_source": tr[1] if tr else None,
                          "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
-                         "launch_ms": ms_tiles},
+                         "launch_ms": ms_tiles,
+                         **({"sustained_peak": SUSTAINED_F6_MFMA / 1e12, "frac_of_sustained": achieved / SUSTAINED_F6_MFMA,
+                             "sustained_source": "tools/f6_shape_probe.hip (profiles/r02_f6_shape_probe.log)"}
+                            if args.search == "f6" else {})},
             "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else "") + ("+all_gather" if shard_prep else ""):
                            ms_proj, "knn_tiles": ms_tiles,
                            "knn_merge_rerank" + ("+certificate+fallback" if use_q8 else ""): ms_merge},
