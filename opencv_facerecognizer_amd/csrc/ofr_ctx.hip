@@ -30,10 +30,11 @@ namespace ctxk {
 
 static inline size_t up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static int grow(char** buf, size_t* cap, size_t need, hipStream_t st) {
+static int grow(char** buf, size_t* cap, size_t need, hipStream_t) {
   if (need <= *cap) return OFR_OK;
-  hipError_t e = hipStreamSynchronize(st);   // earlier calls on the stream may still use the old buffer
-  if (e != hipSuccess) return hip_status(e, "ofr_ctx: stream sync");
+  // earlier calls may still use the old buffer, on this stream or another the caller used before
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_status(e, "ofr_ctx: device sync");
   if (*buf) {
     e = hipFree(*buf);
     if (e != hipSuccess) return hip_status(e, "ofr_ctx: hipFree");
