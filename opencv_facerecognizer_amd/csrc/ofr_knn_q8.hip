@@ -722,11 +722,25 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
       if (vec) {
         const float4* q4 = reinterpret_cast<const float4*>(qr);
         const float4* g4 = reinterpret_cast<const float4*>(gr);
-        for (int64_t j = lane; j < d4; j += 64) {   // distance.py:60, in fp64
-          const float4 x = q4[j], y = g4[j];
-          const double e0 = (double)x.x - (double)y.x, e1 = (double)x.y - (double)y.y;
-          const double e2 = (double)x.z - (double)y.z, e3 = (double)x.w - (double)y.w;
-          a += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+        // DU float4 pairs in flight per lane (a lone query's merge is one block: its loop is bound by
+        // the memory latency); the sum runs in the same order as one float4 per iteration
+        constexpr int DU = 4;
+        for (int64_t j = lane; j < d4; j += 64 * DU) {   // distance.py:60, in fp64
+          float4 x[DU], y[DU];
+#pragma unroll
+          for (int u = 0; u < DU; ++u) {
+            const int64_t jj = j + 64 * u;
+            x[u] = jj < d4 ? q4[jj] : make_float4(0.f, 0.f, 0.f, 0.f);
+            y[u] = jj < d4 ? g4[jj] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int u = 0; u < DU; ++u) {
+            if (j + 64 * u < d4) {
+              const double e0 = (double)x[u].x - (double)y[u].x, e1 = (double)x[u].y - (double)y[u].y;
+              const double e2 = (double)x[u].z - (double)y[u].z, e3 = (double)x[u].w - (double)y[u].w;
+              a += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+            }
+          }
         }
         j0 = d4 * 4;
       }
