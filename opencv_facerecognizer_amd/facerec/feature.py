@@ -104,11 +104,27 @@ class _DeviceProjMixin:
         cache = self.__dict__.get("_dev_proj")
         if cache is None or cache[0] is not src or cache[1] is not shift:
             P = _device.Projection(W)
-            P.W64 = _device.f64_dev(np.asarray(W, np.float64))
+            P.W_host = W
             P.own_shift = None if shift is None else _device.f64_dev(np.asarray(shift, np.float64).reshape(-1))
             cache = (src, shift, P)   # holds src/shift so that the identity check stays valid
             self.__dict__["_dev_proj"] = cache
         return cache[2]
+
+    def _prime_proj(self, W_dev):
+        """Seed the projection cache from the device copy of W [D][d] fp64 that training just
+        produced (the host W in self._eigenvectors is its copy): no upload of W back to the device."""
+        P = _device.Projection(Wt_device=W_dev.t().contiguous(), D=int(W_dev.shape[0]))
+        P.W_host = None
+        P._W64 = W_dev
+        P.own_shift = None
+        self.__dict__["_dev_proj"] = (self._eigenvectors, None, P)
+
+    @staticmethod
+    def _w64(P):
+        """fp64 W on the device (the GEMM path of non-uint8 inputs), uploaded on first use."""
+        if getattr(P, "_W64", None) is None:
+            P._W64 = _device.f64_dev(np.asarray(P.W_host, np.float64))
+        return P._W64
 
     def _shift(self, P, extra):
         """Own shift (PCA mean term) plus an extra centring shift (search layout), fp64 device or None."""
@@ -127,7 +143,7 @@ class _DeviceProjMixin:
         A = X if isinstance(X, np.ndarray) and X.ndim == 2 and not isinstance(X, np.matrix) else _stack_rows(X)
         if A.dtype == np.uint8:
             return P.project(_device.u8_rows(A), shift64=sh, f64=f64)
-        Y = _device.gemm_f64(_device.f64_dev(A.astype(np.float64)), P.W64)
+        Y = _device.gemm_f64(_device.f64_dev(A.astype(np.float64)), self._w64(P))
         if sh is not None:
             Y = _device.center_f64(Y, sh)
         return Y if f64 else _device.center_round(Y, None, P.ldy)
@@ -239,7 +255,7 @@ class PCA(_DeviceProjMixin, AbstractFeature):
 AUTO_DEVICE_MIN = 1024
 
 
-def lda_eigen(Sw, Sb, num_components, solver=None):
+def lda_eigen(Sw, Sb, num_components, solver=None, device_out=False):
     """Leading eigenpairs of inv(Sw) Sb, sorted by eigenvalue (feature.py:170-176).
 
     Sw, Sb: float64 host arrays or device tensors.  solver (or OFR_LDA_SOLVER):
@@ -251,7 +267,8 @@ def lda_eigen(Sw, Sb, num_components, solver=None):
     The pencil solvers scale columns to unit 2-norm like eig's -- the same eigenpairs up to
     column sign for distinct eigenvalues, in O(d^3) symmetric work instead of a general eig of a
     d x d matrix (minutes at d = 10000) -- and fall back to "eig" when Sw is not positive
-    definite.  Returns (float64 (m,), float64 (d, m)) host arrays.
+    definite.  Returns (float64 (m,), float64 (d, m)) host arrays; with device_out the eigenvectors
+    come back as a device tensor (no round trip when the device solver ran).
     """
     solver = solver or os.environ.get("OFR_LDA_SOLVER", "auto")
     if solver not in ("eig", "eigh", "device", "auto"):
@@ -271,7 +288,7 @@ def lda_eigen(Sw, Sb, num_components, solver=None):
                 raise
             warnings.warn("LDA: Sw is not positive definite (%s); using the general eig" % e)
         else:
-            return lam.cpu().numpy(), V.cpu().numpy()
+            return lam.cpu().numpy(), (V.contiguous() if device_out else V.cpu().numpy())
     if isinstance(Sw, torch.Tensor):
         Sw, Sb = Sw.cpu().numpy(), Sb.cpu().numpy()
     if solver == "eigh" and m > 0:
@@ -286,10 +303,12 @@ def lda_eigen(Sw, Sb, num_components, solver=None):
         else:
             order = np.argsort(-lam, kind="stable")[:m]
             V = V[:, order]
-            return lam[order], V / np.linalg.norm(V, axis=0)
+            V = V / np.linalg.norm(V, axis=0)
+            return lam[order], (_device.f64_dev(np.ascontiguousarray(V)) if device_out else V)
     evals, evecs = np.linalg.eig(np.linalg.inv(Sw) @ Sb)
     idx = np.argsort(-evals.real)
-    return evals[idx][:m].real, evecs[:, idx][:, :m].real
+    V = evecs[:, idx][:, :m].real
+    return evals[idx][:m].real, (_device.f64_dev(np.ascontiguousarray(V)) if device_out else V)
 
 
 class LDA(_DeviceProjMixin, AbstractFeature):
@@ -387,9 +406,8 @@ class Fisherfaces(_DeviceProjMixin, AbstractFeature):
             # PCA keeps every pixel dimension (a rotation): LDA in pixel space, W = V directly
             self._regime = "pixel"
             Sw, Sb = training.pixel_scatter(training.pixel_pieces(Xd, D, lay), lay.counts, n)
-            evals, W = lda_eigen(Sw, Sb, m)
+            evals, Wd = lda_eigen(Sw, Sb, m, device_out=True)
             del Sw, Sb
-            Wd = None
         elif n <= D:
             # n x n Gram of the centred faces: U_k = XC^T V_k / sigma_k, features V_k sigma_k
             self._regime = "gram"
@@ -418,8 +436,8 @@ class Fisherfaces(_DeviceProjMixin, AbstractFeature):
             Wd = _device.gemm_f64(Pd, _device.f64_dev(L32))                      # feature.py:229
         self._eigenvalues = np.array(evals, dtype=np.float32, copy=True)      # :226-227 (LDA's, float32)
         self._num_components = m
-        self._eigenvectors = np.asmatrix(Wd.cpu().numpy() if Wd is not None else np.asarray(W, np.float64))
-        self.__dict__.pop("_dev_proj", None)
+        self._eigenvectors = np.asmatrix(Wd.cpu().numpy())
+        self._prime_proj(Wd.contiguous())
         # features of the training set (:231-235): one batched exact projection of the resident faces
         Fd = self.project_device(Xd, f64=True)
         feats = [np.asmatrix(r.reshape(-1, 1)) for r in Fd.cpu().numpy()]
