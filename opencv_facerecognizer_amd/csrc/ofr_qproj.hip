@@ -113,6 +113,87 @@ __global__ void __launch_bounds__(S::NT, 1) project_q8_kernel(Args p) {
   }
 }
 
+// ---- a few faces (B <= 4, the recognizers' one face per call): split-K GEMV ------------------
+// The 256-row MFMA tile engine leaves most of the chip idle for one face (ceil(d/64) = 157
+// workgroups at d = 9,999, each streaming 2.6 MB of slices).  Here workgroup (jb, ks) streams the
+// 128 slice rows of 32-feature block jb over the ks-th of GEMV_KSPLIT K ranges: wave s = slice s,
+// lane l the 16-byte column chunks l, l + 64, ...; per chunk the faces' bytes (x - 128 by XOR 0x80)
+// are loaded once and dotted (v_dot4_i32_i8) with the chunk of each of the wave's 32 rows, so a
+// wave-instruction loads 1 KiB of one row.  The int32 partial sums (exact) are reduced over the
+// wave and added atomically into part [NB][arows]; gemv_finalize_kernel combines the four slices
+// exactly as project_q8_kernel's epilogue (same operations, same order: identical results).
+constexpr int GEMV_KSPLIT = 4;
+
+template <int NB>
+__global__ void __launch_bounds__(256) project_gemv_kernel(const uint8_t* X, int64_t ldx, int64_t D, const int8_t* Aq,
+                                                           int64_t ldk, int64_t arows, int* part) {
+  const int64_t jb = blockIdx.x / GEMV_KSPLIT;
+  const int ks = (int)(blockIdx.x % GEMV_KSPLIT);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row0 = jb * 128 + wave * 32;
+  const int64_t nch = (D + 15) / 16;
+  const int64_t per = (nch + GEMV_KSPLIT - 1) / GEMV_KSPLIT;
+  const int64_t c0 = ks * per, c1 = c0 + per < nch ? c0 + per : nch;
+  int acc[32][NB];
+#pragma unroll
+  for (int r = 0; r < 32; ++r)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[r][b] = 0;
+  for (int64_t c = c0 + lane; c < c1; c += 64) {
+    uint4 xv[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint4 v = *reinterpret_cast<const uint4*>(X + b * ldx + c * 16);
+      xv[b] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u, v.w ^ 0x80808080u);
+    }
+    // the group's row chunks are all loaded before any is used: RG loads in flight per lane
+    constexpr int RG = NB == 1 ? 32 : 16;
+#pragma unroll
+    for (int r0 = 0; r0 < 32; r0 += RG) {
+      uint4 a[RG];
+#pragma unroll
+      for (int r = 0; r < RG; ++r) a[r] = *reinterpret_cast<const uint4*>(Aq + (row0 + r0 + r) * ldk + c * 16);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < RG; ++r)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          int t = acc[r0 + r][b];
+          t = __builtin_amdgcn_sdot4((int)a[r].x, (int)xv[b].x, t, false);
+          t = __builtin_amdgcn_sdot4((int)a[r].y, (int)xv[b].y, t, false);
+          t = __builtin_amdgcn_sdot4((int)a[r].z, (int)xv[b].z, t, false);
+          t = __builtin_amdgcn_sdot4((int)a[r].w, (int)xv[b].w, t, false);
+          acc[r0 + r][b] = t;
+        }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 32; ++r)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      int v = acc[r][b];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) atomicAdd(part + b * arows + row0 + r, v);
+    }
+}
+
+__global__ void gemv_finalize_kernel(const int* part, int64_t arows, int64_t B, const double* scale, const double* K,
+                                     const double* shift, int64_t d, void* Y, int64_t ldy, int y_f64) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * d) return;
+  const int64_t b = t / d, j = t - b * d;
+  const int* pr = part + b * arows + (j >> 5) * 128 + (j & 31);
+  double tv = (double)pr[0];
+  tv += (double)pr[32] * 0x1p-7;
+  tv += (double)pr[64] * 0x1p-14;
+  tv += (double)pr[96] * 0x1p-21;
+  double y = scale[j] * (tv + K[j]);   // exact: x . Wq[:, j]
+  if (shift) y -= shift[j];
+  if (y_f64) ((double*)Y)[b * ldy + j] = y;
+  else ((float*)Y)[b * ldy + j] = (float)y;
+}
+
 // ---- weight preparation: one block per output feature ----------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256) prepare_kernel(const T* Wt, int64_t D, int64_t ldw, int8_t* Aq, int64_t ldk,
@@ -210,6 +291,15 @@ extern "C" int ofr_qproj_prepare(void* stream, int dtype, const void* Wt, int64_
   return OFR_OK;
 }
 
+// OFR_PROJ_GEMV=0 keeps B <= 4 on the tile engine (for comparisons)
+static bool getenv_flag_gemv() {
+  static const bool f = [] {
+    const char* e = getenv("OFR_PROJ_GEMV");
+    return !(e && atoi(e) == 0);
+  }();
+  return f;
+}
+
 extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx, const int8_t* Aq,
                                     int64_t ldk, const double* scale, const double* K, int64_t d, const double* shift,
                                     void* Y, int64_t ldy, int y_dtype) {
@@ -227,6 +317,27 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
                                        q8::S::LDS);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8)");
     attr_done = true;
+  }
+  if (B <= 4 && getenv_flag_gemv()) {
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t arows = cdiv(d, 64) * 256;
+    int* part = nullptr;
+    hipError_t e = hipMallocAsync((void**)&part, (size_t)B * arows * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(part, 0, (size_t)B * arows * 4, st);
+    if (e != hipSuccess) return hip_status(e, "ofr_project_u8_exact: partial sums");
+    const unsigned grid = (unsigned)(cdiv(d, 32) * q8::GEMV_KSPLIT);
+    switch (B) {
+      case 1: hipLaunchKernelGGL(q8::project_gemv_kernel<1>, dim3(grid), dim3(256), 0, st, X, ldx, D, Aq, ldk, arows, part); break;
+      case 2: hipLaunchKernelGGL(q8::project_gemv_kernel<2>, dim3(grid), dim3(256), 0, st, X, ldx, D, Aq, ldk, arows, part); break;
+      case 3: hipLaunchKernelGGL(q8::project_gemv_kernel<3>, dim3(grid), dim3(256), 0, st, X, ldx, D, Aq, ldk, arows, part); break;
+      default: hipLaunchKernelGGL(q8::project_gemv_kernel<4>, dim3(grid), dim3(256), 0, st, X, ldx, D, Aq, ldk, arows, part); break;
+    }
+    OFR_LAUNCH_CHECK("project_gemv_kernel");
+    hipLaunchKernelGGL(q8::gemv_finalize_kernel, dim3((unsigned)cdiv(B * d, 256)), dim3(256), 0, st, part, arows, B,
+                       scale, K, shift, d, Y, ldy, (int)(y_dtype == OFR_DT_F64));
+    OFR_LAUNCH_CHECK("gemv_finalize_kernel");
+    e = hipFreeAsync(part, st);
+    return e == hipSuccess ? OFR_OK : hip_status(e, "ofr_project_u8_exact: hipFreeAsync");
   }
   q8::Args p;
   p.X = X; p.B = B; p.D = D; p.ldx = ldx; p.Aq = Aq; p.ldk = ldk; p.scale = scale; p.K = K; p.shift = shift;

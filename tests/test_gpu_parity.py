@@ -409,6 +409,26 @@ def test_projection_vs_oracle(B, D, d):
     assert err2.max() < 1e-7, err2.max()
 
 
+@pytest.mark.parametrize("D,d", [(4900, 3), (10000, 130), (777, 45)])
+def test_projection_small_batch_gemv_identical(D, d):
+    """B <= 4 runs the split-K GEMV (project_gemv_kernel): results bit-identical to the same faces
+    projected in a batch on the MFMA tile engine (same exact integers, same fp64 combination)."""
+    from opencv_facerecognizer_amd._device import Projection, f64_dev, u8_rows
+    r = _rng(D + d)
+    W = r.normal(0, 1.0 / np.sqrt(D), (D, d))
+    X = r.integers(0, 256, (40, D), dtype=np.uint8)
+    P = Projection(W)
+    c = f64_dev(r.normal(0, 3, d))
+    big = P.project(u8_rows(X), shift64=c, f64=True).cpu().numpy()
+    big32 = P.project(u8_rows(X), shift64=c).cpu().numpy()
+    for B in (1, 2, 3, 4):
+        for s in (0, 7, 36):
+            small = P.project(u8_rows(X[s:s + B]), shift64=c, f64=True).cpu().numpy()
+            np.testing.assert_array_equal(small, big[s:s + B])
+            small32 = P.project(u8_rows(X[s:s + B]), shift64=c).cpu().numpy()
+            np.testing.assert_array_equal(small32, big32[s:s + B])
+
+
 def test_projection_fp32_weights_exact():
     """fp32 weights within 2^4 of their column maximum are represented exactly: the result equals the
     correctly rounded float64 dot product of the fp32 W."""
