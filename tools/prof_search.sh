@@ -5,7 +5,7 @@ set -e
 R=$GRAFT_REPO_ROOT
 K=${1:-tile_kernel_f6|sieve_threshold}
 shift || true
-ARGS=${*:---steps 2 --warmup 1 --small-batches= --stress= --no-cpu}
+ARGS=${*:---steps 2 --warmup 1 --small-batches= --stress= --config1 0 --no-cpu}
 mkdir -p $R/gpurun_out/prof
 cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py $ARGS"
