@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 
 from opencv_facerecognizer_amd import _lib  # noqa: E402
 from opencv_facerecognizer_amd._device import FloatGallery, Projection, col_mean_u8, round_up  # noqa: E402
-from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, merge_topk,  # noqa: E402
+from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, gather_rows_async, merge_topk,  # noqa: E402
                                                 shard_range)
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 
@@ -284,12 +284,17 @@ def main():
         nonlocal qq, qq_loc, Qd
         if events:
             events[0].record()
+        pending = None
         if shard_prep:
             P.project(Xq[b0:b1], shift64=gallery.shift64, out=Qd_loc)   # this rank's faces
             if use_q8:
                 qq_loc = gallery.quantize_queries(Qd_loc, qq_loc, tier=tier0)
                 qq = gallery.gather_queries(qq_loc)
-            Qd = gather_rows(Qd_loc)                                    # RCCL all-gather
+                # the fp32 rows are read from phase 2 on: their all-gather overlaps the tile pass
+                pending = gather_rows_async(Qd_loc)
+                Qd = pending.out
+            else:
+                Qd = gather_rows(Qd_loc)                                # RCCL all-gather
         else:
             P.project(Xq, shift64=gallery.shift64, out=Qd)              # fp32(W^T x - c), exact int8 MFMA
             if use_q8:
@@ -300,6 +305,8 @@ def main():
             gallery.search_q8_phase(1, Qd, qq, k)
         else:
             gallery.search_phase("tiles", Qd, k)
+        if pending is not None:
+            Qd = pending()
         if events:
             events[2].record()
         if use_q8:

@@ -45,6 +45,38 @@ def gather_rows(x, group=None):
     return torch.cat(parts, 0)
 
 
+class PendingRows:
+    """An all-gather of gather_rows in flight: .out is the destination (valid to hand to kernels
+    that do not read it yet, e.g. the quantized search's tile pass), calling it waits (a stream
+    dependency on the collective's stream for RCCL, not a host wait) and returns the rows."""
+
+    def __init__(self, out, work=None, parts=None):
+        self.out, self._work, self._parts = out, work, parts
+
+    def __call__(self):
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+            if self._parts is not None:
+                self.out.copy_(torch.cat(self._parts, 0))
+                self._parts = None
+        return self.out
+
+
+def gather_rows_async(x, group=None):
+    """Start gather_rows(x) and return a PendingRows (the query rows' all-gather overlaps the
+    quantized tile pass, which reads only the gathered fp6 / int8 query tiles)."""
+    _, ws = world()
+    if ws == 1:
+        return PendingRows(x)
+    x = x.contiguous()
+    out = torch.empty((ws * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    if dist.get_backend(group) == "nccl":
+        return PendingRows(out, dist.all_gather_into_tensor(out, x, group=group, async_op=True))
+    parts = [torch.empty_like(x) for _ in range(ws)]
+    return PendingRows(out, dist.all_gather(parts, x, group=group, async_op=True), parts)
+
+
 def exchange_topk(d, i, group=None):
     """All-gather per-rank (B x k) lists -> (B x world*k) tensors, rank-major (list p = rank p)."""
     gd, gi, _ = exchange_lists(d, i, None, group)

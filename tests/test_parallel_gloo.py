@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import facerec_oracle as O
-from opencv_facerecognizer_amd.parallel import exchange_topk, gather_rows, shard_range, world
+from opencv_facerecognizer_amd.parallel import exchange_topk, gather_rows, gather_rows_async, shard_range, world
 
 
 def _free_port():
@@ -84,6 +84,9 @@ def _gather_worker(rank, ws, port, out):
     try:
         x = torch.arange(6 * 5, dtype=torch.float32).reshape(6, 5) + 1000 * rank   # this rank's row block
         g = gather_rows(x)
+        pending = gather_rows_async(x)             # the overlapped form (bench.py): same rows
+        g2 = pending()
+        assert pending.out is g2 and torch.equal(g, g2)
         if rank == 0:
             out.put(g.numpy())
     finally:
