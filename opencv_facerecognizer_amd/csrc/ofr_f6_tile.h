@@ -109,9 +109,10 @@ struct Engine {
   // Stage kt of gallery panel gp and query panel qp -> LDS stage buffer st: DMA_INS
   // wave-instructions of 1 KiB, the first half the gallery block, the second the query block.
   // SKIP (probes only): 2 = no gallery block, 16 = no query block
+  // 128 = the same bytes loaded into the VGPRs *sink instead of LDS (probe: intake without LDS writes)
   template <int SKIP = 0>
   static __device__ __forceinline__ void dma(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst,
-                                             int kt, char* st) {
+                                             int kt, char* st, i32x4* sink = nullptr) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const char* gb = G + (gp * nst + kt) * (int64_t)PANEL;
     const char* qb = Q + (qp * nst + kt) * (int64_t)PANEL;
@@ -121,6 +122,10 @@ struct Engine {
       const bool gal = ins < DMA_INS / 2;
       const int off = (gal ? ins : ins - DMA_INS / 2) * 1024;
       if (((SKIP & 2) && gal) || ((SKIP & 16) && !gal)) continue;
+      if constexpr ((SKIP & 128) != 0) {
+        asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(*sink) : "v"((gal ? gb : qb) + off + lane * 16) : "memory");
+        continue;
+      }
       __builtin_amdgcn_global_load_lds((const OFR_GLOBAL void*)((gal ? gb : qb) + off + lane * 16),
                                        (OFR_LDS void*)(st + (gal ? 0 : PANEL) + off), 16, 0, 0);
     }
@@ -249,8 +254,16 @@ struct Engine16 {
     const i32x8 b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, 4, 5, -1, -1);
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 2, 2, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
   }
+  // probe only (MODE 256): the accumulators pinned to AGPRs through an asm MFMA (the compiler
+  // cannot see its latency: the probe drains the pipe with s_nops before reading them)
+  static __device__ __forceinline__ void mfma_agpr(const i32x6& a, const i32x6& b, f32x4& c, int sc) {
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
+                 : "+a"(c) : "v"(a), "v"(b), "v"(sc));
+  }
 
-  // MODE (probes): 1 = no k-loop DMA
+  // MODE (probes): 1 = no k-loop DMA; 64 = DMA issued but never waited for (wrong results: isolates
+  // the cost of waiting for the DMA from that of moving its bytes); 128 = the k-loop's stage loads
+  // land in VGPRs, not LDS (wrong results: the feed's bytes without its LDS writes)
   template <int MODE>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
                                                   int nst, f32x4 (&acc)[NA][NB]) {
@@ -260,11 +273,21 @@ struct Engine16 {
     for (int i = 0; i < NA; ++i)
 #pragma unroll
       for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    i32x4 sink = {0, 0, 0, 0};
     auto issue = [&](int kt) { Engine<8>::dma<0>(G, gp, Q, qp, nst, kt, smem + (kt % NST) * STAGE); };
+    auto issue_k = [&](int kt) {
+      Engine<8>::dma<MODE & 128>(G, gp, Q, qp, nst, kt, smem + (kt % NST) * STAGE, &sink);
+    };
     const int last = nst - 1;
 #pragma unroll
     for (int s = 0; s < NST; ++s) issue(s < last ? s : last);
     i32x6 a[NA], b[NB];
+    int sc = 0x7f7f7f7f;
+    if constexpr ((MODE & 256) != 0) asm volatile("" : "+v"(sc));
+    auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) {
+      if constexpr ((MODE & 256) != 0) mfma_agpr(x, y, c, sc);
+      else c = mfma(x, y, c);
+    };
     auto readA = [&](const char* st, int i) { a[i] = frag16(st, wr * 128 + i * 16 + r16); };
     auto readB = [&](const char* st, int c) { b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16); };
     if constexpr (MODE == 1) wait_vm<0>();
@@ -278,23 +301,23 @@ struct Engine16 {
     // MFMA is issued (A-major: A[i] after row i's 4 MFMAs, B[c] after row 7's MFMA c), so the
     // fragments need no second register set (acc 128 + fragments 72 registers).
     for (int kt = 0; kt < last; ++kt) {
-      if constexpr (MODE == 1) wait_vm<0>();
-      else wait_vm<IPW>();       // stage kt+1 landed; kt+2 may be in flight
+      if constexpr ((MODE & 1) != 0) wait_vm<0>();
+      else if constexpr ((MODE & 64) == 0) wait_vm<IPW>();   // stage kt+1 landed; kt+2 may be in flight
       barrier();                 // every wave has read stage kt: its buffer takes stage kt+3
-      if constexpr (MODE != 1) {
+      if constexpr ((MODE & 1) == 0) {
         const int nx = kt + NST;
-        issue(nx < last ? nx : last);
+        issue_k(nx < last ? nx : last);
       }
       const char* nxt = smem + ((kt + 1) % NST) * STAGE;
 #pragma unroll
       for (int i = 0; i < NA - 1; ++i) {
 #pragma unroll
-        for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i], b[c], acc[i][c]);
+        for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
         readA(nxt, i);
       }
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
-        acc[NA - 1][c] = mfma(a[NA - 1], b[c], acc[NA - 1][c]);
+        mm(a[NA - 1], b[c], acc[NA - 1][c]);
         readB(nxt, c);
       }
       readA(nxt, NA - 1);
@@ -317,8 +340,10 @@ struct Engine16 {
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll
-      for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i], b[c], acc[i][c]);
+      for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
     wait_vm<0>();
+    if constexpr ((MODE & 256) != 0) asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+    if constexpr ((MODE & 128) != 0) asm volatile("" : "+v"(sink));
     barrier();
   }
 };

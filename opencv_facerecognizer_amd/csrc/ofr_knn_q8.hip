@@ -433,8 +433,8 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
   f6t::f32x4 acc[8][4];
-  E::mainloop<MODE & 1>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt, p.nk,
-                        acc);
+  E::mainloop<MODE & 449>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt, p.nk,
+                          acc);
   // sieve operands after the main loop (the 16x16 engine needs every register in it)
   float ga = __builtin_inff(), gs = 0.f, sq2[4], th[4];
   if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {

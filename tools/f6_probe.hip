@@ -343,7 +343,7 @@ int main(int argc, char** argv) {
     a.gg = 4 < ntg ? 4 : ntg;
     for (int rep = 0; rep < 2; ++rep)
       if (run<8, 8>(a, reps, "sieve32") || run16<0>(a, reps, "sieve16") || run16<4>(a, reps, "noepi16") ||
-          run16<5>(a, reps, "nodma-noepi16") || run<8, 5>(a, reps, "nodma-noepi32"))
+          run16<260>(a, reps, "agpr-noepi16") || run16<261>(a, reps, "agpr-nodma-noepi16") || run16<5>(a, reps, "nodma-noepi16") || run<8, 5>(a, reps, "nodma-noepi32"))
         return 1;
     return 0;
   }
