@@ -220,7 +220,8 @@ def stress_run(P, bank, args, noise, device, N=None):
         e["ms"] += m / args.stress_steps
     acc = float(((out[1][:, 0] // args.per_id) == ids_q).double().mean().item())
     res = {"pixel_noise": noise, "queries_per_s": B / (ms * 1e-3), "ms_per_step": ms,
-           "uncertified_after_each_tier": counts, "fallback_ms_per_step": per_tier,
+           "uncertified_after_each_tier": counts, "skipped_tier": dict(gallery.last_skipped),
+           "fallback_ms_per_step": per_tier,
            "certificate_margin_fp6": certificate_margin(gallery, Qd, qq), "top1_identity_acc": acc}
     del gallery
     torch.cuda.empty_cache()

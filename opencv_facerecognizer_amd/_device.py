@@ -422,10 +422,18 @@ class FloatGallery:
         receives (tier, queries, ms) per stage that ran (HIP events on the current stream)."""
         bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
         counts = [int(bad.numel())]
-        rows = bad                      # indices into the original batch still unresolved
-        tier = qq["tier"]
-        while rows.numel():
-            tier = self.next_tier(tier, int(rows.numel()))
+        chain = self.TIER_CHAIN
+        pending = {}                    # tier -> indices into the original batch waiting for it
+        self.last_skipped = {}
+        self._route(qq["tier"], bad, Qd, qq["stats"].index_select(0, bad), qq["bound"].index_select(0, bad), out, k,
+                    pending)
+        for tier in chain[chain.index(qq["tier"]) + 1:]:
+            rows = pending.pop(tier, None)
+            if rows is None or not rows.numel():
+                continue
+            if tier != "fp32" and int(rows.numel()) <= SMALL_BATCH:   # see next_tier
+                self._queue(pending, "fp32", rows)
+                continue
             if timings is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
@@ -434,7 +442,6 @@ class FloatGallery:
                 d2, i2 = self._search_f32(sub, k, index_base)
                 out[0].index_copy_(0, rows, d2)
                 out[1].index_copy_(0, rows, i2)
-                still = rows[:0]
             else:
                 q2 = self.quantize_queries(sub, tier=tier)
                 d2, i2 = self.search_q8_phase(3, sub, q2, k, index_base)
@@ -442,13 +449,57 @@ class FloatGallery:
                 out[1].index_copy_(0, rows, i2)
                 still = torch.nonzero(q2["cert"] == 0).reshape(-1)
                 counts.append(int(still.numel()))
+                self._route(tier, rows.index_select(0, still), Qd, q2["stats"].index_select(0, still),
+                            q2["bound"].index_select(0, still), out, k, pending)
             if timings is not None:
                 ev[1].record()
                 ev[1].synchronize()
                 timings.append((str(tier), int(rows.numel()), ev[0].elapsed_time(ev[1])))
-            rows = rows.index_select(0, still)
         self.last_fallbacks = tuple(counts)
         return counts[0]
+
+    # the k-th distance must clear the next tier's predicted bound by this factor of the bound's gain
+    ROUTE_SLACK = 1.5
+
+    def _dS(self, tier, stats):
+        """|S - S~| bound of the tier per query (merge_kernel's dS), stats [n][3] fp64."""
+        gm = self._tier_gallery(tier)["gmax"]
+        A, E, T, aux = gm[0], gm[1], gm[2], gm[3]
+        a, e, t = stats[:, 0], stats[:, 1], stats[:, 2]
+        gamma = (2 * -(-self.d // 128) + 64) * 2.0 ** -23 if tier == "f6" else 0.0
+        return 2.0 * (a * E + e * A + e * E + t * T) + 2.0 ** -20 * (aux + 2.0 * a * A) + 2.0 * gamma * a * A
+
+    def _route(self, tier, rows, Qd, stats, bound, out, k, pending):
+        """Queue the queries `tier` left uncertified (rows; their stats and bounds in that tier) for the
+        next stage.  A query whose k-th distance misses even the bound the next quantized tier would
+        give it -- this tier's bound moved by the drop in dS, the candidate order assumed unchanged,
+        with ROUTE_SLACK to spare -- skips that tier: on crowded data (DESIGN.md §5 stress) int8x1
+        rescues a few percent of the fp6 failures for a whole gallery pass.  Only a routing choice:
+        every stage still certifies or hands on, so the results do not depend on it."""
+        if not rows.numel():
+            return
+        chain = self.TIER_CHAIN
+        nxt = chain[chain.index(tier) + 1]
+        after = chain[chain.index(nxt) + 1] if nxt != "fp32" else None
+        if after is None or after == "fp32" or int(rows.numel()) <= SMALL_BATCH:
+            self._queue(pending, nxt, rows)
+            return
+        sub = Qd.index_select(0, rows).contiguous()
+        st_next = self.quantize_queries(sub, tier=nxt)["stats"]
+        gain = self._dS(tier, stats) - self._dS(nxt, st_next)
+        kth = out[0].index_select(0, rows)[:, k - 1]
+        # -inf bound (sieve overflow): no information, try the next tier
+        hopeless = torch.isfinite(bound) & (kth * kth >= bound + self.ROUTE_SLACK * gain)
+        skip = rows[hopeless]
+        keep = rows[~hopeless]
+        self.last_skipped[str(nxt)] = int(skip.numel())
+        self._queue(pending, nxt, keep)
+        self._queue(pending, after, skip)
+
+    @staticmethod
+    def _queue(pending, tier, rows):
+        if rows.numel():
+            pending[tier] = rows if tier not in pending else torch.cat([pending[tier], rows])
 
     def query_rows(self, Q64):
         """Host or device fp64 query features [B][d] -> centred fp32 search rows [B][ld]."""

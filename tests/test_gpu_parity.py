@@ -121,8 +121,32 @@ def test_knn_q8_certificate_forces_fallback(monkeypatch):
     Q = (c + r.normal(0, 1e-6, (100, 64))).astype(np.float32).astype(np.float64)   # every row ~equidistant
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     dd, ii = g.search(g.query_rows(Q), 3)
-    assert len(g.last_fallbacks) == 3 and min(g.last_fallbacks) > 0
+    # every quantized tier that ran left queries uncertified (the fp32 pass resolved them); the fp6
+    # failures miss even the bound int8 x1 would give by far, so they skip it (_route)
+    assert g.last_fallbacks[0] == 100 and min(g.last_fallbacks) > 0
+    assert g.last_skipped.get("1", 0) >= 90, g.last_skipped
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
+
+
+def test_fallback_routing_is_only_a_choice(monkeypatch):
+    """_route may send an fp6 failure past int8 x1; with the skip disabled (every failure runs every
+    tier) the results are identical, on crowded data where both routes are taken."""
+    from opencv_facerecognizer_amd._device import FloatGallery
+    from opencv_facerecognizer_amd import _lib
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(98)
+    d, N, B = 96, 30000, 300
+    protos = r.normal(0, 6, (300, d))
+    G = (protos[np.arange(N) % 300] + r.normal(0, 4, (N, d))).astype(np.float32).astype(np.float64)
+    Q = (protos[r.integers(0, 300, B)] + r.normal(0, 4, (B, d))).astype(np.float32).astype(np.float64)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    dd, ii = g.search(g.query_rows(Q), 1)
+    routed = (g.last_fallbacks, dict(g.last_skipped))
+    monkeypatch.setattr(FloatGallery, "ROUTE_SLACK", float("inf"))   # never skip
+    d2, i2 = g.search(g.query_rows(Q), 1)
+    assert g.last_skipped.get("1", 0) == 0
+    assert torch.equal(ii, i2) and torch.equal(dd, d2), routed
+    _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 1)
 
 
 def test_knn_f6_sieve_overflow_falls_back(monkeypatch):
