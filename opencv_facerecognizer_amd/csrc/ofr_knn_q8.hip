@@ -667,7 +667,14 @@ __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists,
 // (distance.py:60) of the survivors in coarse order, one wave per candidate (float4 loads, lane
 // partial sums, shuffle reduction), until the coarse bound proves the rest cannot reach the
 // k-th; (3) sort by (distance, index) and the certificate.
+// OFR_MERGE_PROBE_V: compile-time probe bits for tools/build_merge_probe.sh only (the library
+// build never defines it): 1 = bucket head instead of its best 16, 2 = no |q|^2 pass, 4 = no
+// exact re-rank -- each gives wrong results, to time the kernel's parts.
+#ifndef OFR_MERGE_PROBE_V
+#define OFR_MERGE_PROBE_V 0
+#endif
 __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
+  constexpr int V = OFR_MERGE_PROBE_V;
   __shared__ Cand lists[256 * KC];
   __shared__ double exact[KC];
   __shared__ double red[4];
@@ -678,7 +685,12 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   if (p.count) {
     const int64_t c = p.count[q];
     overflow = c > p.cap || c < 0;   // rows were dropped (and a tile-level overflow writes none): no candidates
-    block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
+    if constexpr ((V & 1) != 0) {
+      if (threadIdx.x < KC) lists[threadIdx.x] = p.cand[(size_t)q * p.cap + threadIdx.x];
+      __syncthreads();
+    } else {
+      block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
+    }
   } else {
     block_best(p.cand + (size_t)q * p.T * KC, p.T * KC, lists);
   }
@@ -689,7 +701,7 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   // bound by the memory latency, not the bytes
   constexpr int RU = 8;
   double qq = 0;
-  for (int64_t j0 = threadIdx.x; j0 < p.d; j0 += (int64_t)RU * blockDim.x) {
+  for (int64_t j0 = threadIdx.x; (V & 2) == 0 && j0 < p.d; j0 += (int64_t)RU * blockDim.x) {
     float x[RU];
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
@@ -716,7 +728,7 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     const int c = 4 * r + wave;
     const Cand cc = lists[c];
     double a = 0;
-    if (cc.i != CAND_EMPTY) {
+    if (cc.i != CAND_EMPTY && (V & 4) == 0) {
       const float* gr = p.G + (int64_t)cc.i * p.ldg;
       int64_t j0 = 0;
       if (vec) {
