@@ -168,8 +168,10 @@ class FloatGallery:
     invariant), shift None.
     """
 
-    def __init__(self, feats, metric, device=None):
-        """feats: host array [N][d] (any float type; used in fp64)."""
+    def __init__(self, feats, metric, device=None, shift64=None):
+        """feats: host array [N][d] (any float type; used in fp64).  shift64 (Euclidean, fp64 [d]):
+        centre on this vector instead of the rows' mean -- a sharded gallery centres every shard on
+        the same one."""
         device = device or dev()
         self.metric = metric
         F = f64_dev(np.asarray(feats, np.float64), device=device) if not isinstance(feats, torch.Tensor) else \
@@ -177,7 +179,9 @@ class FloatGallery:
         self.N, self.d = int(F.shape[0]), int(F.shape[1])
         self.ld = max(32, round_up(self.d, 32))
         self.shift64 = None
-        if metric == _lib.METRIC_EUCLIDEAN and self.N > 0:
+        if metric == _lib.METRIC_EUCLIDEAN and shift64 is not None:
+            self.shift64 = f64_dev(shift64, device=device).reshape(-1).contiguous()
+        elif metric == _lib.METRIC_EUCLIDEAN and self.N > 0:
             self.shift64 = col_mean_f64(F)
         self.G = center_round(F, self.shift64, self.ld)
         self._finish(device)

@@ -350,7 +350,7 @@ def _as_text(x):
 # pickled by this package (``__getstate__`` drops it); a file that carries such keys must not
 # pre-seed the caches, whose identity checks would then be bypassed.
 def _is_cache_key(k):
-    return isinstance(k, str) and (k.startswith("_dev") or k == "_shift_cache")
+    return isinstance(k, str) and (k.startswith("_dev") or k in ("_shift_cache", "_shard"))
 
 
 def _drop_caches(st):

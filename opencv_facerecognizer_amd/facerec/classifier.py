@@ -13,6 +13,12 @@ k-element host operation, as in the reference.
 Tie order: exact distance ties resolve to the lowest gallery index (the
 reference's quicksort leaves their order unspecified).
 
+Multi-GPU (SURVEY §8e, §8f row 2 "sharding on load"): ``shard()`` under torch.distributed keeps
+only this rank's contiguous block of the gallery rows on its GPU; every rank then calls
+``predict``/``predict_batch``/``search`` with the same queries (SPMD) and gets the global result
+(``parallel.certify_sharded`` for the certified Euclidean tiers, else one all-gather + merge of
+the local exact top-k lists).
+
 Out of scope: ``SVM`` (classifier.py:150-222) needs the absent libsvm.
 """
 from __future__ import annotations
@@ -21,6 +27,7 @@ import operator as op
 import threading
 
 import numpy as np
+import torch
 
 from .. import _lib
 from .._device import Chi2Gallery, FloatGallery
@@ -113,6 +120,44 @@ class NearestNeighbor(AbstractClassifier):
     def _invalidate(self):
         self.__dict__.pop("_dev", None)
 
+    # -- multi-GPU ---------------------------------------------------------------
+    def shard(self, group=None):
+        """Hold only this rank's rows [r*N/G, (r+1)*N/G) of the gallery on this process's GPU
+        (torch.distributed initialised, one process per GPU; G = the group's size).  Every rank
+        keeps the full host state (X, y: the reference's pickled model) and must call the search
+        methods with the same queries.  Returns self."""
+        from ..parallel import world
+        rank, ws = world(group)
+        self.__dict__["_shard"] = (group, rank, ws)
+        self._invalidate()
+        return self
+
+    def _shard_info(self):
+        sh = self.__dict__.get("_shard")
+        return sh if sh is not None and sh[2] > 1 else None
+
+    def _gallery_sharded(self, mid, sh):
+        from ..parallel import shard_range
+        _, rank, ws = sh
+        n = len(self.X)
+        key = (mid, id(self.X), _lib.device(), "shard", rank, ws)
+        cache = self.__dict__.get("_dev")
+        if cache is not None and cache[0] == key and cache[1] == n:
+            return cache[2]
+        if n < ws:
+            raise ValueError(f"a gallery of {n} rows cannot be sharded over {ws} ranks")
+        n0, n1 = shard_range(n, rank, ws)
+        feats = self._stack(self.X[n0:n1])
+        if mid == _lib.METRIC_CHISQUARE:
+            g = Chi2Gallery(feats)
+        else:
+            # the same centre on every rank: the mean of all rows, from the host copy every rank holds
+            shift = self._stack(self.X).mean(0) if mid == _lib.METRIC_EUCLIDEAN else None
+            g = FloatGallery(feats, mid, shift64=shift)
+        g.index_base = n0
+        self.__dict__["_dev"] = (key, n, g)
+        return g
+
     def _gallery(self):
         """Device gallery of self.X, built once and extended in place when items were appended
         (update, or X grown by the caller): an update costs the new rows, not a re-upload."""
@@ -121,6 +166,10 @@ class NearestNeighbor(AbstractClassifier):
         n = len(self.X)
         if n > len(self.y):
             raise Exception("More distances than classes. Is your distance metric correct?")  # classifier.py:109-110
+        sh = self._shard_info()
+        if sh is not None:
+            with _DEVICE_LOCK:
+                return self._gallery_sharded(mid, sh)
         cache = self.__dict__.get("_dev")
         if cache is not None and cache[0] == key and cache[1] == n:
             return cache[2]
@@ -143,7 +192,7 @@ class NearestNeighbor(AbstractClassifier):
         """Seed the device gallery from fp64 device rows F [N][d] equal to self.X (e.g. the training
         features a Fisherfaces.compute just produced on the device)."""
         mid = self._metric()
-        if mid == _lib.METRIC_CHISQUARE or int(F.shape[0]) != len(self.X):
+        if mid == _lib.METRIC_CHISQUARE or int(F.shape[0]) != len(self.X) or self._shard_info() is not None:
             return
         with _DEVICE_LOCK:
             g = FloatGallery(F, mid)
@@ -167,7 +216,25 @@ class NearestNeighbor(AbstractClassifier):
     def _search_device(self, Qd, k):
         g = self._gallery()
         with _DEVICE_LOCK:
-            return g.search(Qd, k)
+            sh = self._shard_info()
+            return g.search(Qd, k) if sh is None else self._search_sharded(g, Qd, k, sh)
+
+    def _search_sharded(self, g, Qd, k, sh):
+        """Global top-k over the shards.  The path is chosen from values every rank shares (metric,
+        batch size, k, search mode), so all ranks run the same collectives."""
+        from ..parallel import certify_sharded, exchange_topk, merge_topk
+        group, _, ws = sh
+        B = int(Qd.shape[0])
+        n0 = g.index_base
+        if isinstance(g, FloatGallery) and g.metric == _lib.METRIC_EUCLIDEAN and g.use_q8(B, k):
+            qq = g.quantize_queries(Qd, tier=g.first_tier())
+            out = g.search_q8_phase(3, Qd, qq, k, n0)
+            (md, mi), counts = certify_sharded(g, Qd, qq, k, out, n0, group)
+            g.last_fallbacks = tuple(counts)
+            return md, mi
+        d, i = g.search(Qd, k, n0)                 # this shard's exact top-k, global row indices
+        gd, gi = exchange_topk(d.to(torch.float64), i.to(torch.int64), group)
+        return merge_topk(gd.contiguous(), gi.contiguous(), ws, k, k)
 
     def _search_prepared(self, Qd, k):
         """Qd already in the gallery's query layout (centred for Euclidean)."""
@@ -175,11 +242,13 @@ class NearestNeighbor(AbstractClassifier):
         if Qd.shape[1] != g.ld:
             raise ValueError("query layout does not match the gallery")
         with _DEVICE_LOCK:
-            return g.search(Qd, k)
+            sh = self._shard_info()
+            return g.search(Qd, k) if sh is None else self._search_sharded(g, Qd, k, sh)
 
     def __getstate__(self):
         st = dict(self.__dict__)
         st.pop("_dev", None)
+        st.pop("_shard", None)
         return st
 
     def __repr__(self):

@@ -32,6 +32,12 @@ class PredictableModel(object):
         if dev is not None and dev[0] == id(features) and hasattr(self.classifier, "adopt_device_rows"):
             self.classifier.adopt_device_rows(dev[1])
 
+    def shard(self, group=None):
+        """Shard the classifier's gallery over the ranks of ``group`` (NearestNeighbor.shard): every
+        rank then predicts the same faces and gets the global result."""
+        self.classifier.shard(group)
+        return self
+
     def predict(self, X):
         """model.py:53-55 (one face)."""
         return self.predict_batch([X])[0]
