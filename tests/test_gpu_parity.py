@@ -895,3 +895,35 @@ def test_sygv_device_not_positive_definite_falls_back():
         lam, V = lda_eigen(Sw, Sb, 3, solver="device")
     le, Ve = lda_eigen(Sw, Sb, 3, solver="eig")
     assert np.array_equal(lam, le) and np.array_equal(V, Ve)
+
+
+def test_model_reload_releases_device_memory(golden):
+    """The ROS recognizer reloads the model on every restart (ocvf_recognizer_ros.py:251-256): the
+    dropped model's device state (projection, gallery, quantized tiers, workspaces) must be freed,
+    so repeated load -> predict -> drop cycles do not grow device memory."""
+    import gc
+    from ocvfacerec.facerec.classifier import NearestNeighbor
+    from ocvfacerec.facerec.distance import EuclideanDistance
+    from ocvfacerec.facerec.serialization import load_model
+    f = golden("individuals_faces.npz")
+    r = _rng(77)
+    G = r.normal(0, 3, (20000, 64))
+    Q = G[:300] + r.normal(0, 0.1, (300, 64))
+
+    def cycle():
+        m = load_model(os.path.join(GOLDEN, "individuals.pkl"))
+        m.predict_batch(list(f["X"]))
+        m.predict(f["X"][0])
+        nn = NearestNeighbor(EuclideanDistance(), k=1)
+        nn.compute(list(G), np.arange(len(G)))
+        nn.predict_batch(Q)          # fp6 sieve tier: gallery tiles, workspaces
+        nn.predict_batch(Q[:3])      # fp6 stream tier
+        del m, nn
+        gc.collect()
+        torch.cuda.synchronize()
+
+    cycle()
+    base = torch.cuda.memory_allocated()
+    for _ in range(4):
+        cycle()
+    assert torch.cuda.memory_allocated() <= base
