@@ -36,8 +36,8 @@ sys.path.insert(0, ROOT)
 
 from opencv_facerecognizer_amd import _lib  # noqa: E402
 from opencv_facerecognizer_amd._device import FloatGallery, Projection, col_mean_u8, round_up  # noqa: E402
-from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, gather_rows_async, merge_topk,  # noqa: E402
-                                                shard_range)
+from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, gather_rows_async,  # noqa: E402
+                                                merge_sharded, merge_topk, shard_range)
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 
 PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
@@ -311,7 +311,7 @@ def main():
         if events:
             events[2].record()
         if use_q8:
-            gallery.search_q8_phase(2, Qd, qq, k, index_base=n0, out=out)
+            merge_sharded(gallery, Qd, qq, k, n0, out)   # world 1: the plain phase 2
             if world > 1:      # global certificate: all-gather + merge + collective fallback
                 res, counts = certify_sharded(gallery, Qd, qq, k, out, n0)
                 fallbacks.append(counts[0])

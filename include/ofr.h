@@ -202,6 +202,23 @@ int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq,
                const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
                void* workspace, size_t workspace_bytes);
+/* Phase 2 of ofr_knn_f6 split for a gallery sharded over ranks (new; replaces the
+ * per-rank re-rank of classifier.py:104-119's loop at G > 1).  After phase 1 on every shard:
+ *   stage 1 selects each query's 16 candidates into the workspace and writes ub[B][k] -- upper
+ *           bounds of the squared distances of its best k candidates (ascending, +inf past the
+ *           list);
+ *   the caller takes, per query, the k-th smallest of every rank's ub values (an upper bound of
+ *           the GLOBAL k-th squared distance) into ub[B];
+ *   stage 2 re-ranks the selection exactly but skips every candidate whose lower bound exceeds
+ *           ub[q] (it cannot be among the global k nearest), then writes out_d/out_i/cert/bound
+ *           as phase 2 does (a shard holding none of a query's neighbours re-ranks nothing).
+ * Same arguments as ofr_knn_f6 (phases replaced by stage; out_d/out_i/cert/bound only read by
+ * stage 2); the workspace carries the selection between the stages.                          */
+int ofr_knn_f6_merge_pruned(void* stream, int stage, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                            const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
+                            int64_t d, const void* Gt, const float* gscale, const float* aux, const double* gmax,
+                            int k, int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
+                            double* ub, void* workspace, size_t workspace_bytes);
 
 /* Merge P sorted (distance, index) lists per query into the best k:
  * in_d/in_i [B][P*kin] (list p at columns [p*kin, (p+1)*kin)), ascending by

@@ -411,6 +411,21 @@ class FloatGallery:
                  ptr(qq["cert"]), ptr(qq["bound"]), ptr(ws), ws.numel())
         return out
 
+    def merge_pruned(self, stage, Qd, qq, k, ub, index_base=0, out=None):
+        """The split fp6 merge of a sharded gallery (ofr_knn_f6_merge_pruned, after phase 1 on this
+        gallery's workspace): stage 1 writes ub [B][k] (this shard's upper bounds), stage 2 re-ranks
+        pruned by ub [B] (the global bound) into out / qq["cert"] / qq["bound"]."""
+        g = self._tier_gallery("f6")
+        B = Qd.shape[0]
+        lib = _lib.load()
+        ws = self.ws.get(lib.ofr_knn_f6_workspace_bytes(B, self.N), Qd.device)
+        o = out if out is not None else (None, None)
+        call("ofr_knn_f6_merge_pruned", stream(), stage, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
+             ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]), ptr(self.aux),
+             ptr(g["gmax"]), k, index_base, ptr(o[0]), ptr(o[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(ub), ptr(ws),
+             ws.numel())
+        return out
+
     def sieve_counts(self, B):
         """Rows kept per query by the last fp6 sieve pass of a B-query batch (int32 device view of
         the workspace, valid until the next search), or None when B <= 32 (no sieve)."""

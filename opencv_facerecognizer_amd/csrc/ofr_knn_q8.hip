@@ -583,6 +583,15 @@ struct MergeArgs {
   const int* count;        // sieve: rows kept per query (null for tile lists)
   const uint32_t* theta;   // sieve: the keep thresholds
   int64_t cap;
+  // split merge of a sharded gallery (ofr_knn_f6_merge_pruned): mode 1 selects the candidates and
+  // writes them (sel [B][KC]), |q|^2, dS and the overflow flag (qd [B][3]) and the squared-distance
+  // upper bounds of the best k (ub_local [B][k]); mode 2 re-ranks the selection, pruned by the
+  // global bound ub [B] (the k-th smallest upper bound over every shard).  Mode 0: both at once.
+  int mode;
+  Cand* sel;
+  double* qd;
+  double* ub_local;
+  const double* ub;
 };
 
 // Best KC (distance, index) of the n candidates at src (16-byte aligned) into lists[0..KC),
@@ -682,49 +691,88 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   const int64_t q = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   bool overflow = false;
-  if (p.count) {
-    const int64_t c = p.count[q];
-    overflow = c > p.cap || c < 0;   // rows were dropped (and a tile-level overflow writes none): no candidates
-    if constexpr ((V & 1) != 0) {
-      if (threadIdx.x < KC) lists[threadIdx.x] = p.cand[(size_t)q * p.cap + threadIdx.x];
-      __syncthreads();
-    } else {
-      block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
-    }
-  } else {
-    block_best(p.cand + (size_t)q * p.T * KC, p.T * KC, lists);
-  }
   const float* qr = p.Q + q * p.ldq;
+  double qq, dS;
+  const int kk = p.k < KC ? p.k : KC;
+  if (p.mode == 2) {   // the selection of a mode-1 launch
+    if (threadIdx.x < KC) lists[threadIdx.x] = p.sel[q * KC + threadIdx.x];
+    qq = p.qd[q * 3 + 0];
+    dS = p.qd[q * 3 + 1];
+    overflow = p.qd[q * 3 + 2] != 0.0;
+    __syncthreads();
+  } else {
+    if (p.count) {
+      const int64_t c = p.count[q];
+      overflow = c > p.cap || c < 0;   // rows were dropped (and a tile-level overflow writes none): no candidates
+      if constexpr ((V & 1) != 0) {
+        if (threadIdx.x < KC) lists[threadIdx.x] = p.cand[(size_t)q * p.cap + threadIdx.x];
+        __syncthreads();
+      } else {
+        block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
+      }
+    } else {
+      block_best(p.cand + (size_t)q * p.T * KC, p.T * KC, lists);
+    }
+    // loads batched 8 deep: with few queries (one block each) a loop with one load per iteration is
+    // bound by the memory latency, not the bytes
+    constexpr int RU = 8;
+    qq = 0;
+    for (int64_t j0 = threadIdx.x; (V & 2) == 0 && j0 < p.d; j0 += (int64_t)RU * blockDim.x) {
+      float x[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int64_t j = j0 + (int64_t)u * blockDim.x;
+        x[u] = j < p.d ? qr[j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) qq += (double)x[u] * (double)x[u];
+    }
+    qq = block_sum_f64(qq, red);
+    // dS(q): |S - S~| <= dS for every row, S = d^2 - |q|^2
+    const double qa = p.qstats[q * 3 + 0], qe = p.qstats[q * 3 + 1], qt = p.qstats[q * 3 + 2];
+    const double A = p.gmax[0], E = p.gmax[1], T = p.gmax[2], auxmax = p.gmax[3];
+    dS = 2.0 * (qa * E + qe * A + qe * E + qt * T) + 0x1p-20 * (auxmax + 2.0 * qa * A) + 2.0 * p.gamma * qa * A;
+    dS = dS * (1.0 + 1e-6) + 1e-300;
+    if (p.mode == 1) {
+      if (threadIdx.x < KC) p.sel[q * KC + threadIdx.x] = lists[threadIdx.x];
+      if (threadIdx.x == 0) {
+        p.qd[q * 3 + 0] = qq;
+        p.qd[q * 3 + 1] = dS;
+        p.qd[q * 3 + 2] = overflow ? 1.0 : 0.0;
+        // upper bound of d^2 of the j-th candidate: its truncated key t is within 256 ulp below
+        // the fp32 coarse score (|sc - t| <= |t| 2^-15, 2^-14 taken), S <= sc + dS, d^2 = S + |q|^2;
+        // the lists are in ascending key order, so the bounds ascend too
+        for (int j = 0; j < kk; ++j) {
+          const Cand c = lists[j];
+          const double t = (double)c.d;
+          p.ub_local[q * kk + j] = c.i == CAND_EMPTY || overflow
+                                       ? __builtin_inf()
+                                       : (t + fabs(t) * 0x1p-14 + dS + qq) * (1.0 + 1e-12) + 1e-300;
+        }
+      }
+      return;
+    }
+  }
   const int64_t d4 = p.d >> 2;
   const bool vec = ((p.ldq | p.ldg) & 3) == 0 && (((uintptr_t)p.Q | (uintptr_t)p.G) & 15) == 0;
-  // loads batched 8 deep: with few queries (one block each) a loop with one load per iteration is
-  // bound by the memory latency, not the bytes
-  constexpr int RU = 8;
-  double qq = 0;
-  for (int64_t j0 = threadIdx.x; (V & 2) == 0 && j0 < p.d; j0 += (int64_t)RU * blockDim.x) {
-    float x[RU];
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int64_t j = j0 + (int64_t)u * blockDim.x;
-      x[u] = j < p.d ? qr[j] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < RU; ++u) qq += (double)x[u] * (double)x[u];
-  }
-  qq = block_sum_f64(qq, red);
-  // dS(q): |S - S~| <= dS for every row, S = d^2 - |q|^2
-  const double qa = p.qstats[q * 3 + 0], qe = p.qstats[q * 3 + 1], qt = p.qstats[q * 3 + 2];
-  const double A = p.gmax[0], E = p.gmax[1], T = p.gmax[2], auxmax = p.gmax[3];
-  double dS = 2.0 * (qa * E + qe * A + qe * E + qt * T) + 0x1p-20 * (auxmax + 2.0 * qa * A) + 2.0 * p.gamma * qa * A;
-  dS = dS * (1.0 + 1e-6) + 1e-300;
   // lower bound of d^2 of any row whose (truncated) coarse score is >= s, less a relative 1e-12
   // for the fp64 evaluation
   auto d2_lower = [&](double s) { return (s - dS + qq) - 1e-12 * (fabs(s) + dS + 2.0 * qq); };
-  const int kk = p.k < KC ? p.k : KC;
+  // sharded (mode 2): no row whose lower bound exceeds ub -- an upper bound of the GLOBAL k-th
+  // squared distance -- can be among the global k nearest, so it need not be re-ranked
+  const double ubq = p.ub ? p.ub[q] : __builtin_inf();
+  int skip_all = 0;
+  if (p.ub) {
+    if (threadIdx.x == 0)
+      stop_flag = lists[0].i == CAND_EMPTY || d2_lower((double)lists[0].d) > ubq;
+    __syncthreads();
+    skip_all = stop_flag;
+    if (skip_all && (int)threadIdx.x < KC) exact[threadIdx.x] = __builtin_inf();
+  }
   // exact fp64 distance (distance.py:60) of the candidates in coarse order, 4 per round (one per
   // wave); stop once the next candidate's lower bound exceeds the k-th exact distance so far:
   // it and every later one (and every row outside the list) are strictly farther
-  for (int r = 0; r < KC / 4; ++r) {
+  for (int r = 0; r < KC / 4 && !skip_all; ++r) {
     const int c = 4 * r + wave;
     const Cand cc = lists[c];
     double a = 0;
@@ -782,8 +830,10 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
             }
             if (lt < kk && kk <= le) kth = v;
           }
-          st = d2_lower((double)lists[done].d) > kth * kth;
+          st = d2_lower((double)lists[done].d) > fmin(kth * kth, ubq);
         }
+      } else if (done < KC && p.ub) {
+        st = lists[done].i == CAND_EMPTY || d2_lower((double)lists[done].d) > ubq;
       }
       stop_flag = st;
     }
@@ -1200,13 +1250,26 @@ static size_t stream_ws_lists(int64_t B, int64_t N) {
   return (size_t)round_up((int64_t)cdiv(N > 0 ? N : 1, q8s::TG) * B * q8s::KC * (int64_t)sizeof(Cand), 256);
 }
 
+// the regime's regions, then the split merge's selection sel [B][KC] and qd [B][3]
+static size_t f6_ws_core(int64_t B, int64_t N) {
+  return B <= 32 ? stream_ws_lists(B, N) + (size_t)round_up((int64_t)(B * q8s::PM * q8s::KC * sizeof(Cand)), 256)
+                 : (size_t)round_up((int64_t)sieve_ws(B, N).bytes, 256);
+}
+static size_t f6_ws_qd(int64_t B) { return (size_t)round_up((int64_t)(B * q8s::KC * sizeof(Cand)), 256); }
+
 extern "C" size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N) {
-  return B <= 32 ? stream_ws_lists(B, N) + (size_t)B * q8s::PM * q8s::KC * sizeof(Cand) : sieve_ws(B, N).bytes;
+  return f6_ws_core(B, N) + f6_ws_qd(B) + (size_t)B * 3 * sizeof(double);
 }
 
 extern "C" size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N) {
   return B <= 32 ? (size_t)-1 : sieve_ws(B, N).count;
 }
+
+static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                       const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
+                       const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
+                       int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
+                       size_t workspace_bytes, int merge_mode, double* ub);
 
 extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                           const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
@@ -1214,6 +1277,27 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
                           int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
                           void* workspace, size_t workspace_bytes) {
   OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_f6: phases must be 1 (tiles), 2 (merge) or 3");
+  return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr);
+}
+
+extern "C" int ofr_knn_f6_merge_pruned(void* stream, int stage, const float* Q, int64_t B, int64_t ldq,
+                                       const void* Qt, const float* qscale, const double* qstats, const float* G,
+                                       int64_t N, int64_t ldg, int64_t d, const void* Gt, const float* gscale,
+                                       const float* aux, const double* gmax, int k, int64_t index_base,
+                                       double* out_d, int64_t* out_i, int* cert, double* bound, double* ub,
+                                       void* workspace, size_t workspace_bytes) {
+  OFR_CHECK_ARG(stage == 1 || stage == 2, "ofr_knn_f6_merge_pruned: stage must be 1 (select) or 2 (re-rank)");
+  OFR_CHECK_ARG(ub != nullptr, "ofr_knn_f6_merge_pruned: null ub");
+  return knn_f6_impl(stream, 2, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, stage, ub);
+}
+
+static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                       const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
+                       const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
+                       int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
+                       size_t workspace_bytes, int merge_mode, double* ub) {
   OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_f6: bad sizes (empty galleries use ofr_knn_f32)");
   if (k < 1 || k > q8s::KC) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6: k must be in [1, 16]");
   if (B == 0) return OFR_OK;
@@ -1282,16 +1366,23 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
     }
   }
   if (phases & 2) {
-    OFR_CHECK_ARG(out_d && out_i && cert, "ofr_knn_f6: null output");
+    OFR_CHECK_ARG(merge_mode == 1 || (out_d && out_i && cert), "ofr_knn_f6: null output");
     // fp32 accumulation over nst * 2 MFMAs: |err| <= (n + 64) 2^-23 sum|q~ g~| / (s_q s_g),
     // sum|q~ g~| <= a_q a_g <= a_q A (tools/mx_probe.hip measures <= 3 * 2^-24 at n = 160)
     const double gamma = (double)(2 * a.nk + 64) * 0x1p-23;
     q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, gamma, k, index_base, out_d, out_i, cert, bound};
+    m.mode = merge_mode;
+    m.sel = reinterpret_cast<Cand*>(wsb + f6_ws_core(B, N));
+    m.qd = reinterpret_cast<double*>(wsb + f6_ws_core(B, N) + f6_ws_qd(B));
+    if (merge_mode == 1) m.ub_local = ub;
+    if (merge_mode == 2) m.ub = ub;
     if (sieve) {
       m.cand = bucket;
       m.count = count;
       m.theta = theta;
       m.cap = q8s::SIEVE_CAP;
+    } else if (merge_mode == 2) {
+      // the selection is read back from sel: no premerge
     } else if (a.ntg > q8s::PM) {
       Cand* pm = reinterpret_cast<Cand*>(wsb + stream_ws_lists(B, N));
       hipLaunchKernelGGL(q8s::premerge_kernel, dim3(q8s::PM, (unsigned)B), dim3(256), 0, st, a.cand, a.ntg, pm);

@@ -222,13 +222,14 @@ class NearestNeighbor(AbstractClassifier):
     def _search_sharded(self, g, Qd, k, sh):
         """Global top-k over the shards.  The path is chosen from values every rank shares (metric,
         batch size, k, search mode), so all ranks run the same collectives."""
-        from ..parallel import certify_sharded, exchange_topk, merge_topk
+        from ..parallel import certify_sharded, exchange_topk, merge_sharded, merge_topk
         group, _, ws = sh
         B = int(Qd.shape[0])
         n0 = g.index_base
         if isinstance(g, FloatGallery) and g.metric == _lib.METRIC_EUCLIDEAN and g.use_q8(B, k):
             qq = g.quantize_queries(Qd, tier=g.first_tier())
-            out = g.search_q8_phase(3, Qd, qq, k, n0)
+            out = g.search_q8_phase(1, Qd, qq, k, n0)
+            merge_sharded(g, Qd, qq, k, n0, out, group)
             (md, mi), counts = certify_sharded(g, Qd, qq, k, out, n0, group)
             g.last_fallbacks = tuple(counts)
             return md, mi

@@ -119,6 +119,26 @@ def exchange_lists(d, i, bound=None, group=None):
     return gd, gi, minb
 
 
+def merge_sharded(gallery, Qd, qq, k, index_base, out, group=None):
+    """Phase 2 of the certified search on a sharded gallery, after phase 1 (the tile pass) on every
+    rank.  fp6 tier: the split merge -- every rank selects its candidates and bounds the squared
+    distance of its best k from above (ofr_knn_f6_merge_pruned stage 1), ONE all-gather of those
+    B x k bounds gives per query the k-th smallest over the ranks, an upper bound of the GLOBAL k-th
+    squared distance, and each rank re-ranks only the candidates that can still fall below it
+    (stage 2): a rank that holds none of a query's neighbours skips its exact re-rank (the rows it
+    skips are farther than k rows of another rank, so the global top-k and the certificate of
+    certify_sharded are unchanged).  Other tiers: the local merge.  Returns out."""
+    _, ws = world(group)
+    if ws == 1 or qq["tier"] != "f6":
+        return gallery.search_q8_phase(2, Qd, qq, k, index_base=index_base, out=out)
+    B = Qd.shape[0]
+    ub_local = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
+    gallery.merge_pruned(1, Qd, qq, k, ub_local, index_base)
+    allb = gather_rows(ub_local, group).reshape(ws, B, k).permute(1, 0, 2).reshape(B, ws * k)
+    ub = allb.kthvalue(k, dim=1).values.contiguous()
+    return gallery.merge_pruned(2, Qd, qq, k, ub, index_base, out)
+
+
 def global_certificate(kth, minb):
     """Query certified iff its GLOBAL k-th squared distance is below every rank's bound.
 

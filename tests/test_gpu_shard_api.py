@@ -67,6 +67,24 @@ def _worker(rank, ws, port, out):
                 d, i = clf.search(Q[:B])
                 labels = [p[0] for p in clf.predict_batch(Q[:B])]
                 res[(metric, B)] = (d, i, labels, clf._gallery().N, clf._gallery().last_fallbacks)
+        # the pruned split merge (parallel.merge_sharded) against the plain per-rank merge, on the
+        # same shard: identical global results; the pruned local lists skip foreign queries
+        from opencv_facerecognizer_amd.parallel import certify_sharded, merge_sharded
+        Q, G, y = _identity_blocks()
+        clf = _classifier("EuclideanDistance")
+        clf.compute(list(G), y)
+        clf.shard()
+        g = clf._gallery()
+        Qd = g.query_rows(Q)
+        qa = g.quantize_queries(Qd, tier="f6")
+        plain = g.search_q8_phase(3, Qd, qa, K, g.index_base)
+        (pd, pi), pc = certify_sharded(g, Qd, qa, K, plain, g.index_base)
+        qb = g.quantize_queries(Qd, tier="f6")
+        loc = g.search_q8_phase(1, Qd, qb, K, g.index_base)
+        merge_sharded(g, Qd, qb, K, g.index_base, loc)
+        skipped = int(torch.isinf(loc[0][:, 0]).sum())
+        (rd, ri), rc = certify_sharded(g, Qd, qb, K, loc, g.index_base)
+        res["pruned"] = (pd.cpu().numpy(), pi.cpu().numpy(), pc, rd.cpu().numpy(), ri.cpu().numpy(), rc, skipped)
         # the fused model path: Fisherfaces projection + sharded certified search
         from ocvfacerec.facerec.feature import Fisherfaces
         from ocvfacerec.facerec.model import PredictableModel
@@ -83,6 +101,15 @@ def _worker(rank, ws, port, out):
         out.put((rank, res))
     finally:
         dist.destroy_process_group()
+
+
+def _identity_blocks():
+    """400 identities x 10 rows, each identity's rows contiguous (so on one shard), 300 queries."""
+    r = np.random.default_rng(75)
+    protos = r.normal(0, 4, (400, 48))
+    G = protos[np.arange(4000) // 10] + r.normal(0, 1, (4000, 48))
+    Q = protos[r.integers(0, 400, 300)] + r.normal(0, 1, (300, 48))
+    return Q.astype(np.float32).astype(np.float64), G.astype(np.float32).astype(np.float64), np.arange(4000) // 10
 
 
 def _faces():
@@ -158,3 +185,17 @@ def test_sharded_predictable_model(sharded):
     F = np.stack([np.asarray(ff.project(x.reshape(-1, 1))).reshape(-1) for x in X])
     Dref = O.pairwise("EuclideanDistance", F[-64:], F[:-64])
     assert (np.argsort(Dref, 1, kind="stable")[:, 0] == idx0[:, 0]).mean() >= 0.98
+
+
+@pytest.mark.timeout(600)
+def test_pruned_merge_equals_plain_merge(sharded):
+    """parallel.merge_sharded (ofr_knn_f6_merge_pruned): the global top-k and the certificate counts
+    equal the plain per-rank merge's; each rank skipped the re-rank of the queries whose neighbours
+    live on the other rank."""
+    for rank in (0, 1):
+        pd, pi, pc, rd, ri, rc, skipped = sharded[rank]["pruned"]
+        assert np.array_equal(pi, ri) and np.array_equal(pd, rd)
+        assert list(pc) == list(rc)
+        assert skipped >= 100, skipped      # of 300 queries, about half belong to the other shard
+    Q, G, _ = _identity_blocks()
+    _check_search("EuclideanDistance", Q, G, sharded[0]["pruned"][3], sharded[0]["pruned"][4], K)

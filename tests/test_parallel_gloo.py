@@ -291,3 +291,56 @@ def test_sharded_training_pieces_allreduce_exactly():
     _, oSw, oSb = O.lda_scatter(X.T.astype(np.float64), y)
     assert np.allclose(Sw, oSw, rtol=0, atol=1e-9 * np.abs(oSw).max())
     assert np.allclose(Sb, oSb, rtol=0, atol=1e-9 * np.abs(oSb).max())
+
+
+class _PrunedMock:
+    """Stands in for FloatGallery.merge_pruned: stage 1 reports rank-specific upper bounds, stage 2
+    records the global bound it was given."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.seen = None
+
+    def merge_pruned(self, stage, Qd, qq, k, ub, index_base=0, out=None):
+        if stage == 1:
+            B = ub.shape[0]
+            base = torch.arange(B, dtype=torch.float64)[:, None] * 10.0
+            ub.copy_(base + torch.arange(k, dtype=torch.float64)[None, :] + (0.5 if self.rank else 0.0))
+            if self.rank == 1:
+                ub[0] = float("inf")          # a shard with no candidates for query 0
+        else:
+            self.seen = ub.clone()
+        return out
+
+
+def _pruned_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from opencv_facerecognizer_amd.parallel import merge_sharded
+        g = _PrunedMock(rank)
+        B, k = 4, 3
+        merge_sharded(g, torch.zeros((B, 8)), {"tier": "f6"}, k, 0, None)
+        q.put((rank, g.seen.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_merge_sharded_global_bound():
+    """The bound handed to stage 2 is, per query, the k-th smallest of every rank's k upper bounds."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pruned_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    B, k = 4, 3
+    for b in range(B):
+        vals = sorted([10.0 * b + j for j in range(k)] + ([] if b == 0 else [10.0 * b + j + 0.5 for j in range(k)])
+                      + ([float("inf")] * k if b == 0 else []))
+        for r in (0, 1):
+            assert res[r][b] == vals[k - 1]

@@ -24,20 +24,23 @@ def main():
     ap.add_argument("--sizes", default="1000000,500000,250000,125000")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--foreign", action="store_true",
+                    help="queries of identities outside the gallery (a shard at G > 1 that does not hold them)")
     a = ap.parse_args()
     dev = _lib.device()
     side, d, per_id, B = 100, 9999, 10, a.batch
     P, _ = bench.build_projection(side * side, d, dev)
     sizes = [int(x) for x in a.sizes.split(",")]
-    bank = IdentityBank(max(sizes) // per_id, side, side, device=dev)
+    bank = IdentityBank(2 * max(sizes) // per_id, side, side, device=dev)
     ld = bench.round_up(d, 32)
-    res = {"B": B, "d": d, "sizes": {}}
+    res = {"B": B, "d": d, "foreign_queries": a.foreign, "sizes": {}}
     for N in sizes:
         gal = bench.build_gallery(P, bank, per_id, 0, N, N, d, ld, dev)
         gal._tier_gallery("f6")
         gq = torch.Generator(device=dev)
         gq.manual_seed(SEED + 7)
-        ids = torch.randint(0, N // per_id, (B,), generator=gq, device=dev)
+        lo = N // per_id if a.foreign else 0
+        ids = torch.randint(lo, lo + N // per_id, (B,), generator=gq, device=dev)
         Qd = torch.zeros((B, ld), dtype=torch.float32, device=dev)
         P.project(bank.images(ids, seed=SEED + 99), shift64=gal.shift64, out=Qd)
         qq = gal.quantize_queries(Qd, tier="f6")
