@@ -8,9 +8,13 @@
 // (ncclCommInitAll, one rank per device) and ofr_knn_sharded.
 //
 // ofr_knn_sharded, per device r (its own stream):
-//   1. ofr_knn_f6 (phases 1+2) on shard r: the certified fp6 tier, local top-k with exact fp64
-//      distances and global row indices, and a lower bound of the squared distance of every local
-//      row outside the candidates (-inf when the rank's sieve bucket overflowed);
+//   1. ofr_knn_f6 phase 1 on shard r (the certified fp6 tier's tile pass), then the split merge
+//      (ofr_knn_f6_merge_pruned): stage 1 bounds each query's best-k squared distances from above,
+//      one grouped all-gather of those bounds, kth_bound_kernel takes per query the k-th smallest
+//      over the shards (an upper bound of the global k-th squared distance), stage 2 re-ranks only
+//      the candidates that can fall below it -- local top-k with exact fp64 distances and global
+//      row indices, and a lower bound of the squared distance of every local row outside the
+//      candidates (-inf when the rank's sieve bucket overflowed);
 //   2. pack [B][2k+1] doubles (distances, indices bit-copied, bound) and ncclAllGather them;
 //   3. merge_certify_kernel: the global top-k of the ndev lists per query, certified iff the global
 //      k-th squared distance is below every rank's bound (a -inf bound never certifies);
@@ -134,6 +138,26 @@ __global__ void merge_certify_kernel(const double* in, int P, int64_t B, int k, 
   }
 }
 
+// ub[q] = the k-th smallest of the P x k upper bounds all[p][q][0..k) (ascending per p)
+__global__ void kth_bound_kernel(const double* all, int P, int64_t B, int k, double* ub) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B) return;
+  double best[OFR_MAX_K];
+  for (int j = 0; j < k; ++j) best[j] = __builtin_inf();
+  for (int p = 0; p < P; ++p)
+    for (int j = 0; j < k; ++j) {
+      const double v = all[((int64_t)p * B + q) * k + j];
+      if (!(v < best[k - 1])) break;   // ascending: the rest of this shard's list is no better
+      int t = k - 1;
+      while (t > 0 && best[t - 1] > v) {
+        best[t] = best[t - 1];
+        --t;
+      }
+      best[t] = v;
+    }
+  ub[q] = best[k - 1];
+}
+
 __global__ void gather_rows_kernel(const float* Q, int64_t ldq, const int64_t* rows, int64_t n, float* out) {
   const int64_t r = blockIdx.x;
   if (r >= n) return;
@@ -142,7 +166,7 @@ __global__ void gather_rows_kernel(const float* Q, int64_t ldq, const int64_t* r
 }
 
 struct WsLayout {
-  size_t knn, loc_d, loc_i, bound, send, recv, sub_q, rows, total;
+  size_t knn, loc_d, loc_i, bound, send, recv, sub_q, rows, ubl, ubr, ub, total;
 };
 
 static WsLayout layout(int64_t B, int64_t N, int64_t ldq, int k, int ndev) {
@@ -158,6 +182,9 @@ static WsLayout layout(int64_t B, int64_t N, int64_t ldq, int k, int ndev) {
   w.recv = off; off += up((size_t)ndev * B * (2 * k + 1) * 8);
   w.sub_q = off; off += up((size_t)B * ldq * 4);
   w.rows = off; off += up((size_t)B * 8);
+  w.ubl = off; off += up((size_t)B * k * 8);
+  w.ubr = off; off += up((size_t)ndev * B * k * 8);
+  w.ub = off; off += up((size_t)B * 8);
   w.total = off;
   return w;
 }
@@ -229,7 +256,7 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
   } restore{cur};
   std::vector<comm::WsLayout> L(P);
   const size_t row_bytes = (size_t)(2 * k + 1) * 8;
-  // 1-2: local certified fp6 search on every shard, pack
+  // 1: the fp6 tile pass and the merge's selection + upper bounds on every shard
   for (int p = 0; p < P; ++p) {
     const ofr_knn_shard& s = shards[p];
     hipError_t e = hipSetDevice(c->devices[p]);
@@ -237,13 +264,49 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
     L[p] = comm::layout(B, s.N, s.ldq, k, P);
     OFR_CHECK_ARG(s.workspace && s.workspace_bytes >= L[p].total, "ofr_knn_sharded: workspace too small");
     char* ws = (char*)s.workspace;
+    int rc = ofr_knn_f6(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt, s.gscale, s.aux,
+                        s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, ws + L[p].knn,
+                        ofr_knn_f6_workspace_bytes(B, s.N));
+    if (rc) return rc;
+    rc = ofr_knn_f6_merge_pruned(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
+                                 s.gscale, s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
+                                 (double*)(ws + L[p].ubl), ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N));
+    if (rc) return rc;
+  }
+  // 2: one grouped all-gather of the bounds; per query the k-th smallest = the global bound;
+  //    the pruned exact re-rank on every shard, pack
+  {
+    int rc = comm::nccl_status(r->GroupStart(), "ncclGroupStart");
+    if (rc) return rc;
+    for (int p = 0; p < P; ++p) {
+      char* ws = (char*)shards[p].workspace;
+      rc = comm::nccl_status(r->AllGather(ws + L[p].ubl, ws + L[p].ubr, (size_t)B * k * 8, OFR_NCCL_UINT8,
+                                          c->comms[p], (hipStream_t)shards[p].stream),
+                             "ncclAllGather");
+      if (rc) {
+        r->GroupEnd();
+        return rc;
+      }
+    }
+    rc = comm::nccl_status(r->GroupEnd(), "ncclGroupEnd");
+    if (rc) return rc;
+  }
+  for (int p = 0; p < P; ++p) {
+    const ofr_knn_shard& s = shards[p];
+    hipError_t e = hipSetDevice(c->devices[p]);
+    if (e != hipSuccess) return hip_status(e, "hipSetDevice");
+    char* ws = (char*)s.workspace;
     double* ld_ = (double*)(ws + L[p].loc_d);
     int64_t* li_ = (int64_t*)(ws + L[p].loc_i);
     double* lb_ = (double*)(ws + L[p].bound);
     int* lc_ = s.cert;   // local certificates land in the caller's cert, overwritten by the merge
-    int rc = ofr_knn_f6(s.stream, 3, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt, s.gscale, s.aux,
-                        s.gmax, k, s.index_base, ld_, li_, lc_, lb_, ws + L[p].knn,
-                        ofr_knn_f6_workspace_bytes(B, s.N));
+    double* ub = (double*)(ws + L[p].ub);
+    hipLaunchKernelGGL(comm::kth_bound_kernel, dim3((unsigned)cdiv(B, 128)), dim3(128), 0, (hipStream_t)s.stream,
+                       (const double*)(ws + L[p].ubr), P, B, k, ub);
+    OFR_LAUNCH_CHECK("kth_bound_kernel");
+    int rc = ofr_knn_f6_merge_pruned(s.stream, 2, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
+                                     s.gscale, s.aux, s.gmax, k, s.index_base, ld_, li_, lc_, lb_, ub, ws + L[p].knn,
+                                     ofr_knn_f6_workspace_bytes(B, s.N));
     if (rc) return rc;
     hipLaunchKernelGGL(comm::pack_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, (hipStream_t)s.stream, ld_, li_,
                        lb_, B, k, (double*)(ws + L[p].send));
