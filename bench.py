@@ -189,7 +189,7 @@ def stress_run(P, bank, args, noise, device, N=None):
     ld = max(32, round_up(d, 32))
     n_ids = (N + args.per_id - 1) // args.per_id
     gallery = build_gallery(P, bank, args.per_id, 0, N, N, d, ld, device, noise=noise)
-    for t in FloatGallery.TIER_CHAIN[:-1]:
+    for t in gallery.tier_path("f6")[:-1]:
         gallery._tier_gallery(t)
     gq = torch.Generator(device=device)
     gq.manual_seed(SEED + 7)
@@ -269,7 +269,7 @@ def main():
     use_q8 = args.search in ("f6", "q8")
     tier0 = "f6" if args.search == "f6" else 1
     if use_q8:
-        for t in FloatGallery.TIER_CHAIN[FloatGallery.TIER_CHAIN.index(tier0):-1]:
+        for t in FloatGallery.tier_path(tier0)[:-1]:
             gallery._tier_gallery(t)                              # quantized gallery tiers (once, untimed)
     qq = None
     fallbacks = []

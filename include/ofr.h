@@ -220,6 +220,29 @@ int ofr_knn_f6_merge_pruned(void* stream, int stage, const float* Q, int64_t B, 
                             int k, int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
                             double* ub, void* workspace, size_t workspace_bytes);
 
+/* Two-slice fp6 tier "f6x2" of the certified chain (new: replaces the same loop,
+ * classifier.py:104-119, for the queries the fp6 tier could not certify on crowded
+ * galleries).  x~ = s (v1 + 2^-4 v2): v1 exactly the fp6 tier's codes and scale (a
+ * gallery shares its f6 tiles as the first slice), v2 the e2m3 codes of
+ * 2^4 (x/s - v1) in a second tiled buffer of ofr_f6_tiles_bytes(R, d) bytes.
+ * stats[3] = (s(|v1| + 2^-4 |v2|), ||x - x~||, s 2^-4 |v2|).  tiles1 may be null
+ * (only the second slice and the stats are written).
+ * ofr_knn_f6x2: the ofr_knn_f6 sieve (B > 32 only) over three segments of stages,
+ * [v1 | v1 | v2] . [w1 | w2 | w1] with E8M0 block scale 2^-4 on the second slices,
+ * i.e. the coarse products v1.w1 + 2^-4 (v1.w2 + v2.w1); the certificate adds
+ * 2 t_q T for the dropped 2^-8 v2.w2 term and the fp32 accumulation bound of
+ * 3 nst MFMAs.  Same contract and workspace (ofr_knn_f6_workspace_bytes).        */
+int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles1,
+                           void* tiles2, size_t tiles_bytes, float* scale, double* stats, const float* aux,
+                           double* maxima);
+int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int64_t row0,
+                              void* tiles1, void* tiles2, size_t tiles_bytes, float* scale, double* stats);
+int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt, const void* Qt2,
+                 const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
+                 const void* Gt, const void* Gt2, const float* gscale, const float* aux, const double* gmax, int k,
+                 int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
+                 size_t workspace_bytes);
+
 /* Merge P sorted (distance, index) lists per query into the best k:
  * in_d/in_i [B][P*kin] (list p at columns [p*kin, (p+1)*kin)), ascending by
  * (distance, index); out [B][k].  Used after the RCCL all-gather of per-rank

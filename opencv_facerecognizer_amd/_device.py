@@ -240,10 +240,13 @@ class FloatGallery:
         self.N, self.G, self.aux = N1, self._Gbuf[:N1], self._auxbuf[:N1]
         if self._twin is not None:                 # Cosine: the unit-row twin grows with it
             self._twin.append(self.unit_rows(self.G[N0:N1])[:, :self.d])
-        for tier, g in (self.q8 or {}).items():
+        for tier, g in (self.q8 or {}).items():     # "f6" before "f6x2": insertion order
             if tier == "f6":
                 call("ofr_f6_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, ptr(g["Gs"]),
                      g["Gs"].numel(), ptr(g["scale"]), ptr(g["stats"]))
+            elif tier == "f6x2":                       # the first slice is the f6 tier's, extended above
+                call("ofr_f6x2_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, None,
+                     ptr(g["Gs2"]), g["Gs2"].numel(), ptr(g["scale"]), ptr(g["stats"]))
             else:
                 call("ofr_q8_quantize_rows", stream(), tier, ptr(self.G[N0:]), n, self.d, self.ld, ptr(g["Gs"][N0:]),
                      g["ld"], ptr(g["scale"][N0:]), ptr(g["stats"][N0:]), None, None)
@@ -252,12 +255,23 @@ class FloatGallery:
 
     # -- certified quantized coarse passes (Euclidean, B > 32) -------------------------------------
     # Tier "f6": one fp6 (e2m3) slice per row with an fp32 row scale (x~ = s v), fp6 MFMA at twice
-    # the int8 rate.  Tier 1, for the queries tier "f6" could not certify: one int8 slice
-    # (x~ = s x1).  Tier 2: two int8 slices (x~ = s (x1 + x2/2^7)).  Last: the fp32 path.  Every
-    # tier ends in the exact fp64 re-rank; the quantized tiers only answer where the certificate
-    # proves the result exact.  OFR_SEARCH picks the first tier: auto (= f6), q8
-    # (tier 1), q8x2 (tier 2) or fp32.
-    TIER_CHAIN = ("f6", 1, 2, "fp32")
+    # the int8 rate.  Tier "f6x2", for the queries tier "f6" could not certify (crowded galleries):
+    # two fp6 slices (x~ = s (v1 + v2/2^4), residual ~1/20 of f6's) in three fp6 MFMA segments.
+    # Tier 1: one int8 slice (x~ = s x1; the first tier of OFR_SEARCH=q8).  Tier 2: two int8 slices
+    # (x~ = s (x1 + x2/2^7)).  Last: the fp32 path.  Every tier ends in the exact fp64 re-rank; the
+    # quantized tiers only answer where the certificate proves the result exact.
+    # OFR_SEARCH picks the first tier: auto (= f6), q8 (tier 1), q8x2 (tier 2) or fp32.  NEXT: the
+    # stage after each tier (f6x2 is finer than int8 x1, so its failures go on to int8 x2).
+    TIER_CHAIN = ("f6", "f6x2", 1, 2, "fp32")
+    NEXT = {"f6": "f6x2", "f6x2": 2, 1: 2, 2: "fp32"}
+
+    @classmethod
+    def tier_path(cls, first):
+        """The stages a query starting at tier `first` can pass through, in order (ends with fp32)."""
+        path = [first]
+        while path[-1] != "fp32":
+            path.append(cls.NEXT[path[-1]])
+        return tuple(path)
 
     # -- certified Cosine search: Euclidean tiers on the unit rows, then the reference formula ----------
     def unit_rows(self, X, shift64=None, out=None):
@@ -318,7 +332,7 @@ class FloatGallery:
         """Stage after `tier` for `nrows` uncertified queries.  The int8 tiers run 256-query tiles
         over 10-30 GB of slices: for <= 32 queries the exact fp32 streaming pass is as cheap, so
         small sets go straight to it (and a small-batch workload never builds the int8 slices)."""
-        nxt = self.TIER_CHAIN[self.TIER_CHAIN.index(tier) + 1]
+        nxt = self.NEXT[tier]
         return "fp32" if nxt != "fp32" and nrows <= SMALL_BATCH else nxt
 
     @staticmethod
@@ -339,18 +353,26 @@ class FloatGallery:
             gs = torch.empty(cap, dtype=torch.float32, device=dev_)
             st = torch.empty((cap, 3), dtype=torch.float64, device=dev_)
             gmax = torch.empty(4, dtype=torch.float64, device=dev_)
+            extra = {}
             if tier == "f6":
                 nbytes = _lib.load().ofr_f6_tiles_bytes(cap, self.d)
                 Gs = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
                 call("ofr_f6_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, ptr(Gs), nbytes,
                      ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
                 ld = 0
+            elif tier == "f6x2":                  # first slice = the f6 tier's tiles (same codes and scale)
+                Gs = self._tier_gallery("f6")["Gs"]
+                nbytes = _lib.load().ofr_f6_tiles_bytes(cap, self.d)
+                Gs2 = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
+                call("ofr_f6x2_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, None, ptr(Gs2),
+                     nbytes, ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
+                ld, extra = 0, dict(Gs2=Gs2)
             else:
                 ld = self._q8_ld(self.d, tier)
                 Gs = torch.empty((cap, ld), dtype=torch.int8, device=dev_)
                 call("ofr_q8_quantize_rows", stream(), tier, ptr(self.G), self.N, self.d, self.ld, ptr(Gs), ld,
                      ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
-            self.q8[tier] = dict(Gs=Gs, scale=gs, stats=st, gmax=gmax, ld=ld)
+            self.q8[tier] = dict(Gs=Gs, scale=gs, stats=st, gmax=gmax, ld=ld, **extra)
         return self.q8[tier]
 
     def quantize_queries(self, Qd, out=None, tier="f6"):
@@ -358,16 +380,23 @@ class FloatGallery:
         B = Qd.shape[0]
         dev_ = Qd.device
         if out is None or out["B"] != B or out["tier"] != tier:
-            if tier == "f6":
-                Qs = torch.empty(max(1, _lib.load().ofr_f6_tiles_bytes(B, self.d)), dtype=torch.uint8, device=dev_)
+            extra = {}
+            if tier in ("f6", "f6x2"):
+                nb = max(1, _lib.load().ofr_f6_tiles_bytes(B, self.d))
+                Qs = torch.empty(nb, dtype=torch.uint8, device=dev_)
+                if tier == "f6x2":
+                    extra = dict(Qs2=torch.empty(nb, dtype=torch.uint8, device=dev_))
             else:
                 Qs = torch.empty((B, self._q8_ld(self.d, tier)), dtype=torch.int8, device=dev_)
             out = dict(Qs=Qs, scale=torch.empty(B, dtype=torch.float32, device=dev_),
                        stats=torch.empty((B, 3), dtype=torch.float64, device=dev_),
                        cert=torch.empty(B, dtype=torch.int32, device=dev_),
-                       bound=torch.empty(B, dtype=torch.float64, device=dev_), tier=tier, B=B)
+                       bound=torch.empty(B, dtype=torch.float64, device=dev_), tier=tier, B=B, **extra)
         if tier == "f6":
             call("ofr_f6_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
+                 out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None)
+        elif tier == "f6x2":
+            call("ofr_f6x2_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]), ptr(out["Qs2"]),
                  out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None)
         else:
             call("ofr_q8_quantize_rows", stream(), tier, ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
@@ -397,9 +426,15 @@ class FloatGallery:
             out = (torch.empty((B, k), dtype=torch.float64, device=Qd.device),
                    torch.empty((B, k), dtype=torch.int64, device=Qd.device))
         lib = _lib.load()
-        nbytes = lib.ofr_knn_f6_workspace_bytes(B, self.N) if tier == "f6" else lib.ofr_knn_q8_workspace_bytes(B, self.N)
+        nbytes = (lib.ofr_knn_f6_workspace_bytes(B, self.N) if tier in ("f6", "f6x2")
+                  else lib.ofr_knn_q8_workspace_bytes(B, self.N))
         ws = (workspace or self.ws).get(nbytes, Qd.device)
-        if tier == "f6":
+        if tier == "f6x2":
+            call("ofr_knn_f6x2", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["Qs2"]),
+                 ptr(qq["scale"]), ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]),
+                 ptr(g["Gs2"]), ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]),
+                 ptr(out[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(ws), ws.numel())
+        elif tier == "f6":
             call("ofr_knn_f6", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
                  ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),
                  ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
@@ -441,12 +476,11 @@ class FloatGallery:
         receives (tier, queries, ms) per stage that ran (HIP events on the current stream)."""
         bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
         counts = [int(bad.numel())]
-        chain = self.TIER_CHAIN
         pending = {}                    # tier -> indices into the original batch waiting for it
         self.last_skipped = {}
         self._route(qq["tier"], bad, Qd, qq["stats"].index_select(0, bad), qq["bound"].index_select(0, bad), out, k,
                     pending)
-        for tier in chain[chain.index(qq["tier"]) + 1:]:
+        for tier in self.tier_path(qq["tier"])[1:]:
             rows = pending.pop(tier, None)
             if rows is None or not rows.numel():
                 continue
@@ -485,7 +519,8 @@ class FloatGallery:
         gm = self._tier_gallery(tier)["gmax"]
         A, E, T, aux = gm[0], gm[1], gm[2], gm[3]
         a, e, t = stats[:, 0], stats[:, 1], stats[:, 2]
-        gamma = (2 * -(-self.d // 128) + 64) * 2.0 ** -23 if tier == "f6" else 0.0
+        nseg = {"f6": 1, "f6x2": 3}.get(tier, 0)
+        gamma = (2 * nseg * -(-self.d // 128) + 64) * 2.0 ** -23 if nseg else 0.0
         return 2.0 * (a * E + e * A + e * E + t * T) + 2.0 ** -20 * (aux + 2.0 * a * A) + 2.0 * gamma * a * A
 
     def _route(self, tier, rows, Qd, stats, bound, out, k, pending):
@@ -497,9 +532,8 @@ class FloatGallery:
         every stage still certifies or hands on, so the results do not depend on it."""
         if not rows.numel():
             return
-        chain = self.TIER_CHAIN
-        nxt = chain[chain.index(tier) + 1]
-        after = chain[chain.index(nxt) + 1] if nxt != "fp32" else None
+        nxt = self.NEXT[tier]
+        after = self.NEXT.get(nxt)
         if after is None or after == "fp32" or int(rows.numel()) <= SMALL_BATCH:
             self._queue(pending, nxt, rows)
             return

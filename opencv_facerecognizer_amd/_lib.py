@@ -67,6 +67,10 @@ SIGNATURES = {
     "ofr_knn_f6_merge_pruned": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp, c_sz]),
+    "ofr_f6x2_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp]),
+    "ofr_f6x2_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp]),
+    "ofr_knn_f6x2": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
+                             c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz]),
     "ofr_topk_merge": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp]),
     "ofr_elbp_codes": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                c_vp]),

@@ -77,6 +77,41 @@ __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// ---- passes over several segments of stages (the two-slice tier f6x2) -----------------------
+// NSEG = 1: stages [0, nst) of the gallery tiles G against the query tiles Q (tier f6).
+// NSEG = 3: stages [0, 3 nst) = the segments [x1 | x1 | x2] . [y1 | y2 | y1] of the two-slice rows
+// x~ = s (x1 + 2^-4 x2): segment 1 runs the MFMA with query block scale 2^-4, segment 2 with gallery
+// block scale 2^-4 (E8M0 operands), so one accumulator holds x1.y1 + 2^-4 (x1.y2 + x2.y1) exactly
+// up to the fp32 accumulation.  G2 / Q2: the second-slice tiles (same layout).
+constexpr int SCALE_ONE = 0x7f7f7f7f;    // E8M0 2^0 in every byte
+constexpr int SCALE_X2 = 0x7b7b7b7b;     // E8M0 2^-4
+constexpr int X2_SHIFT = 4;              // second slice weight 2^-X2_SHIFT
+
+template <int NSEG>
+__device__ __forceinline__ void seg_src(int kt, int nst, const char* G, const char* G2, const char* Q, const char* Q2,
+                                        const char*& g, const char*& q, int& ks) {
+  if constexpr (NSEG == 1) {
+    g = G; q = Q; ks = kt;
+  } else {
+    static_assert(NSEG == 3, "segments");
+    const int sg = kt >= 2 * nst ? 2 : (kt >= nst ? 1 : 0);
+    ks = kt - sg * nst;
+    g = sg == 2 ? G2 : G;
+    q = sg == 1 ? Q2 : Q;
+  }
+}
+
+// E8M0 block scales of stage kt's MFMAs (gallery operand A, query operand B)
+template <int NSEG>
+__device__ __forceinline__ void seg_scales(int kt, int nst, int& sa, int& sb) {
+  if constexpr (NSEG == 1) {
+    sa = SCALE_ONE; sb = SCALE_ONE;
+  } else {
+    sa = kt >= 2 * nst ? SCALE_X2 : SCALE_ONE;
+    sb = (kt >= nst && kt < 2 * nst) ? SCALE_X2 : SCALE_ONE;
+  }
+}
+
 __device__ __forceinline__ i32x8 frag(const char* blk, int j, int h, int row) {
   const char* sb = blk + (2 * j + h) * 6144;
   // opaque part1 address: keeps the compiler from pairing part1 reads of different
@@ -160,9 +195,11 @@ struct Engine {
   // boundary, which exposes the step-0 reads after every barrier: tools/f6_probe.hip).
   // Fragments double-buffered by j; 3 LDS stages (kt+1 read next, kt+2 and kt+3 in flight).
   // MODE (probes): 1 = no k-loop DMA, 2 / 16 = no gallery / query block in the DMA.
-  template <int MODE>
+  // NSEG: segments of nst stages each (seg_src); G2 / Q2 only for NSEG = 3
+  template <int MODE, int NSEG = 1>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
-                                                  int nst, f32x16 (&acc)[4][CT]) {
+                                                  int nst, f32x16 (&acc)[4][CT], const char* G2 = nullptr,
+                                                  const char* Q2 = nullptr) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
 #pragma unroll
@@ -172,9 +209,15 @@ struct Engine {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto issue = [&](int kt) { dma<MODE & 18>(G, gp, Q, qp, nst, kt, smem + (kt % NST) * STAGE); };
+    auto issue = [&](int kt) {
+      const char *g, *q;
+      int ks;
+      seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
+      dma<MODE & 18>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+    };
     // branch-free: a stage past the end re-loads the last one onto itself (same bytes)
-    const int last = nst - 1;
+    const int last = NSEG * nst - 1;
+    int sa = SCALE_ONE, sb = SCALE_ONE;
     static_assert(NST == 3, "hand-off below assumes 3 stages");
 #pragma unroll
     for (int s = 0; s < NST; ++s) issue(s < last ? s : last);
@@ -192,7 +235,7 @@ struct Engine {
 #pragma unroll
         for (int c = 0; c < CT; ++c)
           acc[i][c] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ga[j][i], qb[j][c], acc[i][c], 2, 2, 0,
-                                                                      0x7f7f7f7f, 0, 0x7f7f7f7f);
+                                                                      sa, 0, sb);
     };
 
     if constexpr (MODE == 1) wait_vm<0>();
@@ -200,6 +243,7 @@ struct Engine {
     barrier();
     frags(smem, 0);
     for (int kt = 0; kt < last; ++kt) {
+      seg_scales<NSEG>(kt, nst, sa, sb);
       frags(smem + (kt % NST) * STAGE, 1);
       mfmas(0);
       interleave();
@@ -215,6 +259,7 @@ struct Engine {
       interleave();
       __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
     }
+    seg_scales<NSEG>(last, nst, sa, sb);
     frags(smem + (last % NST) * STAGE, 1);
     mfmas(0);
     interleave();
@@ -249,10 +294,11 @@ struct Engine16 {
     f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
     return f;
   }
-  static __device__ __forceinline__ f32x4 mfma(const i32x6& a, const i32x6& b, const f32x4& c) {
+  static __device__ __forceinline__ f32x4 mfma(const i32x6& a, const i32x6& b, const f32x4& c, int sa = SCALE_ONE,
+                                               int sb = SCALE_ONE) {
     const i32x8 a8 = __builtin_shufflevector(a, a, 0, 1, 2, 3, 4, 5, -1, -1);
     const i32x8 b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, 4, 5, -1, -1);
-    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 2, 2, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 2, 2, 0, sa, 0, sb);
   }
   // probe only (MODE 256): the accumulators pinned to AGPRs through an asm MFMA (the compiler
   // cannot see its latency: the probe drains the pipe with s_nops before reading them)
@@ -264,9 +310,11 @@ struct Engine16 {
   // MODE (probes): 1 = no k-loop DMA; 64 = DMA issued but never waited for (wrong results: isolates
   // the cost of waiting for the DMA from that of moving its bytes); 128 = the k-loop's stage loads
   // land in VGPRs, not LDS (wrong results: the feed's bytes without its LDS writes)
-  template <int MODE>
+  template <int MODE, int NSEG = 1>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
-                                                  int nst, f32x4 (&acc)[NA][NB]) {
+                                                  int nst, f32x4 (&acc)[NA][NB], const char* G2 = nullptr,
+                                                  const char* Q2 = nullptr) {
+    static_assert(NSEG == 1 || (MODE & 256) == 0, "the AGPR probe runs one segment");
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr = wave / WQ, wc = wave % WQ, r16 = lane & 15;
 #pragma unroll
@@ -274,19 +322,28 @@ struct Engine16 {
 #pragma unroll
       for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     i32x4 sink = {0, 0, 0, 0};
-    auto issue = [&](int kt) { Engine<8>::dma<0>(G, gp, Q, qp, nst, kt, smem + (kt % NST) * STAGE); };
-    auto issue_k = [&](int kt) {
-      Engine<8>::dma<MODE & 128>(G, gp, Q, qp, nst, kt, smem + (kt % NST) * STAGE, &sink);
+    auto issue = [&](int kt) {
+      const char *g, *q;
+      int ks;
+      seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
+      Engine<8>::dma<0>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
     };
-    const int last = nst - 1;
+    auto issue_k = [&](int kt) {
+      const char *g, *q;
+      int ks;
+      seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
+      Engine<8>::dma<MODE & 128>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE, &sink);
+    };
+    const int last = NSEG * nst - 1;
 #pragma unroll
     for (int s = 0; s < NST; ++s) issue(s < last ? s : last);
     i32x6 a[NA], b[NB];
     int sc = 0x7f7f7f7f;
     if constexpr ((MODE & 256) != 0) asm volatile("" : "+v"(sc));
+    int sa = SCALE_ONE, sb = SCALE_ONE;
     auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) {
       if constexpr ((MODE & 256) != 0) mfma_agpr(x, y, c, sc);
-      else c = mfma(x, y, c);
+      else c = mfma(x, y, c, sa, sb);
     };
     auto readA = [&](const char* st, int i) { a[i] = frag16(st, wr * 128 + i * 16 + r16); };
     auto readB = [&](const char* st, int c) { b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16); };
@@ -301,6 +358,7 @@ struct Engine16 {
     // MFMA is issued (A-major: A[i] after row i's 4 MFMAs, B[c] after row 7's MFMA c), so the
     // fragments need no second register set (acc 128 + fragments 72 registers).
     for (int kt = 0; kt < last; ++kt) {
+      seg_scales<NSEG>(kt, nst, sa, sb);
       if constexpr ((MODE & 1) != 0) wait_vm<0>();
       else if constexpr ((MODE & 64) == 0) wait_vm<IPW>();   // stage kt+1 landed; kt+2 may be in flight
       barrier();                 // every wave has read stage kt: its buffer takes stage kt+3
@@ -337,6 +395,7 @@ struct Engine16 {
       }
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
+    seg_scales<NSEG>(last, nst, sa, sb);
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll

@@ -63,6 +63,9 @@ struct TileArgs {
   int* count;              // [B] rows kept so far
   Cand* bucket;            // [B][cap] the kept rows (truncated coarse score, row)
   int64_t cap;
+  // two-slice fp6 tier (NSEG = 3 kernels): the second-slice tiles; nk = 3 x the stages of one slice
+  const int8_t* G2;
+  const int8_t* Q2;
 };
 
 // ---- keys of the tile epilogue --------------------------------------------------------
@@ -327,7 +330,7 @@ __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
 // (f6t::Engine).  MODE 0: tile lists (tile t = gallery panel t * gstride, the sieve's sample
 // pass); 8: the sieve.  Probe bits: 1 / 2 / 16 = no k-loop DMA / gallery DMA / query DMA,
 // 4 = no epilogue.
-template <int NW, int MODE>
+template <int NW, int MODE, int NSEG = 1>
 __global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
   using E = f6t::Engine<NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -356,8 +359,9 @@ __global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
     }
   }
   f6t::f32x16 acc[4][CT];
-  E::template mainloop<MODE & 19>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q),
-                                 qt, p.nk, acc);
+  E::template mainloop<MODE & 19, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp,
+                                       reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG, acc,
+                                       reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
   if constexpr ((MODE & 4) != 0) {   // probe: no epilogue (the accumulators kept alive)
     float s = 0.f;
 #pragma unroll
@@ -423,7 +427,7 @@ __device__ __forceinline__ void sieve_epilogue16(char* smem, const TileArgs& p, 
 }
 
 // fp6 sieve pass on the 16x16x128 engine.  MODE probe bits: 1 = no k-loop DMA, 4 = no epilogue.
-template <int MODE>
+template <int MODE, int NSEG = 1>
 __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   using E = f6t::Engine16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -433,8 +437,9 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
   f6t::f32x4 acc[8][4];
-  E::mainloop<MODE & 449>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt, p.nk,
-                          acc);
+  E::mainloop<MODE & 449, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+                                p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
+                                reinterpret_cast<const char*>(p.Q2));
   // sieve operands after the main loop (the 16x16 engine needs every register in it)
   float ga = __builtin_inff(), gs = 0.f, sq2[4], th[4];
   if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
@@ -960,10 +965,18 @@ __device__ __forceinline__ uint32_t e2m3_code(double r, double& q) {
   return (r < 0 && v != 0.0) ? (code | 32u) : code;
 }
 
+// X2: also the second slice of the two-slice tier f6x2, x~ = s (v1 + 2^-4 v2) with v2 = e2m3 of
+// 2^4 (x/s - v1) (|x/s - v1| <= 1/4, so |2^4 (x/s - v1)| <= 4 < 7.5), written to tiles2 in the same
+// layout; tiles (the first slice) may then be null -- a gallery's f6 tier already holds it, the same
+// bytes and scale.  Stats of f6x2: a = s (|v1| + 2^-4 |v2|) >= |x~| (it also bounds the sum of
+// |products| the fp32 accumulation error is proportional to), e = |x - x~|, t = s 2^-4 |v2| (the
+// dropped 2^-8 x2.y2 term is at most t_q t_g).
+template <bool X2>
 __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_t ldx, int64_t d, int64_t nst,
-                                                          int64_t row0, char* tiles, float* scale, double* stats) {
+                                                          int64_t row0, char* tiles, float* scale, double* stats,
+                                                          char* tiles2) {
   __shared__ float redf[4];
-  __shared__ double red[4][2];
+  __shared__ double red[4][3];
   const int64_t row = row0 + blockIdx.x;   // destination row (X row blockIdx.x)
   const float* x = X + (int64_t)blockIdx.x * ldx;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -983,12 +996,12 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
   const double inv_sd = 1.0 / sd;   // x * (1/s) instead of x / s: any rounding of x/s is fine (the
                                     // stats below are of the values actually stored)
   const bool vec4 = ((ldx & 3) == 0) && (((uintptr_t)X & 15) == 0);
-  double sa = 0, se = 0;
+  double sa = 0, se = 0, s2 = 0;
   const int64_t ngroups = nst * 4;
-  char* pbase = tiles + (row >> 8) * nst * (int64_t)f6t::PANEL;
+  const int64_t poff = (row >> 8) * nst * (int64_t)f6t::PANEL;
   const int rl = (int)(row & 255);
   for (int64_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
-    uint32_t w[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t w[6] = {0, 0, 0, 0, 0, 0}, w2[6] = {0, 0, 0, 0, 0, 0};
     float xg[32];
     if (vec4 && g * 32 + 32 <= d) {
 #pragma unroll
@@ -1007,37 +1020,63 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
         const double xv = (double)xg[e];
         double qv;
         const uint32_t c = e2m3_code(xv * inv_sd, qv);
-        const double xt = sd * qv;   // exact: 24-bit s times a 4-bit significand
-        sa += xt * xt;
-        se += (xv - xt) * (xv - xt);
+        double xt = sd * qv;   // exact: 24-bit s times a 4-bit significand
         const int bit = 6 * e;
+        if constexpr (X2) {
+          double qv2;
+          const uint32_t c2 = e2m3_code((xv - xt) * inv_sd * 16.0, qv2);
+          sa += qv * qv;
+          s2 += qv2 * qv2;
+          xt += sd * qv2 * 0.0625;   // exact (a 28-bit significand at most)
+          w2[bit >> 5] |= c2 << (bit & 31);
+          if ((bit & 31) > 26) w2[(bit >> 5) + 1] |= c2 >> (32 - (bit & 31));
+        } else {
+          sa += xt * xt;
+        }
+        se += (xv - xt) * (xv - xt);
         w[bit >> 5] |= c << (bit & 31);
         if ((bit & 31) > 26) w[(bit >> 5) + 1] |= c >> (32 - (bit & 31));
       }
     }
     const int64_t st = g >> 2;
     const int jh = (int)(g & 3);   // 2 j + h
-    char* sb = pbase + st * f6t::PANEL + jh * 6144;
-    *reinterpret_cast<uint4*>(sb + rl * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-    *reinterpret_cast<uint2*>(sb + 4096 + f6t::p1_slot(jh, rl) * 8) = make_uint2(w[4], w[5]);
+    const int64_t off = poff + st * f6t::PANEL + jh * 6144;
+    if (tiles) {
+      *reinterpret_cast<uint4*>(tiles + off + rl * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+      *reinterpret_cast<uint2*>(tiles + off + 4096 + f6t::p1_slot(jh, rl) * 8) = make_uint2(w[4], w[5]);
+    }
+    if constexpr (X2) {
+      *reinterpret_cast<uint4*>(tiles2 + off + rl * 16) = make_uint4(w2[0], w2[1], w2[2], w2[3]);
+      *reinterpret_cast<uint2*>(tiles2 + off + 4096 + f6t::p1_slot(jh, rl) * 8) = make_uint2(w2[4], w2[5]);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     sa += __shfl_xor(sa, o);
     se += __shfl_xor(se, o);
+    s2 += __shfl_xor(s2, o);
   }
   if (lane == 0) {
     red[wave][0] = sa;
     red[wave][1] = se;
+    red[wave][2] = s2;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const double A = red[0][0] + red[1][0] + red[2][0] + red[3][0];
     const double E = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    const double S2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
     scale[row] = s;
-    stats[row * 3 + 0] = sqrt(A) * (1.0 + 1e-12);
-    stats[row * 3 + 1] = sqrt(E) * (1.0 + 1e-12);
-    stats[row * 3 + 2] = 0.0;
+    // norms rounded up a hair so that fp64 summation error never shrinks the bound
+    if constexpr (X2) {
+      stats[row * 3 + 0] = sd * (sqrt(A) + 0.0625 * sqrt(S2)) * (1.0 + 1e-12);
+      stats[row * 3 + 1] = sqrt(E) * (1.0 + 1e-12);
+      stats[row * 3 + 2] = sd * 0.0625 * sqrt(S2) * (1.0 + 1e-12);
+    } else {
+      stats[row * 3 + 0] = sqrt(A) * (1.0 + 1e-12);
+      stats[row * 3 + 1] = sqrt(E) * (1.0 + 1e-12);
+      stats[row * 3 + 2] = 0.0;
+    }
   }
 }
 
@@ -1181,13 +1220,39 @@ extern "C" int ofr_f6_quantize_rows_at(void* stream, const float* X, int64_t R, 
   OFR_CHECK_ARG((uintptr_t)tiles % 16 == 0, "ofr_f6_quantize_rows_at: tiles must be 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
   const int64_t nst = f6t::stages(d);
-  hipLaunchKernelGGL(q8s::quantize_f6_kernel, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
-                     (char*)tiles, scale, stats);
+  hipLaunchKernelGGL(q8s::quantize_f6_kernel<false>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
+                     (char*)tiles, scale, stats, nullptr);
   OFR_LAUNCH_CHECK("f6 quantize_kernel");
   const int64_t end = row0 + R;
   if (end % 256) {
     hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)tiles, end, nst);
     OFR_LAUNCH_CHECK("f6 zero_tail");
+  }
+  return OFR_OK;
+}
+
+extern "C" int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx,
+                                         int64_t row0, void* tiles1, void* tiles2, size_t tiles_bytes, float* scale,
+                                         double* stats) {
+  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d && row0 >= 0, "ofr_f6x2_quantize_rows_at: bad sizes");
+  if (R == 0) return OFR_OK;
+  OFR_CHECK_ARG(X && tiles2 && scale && stats, "ofr_f6x2_quantize_rows_at: null pointer");
+  OFR_CHECK_ARG(row0 + R < 0x7fffffffLL, "ofr_f6x2_quantize_rows_at: too many rows");
+  OFR_CHECK_ARG(tiles_bytes >= ofr_f6_tiles_bytes(row0 + R, d), "ofr_f6x2_quantize_rows_at: tile buffer too small");
+  OFR_CHECK_ARG(((uintptr_t)tiles1 | (uintptr_t)tiles2) % 16 == 0,
+                "ofr_f6x2_quantize_rows_at: tiles must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nst = f6t::stages(d);
+  hipLaunchKernelGGL(q8s::quantize_f6_kernel<true>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
+                     (char*)tiles1, scale, stats, (char*)tiles2);
+  OFR_LAUNCH_CHECK("f6x2 quantize_kernel");
+  const int64_t end = row0 + R;
+  if (end % 256) {
+    for (void* t : {tiles1, tiles2}) {
+      if (!t) continue;
+      hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)t, end, nst);
+      OFR_LAUNCH_CHECK("f6x2 zero_tail");
+    }
   }
   return OFR_OK;
 }
@@ -1203,6 +1268,14 @@ extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int
                                     size_t tiles_bytes, float* scale, double* stats, const float* aux,
                                     double* maxima) {
   const int rc = ofr_f6_quantize_rows_at(stream, X, R, d, ldx, 0, tiles, tiles_bytes, scale, stats);
+  if (rc || R == 0 || !maxima) return rc;
+  return ofr_q8_maxima(stream, stats, aux, R, maxima);
+}
+
+extern "C" int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles1,
+                                      void* tiles2, size_t tiles_bytes, float* scale, double* stats, const float* aux,
+                                      double* maxima) {
+  const int rc = ofr_f6x2_quantize_rows_at(stream, X, R, d, ldx, 0, tiles1, tiles2, tiles_bytes, scale, stats);
   if (rc || R == 0 || !maxima) return rc;
   return ofr_q8_maxima(stream, stats, aux, R, maxima);
 }
@@ -1269,7 +1342,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                        const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
-                       size_t workspace_bytes, int merge_mode, double* ub);
+                       size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2 = nullptr,
+                       const void* Gt2 = nullptr);
 
 extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                           const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
@@ -1279,6 +1353,18 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
   OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_f6: phases must be 1 (tiles), 2 (merge) or 3");
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
                      out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr);
+}
+
+extern "C" int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                            const void* Qt2, const float* qscale, const double* qstats, const float* G, int64_t N,
+                            int64_t ldg, int64_t d, const void* Gt, const void* Gt2, const float* gscale,
+                            const float* aux, const double* gmax, int k, int64_t index_base, double* out_d,
+                            int64_t* out_i, int* cert, double* bound, void* workspace, size_t workspace_bytes) {
+  OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_f6x2: phases must be 1 (tiles), 2 (merge) or 3");
+  OFR_CHECK_ARG(Qt2 && Gt2, "ofr_knn_f6x2: null second-slice tiles");
+  if (B >= 1 && B <= 32) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6x2: needs more than 32 queries (the sieve pass)");
+  return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, Qt2, Gt2);
 }
 
 extern "C" int ofr_knn_f6_merge_pruned(void* stream, int stage, const float* Q, int64_t B, int64_t ldq,
@@ -1297,15 +1383,17 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                        const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
-                       size_t workspace_bytes, int merge_mode, double* ub) {
+                       size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2, const void* Gt2) {
+  const bool two = Gt2 != nullptr;   // the two-slice tier f6x2: three segments of stages (f6t::seg_src)
   OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_f6: bad sizes (empty galleries use ofr_knn_f32)");
   if (k < 1 || k > q8s::KC) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6: k must be in [1, 16]");
   if (B == 0) return OFR_OK;
   OFR_CHECK_ARG(ldq >= d && ldg >= d, "ofr_knn_f6: bad leading dimensions");
   OFR_CHECK_ARG(Q && Qt && qscale && qstats && G && Gt && gscale && aux && gmax && workspace,
                 "ofr_knn_f6: null pointer");
-  OFR_CHECK_ARG(((uintptr_t)Qt | (uintptr_t)Gt | (uintptr_t)workspace) % 16 == 0,
+  OFR_CHECK_ARG(((uintptr_t)Qt | (uintptr_t)Gt | (uintptr_t)Qt2 | (uintptr_t)Gt2 | (uintptr_t)workspace) % 16 == 0,
                 "ofr_knn_f6: tiles and workspace must be 16-byte aligned");
+  OFR_CHECK_ARG(!two || B > 32, "ofr_knn_f6x2: needs more than 32 queries");
   // the sieve's per-query count reaches at most cap + 1 + N (saturating overflow + one per row)
   OFR_CHECK_ARG(N < 0x7fffffffLL - 2 * q8s::SIEVE_CAP, "ofr_knn_f6: N too large for one shard");
   OFR_CHECK_ARG(workspace_bytes >= ofr_knn_f6_workspace_bytes(B, N), "ofr_knn_f6: workspace too small");
@@ -1314,7 +1402,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   q8s::TileArgs a{};
   a.G = (const int8_t*)Gt; a.N = N; a.ld = 0; a.gscale = gscale; a.aux = aux;
   a.Q = (const int8_t*)Qt; a.B = B; a.qscale = qscale;
-  a.nk = (int)f6t::stages(d);
+  a.nk = (int)f6t::stages(d) * (two ? 3 : 1);
+  a.G2 = (const int8_t*)Gt2; a.Q2 = (const int8_t*)Qt2;
   a.cand = reinterpret_cast<Cand*>(workspace);
   a.ntq = f6t::panels(B);
   a.ntg = f6t::panels(N);
@@ -1334,7 +1423,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       static bool attr_done = false;
       if (!attr_done) {
         for (const void* f : {(const void*)q8s::tile_kernel_f6<F6_NW, 0>, (const void*)q8s::tile_kernel_f6<F6_NW, 8>,
-                              (const void*)q8s::tile_kernel_f6s<0>}) {
+                              (const void*)q8s::tile_kernel_f6s<0>, (const void*)q8s::tile_kernel_f6<F6_NW, 0, 3>,
+                              (const void*)q8s::tile_kernel_f6<F6_NW, 8, 3>, (const void*)q8s::tile_kernel_f6s<0, 3>}) {
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
         }
@@ -1346,8 +1436,12 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       s.ntg = cdiv(a.ntg, s.gstride);
       s.gg = s.ntg < q8s::GROUP_G ? s.ntg : q8s::GROUP_G;
       s.cand = reinterpret_cast<Cand*>(wsb + w.lists);
-      hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64), f6t::LDS,
-                         st, s);
+      if (two)
+        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0, 3>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
+                           f6t::LDS, st, s);
+      else
+        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
+                           f6t::LDS, st, s);
       OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
       hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)B), dim3(256), 0, st, s.cand, s.ntg, theta,
                          count);
@@ -1356,8 +1450,14 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       a.count = count;
       a.bucket = bucket;
       a.cap = q8s::SIEVE_CAP;
-      if (f6_shape() == 16)
+      if (f6_shape() == 16 && two)
+        hipLaunchKernelGGL((q8s::tile_kernel_f6s<0, 3>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
+                           f6t::LDS, st, a);
+      else if (f6_shape() == 16)
         hipLaunchKernelGGL((q8s::tile_kernel_f6s<0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
+                           f6t::LDS, st, a);
+      else if (two)
+        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 8, 3>), dim3((unsigned)(a.ntq * a.ntg)), dim3(F6_NW * 64),
                            f6t::LDS, st, a);
       else
         hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 8>), dim3((unsigned)(a.ntq * a.ntg)), dim3(F6_NW * 64),

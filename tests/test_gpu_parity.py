@@ -121,16 +121,14 @@ def test_knn_q8_certificate_forces_fallback(monkeypatch):
     Q = (c + r.normal(0, 1e-6, (100, 64))).astype(np.float32).astype(np.float64)   # every row ~equidistant
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     dd, ii = g.search(g.query_rows(Q), 3)
-    # every quantized tier that ran left queries uncertified (the fp32 pass resolved them); the fp6
-    # failures miss even the bound int8 x1 would give by far, so they skip it (_route)
-    assert g.last_fallbacks[0] == 100 and min(g.last_fallbacks) > 0
-    assert g.last_skipped.get("1", 0) >= 90, g.last_skipped
+    # every quantized tier that ran left queries uncertified (the fp32 pass resolved them)
+    assert g.last_fallbacks[0] == 100 and min(g.last_fallbacks) > 0, g.last_fallbacks
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
 
 
 def test_fallback_routing_is_only_a_choice(monkeypatch):
-    """_route may send an fp6 failure past int8 x1; with the skip disabled (every failure runs every
-    tier) the results are identical, on crowded data where both routes are taken."""
+    """_route may send an fp6 failure past the f6x2 tier; with the skip disabled (every failure runs
+    every tier) the results are identical, on crowded data where both routes are taken."""
     from opencv_facerecognizer_amd._device import FloatGallery
     from opencv_facerecognizer_amd import _lib
     monkeypatch.setenv("OFR_SEARCH", "auto")
@@ -144,7 +142,7 @@ def test_fallback_routing_is_only_a_choice(monkeypatch):
     routed = (g.last_fallbacks, dict(g.last_skipped))
     monkeypatch.setattr(FloatGallery, "ROUTE_SLACK", float("inf"))   # never skip
     d2, i2 = g.search(g.query_rows(Q), 1)
-    assert g.last_skipped.get("1", 0) == 0
+    assert g.last_skipped.get("f6x2", 0) == 0
     assert torch.equal(ii, i2) and torch.equal(dd, d2), routed
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 1)
 
@@ -242,6 +240,81 @@ def test_f6_quantize_rows_vs_host(R, d):
     assert np.all(got[:, 2] == 0)
 
 
+@pytest.mark.parametrize("R,d", [(1, 3), (300, 99), (513, 260), (40, 1000)])
+def test_f6x2_quantize_rows_vs_host(R, d):
+    """ofr_f6x2_quantize_rows: the first slice is byte-identical to ofr_f6_quantize_rows (same scale), the
+    second holds the nearest e2m3 value of 2^4 (x/s - v1), and the stats are (s(|v1| + |v2|/16),
+    |x - x~|, s |v2|/16) of x~ = s (v1 + v2/16)."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._lib import call, ptr, stream
+    r = _rng(R * 5 + d)
+    X = r.normal(0, 3, (R, d)).astype(np.float32)
+    if R > 2:
+        X[2] = 0
+        X[1, 0] = 1e6
+    ldx = d + 3
+    Xd = torch.zeros((R, ldx), dtype=torch.float32, device="cuda")
+    Xd[:, :d] = torch.from_numpy(X).cuda()
+    nbytes = _lib.load().ofr_f6_tiles_bytes(R, d)
+    T1 = torch.full((nbytes,), 0xAB, dtype=torch.uint8, device="cuda")
+    T2 = torch.full((nbytes,), 0xCD, dtype=torch.uint8, device="cuda")
+    T0 = torch.full((nbytes,), 0x11, dtype=torch.uint8, device="cuda")
+    sc, sc0 = (torch.empty(R, dtype=torch.float32, device="cuda") for _ in range(2))
+    st, st0 = (torch.empty((R, 3), dtype=torch.float64, device="cuda") for _ in range(2))
+    call("ofr_f6x2_quantize_rows", stream(), ptr(Xd), R, d, ldx, ptr(T1), ptr(T2), nbytes, ptr(sc), ptr(st), None,
+         None)
+    call("ofr_f6_quantize_rows", stream(), ptr(Xd), R, d, ldx, ptr(T0), nbytes, ptr(sc0), ptr(st0), None, None)
+    torch.cuda.synchronize()
+    assert torch.equal(T1, T0) and torch.equal(sc, sc0)
+    P = -(-R // 256) * 256
+    V1 = _decode_f6_tiles(T1.cpu().numpy(), P, d)
+    V2 = _decode_f6_tiles(T2.cpu().numpy(), P, d)
+    assert np.all(V2[R:] == 0) and np.all(V2[:R, d:] == 0)
+    V1, V2 = V1[:R, :d], V2[:R, :d]
+    s = sc.cpu().numpy().astype(np.float64)[:, None]
+    u = 16.0 * (X.astype(np.float64) - s * V1) / s
+    assert np.all(np.abs(u) <= 4.0 + 1e-9)
+    grid = _e2m3_values()
+    best = np.abs(np.abs(u)[..., None] - grid).min(-1)
+    assert np.all(np.abs(np.abs(V2) - np.abs(u)) <= best + 1e-9)             # nearest (ties either way)
+    assert np.all((np.sign(V2) == np.sign(u)) | (V2 == 0) | (np.abs(u) < 1e-9))
+    Xt = s * (V1 + V2 / 16.0)
+    got = st.cpu().numpy()
+    a = s[:, 0] * (np.linalg.norm(V1, axis=1) + np.linalg.norm(V2, axis=1) / 16.0)
+    e = np.linalg.norm(X.astype(np.float64) - Xt, axis=1)
+    t = s[:, 0] * np.linalg.norm(V2, axis=1) / 16.0
+    for j, ref in enumerate((a, e, t)):
+        np.testing.assert_allclose(got[:, j], ref, rtol=1e-11, atol=0)
+        assert np.all(got[:, j] >= ref)
+    assert np.all(got[:, 0] >= np.linalg.norm(Xt, axis=1))
+    # the second slice cuts the residual by more than 10x on Gaussian rows
+    e1 = st0.cpu().numpy()[:, 1]
+    ok = e1 > 0
+    assert np.median(got[ok, 1] / e1[ok]) < 0.1
+
+
+@pytest.mark.parametrize("k", [1, 4])
+def test_knn_f6x2_certifies_crowded_clusters(monkeypatch, k):
+    """Clusters of 40 rows (sigma 0.5 around unit-variance centres, d = 128): the 16 candidates all lie
+    in the query's cluster, within a fraction of the fp6 tier's bound of each other, so the fp6 tier
+    certifies none; the two-slice tier (residual ~1/30 of fp6's) must certify them, with the oracle's
+    neighbours."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(3)
+    d, K, per, B = 128, 200, 40, 300
+    mu = r.normal(0, 1, (K, d))
+    G = (mu[np.arange(K * per) % K] + r.normal(0, 0.5, (K * per, d))).astype(np.float32).astype(np.float64)
+    Q = (mu[r.integers(0, K, B)] + r.normal(0, 0.5, (B, d))).astype(np.float32).astype(np.float64)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    dd, ii = g.search(g.query_rows(Q), k)
+    fb = g.last_fallbacks
+    assert fb[0] >= 0.9 * B and len(fb) >= 2 and fb[1] <= 0.02 * B, fb
+    assert g.last_skipped.get("f6x2", 0) == 0
+    _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
+
+
 def test_knn_f6_tier_certifies_separated_data(monkeypatch):
     """f6 tier on well-separated identities (integer prototypes, +-1 noise, 10 rows per identity so
     that the 16 candidates reach past the query's own identity): the fp6 tier alone must certify
@@ -293,6 +366,7 @@ def test_gallery_append_in_place_vs_oracle(monkeypatch, mode):
             g.search(g.query_rows(Q[:64]), 1)       # build the first tier before the next appends
             if mode == "auto":
                 g._tier_gallery(1)                  # and the int8 tier
+                g._tier_gallery("f6x2")             # and the two-slice fp6 tier
         g.append(G[n:n + m])
         n += m
         assert g.N == n and g.G.shape[0] == n
@@ -301,6 +375,12 @@ def test_gallery_append_in_place_vs_oracle(monkeypatch, mode):
             _check_search("EuclideanDistance", Q[:B], G[:n], dd.cpu().numpy(), ii.cpu().numpy(), k)
         if mode == "auto":
             assert g.last_fallbacks[0] <= 30
+        if mode == "auto" and g.q8 and "f6x2" in g.q8:   # extended in place == built from scratch
+            fresh = FloatGallery.from_device_rows(g.G.clone(), d, _lib.METRIC_EUCLIDEAN, shift64=g.shift64)
+            a_, b_ = g.q8["f6x2"], fresh._tier_gallery("f6x2")
+            nb = _lib.load().ofr_f6_tiles_bytes(n, d)
+            assert torch.equal(a_["Gs"][:nb], b_["Gs"][:nb]) and torch.equal(a_["Gs2"][:nb], b_["Gs2"][:nb])
+            assert torch.equal(a_["stats"][:n], b_["stats"][:n]) and torch.equal(a_["gmax"], b_["gmax"])
 
 
 def test_nearest_neighbor_update_extends_device_gallery():
