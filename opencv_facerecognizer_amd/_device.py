@@ -527,8 +527,8 @@ class FloatGallery:
         """Queue the queries `tier` left uncertified (rows; their stats and bounds in that tier) for the
         next stage.  A query whose k-th distance misses even the bound the next quantized tier would
         give it -- this tier's bound moved by the drop in dS, the candidate order assumed unchanged,
-        with ROUTE_SLACK to spare -- skips that tier: on crowded data (DESIGN.md §5 stress) int8x1
-        rescues a few percent of the fp6 failures for a whole gallery pass.  Only a routing choice:
+        with ROUTE_SLACK to spare -- skips that tier (from f6: a query f6x2 cannot rescue goes straight
+        to int8 x2 instead of paying a three-segment pass for nothing).  Only a routing choice:
         every stage still certifies or hands on, so the results do not depend on it."""
         if not rows.numel():
             return
