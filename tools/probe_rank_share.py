@@ -1,0 +1,103 @@
+"""Probe: one rank's share of the sharded bench step at G GPUs, timed on one GPU.
+
+At G GPUs (bench.py under torch.distributed.run) a rank projects and quantizes B/G of the faces,
+searches its N/G gallery rows for the whole batch and merges.  This probe runs those pieces at the
+sizes one rank sees (no collectives: they are absent on one GPU) and times each with HIP events,
+so the fixed costs that do not shrink with G show up beside the tile pass that does:
+projection + quantization of B/G faces, the fp6 sample pass + thresholds + sieve pass over N/G
+rows, the split merge (stage 1, stage 2), and the whole local step.  One JSON line.
+
+    python tools/probe_rank_share.py [--gpus 8] [--reps 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from opencv_facerecognizer_amd import _lib  # noqa: E402
+from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
+
+
+def timed(fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--gallery", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    dev = _lib.device()
+    side, d, per_id, B, k, G = 100, 9999, 10, a.batch, 1, a.gpus
+    N = a.gallery // G
+    P, _ = bench.build_projection(side * side, d, dev)
+    bank = IdentityBank(a.gallery // per_id, side, side, device=dev)
+    ld = bench.round_up(d, 32)
+    g = bench.build_gallery(P, bank, per_id, 0, N, a.gallery, d, ld, dev)          # rank 0's rows
+    g._tier_gallery("f6")
+    gq = torch.Generator(device=dev)
+    gq.manual_seed(SEED + 7)
+    ids = torch.randint(0, a.gallery // per_id, (B,), generator=gq, device=dev)
+    Xq = bank.images(ids, seed=SEED + 99)
+    b1 = B // G
+    Qloc = torch.zeros((b1, ld), dtype=torch.float32, device=dev)
+    Qd = torch.zeros((B, ld), dtype=torch.float32, device=dev)
+    P.project(Xq, shift64=g.shift64, out=Qd)
+    qq = g.quantize_queries(Qd, tier="f6")
+    ql = {}
+
+    def prep():
+        P.project(Xq[:b1], shift64=g.shift64, out=Qloc)
+        ql["q"] = g.quantize_queries(Qloc, ql.get("q"), tier="f6")
+
+    ub_loc = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out = (torch.empty((B, k), dtype=torch.float64, device=dev), torch.empty((B, k), dtype=torch.int64, device=dev))
+
+    def tiles():
+        g.search_q8_phase(1, Qd, qq, k)
+
+    def stage1():
+        g.merge_pruned(1, Qd, qq, k, ub_loc)
+
+    ub = torch.full((B,), float("inf"), dtype=torch.float64, device=dev)
+
+    def stage2():
+        g.merge_pruned(2, Qd, qq, k, ub, 0, out)
+
+    def local_step():
+        prep()
+        tiles()
+        stage1()
+        ub.copy_(ub_loc[:, k - 1])
+        stage2()
+
+    tiles()
+    stage1()
+    ub.copy_(ub_loc[:, k - 1])            # this shard's own k-th bound (no other ranks here)
+    res = {"gpus": G, "rows_per_rank": N, "batch": B, "faces_projected_per_rank": b1,
+           "prep_ms": timed(prep, a.reps), "tiles_ms": timed(tiles, a.reps), "merge_stage1_ms": timed(stage1, a.reps),
+           "merge_stage2_ms": timed(stage2, a.reps), "local_step_ms": timed(local_step, a.reps)}
+    full = {"prep_full_batch_ms": timed(lambda: (P.project(Xq, shift64=g.shift64, out=Qd),
+                                                 g.quantize_queries(Qd, qq, tier="f6")), a.reps)}
+    res.update(full)
+    res["uncertified_local"] = int((qq["cert"] == 0).sum())
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
