@@ -663,15 +663,39 @@ __global__ void __launch_bounds__(256) premerge_kernel(const Cand* cand, int64_t
 }
 
 // Sieve thresholds from the sample pass's tile lists: theta[q] = the 16th best key (KEY_NONE
-// when the sample holds fewer than 16 rows); resets the bucket counts.
+// when the sample holds fewer than 16 rows); resets the bucket counts.  One wave per query (four
+// per block): each lane keeps the best 16 keys of its strided share (KeyList, one v_med3 per slot),
+// then six shuffle rounds merge the lanes' lists (the same value as sorting the whole list by
+// (score, index): only the 16th score is used, and score_key is monotone).
 __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists, int64_t T, uint32_t* theta,
-                                                              int* count) {
-  __shared__ Cand best[256 * KC];
-  const int64_t q = blockIdx.x;
-  block_best(lists + (size_t)q * T * KC, T * KC, best);
-  if (threadIdx.x == 0) {
-    const Cand c = best[KC - 1];
-    theta[q] = c.i != CAND_EMPTY ? score_key(c.d, 0) : KEY_NONE;
+                                                              int* count, int64_t B) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= B) return;
+  const Cand* src = lists + (size_t)q * T * KC;
+  const int64_t n = T * KC;
+  KeyList L;
+  L.init();
+  constexpr int U = 4;   // loads in flight per lane
+  for (int64_t e0 = lane; e0 < n; e0 += 64 * U) {
+    Cand c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = e0 + 64 * u;
+      c[u] = e < n ? src[e] : Cand{__builtin_inff(), CAND_EMPTY};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) L.insert(c[u].i != CAND_EMPTY ? score_key(c[u].d, 0) : KEY_NONE);
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t o[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) o[j] = (uint32_t)__shfl_xor((int)L.k[j], off);
+    L.merge(o);
+  }
+  if (lane == 0) {
+    theta[q] = L.k[KC - 1];
     count[q] = 0;
   }
 }
@@ -1443,8 +1467,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
                            f6t::LDS, st, s);
       OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
-      hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)B), dim3(256), 0, st, s.cand, s.ntg, theta,
-                         count);
+      hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, s.cand, s.ntg,
+                         theta, count, B);
       OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
       a.theta = theta;
       a.count = count;
