@@ -166,6 +166,29 @@ struct Engine {
     }
   }
 
+  // The same copy by MUBUF buffer_load ... lds (probe: Engine16 MODE 1024).  A FLAT global_load_lds in
+  // flight makes the compiler's waitcnt pass treat LDS reads as unordered (every first use of a fresh
+  // fragment then waits lgkmcnt(0)); the buffer form keeps them counted.  One descriptor per operand
+  // panel (nst stages, < 2^32 bytes), voffset = stage + instruction + lane.
+  static __device__ __forceinline__ void dma_buf(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst,
+                                                 int kt, char* st) {
+    // the wave index as a scalar: the descriptor choice below must be uniform (no waterfall loop)
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    const int pb = (int)(nst * PANEL);
+    __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(G + gp * nst * (int64_t)PANEL), 0, pb,
+                                                                  0x00020000);
+    __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * nst * (int64_t)PANEL), 0, pb,
+                                                                  0x00020000);
+#pragma unroll
+    for (int t = 0; t < IPW; ++t) {
+      const int ins = wave * IPW + t;
+      const bool gal = ins < DMA_INS / 2;
+      const int off = (gal ? ins : ins - DMA_INS / 2) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(gal ? rg : rq, (OFR_LDS void*)(st + (gal ? 0 : PANEL) + off), 16,
+                                               kt * PANEL + off + lane * 16, 0, 0, 0);
+    }
+  }
+
   // reads threaded through MFMAs: NFR reads over MF MFMAs, front-loaded (2 after each MFMA while
   // they last, then 1, then none)
   static __device__ __forceinline__ void interleave() {
@@ -336,7 +359,16 @@ struct Engine16 {
     };
     const int last = NSEG * nst - 1;
 #pragma unroll
-    for (int s = 0; s < NST; ++s) issue(s < last ? s : last);
+    for (int s = 0; s < NST; ++s) {
+      if constexpr ((MODE & 1024) != 0) {   // no FLAT DMA anywhere in the probe variant
+        const char *g, *q;
+        int ks;
+        seg_src<NSEG>(s < last ? s : last, nst, G, G2, Q, Q2, g, q, ks);
+        Engine<8>::dma_buf(g, gp, q, qp, nst, ks, smem + (s % NST) * STAGE);
+      } else {
+        issue(s < last ? s : last);
+      }
+    }
     i32x6 a[NA], b[NB];
     int sc = 0x7f7f7f7f;
     if constexpr ((MODE & 256) != 0) asm volatile("" : "+v"(sc));
@@ -350,10 +382,127 @@ struct Engine16 {
     if constexpr (MODE == 1) wait_vm<0>();
     else wait_vm<2 * IPW>();
     barrier();
+    if constexpr ((MODE & 2048) != 0) {   // the loop's read order, so that its waits stay counted
 #pragma unroll
-    for (int i = 0; i < NA; ++i) readA(smem, i);
+      for (int i = 0; i < 4; ++i) readA(smem, i);
 #pragma unroll
-    for (int c = 0; c < NB; ++c) readB(smem, c);
+      for (int c = 0; c < NB; ++c) readB(smem, c);
+#pragma unroll
+      for (int i = 4; i < NA; ++i) readA(smem, i);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) readA(smem, i);
+#pragma unroll
+      for (int c = 0; c < NB; ++c) readB(smem, c);
+    }
+    if constexpr ((MODE & 1024) != 0) {
+      // Probe: two barriers per stage.  Top of stage kt: stage kt+1 landed (own DMAs: vmcnt) and
+      // visible (s_barrier) -- no LDS drain.  Rows 0-3 with the refills of a[0..3] (8 LDS reads), then
+      // lgkmcnt(8) (every read of stage kt's buffer, all issued in stage kt-1, is done) + s_barrier,
+      // and only then stage kt+3's DMA into that buffer (1.5 stages of lead instead of 2).
+      auto issue_b = [&](int kt) {
+        const char *g, *q;
+        int ks;
+        seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
+        Engine<8>::dma_buf(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+      };
+      for (int kt = 0; kt < last; ++kt) {
+        seg_scales<NSEG>(kt, nst, sa, sb);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_vm<IPW>();   // stage kt+1 landed (kt+2 may be in flight)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const char* nxt = smem + ((kt + 1) % NST) * STAGE;
+        if constexpr ((MODE & 2048) != 0) {
+          // column-major halves: rows 0-3 against b[0], b[1], b[2], b[3] in turn; a[0..3] refilled
+          // after their last MFMA (the half's last four)
+#pragma unroll
+          for (int c = 0; c < NB; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              mm(a[i], b[c], acc[i][c]);
+              if (c == NB - 1) readA(nxt, i);
+            }
+          __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
+            readA(nxt, i);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        {
+          const int nx = kt + NST;
+          issue_b(nx < last ? nx : last);
+        }
+        if constexpr ((MODE & 2048) != 0) {
+          // rows 4-7 column-major: b[c] refilled after its last MFMA (row 7), a[4..7] after column 3
+#pragma unroll
+          for (int c = 0; c < NB; ++c) {
+#pragma unroll
+            for (int i = 4; i < NA; ++i) mm(a[i], b[c], acc[i][c]);
+            readB(nxt, c);   // b3 before a4..a7: the next stage needs b3 at its 13th MFMA, a4 at its 17th
+          }
+#pragma unroll
+          for (int i = 4; i < NA; ++i) readA(nxt, i);
+          __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
+#pragma unroll
+          for (int c = 0; c < NB; ++c) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+          continue;
+        }
+#pragma unroll
+        for (int i = 4; i < NA - 1; ++i) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
+          readA(nxt, i);
+        }
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+          mm(a[NA - 1], b[c], acc[NA - 1][c]);
+          readB(nxt, c);
+        }
+        readA(nxt, NA - 1);
+        __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
+#pragma unroll
+        for (int i = 4; i < NA - 1; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      seg_scales<NSEG>(last, nst, sa, sb);
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
+      wait_vm<0>();
+      barrier();
+      return;
+    }
     // Per stage kt: MFMAs of stage kt, each fragment replaced by stage kt+1's as soon as its last
     // MFMA is issued (A-major: A[i] after row i's 4 MFMAs, B[c] after row 7's MFMA c), so the
     // fragments need no second register set (acc 128 + fragments 72 registers).

@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
   f6t::f32x4 acc[8][4];
-  E::mainloop<MODE & 449, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+  E::mainloop<MODE & 3521, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
                                 p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
                                 reinterpret_cast<const char*>(p.Q2));
   // sieve operands after the main loop (the 16x16 engine needs every register in it)
@@ -1306,6 +1306,12 @@ extern "C" int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, i
 
 // waves of the fp6 tile engine (f6t::Engine; tools/f6_probe.hip times both)
 constexpr int F6_NW = 8;
+// main-loop variant of the 16x16 sieve pass (f6t::Engine16::mainloop MODE bits): 1024 = the stage
+// copies by MUBUF buffer_load ... lds (LDS reads stay counted for the compiler) and the stage barrier
+// split into a visibility barrier (top, no LDS drain) and a counted-wait barrier before the re-fill
+// (mid-stage); 2048 = column-major halves on top of it.  0 = the FLAT global_load_lds loop with one
+// draining barrier per stage (tools/f6_probe.hip times all of them).
+constexpr int F6S_MODE = 1024;
 
 // MFMA shape of the sieve pass: 16 = v_mfma_scale_f32_16x16x128 (f6t::Engine16, default),
 // 32 = the 32x32x64 engine (OFR_F6_SHAPE=32)
@@ -1447,8 +1453,9 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       static bool attr_done = false;
       if (!attr_done) {
         for (const void* f : {(const void*)q8s::tile_kernel_f6<F6_NW, 0>, (const void*)q8s::tile_kernel_f6<F6_NW, 8>,
-                              (const void*)q8s::tile_kernel_f6s<0>, (const void*)q8s::tile_kernel_f6<F6_NW, 0, 3>,
-                              (const void*)q8s::tile_kernel_f6<F6_NW, 8, 3>, (const void*)q8s::tile_kernel_f6s<0, 3>}) {
+                              (const void*)q8s::tile_kernel_f6s<F6S_MODE>, (const void*)q8s::tile_kernel_f6<F6_NW, 0, 3>,
+                              (const void*)q8s::tile_kernel_f6<F6_NW, 8, 3>,
+                              (const void*)q8s::tile_kernel_f6s<F6S_MODE, 3>}) {
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
         }
@@ -1475,10 +1482,10 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       a.bucket = bucket;
       a.cap = q8s::SIEVE_CAP;
       if (f6_shape() == 16 && two)
-        hipLaunchKernelGGL((q8s::tile_kernel_f6s<0, 3>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
-                           f6t::LDS, st, a);
+        hipLaunchKernelGGL((q8s::tile_kernel_f6s<F6S_MODE, 3>), dim3((unsigned)(a.ntq * a.ntg)),
+                           dim3(f6t::Engine16::NT), f6t::LDS, st, a);
       else if (f6_shape() == 16)
-        hipLaunchKernelGGL((q8s::tile_kernel_f6s<0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
+        hipLaunchKernelGGL((q8s::tile_kernel_f6s<F6S_MODE>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
                            f6t::LDS, st, a);
       else if (two)
         hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 8, 3>), dim3((unsigned)(a.ntq * a.ntg)), dim3(F6_NW * 64),

@@ -35,7 +35,7 @@ def counters(kname):
 
 def main():
     name = sys.argv[1]
-    knames = (sys.argv[2] if len(sys.argv) > 2 else "tile_kernel_f6<8, 0, 1>;sieve_threshold_kernel;tile_kernel_f6s<0, 1>").split(";")
+    knames = (sys.argv[2] if len(sys.argv) > 2 else "tile_kernel_f6<8, 0, 1>;sieve_threshold_kernel;tile_kernel_f6s<").split(";")
     stats = os.path.join(P, "kt", "kt_kernel_stats.csv")
     shutil.copy(stats, os.path.join(ROOT, "profiles", f"{name}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
