@@ -400,6 +400,10 @@ struct Engine16 {
       // visible (s_barrier) -- no LDS drain.  Rows 0-3 with the refills of a[0..3] (8 LDS reads), then
       // lgkmcnt(8) (every read of stage kt's buffer, all issued in stage kt-1, is done) + s_barrier,
       // and only then stage kt+3's DMA into that buffer (1.5 stages of lead instead of 2).
+      // rows before the re-fill barrier (their refills are the only LDS reads it lets through):
+      // 4 by default, 2 (MODE 4096), 6 (MODE 8192) or 1 (both) in the probe
+      constexpr int RS = (MODE & 4096) && (MODE & 8192) ? 1 : ((MODE & 4096) ? 2 : ((MODE & 8192) ? 6 : 4));
+      static_assert((MODE & 2048) == 0 || RS == 4, "column-major halves split at row 4");
       auto issue_b = [&](int kt) {
         const char *g, *q;
         int ks;
@@ -431,19 +435,22 @@ struct Engine16 {
           }
         } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+          for (int i = 0; i < RS; ++i) {
 #pragma unroll
             for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
             readA(nxt, i);
           }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+          for (int i = 0; i < RS; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        if constexpr (RS == 1) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        else if constexpr (RS == 2) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+        else if constexpr (RS == 6) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         {
@@ -470,7 +477,7 @@ struct Engine16 {
           continue;
         }
 #pragma unroll
-        for (int i = 4; i < NA - 1; ++i) {
+        for (int i = RS; i < NA - 1; ++i) {
 #pragma unroll
           for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
           readA(nxt, i);
@@ -483,7 +490,7 @@ struct Engine16 {
         readA(nxt, NA - 1);
         __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
 #pragma unroll
-        for (int i = 4; i < NA - 1; ++i) {
+        for (int i = RS; i < NA - 1; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
         }

@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
   f6t::f32x4 acc[8][4];
-  E::mainloop<MODE & 3521, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+  E::mainloop<MODE & 15809, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
                                 p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
                                 reinterpret_cast<const char*>(p.Q2));
   // sieve operands after the main loop (the 16x16 engine needs every register in it)
@@ -1309,9 +1309,11 @@ constexpr int F6_NW = 8;
 // main-loop variant of the 16x16 sieve pass (f6t::Engine16::mainloop MODE bits): 1024 = the stage
 // copies by MUBUF buffer_load ... lds (LDS reads stay counted for the compiler) and the stage barrier
 // split into a visibility barrier (top, no LDS drain) and a counted-wait barrier before the re-fill
-// (mid-stage); 2048 = column-major halves on top of it.  0 = the FLAT global_load_lds loop with one
-// draining barrier per stage (tools/f6_probe.hip times all of them).
-constexpr int F6S_MODE = 1024;
+// (after the first rows); 4096 / 8192 / both: that barrier after rows 0-1 / 0-5 / row 0 (default 0-3);
+// 2048 = column-major halves.  0 = the FLAT global_load_lds loop with one draining barrier per stage.
+// tools/f6_probe.hip times them: 1024 + 4096 + 8192 (re-fill barrier after row 0: 1.9 stages of
+// copy lead) is the fastest, 22.5 against 23.3 ms for 0.
+constexpr int F6S_MODE = 1024 + 4096 + 8192;
 
 // MFMA shape of the sieve pass: 16 = v_mfma_scale_f32_16x16x128 (f6t::Engine16, default),
 // 32 = the 32x32x64 engine (OFR_F6_SHAPE=32)

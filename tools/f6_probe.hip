@@ -342,8 +342,8 @@ int main(int argc, char** argv) {
   if (getenv("SHAPE16")) {   // the 16x16x128 sieve engine next to the 32x32x64 one
     a.gg = 4 < ntg ? 4 : ntg;
     for (int rep = 0; rep < 2; ++rep)
-      if (run16<0>(a, reps, "sieve16") || run16<1024>(a, reps, "mubuf2b16") || run16<3072>(a, reps, "mubuf2b-cm16") ||
-          run16<4>(a, reps, "noepi16") || run16<1028>(a, reps, "mubuf2b-noepi16") || run16<3076>(a, reps, "mubuf2b-cm-noepi16"))
+      if (run16<0>(a, reps, "sieve16") || run16<1024>(a, reps, "mubuf2b16") || run16<1024 + 4096>(a, reps, "mubuf2b-rs2") ||
+          run16<1024 + 4096 + 8192>(a, reps, "mubuf2b-rs1"))
         return 1;
     return 0;
   }
