@@ -265,7 +265,7 @@ def main():
     torch.cuda.synchronize()
     log(rank, f"setup {time.perf_counter() - t0:.1f}s: gallery rows {nl}/{N} per rank, d={d}, D={D}, B={B}")
 
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     use_q8 = args.search in ("f6", "q8")
     tier0 = "f6" if args.search == "f6" else 1
     if use_q8:
@@ -277,82 +277,101 @@ def main():
     # all-gathered (fp6 panels need whole 256-row blocks per rank)
     b0, b1 = shard_range(B, rank, world)
     shard_prep = world > 1 and B % world == 0 and (tier0 != "f6" or (B // world) % 256 == 0)
-    # two query buffers: batch s+1 is prepared (projection, quantization, its all-gathers) while the
-    # host waits on batch s's certificate, so the GPU does not idle between steps
+    # two query buffers: batch s+1 is prepared (projection, quantization, its all-gathers) on a side
+    # stream once batch s's tile pass is done, so it overlaps batch s's merge / certificate / host sync
+    # instead of following them (the tile pass itself keeps the whole chip)
     bufs = [dict(Qd=Qd if j == 0 else torch.zeros_like(Qd), qq=None, pending=None, qq_loc=None,
                  Qd_loc=torch.zeros((b1 - b0, ld), dtype=torch.float32, device=device) if shard_prep else None)
             for j in range(2)]
+    main_stream = torch.cuda.current_stream(device)
+    # OFR_BENCH_OVERLAP=0: the preparation on the main stream (behind the tile pass, before the merge)
+    side = torch.cuda.Stream(device=device) if os.environ.get("OFR_BENCH_OVERLAP", "1") == "1" else main_stream
+    ev_ready = [torch.cuda.Event() for _ in range(2)]   # buffer j prepared (side stream)
+    ev_free = [torch.cuda.Event() for _ in range(2)]    # buffer j's last reader done (main stream)
+    ev_tiles = torch.cuda.Event()                        # the latest tile pass done (main stream)
 
-    def prep(b, events=None):
-        """Query batch -> centred fp32 search rows (+ the first tier's quantized rows) in buffer b."""
-        if events:
-            events[0].record()
-        if shard_prep:
-            P.project(Xq[b0:b1], shift64=gallery.shift64, out=b["Qd_loc"])   # this rank's faces
-            if use_q8:
-                b["qq_loc"] = gallery.quantize_queries(b["Qd_loc"], b["qq_loc"], tier=tier0)
-                b["qq"] = gallery.gather_queries(b["qq_loc"])
-                # the fp32 rows are read from phase 2 on: their all-gather overlaps the tile pass
-                b["pending"] = gather_rows_async(b["Qd_loc"])
-                b["Qd"] = b["pending"].out
+    def prep(j, events=None):
+        """Query batch -> centred fp32 search rows (+ the first tier's quantized rows) in buffer j."""
+        b = bufs[j]
+        side.wait_event(ev_free[j])
+        side.wait_event(ev_tiles)
+        with torch.cuda.stream(side):
+            if events:
+                events[0].record()
+            if shard_prep:
+                P.project(Xq[b0:b1], shift64=gallery.shift64, out=b["Qd_loc"])   # this rank's faces
+                if use_q8:
+                    b["qq_loc"] = gallery.quantize_queries(b["Qd_loc"], b["qq_loc"], tier=tier0)
+                    b["qq"] = gallery.gather_queries(b["qq_loc"])
+                    # the fp32 rows are read from phase 2 on: their all-gather overlaps the tile pass
+                    b["pending"] = gather_rows_async(b["Qd_loc"])
+                    b["Qd"] = b["pending"].out
+                else:
+                    b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
             else:
-                b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
-        else:
-            P.project(Xq, shift64=gallery.shift64, out=b["Qd"])          # fp32(W^T x - c), exact int8 MFMA
-            if use_q8:
-                b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier0)
-        if events:
-            events[1].record()
+                P.project(Xq, shift64=gallery.shift64, out=b["Qd"])          # fp32(W^T x - c), exact int8 MFMA
+                if use_q8:
+                    b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier0)
+            if events:
+                events[1].record()
+            ev_ready[j].record(side)
 
-    def search(b, events=None, then=None):
-        """Tile pass, merge, certificate (+ fallback tiers) of the batch in buffer b.  then(): enqueued
-        after the merge, before the host reads the certificate (the next batch's prep)."""
+    def search(j, events=None, then=None):
+        """Tile pass, merge, certificate (+ fallback tiers) of the batch in buffer j.  then(): the next
+        batch's prep, enqueued right after this tile pass (it runs on the side stream)."""
+        b = bufs[j]
+        main_stream.wait_event(ev_ready[j])
+        if events:
+            events[4].record()
         Qd_, qq_ = b["Qd"], b["qq"]
         if use_q8:
             gallery.search_q8_phase(1, Qd_, qq_, k)
         else:
             gallery.search_phase("tiles", Qd_, k)
+        if events:
+            events[2].record()
+        ev_tiles.record(main_stream)
+        if then is not None:
+            then()
         if b["pending"] is not None:
             Qd_ = b["pending"]()
             b["pending"] = None
-        if events:
-            events[2].record()
         if use_q8:
             merge_sharded(gallery, Qd_, qq_, k, n0, out)   # world 1: the plain phase 2
         else:
             gallery.search_phase("merge", Qd_, k, index_base=n0, out=out)
         if events:
             events[3].record()
-        if then is not None:
-            then()
+        res = out
         if use_q8:
             if world > 1:      # global certificate: all-gather + merge + collective fallback
                 res, counts = certify_sharded(gallery, Qd_, qq_, k, out, n0)
                 fallbacks.append(counts[0])
                 last_counts[:] = counts
-                return res
-            fallbacks.append(gallery.fallback(Qd_, qq_, k, out, index_base=n0))
-            last_counts[:] = list(gallery.last_fallbacks)
-        if world > 1:
+            else:
+                fallbacks.append(gallery.fallback(Qd_, qq_, k, out, index_base=n0))
+                last_counts[:] = list(gallery.last_fallbacks)
+        elif world > 1:
             gd, gi = exchange_topk(out[0], out[1])
-            return merge_topk(gd, gi, world, k, k)
-        return out
+            res = merge_topk(gd, gi, world, k, k)
+        ev_free[j].record(main_stream)
+        return res
 
     for w in range(max(args.warmup, 2)):     # both buffers warmed (their quantized rows allocated)
-        prep(bufs[w % 2])
+        prep(w % 2)
         if w < args.warmup:
-            search(bufs[w % 2])
+            search(w % 2)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     # exactly K preps and K searches inside the timed region: batch 0's prep first, batch s+1's
-    # enqueued behind batch s's merge, none after the last
-    prep(bufs[0], ev[0])
+    # enqueued behind batch s's tile pass, none after the last
+    prep(0, ev[0])
     for s in range(args.steps):
-        nxt = (lambda s=s: prep(bufs[(s + 1) % 2], ev[s + 1])) if s + 1 < args.steps else None
-        res = search(bufs[s % 2], ev[s], then=nxt)
+        nxt = (lambda s=s: prep((s + 1) % 2, ev[s + 1])) if s + 1 < args.steps else None
+        res = search(s % 2, ev[s], then=nxt)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -365,7 +384,7 @@ def main():
     Qd, qq = bufs[(args.steps - 1) % 2]["Qd"], bufs[(args.steps - 1) % 2]["qq"]
 
     ms_proj = np.mean([e[0].elapsed_time(e[1]) for e in ev])
-    ms_tiles = np.mean([e[1].elapsed_time(e[2]) for e in ev])
+    ms_tiles = np.mean([e[4].elapsed_time(e[2]) for e in ev])     # the tile pass on the main stream
     ms_merge = np.mean([e[2].elapsed_time(e[3]) for e in ev])
     idx = res[1][:, 0]
     acc = float(((idx // args.per_id) == ids_q).double().mean().item())
