@@ -447,6 +447,11 @@ struct Engine16 {
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+        // lgkmcnt(2 RS): each refill is exactly two LDS instructions (frag16: ds_read_b128 + ds_read_b64,
+        // the part1 address opaque so they cannot be fused), and LDS returns in order, so at most the
+        // 2 RS reads issued above may still be in flight and every read of the previous stage (all
+        // from the buffer re-filled below) is done.  Scalar loads sharing the counter can only make the
+        // wait stricter.  (More instructions per refill would also be safe; fewer would not.)
         if constexpr (RS == 1) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
         else if constexpr (RS == 2) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
         else if constexpr (RS == 6) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
