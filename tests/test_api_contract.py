@@ -113,3 +113,18 @@ def test_shard_is_derived_state():
     assert _safepickle._is_cache_key("_shard")
     clf2 = pickle.loads(pickle.dumps(clf))
     assert "_shard" not in clf2.__dict__ and clf2.k == 1
+
+
+def test_certified_tier_paths():
+    """The certified search chain (host logic, _device.FloatGallery): fp6 -> two-slice fp6 -> int8 x2
+    -> fp32 for the default first tier; OFR_SEARCH=q8 / q8x2 start at the int8 tiers; sets of <= 32
+    open queries go straight to the exact fp32 pass."""
+    from opencv_facerecognizer_amd._device import SMALL_BATCH, FloatGallery
+    assert FloatGallery.tier_path("f6") == ("f6", "f6x2", 2, "fp32")
+    assert FloatGallery.tier_path(1) == (1, 2, "fp32")
+    assert FloatGallery.tier_path(2) == (2, "fp32")
+    g = FloatGallery.__new__(FloatGallery)
+    assert g.next_tier("f6", SMALL_BATCH + 1) == "f6x2" and g.next_tier("f6x2", 4096) == 2
+    assert g.next_tier("f6", SMALL_BATCH) == "fp32" and g.next_tier(2, 4096) == "fp32"
+    for t in FloatGallery.TIER_CHAIN[:-1]:
+        assert FloatGallery.tier_path(t)[-1] == "fp32"
