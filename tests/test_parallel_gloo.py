@@ -344,3 +344,42 @@ def test_merge_sharded_global_bound():
                       + ([float("inf")] * k if b == 0 else []))
         for r in (0, 1):
             assert res[r][b] == vals[k - 1]
+
+
+def _gather_queries_worker(rank, ws, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from opencv_facerecognizer_amd._device import FloatGallery
+        g = FloatGallery.__new__(FloatGallery)
+        r = np.random.Generator(np.random.PCG64(11 + rank))
+        qq = dict(tier="f6", B=256, Qs=torch.full((64,), rank, dtype=torch.uint8),
+                  scale=torch.from_numpy(r.random(256).astype(np.float32)),
+                  stats=torch.from_numpy(r.random((256, 3))))
+        o = g.gather_queries(qq)
+        if rank == 0:
+            out.put((o["Qs"].numpy(), o["scale"].numpy(), o["stats"].numpy(), o["B"], str(o["scale"].dtype)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_queries_packs_scales_and_stats():
+    """Sharded query preparation (FloatGallery.gather_queries): the fp6 tiles, the fp32 scales and the
+    fp64 stats of every rank's 256-row block, rank-major, scales exact through their fp64 packing."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_queries_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    Qs, scale, stats, B, dt = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert B == 512 and dt == "torch.float32"
+    assert np.array_equal(Qs, np.concatenate([np.zeros(64, np.uint8), np.ones(64, np.uint8)]))
+    for rank in range(2):
+        r = np.random.Generator(np.random.PCG64(11 + rank))
+        s, st = r.random(256).astype(np.float32), r.random((256, 3))
+        assert np.array_equal(scale[256 * rank:256 * (rank + 1)], s)
+        assert np.array_equal(stats[256 * rank:256 * (rank + 1)], st)
