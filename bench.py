@@ -195,24 +195,48 @@ def stress_run(P, bank, args, noise, device, N=None):
     gq.manual_seed(SEED + 7)
     ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
     Xq = bank.images(ids_q, seed=SEED + 99, noise=noise)
-    Qd = torch.zeros((B, ld), dtype=torch.float32, device=device)
     out = (torch.empty((B, k), dtype=torch.float64, device=device), torch.empty((B, k), dtype=torch.int64, device=device))
-    qq, tiers, counts = None, [], None
+    tiers, counts = [], None
+    # the headline's pipelined step (main()): batch s+1 prepared on a side stream behind batch s's
+    # tile pass, two query buffers, exactly K preparations and K searches in the timed region
+    bufs = [dict(Qd=torch.zeros((B, ld), dtype=torch.float32, device=device), qq=None) for _ in range(2)]
+    main_stream = torch.cuda.current_stream(device)
+    side = torch.cuda.Stream(device=device)
+    ev_ready, ev_free, ev_tiles = [torch.cuda.Event() for _ in range(2)], [torch.cuda.Event() for _ in range(2)], \
+        torch.cuda.Event()
 
-    def step(timings=None):
-        nonlocal qq
-        P.project(Xq, shift64=gallery.shift64, out=Qd)
-        qq = gallery.quantize_queries(Qd, qq, tier="f6")
-        gallery.search_q8_phase(3, Qd, qq, k, out=out)
-        gallery.fallback(Qd, qq, k, out, timings=timings)
+    def prep(j):
+        b = bufs[j]
+        side.wait_event(ev_free[j])
+        side.wait_event(ev_tiles)
+        with torch.cuda.stream(side):
+            P.project(Xq, shift64=gallery.shift64, out=b["Qd"])
+            b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier="f6")
+            ev_ready[j].record(side)
 
-    step()
+    def search(j, timings=None, then=None):
+        b = bufs[j]
+        main_stream.wait_event(ev_ready[j])
+        gallery.search_q8_phase(1, b["Qd"], b["qq"], k)
+        ev_tiles.record(main_stream)
+        if then is not None:
+            then()
+        gallery.search_q8_phase(2, b["Qd"], b["qq"], k, out=out)
+        gallery.fallback(b["Qd"], b["qq"], k, out, timings=timings)
+        ev_free[j].record(main_stream)
+
+    for j in range(2):
+        prep(j)
+        search(j)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.stress_steps):
-        step(tiers)
+    K = args.stress_steps
+    prep(0)
+    for s in range(K):
+        search(s % 2, tiers, then=(lambda s=s: prep((s + 1) % 2)) if s + 1 < K else None)
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / args.stress_steps
+    ms = (time.perf_counter() - t0) * 1e3 / K
+    Qd, qq = bufs[(K - 1) % 2]["Qd"], bufs[(K - 1) % 2]["qq"]
     counts = list(gallery.last_fallbacks)
     per_tier = {}
     for t, n, m in tiers:
