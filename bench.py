@@ -35,10 +35,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from opencv_facerecognizer_amd import _lib  # noqa: E402
-from opencv_facerecognizer_amd._device import FloatGallery, Projection, col_mean_u8, round_up  # noqa: E402
+from opencv_facerecognizer_amd._device import FloatGallery, round_up  # noqa: E402
 from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, gather_rows_async,  # noqa: E402
                                                 merge_sharded, merge_topk, shard_range)
-from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
+from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_gallery, build_projection  # noqa: E402
 
 PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
 PEAK_I8_MFMA = 5.0e15       # int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, matrix cores)
@@ -77,15 +77,6 @@ def parse():
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
-
-
-def build_projection(D, d, device):
-    """Random W (no trained checkpoint exists at this scale): N(0, 1/D), prepared for the exact int8 kernel."""
-    g = torch.Generator(device=device)
-    g.manual_seed(SEED + 5)
-    Wt = torch.randn((d, D), generator=g, device=device) / np.sqrt(D)
-    P = Projection(Wt_device=Wt, D=D, device=device)
-    return P, Wt
 
 
 def cpu_baseline(Wt, gallery, Xq, N_total, seconds):
@@ -143,23 +134,6 @@ def committed_traffic(cfg):
         if s.get("config") == cfg:
             best = (s["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
     return best
-
-
-def build_gallery(P, bank, per_id, n0, nl, N, d, ld, device, noise=12.0):
-    """Gallery rows [n0, n0 + nl) of the N-image synthetic gallery, projected exactly and centred on
-    c = W^T round(mean image of the gallery's first chunk) (fp64, the same on every rank)."""
-    chunk = 8192
-    G = torch.zeros((nl, ld), dtype=torch.float32, device=device)
-    rows = torch.arange(0, min(N, chunk), device=device)
-    m = col_mean_u8(bank.images(rows // per_id, seed=SEED + 1000, noise=noise), P.D)
-    m_img = torch.clamp(torch.round(m), 0, 255).to(torch.uint8).reshape(1, -1).contiguous()
-    centre = P.project(m_img, f64=True)[0].contiguous()
-    for c0 in range(0, nl, chunk):
-        c1 = min(nl, c0 + chunk)
-        rows = torch.arange(n0 + c0, n0 + c1, device=device)
-        imgs = bank.images(rows // per_id, seed=SEED + 1000 + (n0 + c0) // chunk, noise=noise)
-        P.project(imgs, shift64=centre, out=G[c0:c1])
-    return FloatGallery.from_device_rows(G, d, _lib.METRIC_EUCLIDEAN, shift64=centre)
 
 
 def certificate_margin(gallery, Qd, qq, nsample=64):
@@ -471,8 +445,7 @@ def main():
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
     if args.search == "f6":
-        sieve = ("q8s::tile_kernel_f6s<0> sieve pass (16x16x128 engine)"
-                 if os.environ.get("OFR_F6_SHAPE", "16") == "16" else "q8s::tile_kernel_f6<8, 8> sieve pass (32x32x64 engine)")
+        sieve = _lib.load().ofr_f6_sieve_kernel().decode() + " sieve pass"     # the variant the library launches
         peak, kname = PEAK_F6_MFMA, ("ofr_knn_f6 phase 1 (fp6 e2m3): q8s::tile_kernel_f6<8, 0> sample pass + "
                                      "sieve_threshold_kernel + " + sieve)
         alg_bytes_tiles = 0.75 * (nl * d + B * d)                    # 6 bits per feature, gallery + queries

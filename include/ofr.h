@@ -197,6 +197,8 @@ size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N);
 size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N);
 int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
                          size_t tiles_bytes, float* scale, double* stats, const float* aux, double* maxima);
+/* The fp6 sieve kernel ofr_knn_f6 launches for B > 32, as the profiler names it (profiling labels). */
+const char* ofr_f6_sieve_kernel(void);
 int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
@@ -369,10 +371,17 @@ int ofr_row_div_f64(void* stream, const double* A, int64_t rows, int64_t cols, i
  * rows + fp6 tiles, as for ofr_knn_f6).  Every shard runs the certified fp6 tier,
  * ONE ncclAllGather exchanges the (distance, index, bound) lists, every device
  * merges them (ofr_topk_merge_certify) and certifies a query iff the global k-th
- * squared distance is below every rank's bound; uncertified queries are re-run
- * exactly (ofr_knn_f32) on every shard and exchanged once more.  Output on
- * EVERY device: out_d / out_i [B][k] = the exact top-k of the whole gallery
- * (classifier.py:104-119), cert [B] = 1 if the fp6 tier certified the query.
+ * squared distance is below every rank's bound.  Uncertified queries go down the
+ * tier chain of the single-GPU search on every shard, each stage exchanged and
+ * certified the same way: the two-slice fp6 tier (f6x2, when every shard gives
+ * Gt2 / gscale2 / gmax2 from ofr_f6x2_quantize_rows), the two-slice int8 tier
+ * (when every shard gives G8 / ld8 / gscale8 / gmax8 from ofr_q8_quantize_rows,
+ * slices 2), then the exact fp32 pass (ofr_knn_f32); a stage with <= 32 open
+ * queries goes straight to the exact pass.  Output on EVERY device: out_d / out_i
+ * [B][k] = the exact top-k of the whole gallery (classifier.py:104-119), cert [B]
+ * = 1 if a quantized tier certified the query (0: the exact pass resolved it);
+ * tier_counts (optional, [4]): open queries after the fp6 tier, after f6x2,
+ * after int8 x2, and the number the exact pass ran (-1: stage not run).
  * Euclidean, k <= 16.  workspace: ofr_knn_sharded_workspace_bytes per shard.   */
 typedef struct ofr_comm ofr_comm;
 typedef struct ofr_knn_shard {
@@ -395,6 +404,15 @@ typedef struct ofr_knn_shard {
   double* out_d;
   int64_t* out_i;
   int* cert;
+  /* optional finer tiers (null pointers: the stage is skipped) */
+  const void* Gt2;          /* f6x2: second-slice tiles of the shard's rows (first slice = Gt) */
+  const float* gscale2;     /* f6x2: row scales */
+  const double* gmax2;      /* f6x2: gallery maxima */
+  const int8_t* G8;         /* int8 x2: slices [N][ld8] */
+  int64_t ld8;
+  const float* gscale8;
+  const double* gmax8;
+  int64_t* tier_counts;     /* optional out [4] (read on shard 0) */
 } ofr_knn_shard;
 int ofr_comm_init_all(int ndev, const int* devices, ofr_comm** comm);
 int ofr_comm_destroy(ofr_comm* comm);

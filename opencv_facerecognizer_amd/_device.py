@@ -599,8 +599,40 @@ class FloatGallery:
         return out_d, out_i
 
 
+_COUNT_DT = {1: (_lib.DT_U8, torch.uint8, np.uint8, 255), 2: (_lib.DT_U16, torch.int16, np.uint16, 65535),
+             4: (_lib.DT_U32, torch.int32, np.uint32, 2 ** 32 - 1)}
+
+
+def counts_of(F, denom, count_bytes=None):
+    """Float rows F [n][nbins] that are EXACTLY integer counts / denom (the SpatialHistogram values,
+    feature.py:298-299) -> (uint counts host array, bytes per count); None when they are not."""
+    F = np.asarray(F, np.float64)
+    if F.size and not np.isfinite(F).all():
+        return None
+    C = np.rint(F * denom)
+    if F.size and (C.min() < 0 or not np.array_equal(C / denom, F)):
+        return None
+    top = C.max() if C.size else 0
+    cb = count_bytes or next(b for b in (1, 2, 4) if top <= _COUNT_DT[b][3])
+    if top > _COUNT_DT[cb][3]:
+        return None
+    return C.astype(_COUNT_DT[cb][2]), cb
+
+
+def infer_count_denom(F):
+    """The cell pixel count of LBP spatial histograms F (floats = count / cell): 1 / the smallest
+    positive value when that divides every value exactly, else None (not a count histogram)."""
+    F = np.asarray(F, np.float64)
+    pos = F[F > 0]
+    if not pos.size:
+        return None
+    denom = float(np.rint(1.0 / pos.min()))
+    return denom if denom >= 1 and counts_of(F, denom) is not None else None
+
+
 class Chi2Gallery:
-    """Device gallery for ChiSquare search: fp32 values, or integer counts with a denominator."""
+    """Device gallery for ChiSquare search: fp32 values, or integer counts with a denominator
+    (the LBP spatial histograms: count / cell, held as the counts -- exact and 4x smaller)."""
 
     def __init__(self, rows, dtype=_lib.DT_F32, denom=1.0, nbins=None, device=None):
         device = device or dev()
@@ -618,9 +650,43 @@ class Chi2Gallery:
         self.ws = Workspace()
         self.last_fallbacks = ()
 
+    @classmethod
+    def from_counts(cls, C, count_bytes, denom, device=None):
+        """Host or device counts [n][nbins] (uint8 / uint16 / uint32 values) -> a counts gallery."""
+        dt, tdt, ndt, _ = _COUNT_DT[count_bytes]
+        device = device or dev()
+        if not isinstance(C, torch.Tensor):
+            C = torch.from_numpy(np.ascontiguousarray(np.asarray(C).astype(ndt).view(
+                {1: np.uint8, 2: np.int16, 4: np.int32}[count_bytes])))
+        nbins = int(C.shape[1])
+        ld = round_up(max(nbins, 1), 16 // count_bytes)      # 16-byte rows for the tile kernel's loads
+        G = C.to(device=device, dtype=tdt)
+        if ld != nbins:
+            Gp = torch.zeros((G.shape[0], ld), dtype=tdt, device=device)
+            Gp[:, :nbins] = G
+            G = Gp
+        return cls(G, dtype=dt, denom=denom, nbins=nbins, device=device)
+
+    @property
+    def count_bytes(self):
+        return {_lib.DT_U8: 1, _lib.DT_U16: 2, _lib.DT_U32: 4}.get(self.dtype)
+
+    def counts_rows(self, arr):
+        """Host float rows -> device counts rows of this (counts) gallery, or None when the rows are not
+        exactly counts / denom in range (the caller then uses a float gallery)."""
+        cb = self.count_bytes
+        got = counts_of(np.asarray(arr, np.float64).reshape(-1, self.nbins), self.denom, cb) if cb else None
+        if got is None:
+            return None
+        C = torch.from_numpy(np.ascontiguousarray(got[0].view({1: np.uint8, 2: np.int16, 4: np.int32}[cb])))
+        out = torch.zeros((C.shape[0], self.G.shape[1]), dtype=self.G.dtype, device=self.G.device)
+        out[:, :self.nbins] = C.to(self.G.device)
+        return out
+
     def append(self, rows):
-        """Append rows in place (NearestNeighbor.update): host float rows for fp32 galleries, or a
-        device tensor of the gallery's element type; geometric growth.  Returns the new row count."""
+        """Append rows in place (NearestNeighbor.update): host float rows (for a counts gallery they must
+        be exact counts / denom, else TypeError) or a device tensor of the gallery's element type;
+        geometric growth.  Returns the new row count."""
         if isinstance(rows, torch.Tensor) and rows.dtype == self._Gbuf.dtype:
             new = torch.zeros((rows.shape[0], self._Gbuf.shape[1]), dtype=rows.dtype, device=self._Gbuf.device)
             new[:, :rows.shape[1]] = rows.to(self._Gbuf.device)
@@ -628,7 +694,10 @@ class Chi2Gallery:
             new = f32_rows(np.asarray(rows, np.float64).reshape(-1, self.nbins), ld=self._Gbuf.shape[1],
                            device=self._Gbuf.device)
         else:
-            raise TypeError("append to a count gallery takes a device tensor of its element type")
+            new = None if isinstance(rows, torch.Tensor) else self.counts_rows(rows)
+            if new is None:
+                raise TypeError("append to a count gallery takes counts / denom rows or a device tensor of its "
+                                "element type")
         n = int(new.shape[0])
         N0, N1 = self.N, self.N + n
         if N1 > self._Gbuf.shape[0]:
@@ -672,6 +741,10 @@ class Chi2Gallery:
         return out_d, out_i
 
     def query_rows(self, arr):
+        """Host float query rows -> device rows of this gallery's element type; None for a counts
+        gallery when the rows are not counts / denom."""
+        if self.dtype != _lib.DT_F32:
+            return self.counts_rows(arr)
         return f32_rows(np.asarray(arr, np.float64), ld=self.G.shape[1])
 
 

@@ -60,6 +60,7 @@ SIGNATURES = {
     "ofr_f6_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp]),
     "ofr_q8_maxima": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "ofr_knn_f6_workspace_bytes": (c_sz, [c_i64, c_i64]),
+    "ofr_f6_sieve_kernel": (ctypes.c_char_p, []),
     "ofr_knn_f6_sieve_counts_offset": (c_sz, [c_i64, c_i64]),
     "ofr_f6_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp]),
     "ofr_knn_f6": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
@@ -122,7 +123,9 @@ class KnnShard(ctypes.Structure):
     _fields_ = [("stream", c_vp), ("Q", c_vp), ("ldq", c_i64), ("Qt", c_vp), ("qscale", c_vp), ("qstats", c_vp),
                 ("G", c_vp), ("N", c_i64), ("ldg", c_i64), ("Gt", c_vp), ("gscale", c_vp), ("aux", c_vp),
                 ("gmax", c_vp), ("index_base", c_i64), ("workspace", c_vp), ("workspace_bytes", c_sz),
-                ("out_d", c_vp), ("out_i", c_vp), ("cert", c_vp)]
+                ("out_d", c_vp), ("out_i", c_vp), ("cert", c_vp),
+                ("Gt2", c_vp), ("gscale2", c_vp), ("gmax2", c_vp), ("G8", c_vp), ("ld8", c_i64), ("gscale8", c_vp),
+                ("gmax8", c_vp), ("tier_counts", c_vp)]
 
 
 class OfrError(RuntimeError):

@@ -18,9 +18,11 @@
 //   2. pack [B][2k+1] doubles (distances, indices bit-copied, bound) and ncclAllGather them;
 //   3. merge_certify_kernel: the global top-k of the ndev lists per query, certified iff the global
 //      k-th squared distance is below every rank's bound (a -inf bound never certifies);
-//   4. uncertified queries (host reads the certificate once): their rows are gathered and searched
-//      exactly on every shard (ofr_knn_f32), all-gathered again and merged -- the result is the
-//      exact fp64 top-k of the whole gallery (classifier.py:104-119) on every device.
+//   4. uncertified queries (host reads the certificate): their rows are gathered and go down the
+//      single-GPU search's tier chain on every shard -- two-slice fp6 (f6x2), two-slice int8, then
+//      the exact fp32 pass (ofr_knn_f32) -- each stage all-gathered, merged and certified again, so
+//      the result is the exact fp64 top-k of the whole gallery (classifier.py:104-119) on every
+//      device.
 // RCCL is bound at run time (dlopen of librccl.so.1, the soname torch's own copy also carries), so
 // the library loads and the single-GPU path works where RCCL is absent.
 #include <dlfcn.h>
@@ -166,14 +168,18 @@ __global__ void gather_rows_kernel(const float* Q, int64_t ldq, const int64_t* r
 }
 
 struct WsLayout {
-  size_t knn, loc_d, loc_i, bound, send, recv, sub_q, rows, ubl, ubr, ub, total;
+  size_t knn, loc_d, loc_i, bound, send, recv, sub_q, rows, ubl, ubr, ub, qt1, qt2, qscale, qstats, q8, scert,
+      tiles_bytes, total;
 };
 
+// per shard: the tier passes' workspace, the local lists, the packed exchange buffers, the open
+// queries' rows and their quantized forms (sized for the whole batch; d <= ldq bounds the tiles)
 static WsLayout layout(int64_t B, int64_t N, int64_t ldq, int k, int ndev) {
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
   WsLayout w{};
   size_t off = 0;
-  const size_t knn = std::max(ofr_knn_f6_workspace_bytes(B, N), ofr_knn_workspace_bytes(B, N, k));
+  const size_t knn = std::max({ofr_knn_f6_workspace_bytes(B, N), ofr_knn_workspace_bytes(B, N, k),
+                               ofr_knn_q8_workspace_bytes(B, N)});
   w.knn = off; off += up(knn);
   w.loc_d = off; off += up((size_t)B * k * 8);
   w.loc_i = off; off += up((size_t)B * k * 8);
@@ -185,9 +191,29 @@ static WsLayout layout(int64_t B, int64_t N, int64_t ldq, int k, int ndev) {
   w.ubl = off; off += up((size_t)B * k * 8);
   w.ubr = off; off += up((size_t)ndev * B * k * 8);
   w.ub = off; off += up((size_t)B * 8);
+  w.tiles_bytes = ofr_f6_tiles_bytes(B, ldq);
+  w.qt1 = off; off += up(w.tiles_bytes);
+  w.qt2 = off; off += up(w.tiles_bytes);
+  w.qscale = off; off += up((size_t)B * 4);
+  w.qstats = off; off += up((size_t)B * 3 * 8);
+  w.q8 = off; off += up((size_t)B * 2 * round_up(ldq, 64));
+  w.scert = off; off += up((size_t)B * 4);
   w.total = off;
   return w;
 }
+
+// synchronises every shard's stream when the scope ends while armed (an early error return must
+// not free host vectors that asynchronous uploads may still read)
+struct SyncAll {
+  const ofr_comm* c;
+  const ofr_knn_shard* shards;
+  bool armed = true;
+  ~SyncAll() {
+    if (!armed) return;
+    for (int p = 0; p < c->ndev; ++p)
+      if (hipSetDevice(c->devices[p]) == hipSuccess) (void)hipStreamSynchronize((hipStream_t)shards[p].stream);
+  }
+};
 
 }  // namespace comm
 }  // namespace ofr
@@ -342,51 +368,109 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
   };
   int rc = exchange(B, nullptr, true);
   if (rc) return rc;
-  // 4: the queries no tier certified -> the exact fp32 pass on every shard, exchanged and merged
-  std::vector<int> cert((size_t)B);
-  hipError_t e = hipSetDevice(c->devices[0]);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(cert.data(), shards[0].cert, (size_t)B * 4, hipMemcpyDeviceToHost,
-                                (hipStream_t)shards[0].stream);
-  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)shards[0].stream);
-  if (e != hipSuccess) return hip_status(e, "ofr_knn_sharded: certificate readback");
-  std::vector<int64_t> rows;
-  for (int64_t b = 0; b < B; ++b)
-    if (!cert[(size_t)b]) rows.push_back(b);
-  const int64_t n = (int64_t)rows.size();
-  if (n == 0) return OFR_OK;
-  std::vector<const int64_t*> rows_dev(P);
+  // 4: the queries the fp6 tier left open go down the chain on every shard: f6x2, int8 x2, exact fp32;
+  //    each stage searches their rows, exchanges the lists (with its bound) and certifies again
+  enum Stage { F6X2 = 1, Q8X2 = 2, F32 = 3 };
+  bool have_f6x2 = true, have_q8x2 = true;
   for (int p = 0; p < P; ++p) {
-    const ofr_knn_shard& s = shards[p];
-    e = hipSetDevice(c->devices[p]);
-    if (e != hipSuccess) return hip_status(e, "hipSetDevice");
-    char* ws = (char*)s.workspace;
-    int64_t* rd = (int64_t*)(ws + L[p].rows);
-    e = hipMemcpyAsync(rd, rows.data(), (size_t)n * 8, hipMemcpyHostToDevice, (hipStream_t)s.stream);
-    if (e != hipSuccess) return hip_status(e, "ofr_knn_sharded: rows upload");
-    rows_dev[p] = rd;
-    float* sq = (float*)(ws + L[p].sub_q);
-    hipLaunchKernelGGL(comm::gather_rows_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)s.stream, s.Q, s.ldq, rd,
-                       n, sq);
-    OFR_LAUNCH_CHECK("gather_rows_kernel");
-    double* ld_ = (double*)(ws + L[p].loc_d);
-    int64_t* li_ = (int64_t*)(ws + L[p].loc_i);
-    rc = ofr_knn_f32(s.stream, OFR_METRIC_EUCLIDEAN, sq, n, s.ldq, s.G, s.N, s.ldg, d, s.aux, k, s.index_base, ld_, li_,
-                     ws + L[p].knn, ofr_knn_workspace_bytes(n, s.N, k));
-    if (rc) return rc;
-    hipLaunchKernelGGL(comm::pack_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)s.stream, ld_, li_,
-                       (const double*)nullptr, n, k, (double*)(ws + L[p].send));
-    OFR_LAUNCH_CHECK("pack_kernel");
+    have_f6x2 = have_f6x2 && shards[p].Gt2 && shards[p].gscale2 && shards[p].gmax2;
+    have_q8x2 = have_q8x2 && shards[p].G8 && shards[p].gscale8 && shards[p].gmax8 &&
+                shards[p].ld8 >= 2 * round_up(d, 64) && shards[p].ld8 <= 2 * round_up(shards[p].ldq, 64);
   }
-  // the exact pass leaves cert 0 on these rows: 0 = resolved by the exact tier
-  std::vector<const int64_t*> rptr(rows_dev.begin(), rows_dev.end());
-  rc = exchange(n, rptr.data(), false);
+  int64_t* counts = shards[0].tier_counts;
+  if (counts)
+    for (int j = 0; j < 4; ++j) counts[j] = -1;
+  comm::SyncAll guard{c, shards};
+  std::vector<int> cert((size_t)B);
+  std::vector<int64_t> rows((size_t)B);
+  for (int64_t b = 0; b < B; ++b) rows[(size_t)b] = b;
+  int64_t n = B;
+  auto open_rows = [&]() -> int {   // rows whose certificate (device 0's copy) is 0, in place
+    hipError_t e = hipSetDevice(c->devices[0]);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(cert.data(), shards[0].cert, (size_t)B * 4, hipMemcpyDeviceToHost, (hipStream_t)shards[0].stream);
+    for (int p = 0; p < P && e == hipSuccess; ++p) {   // every stream done with the rows uploaded from `rows`
+      e = hipSetDevice(c->devices[p]);
+      if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)shards[p].stream);
+    }
+    if (e != hipSuccess) return hip_status(e, "ofr_knn_sharded: certificate readback");
+    int64_t m = 0;
+    for (int64_t j = 0; j < n; ++j)
+      if (!cert[(size_t)rows[(size_t)j]]) rows[(size_t)m++] = rows[(size_t)j];
+    n = m;
+    return OFR_OK;
+  };
+  rc = open_rows();
   if (rc) return rc;
+  if (counts) counts[0] = n;
+  for (int stage : {(int)F6X2, (int)Q8X2, (int)F32}) {
+    if (n == 0) break;
+    if (stage == F6X2 && !have_f6x2) continue;
+    if (stage == Q8X2 && !have_q8x2) continue;
+    if (stage != F32 && n <= 32) continue;   // a handful of queries: the exact streaming pass is as cheap
+    std::vector<const int64_t*> rows_dev(P);
+    for (int p = 0; p < P; ++p) {
+      const ofr_knn_shard& s = shards[p];
+      hipError_t e = hipSetDevice(c->devices[p]);
+      if (e != hipSuccess) return hip_status(e, "hipSetDevice");
+      const hipStream_t st = (hipStream_t)s.stream;
+      char* ws = (char*)s.workspace;
+      int64_t* rd = (int64_t*)(ws + L[p].rows);
+      e = hipMemcpyAsync(rd, rows.data(), (size_t)n * 8, hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) return hip_status(e, "ofr_knn_sharded: rows upload");
+      rows_dev[p] = rd;
+      float* sq = (float*)(ws + L[p].sub_q);
+      hipLaunchKernelGGL(comm::gather_rows_kernel, dim3((unsigned)n), dim3(256), 0, st, s.Q, s.ldq, rd, n, sq);
+      OFR_LAUNCH_CHECK("gather_rows_kernel");
+      double* ld_ = (double*)(ws + L[p].loc_d);
+      int64_t* li_ = (int64_t*)(ws + L[p].loc_i);
+      double* lb_ = (double*)(ws + L[p].bound);
+      int* lc_ = (int*)(ws + L[p].scert);
+      float* qs = (float*)(ws + L[p].qscale);
+      double* qst = (double*)(ws + L[p].qstats);
+      if (stage == F6X2) {
+        rc = ofr_f6x2_quantize_rows(s.stream, sq, n, d, s.ldq, ws + L[p].qt1, ws + L[p].qt2, L[p].tiles_bytes, qs, qst,
+                                    nullptr, nullptr);
+        if (rc) return rc;
+        rc = ofr_knn_f6x2(s.stream, 3, sq, n, s.ldq, ws + L[p].qt1, ws + L[p].qt2, qs, qst, s.G, s.N, s.ldg, d, s.Gt,
+                          s.Gt2, s.gscale2, s.aux, s.gmax2, k, s.index_base, ld_, li_, lc_, lb_, ws + L[p].knn,
+                          ofr_knn_f6_workspace_bytes(n, s.N));
+      } else if (stage == Q8X2) {
+        // the query slices share the gallery's row layout (ofr_knn_q8 takes one ld for both)
+        rc = ofr_q8_quantize_rows(s.stream, 2, sq, n, d, s.ldq, (int8_t*)(ws + L[p].q8), s.ld8, qs, qst, nullptr,
+                                  nullptr);
+        if (rc) return rc;
+        rc = ofr_knn_q8(s.stream, 3, 2, sq, n, s.ldq, (const int8_t*)(ws + L[p].q8), qs, qst, s.G, s.N, s.ldg, d, s.G8,
+                        s.ld8, s.gscale8, s.aux, s.gmax8, k, s.index_base, ld_, li_, lc_, lb_, ws + L[p].knn,
+                        ofr_knn_q8_workspace_bytes(n, s.N));
+      } else {
+        rc = ofr_knn_f32(s.stream, OFR_METRIC_EUCLIDEAN, sq, n, s.ldq, s.G, s.N, s.ldg, d, s.aux, k, s.index_base, ld_,
+                         li_, ws + L[p].knn, ofr_knn_workspace_bytes(n, s.N, k));
+      }
+      if (rc) return rc;
+      hipLaunchKernelGGL(comm::pack_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, ld_, li_,
+                         stage == F32 ? (const double*)nullptr : (const double*)lb_, n, k, (double*)(ws + L[p].send));
+      OFR_LAUNCH_CHECK("pack_kernel");
+    }
+    // the exact pass leaves cert 0 on its rows (0 = resolved by the exact tier); a quantized tier
+    // writes its global certificate there
+    std::vector<const int64_t*> rptr(rows_dev.begin(), rows_dev.end());
+    rc = exchange(n, rptr.data(), stage != F32);
+    if (rc) return rc;
+    if (stage == F32) {
+      if (counts) counts[3] = n;
+      break;
+    }
+    rc = open_rows();
+    if (rc) return rc;
+    if (counts) counts[stage] = n;
+  }
   // every device's stream must finish its reads of `rows` (host vector) before it goes out of scope
   for (int p = 0; p < P; ++p) {
-    e = hipSetDevice(c->devices[p]);
+    hipError_t e = hipSetDevice(c->devices[p]);
     if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)shards[p].stream);
     if (e != hipSuccess) return hip_status(e, "ofr_knn_sharded: stream sync");
   }
+  guard.armed = false;
   return OFR_OK;
 }

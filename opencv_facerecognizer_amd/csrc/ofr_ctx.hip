@@ -132,6 +132,7 @@ extern "C" int ofr_project_u8(ofr_ctx* c, void* stream, const uint8_t* X, int64_
   OFR_CHECK_ARG((flags & ~(OFR_FP64_ACC | OFR_PROJ_REUSE_W)) == 0, "ofr_project_u8: unknown flags");
   if (B == 0) return OFR_OK;
   OFR_CHECK_ARG(X && W && Y, "ofr_project_u8: null pointer");
+  OFR_DEVICE_GUARD(c->device, "ofr_project_u8: set device");
   hipStream_t st = (hipStream_t)stream;
   const int64_t ldk = round_up(D, 128);
   const size_t aq = ofr_qproj_bytes(D, d);
@@ -139,6 +140,9 @@ extern "C" int ofr_project_u8(ofr_ctx* c, void* stream, const uint8_t* X, int64_
   const bool reuse = (flags & OFR_PROJ_REUSE_W) && c->proj && c->proj_W == W && c->proj_D == D && c->proj_d == d;
   int rc;
   if (!reuse) {
+    // the cache names W only once its slices are complete: a failed grow / prepare below must not
+    // leave an older W's name on a half-overwritten projection
+    c->proj_W = nullptr;
     // W [D][d] -> W^T [d][D] in the scratch, then the int8 slices into the context's projection
     rc = ctxk::grow(&c->ws, &c->cap, ctxk::up((size_t)d * D * 4), st);
     if (rc) return rc;
@@ -187,6 +191,7 @@ extern "C" int ofr_gram(ofr_ctx* c, void* stream, const float* A, int64_t rows, 
                     (prec == OFR_DT_F32 || prec == OFR_DT_F64),
                 "ofr_gram: bad arguments");
   OFR_CHECK_ARG(A && G, "ofr_gram: null pointer");
+  OFR_DEVICE_GUARD(c->device, "ofr_gram: set device");
   hipStream_t st = (hipStream_t)stream;
   const int64_t n = side == OFR_GRAM_ATA ? cols : rows;
   const size_t s_a = 0, s_g = ctxk::up((size_t)rows * cols * 8);
@@ -215,6 +220,7 @@ extern "C" int ofr_scatter(ofr_ctx* c, void* stream, const float* F, const int32
   OFR_CHECK_ARG(c, "ofr_scatter: null context");
   OFR_CHECK_ARG(N >= 1 && d >= 1 && ncls >= 1, "ofr_scatter: bad sizes");
   OFR_CHECK_ARG(F && y && Sw && Sb, "ofr_scatter: null pointer");
+  OFR_DEVICE_GUARD(c->device, "ofr_scatter: set device");
   hipStream_t st = (hipStream_t)stream;
   // labels -> class-grouped row order (host: one read of y, as the reference iterates range(c))
   std::vector<int32_t> yh((size_t)N);
@@ -239,6 +245,7 @@ extern "C" int ofr_scatter(ofr_ctx* c, void* stream, const float* F, const int32
   int rc = ctxk::grow(&c->ws, &c->cap, s_end, st);
   if (rc) return rc;
   char* w = c->ws;
+  ::ofr::StreamSyncGuard uploads(st);   // perm / offsets are read asynchronously until the stream syncs
   e = hipMemcpyAsync(w + s_perm, perm.data(), (size_t)N * 8, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(w + s_off, offsets.data(), (size_t)(ncls + 1) * 8, hipMemcpyHostToDevice, st);
@@ -261,6 +268,7 @@ extern "C" int ofr_scatter(ofr_ctx* c, void* stream, const float* F, const int32
   if (rc) return rc;
   // the host vectors above were uploaded asynchronously: finish before they go out of scope
   e = hipStreamSynchronize(st);
+  uploads.disarm();
   return e == hipSuccess ? OFR_OK : hip_status(e, "ofr_scatter: sync");
 }
 
@@ -274,6 +282,7 @@ extern "C" int ofr_knn(ofr_ctx* c, void* stream, int metric, const float* Q, int
   if (k < 1 || k > OFR_MAX_K) return fail(OFR_E_UNSUPPORTED, "ofr_knn: k must be in [1, 16]");
   if (B == 0) return OFR_OK;
   OFR_CHECK_ARG(Q && G && out_d && out_i, "ofr_knn: null pointer");
+  OFR_DEVICE_GUARD(c->device, "ofr_knn: set device");
   hipStream_t st = (hipStream_t)stream;
   const bool chi = metric == OFR_METRIC_CHISQUARE;
   const int64_t ld = chi ? round_up(d, 4) : round_up(d, 32);
@@ -328,6 +337,7 @@ extern "C" int ofr_knn(ofr_ctx* c, void* stream, int metric, const float* Q, int
     if (n) {
       const size_t x_knn = ofr_chi2_workspace_bytes(n, N, k);
       char* x = c->ws + s_end;
+      ::ofr::StreamSyncGuard upload(st);   // `open` is read asynchronously until the stream syncs
       e = hipMemcpyAsync(x + x_rows, open.data(), (size_t)n * 8, hipMemcpyHostToDevice, st);
       if (e != hipSuccess) return hip_status(e, "ofr_knn: rows upload");
       hipLaunchKernelGGL(ctxk::rows_kernel<float>, dim3((unsigned)n), dim3(256), 0, st, Qp, ld,
@@ -343,6 +353,7 @@ extern "C" int ofr_knn(ofr_ctx* c, void* stream, int metric, const float* Q, int
                          (int64_t)k, (const int64_t*)(x + x_rows), n, out_i, 1);
       OFR_LAUNCH_CHECK("rows_kernel");
       e = hipStreamSynchronize(st);   // `open` is read by the upload above
+      upload.disarm();
       if (e != hipSuccess) return hip_status(e, "ofr_knn: sync");
     }
   }

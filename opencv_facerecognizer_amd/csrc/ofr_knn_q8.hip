@@ -1315,6 +1315,16 @@ constexpr int F6_NW = 8;
 // copy lead) is the fastest, 22.5 against 23.3 ms for 0.
 constexpr int F6S_MODE = 1024 + 4096 + 8192;
 
+// name of the fp6 sieve kernel ofr_knn_f6 launches for B > 32, as rocprofv3 reports it (bench.py
+// labels its roofline entry with it, so the record names the variant that actually ran)
+static int f6_shape();
+extern "C" const char* ofr_f6_sieve_kernel(void) {
+  static const std::string names[2] = {
+      "q8s::tile_kernel_f6s<" + std::to_string(F6S_MODE) + ", 1> (16x16x128 fp6 engine)",
+      "q8s::tile_kernel_f6<" + std::to_string(F6_NW) + ", 8> (32x32x64 fp6 engine)"};
+  return names[f6_shape() == 16 ? 0 : 1].c_str();
+}
+
 // MFMA shape of the sieve pass: 16 = v_mfma_scale_f32_16x16x128 (f6t::Engine16, default),
 // 32 = the 32x32x64 engine (OFR_F6_SHAPE=32)
 static int f6_shape() {

@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from .. import _lib
-from .._device import Chi2Gallery, FloatGallery
+from .._device import Chi2Gallery, FloatGallery, counts_of, infer_count_denom
 from .distance import EuclideanDistance
 
 
@@ -103,10 +103,10 @@ class NearestNeighbor(AbstractClassifier):
     def search(self, Q, k=None):
         """Top-k gallery rows of every query: (distances fp64 [B,k], gallery indices int64 [B,k]) on host."""
         k = int(self.k if k is None else k)
-        Qd, B = self._queries(Q)
+        Qd, B, g = self._queries(Q)
         if B == 0:
             return np.zeros((0, k)), np.zeros((0, k), np.int64)
-        dist, idx = self._search_device(Qd, k)
+        dist, idx = self._search_device(Qd, k, g)
         return dist.cpu().numpy(), idx.cpu().numpy()
 
     # -- device state ----------------------------------------------------------
@@ -118,7 +118,8 @@ class NearestNeighbor(AbstractClassifier):
         return mid
 
     def _invalidate(self):
-        self.__dict__.pop("_dev", None)
+        for key in ("_dev", "_dev_f32", "_chi2_denom"):
+            self.__dict__.pop(key, None)
 
     # -- multi-GPU ---------------------------------------------------------------
     def shard(self, group=None):
@@ -149,7 +150,7 @@ class NearestNeighbor(AbstractClassifier):
         n0, n1 = shard_range(n, rank, ws)
         feats = self._stack(self.X[n0:n1])
         if mid == _lib.METRIC_CHISQUARE:
-            g = Chi2Gallery(feats)
+            g = self._chi2_gallery(feats)
         else:
             # the same centre on every rank: the mean of all rows, from the host copy every rank holds
             shift = self._stack(self.X).mean(0) if mid == _lib.METRIC_EUCLIDEAN else None
@@ -180,13 +181,28 @@ class NearestNeighbor(AbstractClassifier):
                 if n0 == n:
                     return g
                 if 0 < n0 < n and g.N == n0:
-                    g.append(self._stack(self.X[n0:]))
-                    self.__dict__["_dev"] = (key, n, g)
-                    return g
+                    try:
+                        g.append(self._stack(self.X[n0:]))
+                    except TypeError:      # a counts gallery and rows that are not counts: rebuild below
+                        pass
+                    else:
+                        self.__dict__["_dev"] = (key, n, g)
+                        return g
             feats = self._stack(self.X) if n else np.zeros((0, 1))
-            g = Chi2Gallery(feats) if mid == _lib.METRIC_CHISQUARE else FloatGallery(feats, mid)
+            g = self._chi2_gallery(feats) if mid == _lib.METRIC_CHISQUARE else FloatGallery(feats, mid)
             self.__dict__["_dev"] = (key, n, g)
             return g
+
+    def _chi2_gallery(self, feats):
+        """ChiSquare gallery of host rows: the LBP spatial histograms (count / cell, feature.py:298-299)
+        are held as their integer counts (exact, a quarter of the fp32 bytes); anything else as fp32."""
+        hint = self.__dict__.get("_chi2_denom")
+        denom = hint if hint is not None else (infer_count_denom(feats) if len(feats) else None)
+        got = counts_of(feats, denom) if denom else None
+        if got is None:
+            return Chi2Gallery(feats)
+        self.__dict__["_chi2_denom"] = denom
+        return Chi2Gallery.from_counts(got[0], got[1], denom)
 
     def adopt_device_rows(self, F):
         """Seed the device gallery from fp64 device rows F [N][d] equal to self.X (e.g. the training
@@ -197,6 +213,35 @@ class NearestNeighbor(AbstractClassifier):
         with _DEVICE_LOCK:
             g = FloatGallery(F, mid)
             self.__dict__["_dev"] = ((mid, id(self.X), _lib.device()), len(self.X), g)
+
+    def adopt_device_counts(self, C, cell, count_bytes):
+        """Seed the ChiSquare gallery from device counts C [N][nbins] whose histograms (C / cell) are
+        self.X (SpatialHistogram.compute just produced them on the device): no float64 upload."""
+        mid = self._metric()
+        if mid != _lib.METRIC_CHISQUARE or int(C.shape[0]) != len(self.X) or self._shard_info() is not None:
+            return
+        with _DEVICE_LOCK:
+            g = Chi2Gallery.from_counts(C, count_bytes, float(cell))
+            self.__dict__["_chi2_denom"] = float(cell)
+            self.__dict__["_dev"] = ((mid, id(self.X), _lib.device()), len(self.X), g)
+
+    def search_counts(self, C, cell, count_bytes, k=None):
+        """LBPH queries as device counts C [B][nbins] of `cell`-pixel cells (SpatialHistogram.counts_batch):
+        the counts go straight to a counts gallery of the same cell size; otherwise (a float gallery,
+        another cell size) the histograms C / cell take the host path.  -> (distances, indices) device."""
+        k = int(self.k if k is None else k)
+        g = self._gallery()
+        B = int(C.shape[0])
+        if B and len(self.X) and int(C.shape[1]) != g.nbins:
+            raise ValueError(f"query dimension {int(C.shape[1])} does not match the gallery")
+        if (isinstance(g, Chi2Gallery) and g.count_bytes == count_bytes and g.denom == float(cell)
+                and B and g.N):
+            Qd = C if C.shape[1] % (16 // count_bytes) == 0 else Chi2Gallery.from_counts(C, count_bytes, cell).G
+            return self._search_device(Qd.contiguous(), k, g)
+        from .._device import counts_numpy
+        H = counts_numpy(C, count_bytes).astype(np.float64) / float(cell)
+        d, i = self.search(H, k)
+        return torch.from_numpy(d), torch.from_numpy(i)
 
     @staticmethod
     def _stack(items):
@@ -211,10 +256,31 @@ class NearestNeighbor(AbstractClassifier):
         B = arr.shape[0]
         if B and len(self.X) and arr.shape[1] != (g.nbins if isinstance(g, Chi2Gallery) else g.d):
             raise ValueError(f"query dimension {arr.shape[1]} does not match the gallery")
-        return g.query_rows(arr), B
+        Qd = g.query_rows(arr)
+        if Qd is None:                 # ChiSquare: counts gallery, rows that are not counts / denom
+            g = self._float_twin()
+            Qd = g.query_rows(arr)
+        return Qd, B, g
 
-    def _search_device(self, Qd, k):
+    def _float_twin(self):
+        """fp32 copy of a counts ChiSquare gallery (built once) for queries that are not counts."""
         g = self._gallery()
+        tw = self.__dict__.get("_dev_f32")
+        if tw is None or tw[0] is not g or tw[1] != g.N:
+            feats = self._stack(self.X[:g.N]) if self._shard_info() is None else None
+            if feats is None:
+                from ..parallel import shard_range
+                _, rank, ws = self._shard_info()
+                n0, n1 = shard_range(len(self.X), rank, ws)
+                feats = self._stack(self.X[n0:n1])
+            t = Chi2Gallery(feats)
+            t.index_base = getattr(g, "index_base", 0)
+            tw = (g, g.N, t)
+            self.__dict__["_dev_f32"] = tw
+        return tw[2]
+
+    def _search_device(self, Qd, k, g=None):
+        g = g or self._gallery()
         with _DEVICE_LOCK:
             sh = self._shard_info()
             return g.search(Qd, k) if sh is None else self._search_sharded(g, Qd, k, sh)
@@ -225,7 +291,7 @@ class NearestNeighbor(AbstractClassifier):
         from ..parallel import certify_sharded, exchange_topk, merge_sharded, merge_topk
         group, _, ws = sh
         B = int(Qd.shape[0])
-        n0 = g.index_base
+        n0 = getattr(g, "index_base", 0)
         if isinstance(g, FloatGallery) and g.metric == _lib.METRIC_EUCLIDEAN and g.use_q8(B, k):
             qq = g.quantize_queries(Qd, tier=g.first_tier())
             out = g.search_q8_phase(1, Qd, qq, k, n0)
@@ -248,8 +314,8 @@ class NearestNeighbor(AbstractClassifier):
 
     def __getstate__(self):
         st = dict(self.__dict__)
-        st.pop("_dev", None)
-        st.pop("_shard", None)
+        for key in ("_dev", "_shard", "_dev_f32", "_chi2_denom"):   # derived state, never pickled
+            st.pop(key, None)
         return st
 
     def __repr__(self):

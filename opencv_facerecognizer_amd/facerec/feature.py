@@ -500,7 +500,14 @@ from .lbp import ExtendedLBP, LocalDescriptor  # noqa: E402  (feature.py:263)
 
 
 class SpatialHistogram(AbstractFeature):
-    """feature.py:266-305: per-cell LBP histograms, concatenated row-major over the grid."""
+    """feature.py:266-305: per-cell LBP histograms, concatenated row-major over the grid.
+
+    The histograms are integer counts on the device (one ``ofr_elbp_hist`` launch per batch of
+    same-sized faces); the float64 histograms the reference API returns are count / (py * px),
+    which is exactly what numpy's ``np.histogram(..., density=True)`` gives for one cell
+    (feature.py:298-299).  ``compute`` leaves the device counts for the classifier
+    (``PredictableModel.compute``): the LBPH gallery stays resident as counts, never rebuilt from
+    the float64 list."""
 
     def __init__(self, lbp_operator=ExtendedLBP(), sz=(8, 8)):
         AbstractFeature.__init__(self)
@@ -510,7 +517,10 @@ class SpatialHistogram(AbstractFeature):
         self.sz = sz
 
     def compute(self, X, y):
-        return list(self.histograms(X))
+        feats, dev = self._histograms(X, keep_device=True)
+        if dev is not None:      # one face size: the counts go to the classifier's device gallery
+            self.__dict__["_dev_features"] = (id(feats), dev)
+        return feats
 
     def extract(self, X):
         return self.histograms([X])[0]
@@ -528,12 +538,25 @@ class SpatialHistogram(AbstractFeature):
         counts, cell, cb = _device.elbp_hist(_device.u8_images(imgs), self.lbp_operator.geometry(), tuple(self.sz))
         return counts, cell, cb
 
+    def counts_batch(self, X):
+        """Faces of one size (list, array [n][H][W] or a uint8 device tensor such as ``ingest.faces``
+        returns) -> (counts [n][cells * 2^P] device tensor, cell pixel count, bytes per count), one
+        launch.  The histogram of face i is counts[i] / cell."""
+        counts, cell, cb = self.counts_device(X if hasattr(X, "device") else list(X))
+        return counts.reshape(counts.shape[0], -1), cell, cb
+
     def histograms(self, X):
         """List of images -> list of float64 histograms = count/(py*px) (np.histogram density, :298-299)."""
+        return self._histograms(X)[0]
+
+    def _histograms(self, X, keep_device=False):
+        if hasattr(X, "device"):          # a device face batch [n][H][W]
+            X = X.cpu().numpy()
         if len(X) == 0:
-            return []
+            return [], None
         shapes = {np.asarray(x).shape for x in X}
         out = [None] * len(X)
+        dev = None
         for shp in shapes:   # images of one size per launch
             sel = [i for i, x in enumerate(X) if np.asarray(x).shape == shp]
             counts, cell, cb = self.counts_device([X[i] for i in sel])
@@ -542,7 +565,14 @@ class SpatialHistogram(AbstractFeature):
                 h = c.astype(np.float64) / float(cell)
             for j, i in enumerate(sel):
                 out[i] = h[j]
-        return out
+            if keep_device and len(shapes) == 1 and cell > 0:
+                dev = ("counts", counts.reshape(len(sel), -1), cell, cb)
+        return out, dev
+
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st.pop("_dev_features", None)      # derived device state, never pickled
+        return st
 
     def __repr__(self):
         return "SpatialHistogram (operator=%s, grid=%s)" % (repr(self.lbp_operator), str(self.sz))

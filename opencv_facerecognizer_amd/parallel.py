@@ -31,8 +31,8 @@ def shard_range(N, rank, world_size):
 
 
 def gather_rows(x, group=None):
-    """All-gather equal-size row blocks (dim 0) of every rank, rank-major: [G * rows, ...]."""
-    _, ws = world()
+    """All-gather equal-size row blocks (dim 0) of every rank of `group`, rank-major: [G * rows, ...]."""
+    _, ws = world(group)
     if ws == 1:
         return x
     x = x.contiguous()
@@ -66,7 +66,7 @@ class PendingRows:
 def gather_rows_async(x, group=None):
     """Start gather_rows(x) and return a PendingRows (the query rows' all-gather overlaps the
     quantized tile pass, which reads only the gathered fp6 / int8 query tiles)."""
-    _, ws = world()
+    _, ws = world(group)
     if ws == 1:
         return PendingRows(x)
     x = x.contiguous()
@@ -94,7 +94,7 @@ def merge_topk(gd, gi, nlists, kin, k):
 def sharded_search(local_search, k, group=None):
     """local_search(k) -> (d, i) on this rank's shard with global indices; returns the global top-k."""
     d, i = local_search(k)
-    _, ws = world()
+    _, ws = world(group)
     gd, gi = exchange_topk(d, i, group)
     return merge_topk(gd, gi, ws, k, k)
 
@@ -295,16 +295,20 @@ class DeviceComm:
     def __exit__(self, *exc):
         self.close()
 
-    def knn(self, galleries, queries, k):
+    def knn(self, galleries, queries, k, tiers=("f6x2", 2)):
         """galleries[r]: the FloatGallery of shard r (on devices[r], global row offset in
         .index_base, default 0 for one shard); queries[r]: the centred fp32 query rows [B][ld] on
-        devices[r] (the same batch on every device).  Returns per device (out_d, out_i, cert)."""
+        devices[r] (the same batch on every device).  tiers: the finer stages the open queries may
+        take before the exact pass ("f6x2" and / or 2 = int8 x2; built on the galleries if missing).
+        Returns per device (out_d, out_i, cert); self.last_tier_counts = open queries after fp6,
+        after f6x2, after int8 x2, and the number the exact pass ran (-1: stage not run)."""
         import ctypes
         from . import _lib
         lib = _lib.load()
         B, d = int(queries[0].shape[0]), galleries[0].d
         shards = (_lib.KnnShard * len(galleries))()
-        keep = []
+        counts = np.full(4, -1, dtype=np.int64)
+        keep = [counts]
         for r, (g, Qd) in enumerate(zip(galleries, queries)):
             with torch.cuda.device(Qd.device):
                 qq = g.quantize_queries(Qd, tier="f6")
@@ -323,6 +327,16 @@ class DeviceComm:
                 s.index_base = int(getattr(g, "index_base", 0))
                 s.workspace, s.workspace_bytes = ws.data_ptr(), nbytes
                 s.out_d, s.out_i, s.cert = out_d.data_ptr(), out_i.data_ptr(), cert.data_ptr()
+                if "f6x2" in tiers:
+                    t2 = g._tier_gallery("f6x2")
+                    s.Gt2, s.gscale2, s.gmax2 = t2["Gs2"].data_ptr(), t2["scale"].data_ptr(), t2["gmax"].data_ptr()
+                if 2 in tiers:
+                    t8 = g._tier_gallery(2)
+                    s.G8, s.ld8 = t8["Gs"].data_ptr(), t8["ld"]
+                    s.gscale8, s.gmax8 = t8["scale"].data_ptr(), t8["gmax"].data_ptr()
+                if r == 0:
+                    s.tier_counts = counts.ctypes.data
                 keep.append((qq, ws, out_d, out_i, cert))
         _lib.call("ofr_knn_sharded", self.handle, ctypes.cast(shards, ctypes.c_void_p), B, d, k)
-        return [(o[2], o[3], o[4]) for o in keep]
+        self.last_tier_counts = [int(x) for x in counts]
+        return [(o[2], o[3], o[4]) for o in keep[1:]]

@@ -169,6 +169,120 @@ def test_config2_sharded_overflow_rank_not_certified():
 
 
 # ---------------------------------------------------------------------------
+# configs[2] at full size: 1M x 9999 gallery in two 500k shards, B = 4096
+# ---------------------------------------------------------------------------
+C2 = dict(N=1_000_000, per=10, side=100, d=9999, B=4096, k=1)
+
+
+def _c2_setup(dev):
+    from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_projection
+    n_ids = C2["N"] // C2["per"]
+    P, _ = build_projection(C2["side"] ** 2, C2["d"], dev)
+    bank = IdentityBank(n_ids, C2["side"], C2["side"], device=dev)
+    gq = torch.Generator(device=dev)
+    gq.manual_seed(SEED + 7)
+    ids_q = torch.randint(0, n_ids, (C2["B"],), generator=gq, device=dev)
+    return P, bank, ids_q, bank.images(ids_q, seed=SEED + 99)
+
+
+def _c2_worker(rank, ws, port, out):
+    """bench.py's sharded step on one rank: gallery rows [r N/G, (r+1) N/G), this rank's block of the
+    query batch projected + quantized and all-gathered, the fp6 tile pass, the pruned split merge,
+    the global certificate and the collective fallback chain."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from opencv_facerecognizer_amd._device import round_up
+        from opencv_facerecognizer_amd.parallel import certify_sharded, gather_rows, merge_sharded, shard_range
+        from opencv_facerecognizer_amd.synthetic import build_gallery
+        dev = torch.device("cuda", 0)
+        N, d, B, k = C2["N"], C2["d"], C2["B"], C2["k"]
+        P, bank, ids_q, Xq = _c2_setup(dev)
+        n0, n1 = shard_range(N, rank, ws)
+        g = build_gallery(P, bank, C2["per"], n0, n1 - n0, N, d, max(32, round_up(d, 32)), dev)
+        print(f"config2 rank {rank}: shard of {g.N} rows built", flush=True)
+        b0, b1 = shard_range(B, rank, ws)
+        Qd_loc = P.project(Xq[b0:b1], shift64=g.shift64)
+        qq = g.gather_queries(g.quantize_queries(Qd_loc, tier="f6"))
+        Qd = gather_rows(Qd_loc)
+        g.search_q8_phase(1, Qd, qq, k, n0)
+        out_ = (torch.empty((B, k), dtype=torch.float64, device=dev), torch.empty((B, k), dtype=torch.int64, device=dev))
+        merge_sharded(g, Qd, qq, k, n0, out_)
+        (md, mi), counts = certify_sharded(g, Qd, qq, k, out_, n0)
+        kept = g.sieve_counts(B)
+        torch.cuda.synchronize()
+        out.put((rank, md.cpu().numpy(), mi.cpu().numpy(), counts, g.N, int(kept.max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def _c2_exact_top1(sample):
+    """float64 top-1 of the sampled queries over the WHOLE 1M gallery (the reference's features,
+    feature.py:241-242, exact projection in fp64), streamed in chunks: ||g||^2 - 2 q.g on the host
+    (numpy BLAS) shortlists 32 rows per chunk, distance.py:60 (the oracle) ranks the shortlist."""
+    from opencv_facerecognizer_amd.synthetic import gallery_centre, gallery_chunks
+    dev = torch.device("cuda", 0)
+    P, bank, ids_q, Xq = _c2_setup(dev)
+    centre = gallery_centre(P, bank, C2["per"], C2["N"], dev)
+    Q = P.project(Xq[torch.from_numpy(sample).to(dev)], shift64=centre, f64=True).cpu().numpy()
+    best_d = np.full(len(sample), np.inf)
+    best_i = np.full(len(sample), -1, np.int64)
+    second = np.full(len(sample), np.inf)
+    for c0, Y in gallery_chunks(P, bank, C2["per"], 0, C2["N"], C2["N"], centre, f64=True):
+        if c0 % (16 * 8192) == 0:
+            print(f"config2 oracle: gallery rows {c0}/{C2['N']}", flush=True)   # progress (long test)
+        G = Y.cpu().numpy()
+        S = np.einsum("ij,ij->i", G, G)[None, :] - 2.0 * (Q @ G.T)
+        cand = np.argpartition(S, 32, axis=1)[:, :32]
+        for b in range(len(sample)):
+            for j in cand[b]:
+                dj = O.euclidean(G[j].reshape(-1, 1), Q[b].reshape(-1, 1))
+                if dj < best_d[b] or (dj == best_d[b] and c0 + j < best_i[b]):
+                    second[b] = best_d[b]
+                    best_d[b], best_i[b] = dj, c0 + j
+                elif dj < second[b]:
+                    second[b] = dj
+    return best_i, best_d, second, ids_q.cpu().numpy()
+
+
+@pytest.mark.timeout(1200)
+def test_config2_full_size_two_rank_sharded():
+    """BASELINE configs[2] at its own size through bench.py's sharded step: 2 gloo ranks on the box's
+    one device, each holding 500,000 of the 1,000,000 rows (d = 9,999), a 4,096-face batch.
+    Properties on the whole batch (both ranks return the same global top-1, uncertified counts,
+    identity accuracy) and 64 sampled queries against the float64 top-1 over the whole gallery
+    (classifier.py:104-119 + distance.py:57-60), with the near-tie rule of _check_search."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c2_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        item = q.get(timeout=900)
+        res[item[0]] = item[1:]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (md0, mi0, c0_, n_0, kept0), (md1, mi1, c1_, n_1, kept1) = res[0], res[1]
+    assert n_0 == n_1 == C2["N"] // 2
+    assert np.array_equal(mi0, mi1) and np.array_equal(md0, md1)     # the global result on both ranks
+    assert list(c0_) == list(c1_) and c0_[0] <= C2["B"] // 100, c0_  # identity data: fp6 certifies ~all
+    assert max(kept0, kept1) <= 32768
+    sample = np.random.default_rng(6).choice(C2["B"], 64, replace=False)
+    ri, rd, r2, ids_q = _c2_exact_top1(sample)
+    acc = float(np.mean(mi0[:, 0] // C2["per"] == ids_q))
+    assert acc >= 0.99, acc
+    near = (r2 - rd) <= 1e-4 * rd
+    assert np.all((mi0[sample, 0] == ri) | near), (mi0[sample, 0], ri)
+    assert np.allclose(md0[sample, 0], rd, rtol=1e-4, atol=0)
+
+
+# ---------------------------------------------------------------------------
 # configs[4]: training
 # ---------------------------------------------------------------------------
 def _faces(n, ids, side, seed):
@@ -216,23 +330,47 @@ def test_config4_training_4k_vs_oracle():
     assert np.array_equal(labels[:64], y[ri])
 
 
-@pytest.mark.timeout(900)
-def test_config4_training_full_100k(monkeypatch):
-    """Full configs[4]: 100,000 faces of 10,000 identities, D = 10,000 -> W 10,000 x 9,999 (symmetric-
-    definite LDA solve: the reference's general eig of a 9,999^2 matrix takes hours on the host)."""
+@pytest.mark.timeout(1200)
+def test_config4_training_full_100k_default_solver_vs_eigh(monkeypatch):
+    """Full configs[4]: 100,000 faces of 10,000 identities, D = 10,000 -> W 10,000 x 9,999, trained
+    twice: with the DEFAULT solver (OFR_LDA_SOLVER=auto: above order 1024 the pencil
+    Sb v = lambda Sw v on the device, rocSOLVER dsygvd -- the path behind configs[4]'s timing) and
+    with the host LAPACK pencil (scipy sygvd).  feature.py:170-176 asks for the eigenpairs of
+    inv(Sw) Sb; both solvers give the same pencil's, columns at unit 2-norm.  Checked: the
+    eigenvalues agree, the W columns of well-separated eigenvalues agree up to sign
+    (|cos| > 1 - 1e-6), the resubstitution labels of the two models are equal, and fresh faces are
+    recognised."""
     from ocvfacerec.facerec.classifier import NearestNeighbor
     from ocvfacerec.facerec.distance import EuclideanDistance
     from ocvfacerec.facerec.feature import Fisherfaces
     from ocvfacerec.facerec.model import PredictableModel
-    monkeypatch.setenv("OFR_LDA_SOLVER", "eigh")
     n, c, side = 100_000, 10_000, 100
     X, y = _faces(n, c, side, 20261015 + 21)
-    model = PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=1))
-    model.compute(list(X), y)
-    W = np.asarray(model.feature._eigenvectors)
-    assert W.shape == (side * side, c - 1) and np.isfinite(W).all()
+    Xl = list(X)
+    models = {}
+    for solver in ("auto", "eigh"):
+        print(f"config4: training with OFR_LDA_SOLVER={solver}", flush=True)   # progress (long test)
+        monkeypatch.setenv("OFR_LDA_SOLVER", solver)
+        model = PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=1))
+        model.compute(Xl, y)
+        W = np.asarray(model.feature._eigenvectors)
+        assert W.shape == (side * side, c - 1) and np.isfinite(W).all(), solver
+        models[solver] = model
+    Wa, We = (np.asarray(models[s].feature._eigenvectors) for s in ("auto", "eigh"))
+    ea, ee = (np.asarray(models[s].feature._eigenvalues, np.float64) for s in ("auto", "eigh"))
+    assert np.allclose(ea, ee, rtol=1e-4, atol=1e-6 * ee.max())
+    gap = np.minimum(np.abs(np.diff(np.r_[np.inf, ee])), np.abs(np.diff(np.r_[ee, -np.inf])))
+    ok = gap > 1e-3 * ee.max()
+    cos = np.abs(np.einsum("ij,ij->j", Wa, We)) / (np.linalg.norm(Wa, axis=0) * np.linalg.norm(We, axis=0))
+    assert ok.sum() >= 3 and np.all(cos[ok] > 1 - 1e-6), (ok.sum(), cos[ok].min())
+    # resubstitution (every 6th training face, 4,096 per batch): equal labels under both models
+    sel = np.arange(0, n, 6)
+    lab = {s: np.concatenate([[p[0] for p in models[s].predict_batch(X[sel[i:i + 4096]])]
+                              for i in range(0, len(sel), 4096)]) for s in models}
+    assert np.array_equal(lab["auto"], lab["eigh"])
+    assert np.mean(lab["auto"] == y[sel]) >= 0.999
     Xq, yq = _faces(4096, c, side, 20261015 + 24)
-    labels = np.array([p[0] for p in model.predict_batch(Xq)])
+    labels = np.array([p[0] for p in models["auto"].predict_batch(Xq)])
     assert np.mean(labels == yq) >= 0.99
 
 

@@ -876,11 +876,14 @@ def test_topk_merge_certify_kernel():
     assert rc.min() == 0 and rc.max() == 1
 
 
-@pytest.mark.parametrize("data", ["separated", "sphere"])
+@pytest.mark.parametrize("data", ["separated", "sphere", "crowded"])
 def test_knn_sharded_c_abi_one_device(monkeypatch, data):
     """ofr_comm_init_all + ofr_knn_sharded (single process, RCCL) on this box's one device: the fp6
-    tier, the all-gather, the global certificate and the exact fallback of uncertified queries, against
-    the oracle.  'sphere' (equidistant rows) leaves every query uncertified, forcing the fallback."""
+    tier, the all-gather, the global certificate and the tier chain of uncertified queries (f6x2,
+    int8 x2, exact fp32), against the oracle.  'sphere' (equidistant rows) leaves every query
+    uncertified by every quantized tier, forcing the exact pass; 'crowded' (tight clusters) is
+    certified by f6x2 after fp6 fails -- with the same per-tier counts as the single-process
+    chain (FloatGallery.search)."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
     from opencv_facerecognizer_amd.parallel import DeviceComm
@@ -889,19 +892,37 @@ def test_knn_sharded_c_abi_one_device(monkeypatch, data):
         protos = r.normal(0, 30, (300, 96))
         G = (protos[np.arange(3000) % 300] + r.normal(0, 5, (3000, 96)))
         Q = (protos[r.integers(0, 300, 100)] + r.normal(0, 5, (100, 96)))
-    else:
+    elif data == "sphere":
         c = r.normal(0, 50, 64)
         U = r.normal(0, 1, (2000, 64))
         G = c + 100.0 * U / np.linalg.norm(U, axis=1, keepdims=True)
         Q = c + r.normal(0, 1e-6, (100, 64))
+    else:   # test_knn_f6x2_certifies_crowded_clusters' data
+        r = _rng(3)
+        mu = r.normal(0, 1, (200, 128))
+        G = mu[np.arange(8000) % 200] + r.normal(0, 0.5, (8000, 128))
+        Q = mu[r.integers(0, 200, 300)] + r.normal(0, 0.5, (300, 128))
     G = G.astype(np.float32).astype(np.float64)
     Q = Q.astype(np.float32).astype(np.float64)
+    k = 3 if data != "crowded" else 1
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     with DeviceComm([0]) as comm:
-        (dd, ii, cert), = comm.knn([g], [g.query_rows(Q)], 3)
-    _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), 3)
+        (dd, ii, cert), = comm.knn([g], [g.query_rows(Q)], k)
+        counts = comm.last_tier_counts
+    _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
     c = cert.cpu().numpy()
-    assert (c.min() == 1) if data == "separated" else (c.max() == 0)
+    if data == "separated":
+        assert c.min() == 1 and counts == [0, -1, -1, -1]
+    elif data == "sphere":
+        assert c.max() == 0 and counts[0] == len(Q) and counts[3] == counts[2] == counts[1] == len(Q), counts
+    else:
+        monkeypatch.setenv("OFR_SEARCH", "auto")
+        g.search(g.query_rows(Q), k)                    # the single-process chain on the same gallery
+        fb = list(g.last_fallbacks)
+        assert counts[0] >= 0.9 * len(Q) and counts[1] <= 0.02 * len(Q), counts
+        assert counts[:2] == fb[:2], (counts, fb)
+        # cert 0 marks exactly the queries the exact pass resolved
+        assert int((c == 0).sum()) == max(counts[3], 0), (counts, int((c == 0).sum()))
 
 
 def _spd(r, n, extra=0.2):

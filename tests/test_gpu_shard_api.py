@@ -96,7 +96,9 @@ def _worker(rank, ws, port, out):
         model = PredictableModel(ff, _classifier("EuclideanDistance"))
         model.classifier.compute([ff.project(x.reshape(-1, 1)) for x in X[:-64]], yf[:-64])
         model.shard()
-        res["model"] = ([p[0] for p in model.predict_batch(list(X[-64:]))], model.search_batch(list(X[-64:]))[1])
+        sd, si = model.search_batch(list(X[-64:]))
+        res["model"] = ([p[0] for p in model.predict_batch(list(X[-64:]))], si)
+        res["model_d"] = sd
         torch.cuda.synchronize()
         out.put((rank, res))
     finally:
@@ -160,8 +162,19 @@ def test_sharded_classifier_equals_oracle(sharded, metric, B):
     ref = [p[0] for p in clf.predict_batch(Q[:B])]
     dr, ir = clf.search(Q[:B])
     same = (ir == i0).all(1)
-    assert same.mean() >= 0.98, same.mean()                     # differences only at oracle near-ties
+    # the unsharded result differs only where the oracle has near-ties at the differing ranks
+    _agree_except_near_ties(metric, Q[:B], G, i0, ir)
     assert [a for a, s in zip(lab0, same) if s] == [b for b, s in zip(ref, same) if s]
+
+
+def _agree_except_near_ties(metric, Q, G, ia, ib, near_rel=1e-4):
+    """Two top-k index lists of the same queries agree except where the oracle distances of the
+    differing rows are within near_rel of each other (SURVEY §8c's near-tie rule, as _check_search)."""
+    D = O.pairwise(metric, Q, G)
+    for b in np.nonzero(~(ia == ib).all(1))[0]:
+        for j in np.nonzero(ia[b] != ib[b])[0]:
+            a, c = D[b, ia[b, j]], D[b, ib[b, j]]
+            assert abs(a - c) <= near_rel * max(abs(c), 1e-300) + 1e-6 * np.linalg.norm(Q[b]), (b, j, a, c)
 
 
 @pytest.mark.timeout(600)
@@ -179,12 +192,13 @@ def test_sharded_predictable_model(sharded):
     ff._num_components = W.shape[1]
     model = PredictableModel(ff, _classifier("EuclideanDistance"))
     model.classifier.compute([ff.project(x.reshape(-1, 1)) for x in X[:-64]], yf[:-64])
-    ref = model.search_batch(list(X[-64:]))[1]
-    assert (ref == idx0).all(1).mean() >= 0.98
-    # against the float64 oracle on the projected features
+    dref, ref = model.search_batch(list(X[-64:]))
+    # against the float64 oracle on the projected features (feature.py:241-242 in fp64), and the
+    # unsharded model, both with the near-tie rule
     F = np.stack([np.asarray(ff.project(x.reshape(-1, 1))).reshape(-1) for x in X])
-    Dref = O.pairwise("EuclideanDistance", F[-64:], F[:-64])
-    assert (np.argsort(Dref, 1, kind="stable")[:, 0] == idx0[:, 0]).mean() >= 0.98
+    _agree_except_near_ties("EuclideanDistance", F[-64:], F[:-64], idx0, ref)
+    d0 = sharded[0]["model_d"]
+    _check_search("EuclideanDistance", F[-64:], F[:-64], d0, idx0, K)
 
 
 @pytest.mark.timeout(600)

@@ -383,3 +383,53 @@ def test_gather_queries_packs_scales_and_stats():
         s, st = r.random(256).astype(np.float32), r.random((256, 3))
         assert np.array_equal(scale[256 * rank:256 * (rank + 1)], s)
         assert np.array_equal(stats[256 * rank:256 * (rank + 1)], st)
+
+
+def _subgroup_worker(rank, ws, port, out):
+    """Ranks 0 and 2 of a 3-rank job form a sub-group; every collective of parallel.py runs on it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from opencv_facerecognizer_amd.parallel import sharded_search
+        grp = dist.new_group([0, 2])          # every rank takes part in the creation
+        if rank in (0, 2):
+            gr, gws = world(grp)
+            assert gws == 2 and gr == (0 if rank == 0 else 1)
+            x = torch.arange(12, dtype=torch.float32).reshape(4, 3) + 100 * gr
+            g = gather_rows(x, grp)
+            g2 = gather_rows_async(x, grp)()
+            Q, G = _data()
+            n0, n1 = shard_range(len(G), gr, gws)
+
+            def local(k):
+                d, i = O.nn_search_vectorized("EuclideanDistance", Q, G[n0:n1], k)
+                return torch.from_numpy(d), torch.from_numpy(i + n0)
+
+            import opencv_facerecognizer_amd.parallel as par
+            par.merge_topk = _host_merge
+            md, mi = sharded_search(local, 2, grp)
+            if gr == 0:
+                out.put((g.numpy(), g2.numpy(), md.numpy(), mi.numpy()))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collectives_on_a_sub_group():
+    """gather_rows / gather_rows_async / sharded_search take the sub-group's size, not the world's
+    (NearestNeighbor.shard(group) records a sub-group's rank and size): 2 of 3 ranks, exact results."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    g, g2, md, mi = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    base = np.arange(12, dtype=np.float32).reshape(4, 3)
+    assert np.array_equal(g, np.concatenate([base, base + 100])) and np.array_equal(g2, g)
+    Q, G = _data()
+    ref_d, ref_i = O.nn_search_vectorized("EuclideanDistance", Q, G, 2)
+    assert np.array_equal(mi, ref_i) and np.array_equal(md, ref_d)
