@@ -268,16 +268,18 @@ int ofr_elbp_codes(void* stream, const uint8_t* imgs, int64_t n, int H, int W, i
 /* counts: [n][gr*gc][2^P] of `count_bytes` (1, 2 or 4) unsigned integers;
  * cell (r,c) covers code rows [r*py,(r+1)*py) x cols [c*px,(c+1)*px),
  * py = floor(dy/gr), px = floor(dx/gc).  The float histogram of the
- * reference is count / (py*px) exactly (np.histogram density=True).  P <= 15. */
-int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H, int W, int P,
-                  const int32_t* offs_host, const double* w_host, int oy, int ox, int by, int bx,
-                  int gr, int gc, void* counts, int count_bytes);
+ * reference is count / (py*px) exactly (np.histogram density=True).  P <= 15.
+ * (The geometry form the package binds; SURVEY §8b's context form is
+ * ofr_elbp_hist, declared with the other context entry points below.)      */
+int ofr_elbp_hist_geom(void* stream, const uint8_t* imgs, int64_t n, int H, int W, int P,
+                       const int32_t* offs_host, const double* w_host, int oy, int ox, int by, int bx,
+                       int gr, int gc, void* counts, int count_bytes);
 
 /* Chi-square search ----------------------------------------------------------
  * Replaces ChiSquareDistance distance.py:112-116 inside NearestNeighbor.predict.
  * Q [B][ldq], G [N][ldg] rows of `nbins` values of type dtype (OFR_DT_*); the
  * reference value of an element is x / denom (denom = py*px for the counts
- * of ofr_elbp_hist, whose float histogram is count/(py*px); 1.0 for fp32).
+ * of ofr_elbp_hist / ofr_elbp_hist_geom, whose float histogram is count/(py*px); 1.0 for fp32).
  * Rows must be 16-byte aligned.  Coarse fp32 VALU pass + exact fp64
  * re-evaluation of the reference formula on the best candidates; outputs as
  * ofr_knn_f32.  cert (nullable, [B]): 1 iff the result is provably the exact
@@ -478,7 +480,15 @@ int ofr_sygv_f64(void* stream, int64_t n, double* Sb, double* Sw, int64_t m, dou
  *   Cosine: exact fp64 re-rank of the fp32-MFMA candidates; ChiSquare: the
  *   certified fp32 pass + exact fp64 pass for the rest, values used as given);
  *   g_norms nullable (EUCLIDEAN: ||g||^2, COSINE: 1/||g||, as ofr_row_aux);
- *   out_d fp32 [B][k] (distance.py values), out_i int64 [B][k] (+ index_base). */
+ *   out_d fp32 [B][k] (distance.py values), out_i int64 [B][k] (+ index_base).
+ * ofr_elbp_hist: ExtendedLBP codes + SpatialHistogram counts (lbp.py:80-130,
+ *   feature.py:286-302) of uint8 faces imgs [n][H][W]; host arrays w [P][4] fp64
+ *   and off [P][4] int32 = (fy, fx, cy, cx) of each sample point RELATIVE TO THE CENTRE
+ *   pixel (floor / ceil of the reference's sample point, lbp.py:84-121); the
+ *   block origin and size follow from them as in lbp.py:90-97.  counts uint8
+ *   [n][gr*gc][2^P] (cells of at most 255 pixels, else OFR_E_UNSUPPORTED: use
+ *   ofr_elbp_hist_geom with wider counts); the reference histogram is
+ *   count / (py*px).                                                             */
 typedef struct ofr_ctx ofr_ctx;
 enum { OFR_FP64_ACC = 1, OFR_PROJ_REUSE_W = 2 };
 enum { OFR_GRAM_ATA = 0, OFR_GRAM_AAT = 1 };
@@ -492,6 +502,8 @@ int ofr_scatter(ofr_ctx* ctx, void* stream, const float* F, const int32_t* y, in
 int ofr_knn(ofr_ctx* ctx, void* stream, int metric, const float* Q, int64_t B, const float* G,
             const float* g_norms_or_null, int64_t N, int64_t d, int k, int64_t index_base, float* out_d,
             int64_t* out_i);
+int ofr_elbp_hist(ofr_ctx* ctx, void* stream, const uint8_t* imgs, int64_t n, int H, int W, const double* w,
+                  const int32_t* off, int P, int gr, int gc, uint8_t* counts);
 
 #ifdef __cplusplus
 }

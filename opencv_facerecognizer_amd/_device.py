@@ -788,7 +788,7 @@ def elbp_hist(imgs_u8, geom, grid, count_bytes=None):
     out = torch.empty((n, gr * gc, 1 << P), dtype=tdt, device=imgs_u8.device)
     offs32 = np.ascontiguousarray(offs, dtype=np.int32)
     w64 = np.ascontiguousarray(wts, dtype=np.float64)
-    call("ofr_elbp_hist", stream(), ptr(imgs_u8), n, H, W, P, offs32.ctypes.data_as(_lib.c_vp),
+    call("ofr_elbp_hist_geom", stream(), ptr(imgs_u8), n, H, W, P, offs32.ctypes.data_as(_lib.c_vp),
          w64.ctypes.data_as(_lib.c_vp), oy, ox, by, bx, gr, gc, ptr(out), count_bytes)
     return out, cell, count_bytes
 

@@ -75,8 +75,9 @@ SIGNATURES = {
     "ofr_topk_merge": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp]),
     "ofr_elbp_codes": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                c_vp]),
-    "ofr_elbp_hist": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
-                              c_int, c_int, c_vp, c_int]),
+    "ofr_elbp_hist_geom": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                   c_int, c_int, c_vp, c_int]),
+    "ofr_elbp_hist": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "ofr_chi2_workspace_bytes": (c_sz, [c_i64, c_i64, c_int]),
     "ofr_chi2_knn": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_dbl, c_int, c_i64, c_vp,
                              c_vp, c_vp, c_sz, c_vp]),

@@ -8,6 +8,7 @@
 //   ofr_scatter    -> ofr_class_center_f64 + two ofr_gemm_f64 (feature.py:160-168)
 //   ofr_knn        -> ofr_knn_f32 (Euclidean / Cosine, fp32 MFMA tiles + exact fp64 re-rank) or
 //                     ofr_chi2_knn + ofr_chi2_knn_exact for the queries it leaves uncertified
+//   ofr_elbp_hist  -> ofr_elbp_hist_geom (centre-relative sample offsets -> block geometry)
 // A context belongs to one device and one thread at a time (the reference's calls are
 // synchronous per caller); calls on it are ordered on the stream they are given.
 #include <vector>
@@ -360,4 +361,34 @@ extern "C" int ofr_knn(ofr_ctx* c, void* stream, int metric, const float* Q, int
   hipLaunchKernelGGL(ctxk::narrow_f64_kernel, dim3(ctxk::blocks(B * k)), dim3(256), 0, st, od, B * (int64_t)k, out_d);
   OFR_LAUNCH_CHECK("narrow_f64_kernel");
   return OFR_OK;
+}
+
+extern "C" int ofr_elbp_hist(ofr_ctx* c, void* stream, const uint8_t* imgs, int64_t n, int H, int W, const double* w,
+                             const int32_t* off, int P, int gr, int gc, uint8_t* counts) {
+  OFR_CHECK_ARG(c, "ofr_elbp_hist: null context");
+  OFR_CHECK_ARG(w && off, "ofr_elbp_hist: null geometry");
+  OFR_CHECK_ARG(P >= 1 && P <= 15, "ofr_elbp_hist: neighbors must be in [1, 15]");
+  OFR_CHECK_ARG(H >= 1 && W >= 1 && gr >= 1 && gc >= 1 && n >= 0, "ofr_elbp_hist: bad sizes");
+  // lbp.py:90-97 from the centre-relative floor / ceil offsets: the block spans
+  // [min(0, min floor), max(0, max ceil)] on each axis and the centre sits at -min(0, min floor)
+  int y0 = 0, x0 = 0, y1 = 0, x1 = 0;
+  for (int i = 0; i < P; ++i) {
+    y0 = std::min(y0, off[4 * i + 0]);
+    x0 = std::min(x0, off[4 * i + 1]);
+    y1 = std::max(y1, off[4 * i + 2]);
+    x1 = std::max(x1, off[4 * i + 3]);
+  }
+  const int oy = -y0, ox = -x0, by = y1 - y0 + 1, bx = x1 - x0 + 1;
+  std::vector<int32_t> boff((size_t)P * 4);
+  for (int i = 0; i < P; ++i) {
+    boff[(size_t)(4 * i + 0)] = off[4 * i + 0] + oy;
+    boff[(size_t)(4 * i + 1)] = off[4 * i + 1] + ox;
+    boff[(size_t)(4 * i + 2)] = off[4 * i + 2] + oy;
+    boff[(size_t)(4 * i + 3)] = off[4 * i + 3] + ox;
+  }
+  const int dy = H - by + 1, dx = W - bx + 1;
+  const int64_t cell = (int64_t)(dy > 0 ? dy / gr : 0) * (dx > 0 ? dx / gc : 0);
+  if (cell > 255) return fail(OFR_E_UNSUPPORTED, "ofr_elbp_hist: cells of more than 255 pixels need ofr_elbp_hist_geom");
+  OFR_DEVICE_GUARD(c->device, "ofr_elbp_hist: set device");
+  return ofr_elbp_hist_geom(stream, imgs, n, H, W, P, boff.data(), w, oy, ox, by, bx, gr, gc, counts, 1);
 }

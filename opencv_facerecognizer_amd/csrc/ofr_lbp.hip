@@ -365,12 +365,12 @@ extern "C" int ofr_elbp_codes(void* stream, const uint8_t* imgs, int64_t n, int 
   return OFR_OK;
 }
 
-extern "C" int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H, int W, int P,
+extern "C" int ofr_elbp_hist_geom(void* stream, const uint8_t* imgs, int64_t n, int H, int W, int P,
                              const int32_t* offs_host, const double* w_host, int oy, int ox, int by, int bx, int gr,
                              int gc, void* counts, int count_bytes) {
-  OFR_CHECK_ARG(n >= 0 && H >= 1 && W >= 1 && gr >= 1 && gc >= 1, "ofr_elbp_hist: bad sizes");
-  OFR_CHECK_ARG(count_bytes == 1 || count_bytes == 2 || count_bytes == 4, "ofr_elbp_hist: count_bytes must be 1, 2 or 4");
-  if (P > 15) return fail(OFR_E_UNSUPPORTED, "ofr_elbp_hist: neighbors must be <= 15 for the LDS histogram");
+  OFR_CHECK_ARG(n >= 0 && H >= 1 && W >= 1 && gr >= 1 && gc >= 1, "ofr_elbp_hist_geom: bad sizes");
+  OFR_CHECK_ARG(count_bytes == 1 || count_bytes == 2 || count_bytes == 4, "ofr_elbp_hist_geom: count_bytes must be 1, 2 or 4");
+  if (P > 15) return fail(OFR_E_UNSUPPORTED, "ofr_elbp_hist_geom: neighbors must be <= 15 for the LDS histogram");
   LbpGeom g;
   int rc = make_geom(g, H, W, P, offs_host, w_host, oy, ox, by, bx);
   if (rc) return rc;
@@ -383,10 +383,10 @@ extern "C" int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H
   a.count_bytes = count_bytes;
   const int64_t nb = 1LL << P;
   const int64_t cell_px = (int64_t)a.py * a.px;
-  if (count_bytes == 1) OFR_CHECK_ARG(cell_px <= 255, "ofr_elbp_hist: cell too large for 1-byte counts");
-  if (count_bytes == 2) OFR_CHECK_ARG(cell_px <= 65535, "ofr_elbp_hist: cell too large for 2-byte counts");
+  if (count_bytes == 1) OFR_CHECK_ARG(cell_px <= 255, "ofr_elbp_hist_geom: cell too large for 1-byte counts");
+  if (count_bytes == 2) OFR_CHECK_ARG(cell_px <= 65535, "ofr_elbp_hist_geom: cell too large for 2-byte counts");
   if (n == 0) return OFR_OK;
-  OFR_CHECK_ARG(imgs && counts, "ofr_elbp_hist: null pointer");
+  OFR_CHECK_ARG(imgs && counts, "ofr_elbp_hist_geom: null pointer");
   hipStream_t st = (hipStream_t)stream;
   if (cell_px == 0) {  // empty cells: all counts zero (the reference's histogram is then NaN)
     hipError_t e = hipMemsetAsync(counts, 0, (size_t)n * gr * gc * nb * count_bytes, st);
@@ -424,7 +424,7 @@ extern "C" int ofr_elbp_hist(void* stream, const uint8_t* imgs, int64_t n, int H
   const int64_t lds_cap = 64 * 1024;  // bytes of u32 counters per workgroup
   const int64_t row_bytes = (int64_t)gc * nb * 4;
   if (row_bytes > lds_cap) {
-    return fail(OFR_E_UNSUPPORTED, "ofr_elbp_hist: grid_cols * 2^P too large for one LDS band");
+    return fail(OFR_E_UNSUPPORTED, "ofr_elbp_hist_geom: grid_cols * 2^P too large for one LDS band");
   }
   a.rows_per_wg = (int)std::max<int64_t>(1, std::min<int64_t>(gr, lds_cap / row_bytes));
   const unsigned gx = (unsigned)cdiv(gr, a.rows_per_wg);

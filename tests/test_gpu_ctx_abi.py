@@ -112,3 +112,26 @@ def test_knn(ctx, metric):
     Qd, Gd = _dev(Q.astype(np.float32)), _dev(G.astype(np.float32))
     call("ofr_knn", ctx, stream(), m, ptr(Qd), B, ptr(Gd), None, N, d, k, 0, ptr(od), ptr(oi))
     _check_search(metric, Q, G, od.cpu().numpy().astype(np.float64), oi.cpu().numpy(), k, near_rel=2e-4)
+
+
+@pytest.mark.parametrize("r,P,grid,shape", [(1, 8, (8, 8), (128, 128)), (2, 8, (4, 5), (61, 93)), (3, 4, (7, 7), (70, 70))])
+def test_elbp_hist(ctx, r, P, grid, shape):
+    """SURVEY §8b's ofr_elbp_hist(ctx, stream, imgs, n, H, W, w[P][4], off[P][4], P, gr, gc, counts): the sample
+    offsets relative to the centre pixel (lbp.py:84-121 before the block origin is added), uint8 counts,
+    bit-exact against the oracle's ExtendedLBP + per-cell histogram counts (feature.py:286-302)."""
+    from opencv_facerecognizer_amd._lib import c_vp, call, ptr, stream
+    from opencv_facerecognizer_amd.facerec.lbp import elbp_geometry
+    (oy, ox), _, offs, wts = elbp_geometry(r, P)
+    off_c = np.ascontiguousarray(offs - np.array([oy, ox, oy, ox], np.int32), dtype=np.int32)
+    w = np.ascontiguousarray(wts, dtype=np.float64)
+    g = _rng(63)
+    imgs = g.integers(0, 256, (12,) + shape, dtype=np.uint8)
+    imgs[:4] = (imgs[:4] // 64) * 64 + 31                   # tie-heavy
+    gr, gc = grid
+    out = torch.empty((12, gr * gc, 1 << P), dtype=torch.uint8, device="cuda")
+    call("ofr_elbp_hist", ctx, stream(), ptr(_dev(imgs)), 12, shape[0], shape[1], w.ctypes.data_as(c_vp),
+         off_c.ctypes.data_as(c_vp), P, gr, gc, ptr(out))
+    got = out.cpu().numpy().astype(np.int64)
+    for i in range(12):
+        ref, _ = O.spatial_histogram_counts(O.elbp(imgs[i], r, P), P, grid)
+        assert np.array_equal(got[i], ref), i

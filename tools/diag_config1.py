@@ -25,7 +25,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gallery", type=int, default=100_000)
     ap.add_argument("--ids", type=int, default=100_000, help="identities in the bank (bench: 1M / 10)")
+    ap.add_argument("--bench-loop", type=int, default=0,
+                    help="instead: bench.stress_run's pipelined step (side-stream preparation) this many times")
     args = ap.parse_args()
+    if args.bench_loop:
+        return bench_loop(args)
     dev = _lib.device()
     D, d, B, k, per = 10000, 9999, 4096, 1, 10
     N = args.gallery
@@ -60,6 +64,20 @@ def main():
         "max_rel_dist_diff_where_rows_differ": float(rel[diff].max()) if int(diff.sum()) else 0.0,
     }
     print(json.dumps(res), flush=True)
+
+
+def bench_loop(args):
+    """bench.py's configs[1] line (stress_run at N = 100k, noise 12) in a fresh process, repeated."""
+    import types
+    import bench
+    dev = _lib.device()
+    P, _ = build_projection(10000, 9999, dev)
+    bank = IdentityBank(args.ids, 100, 100, device=dev)
+    a = types.SimpleNamespace(gallery=1_000_000, per_id=10, batch=4096, dim=9999, k=1, stress_steps=3)
+    for rep in range(args.bench_loop):
+        r = bench.stress_run(P, bank, a, 12.0, dev, N=args.gallery)
+        print(json.dumps({"rep": rep, "queries_per_s": r["queries_per_s"], "uncertified": r["uncertified_after_each_tier"],
+                          "acc": r["top1_identity_acc"], "margin": r["certificate_margin_fp6"]}), flush=True)
 
 
 if __name__ == "__main__":
