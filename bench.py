@@ -178,6 +178,11 @@ def stress_run(P, bank, args, noise, device, N=None):
     side = torch.cuda.Stream(device=device)
     ev_ready, ev_free, ev_tiles = [torch.cuda.Event() for _ in range(2)], [torch.cuda.Event() for _ in range(2)], \
         torch.cuda.Event()
+    # the side stream starts behind everything the main stream has queued (gallery and tier builds, the
+    # query images, the buffers' zero fills): an unrecorded event is no dependency, and once the caching
+    # allocator stops calling hipMalloc (which synchronises) nothing else would order the first preps
+    # (without this, a second stress_run in one process projected stale / half-generated queries)
+    side.wait_stream(main_stream)
 
     def prep(j):
         b = bufs[j]
@@ -287,6 +292,8 @@ def main():
     ev_ready = [torch.cuda.Event() for _ in range(2)]   # buffer j prepared (side stream)
     ev_free = [torch.cuda.Event() for _ in range(2)]    # buffer j's last reader done (main stream)
     ev_tiles = torch.cuda.Event()                        # the latest tile pass done (main stream)
+    if side is not main_stream:
+        side.wait_stream(main_stream)                    # first preps behind the setup work (see stress_run)
 
     def prep(j, events=None):
         """Query batch -> centred fp32 search rows (+ the first tier's quantized rows) in buffer j."""

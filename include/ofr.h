@@ -290,6 +290,12 @@ int ofr_elbp_hist_geom(void* stream, const uint8_t* imgs, int64_t n, int H, int 
  * (the reference formula in every tile; its cert covers the fp32 tile keys).   */
 
 size_t ofr_chi2_workspace_bytes(int64_t B, int64_t N, int k);
+/* uint8 counts (dtype 0, nbins % 64 == 0, 16-byte rows) take a low-rank MFMA coarse pass instead
+ * of the VALU one: (a-c)^2/(a+c) = a + c - 4 ac/(a+c) and ac/(a+c) ~= sum_{r<8} U[a][r] U[c][r]
+ * (an fp16 table, v_mfma_f32_16x16x32_f16), |S - S~| <= bound * (Tq + Tg) in count units with
+ * Tq, Tg the rows' total counts; ofr_chi2_mfma_bound(nbins) returns that factor.
+ * OFR_CHI2_ENGINE=valu keeps the VALU pass.                                    */
+double ofr_chi2_mfma_bound(int64_t nbins);
 int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
                  int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
                  int64_t* out_i, void* workspace, size_t workspace_bytes, int* cert);

@@ -13,6 +13,14 @@
 // kernel then re-evaluates the reference formula EXACTLY in fp64 on the
 // survivors, with p = value/denom (denom = cell pixel count for counts, the
 // reference histogram being count/(py*px)) and eps = 2^-52.
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ofr_f6_tile.h"
+#include "ofr_i8_tile.h"
+#include "ofr_keys.h"
 #include "ofr_topk.h"
 
 namespace ofr {
@@ -249,6 +257,10 @@ struct Chi2MergeArgs {
   int* cert;      // nullable: 1 iff the result is provably the exact fp64 top-k
   double gamma;   // relative error bound of the coarse scores (and their keys)
   double scale;   // coarse score -> reference units (1 / denom for the fp32 pass, 1 for the exact pass)
+  // MFMA pass (abs_c1 > 0): |S - S~| <= abs_c1 (Tq + Tg) in count units, Tq = the query's total
+  // count, Tg <= *tg_max (the gallery's largest row total)
+  double abs_c1;
+  const float* tg_max;
 };
 
 template <int DT, int KC>
@@ -259,6 +271,12 @@ __global__ void __launch_bounds__(256) chi2_merge_rerank_kernel(Chi2MergeArgs p)
   const int64_t q = blockIdx.x;
   select_candidates<KC>(p.cand, p.T, p.B, q, lists);
   const double eps = 2.220446049250313e-16;  // np.finfo('float').eps, distance.py:115
+  double tq = 0;
+  if (p.abs_c1 > 0) {
+    double a = 0;
+    for (int64_t b = threadIdx.x; b < p.nbins; b += blockDim.x) a += load1<DT>(p.Q, q * p.ldq + b);
+    tq = block_sum_f64(a, red);
+  }
   for (int c = 0; c < KC; ++c) {
     const Cand cc = lists[c];
     double val = __builtin_inf();
@@ -287,7 +305,10 @@ __global__ void __launch_bounds__(256) chi2_merge_rerank_kernel(Chi2MergeArgs p)
       const Cand last = lists[KC - 1];
       const double dk = od[kk - 1];
       double bnd = __builtin_inf();
-      if (last.i != CAND_EMPTY) bnd = (double)last.d * p.scale / (1.0 + p.gamma) * (1.0 - 1e-12);
+      if (last.i != CAND_EMPTY && p.abs_c1 > 0)
+        bnd = ((double)last.d - p.abs_c1 * (tq + (double)*p.tg_max)) * p.scale * (1.0 - 1e-12);
+      else if (last.i != CAND_EMPTY)
+        bnd = (double)last.d * p.scale / (1.0 + p.gamma) * (1.0 - 1e-12);
       p.cert[q] = (dk == dk) && (dk < bnd);
     }
   }
@@ -312,14 +333,453 @@ static int chi2_dispatch(hipStream_t st, int kc, const Chi2Args& a, const Chi2Me
   return kc == 8 ? launch_chi2<DT, 8>(st, a, m, exact) : launch_chi2<DT, 16>(st, a, m, exact);
 }
 
+// ---- MFMA coarse pass for uint8 counts (the LBP spatial histograms) -------------------------
+// chi^2 has no bilinear form, but for counts it has a short low-rank one.  Per bin
+//     T(a, c) = (a - c)^2 / (a + c) = (a + c) - 4 F(a, c),   F(a, c) = a c / (a + c)  (0 at a = c = 0)
+// so S(q, g) = sum_b T(a_b, c_b) = Tq + Tg - 4 sum_b F(a_b, c_b) with the row totals Tq, Tg exact.
+// F is a positive semidefinite kernel on 0..255 whose spectrum falls off fast; its eight leading
+// eigenpairs (of the (a+1)^-1/2-weighted matrix, so that the error scales with a + c) give
+// F(a, c) ~= sum_r U[a][r] U[c][r], U an fp16 table [256][8] with U[0] = 0 (exact: F(0, c) = 0).
+// One v_mfma_f32_16x16x32_f16 then sums 4 bins x 8 components for a 16 x 16 block: lane group q
+// (lanes 16q..16q+15) supplies, for its row, the table row of its bin's count, gathered from LDS.
+// Rigorous coarse-score bound (host-computed constants, chi2_table):
+//   |S - S~| <= 4 (eta + gamma kappa)(Tq + Tg) + 2^-22 (Tq + Tg),
+//   eta   = max_{a+c>0} |F(a,c) - sum_r U16[a][r] U16[c][r]| / (a + c)     (rank + fp16 rounding)
+//   kappa = max_{a+c>0} sum_r |U16[a][r] U16[c][r]| / (a + c)              (sum |products| per bin)
+//   gamma = (n_mfma + 64) 2^-23, n_mfma = nbins / 4 per accumulator       (fp32 accumulation, the
+//           fp6 tier's budget: tools/mx_probe.hip measured <= 3 2^-24 per MFMA step)
+// the last term covering the fp32 evaluation of Tq + Tg - 4 acc.  The merge re-ranks the best 16
+// exactly (the reference formula, fp64) and certifies with this absolute bound.
+namespace c2m {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int TG = 256, TQ = 256;          // gallery x query rows per tile
+constexpr int NW = 8, NT = NW * 64;        // 8 waves (2 per SIMD), wave grid 2 (gallery) x 4 (queries)
+constexpr int WQ = 4, QW = 64, NA = 8, NB = 4;   // wave: 128 gallery rows (8 blocks) x 64 queries (4)
+constexpr int BB = 64;                     // bins per LDS stage = 16 MFMA k-steps of 4 bins
+constexpr int PANEL = 256 * BB;            // 16 KiB: 256 rows x 64 count bytes
+constexpr int STAGE = 2 * PANEL;
+constexpr int NST = 3;
+constexpr int TABLE = 256 * 16;            // fp16 [256][8]
+constexpr int LDS = NST * STAGE + TABLE;   // 100 KiB
+constexpr int DMA_INS = STAGE / 1024;      // 32 one-KiB copies per stage
+constexpr int IPW = DMA_INS / NW;          // 4 per wave
+constexpr int KC = keys::KC;               // candidates per (query, tile)
+
+// LDS image of a stage panel: row r's 64 bytes = four 16-byte chunks, chunk g at position
+// g ^ ((r >> 2) & 3), so that the 16 rows a lane group reads hit distinct banks
+__device__ __forceinline__ int off(int row, int chunk) { return row * BB + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+struct Args {
+  const uint8_t* Q;
+  int64_t B, ldq;
+  const uint8_t* G;
+  int64_t N, ldg, nbins;
+  const uint16_t* table;   // fp16 bits [256][8]
+  const float* tq;         // [B] query row totals
+  const float* tg;         // [N] gallery row totals
+  Cand* cand;              // [ntg][B][KC], tile-major
+  int64_t ntq, ntg, gg;
+};
+
+// stage kt (bins [64 kt, 64 kt + 64)) of the tile's gallery rows [g0, g0 + 256) and query rows
+// [q0, q0 + 256) -> LDS stage buffer st; rows past the end re-read the last row (never scored)
+__device__ __forceinline__ void dma(const Args& p, int64_t g0, int64_t q0, int kt, char* st) {
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const int ng = (int)(p.N - g0 < TG ? p.N - g0 : TG), nq = (int)(p.B - q0 < TQ ? p.B - q0 : TQ);
+  __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(p.G + g0 * p.ldg), 0,
+                                                                (int)((int64_t)ng * p.ldg), 0x00020000);
+  __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)(p.Q + q0 * p.ldq), 0,
+                                                                (int)((int64_t)nq * p.ldq), 0x00020000);
+#pragma unroll
+  for (int t = 0; t < IPW; ++t) {
+    const int ins = wave * IPW + t;   // a wave's four copies are all gallery (waves 0-3) or all queries
+    const bool gal = ins < DMA_INS / 2;
+    const int row = (ins & 15) * 16 + (lane >> 2);
+    const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+    const int lim = gal ? ng : nq;
+    const int r = row < lim ? row : lim - 1;
+    const int voff = r * (int)(gal ? p.ldg : p.ldq) + kt * BB + chunk * 16;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(gal ? rg : rq, (OFR_LDS void*)(st + (gal ? 0 : PANEL) + (ins & 15) * 1024),
+                                             16, voff, 0, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(NT, 1) chi2_mfma_kernel(Args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t gt, qt;
+  i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
+  const int64_t g0 = gt * TG, q0 = qt * TQ;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave / WQ, wc = wave % WQ, r16 = lane & 15, lq = lane >> 4;
+  char* tab = smem + NST * STAGE;
+  reinterpret_cast<uint2*>(tab)[threadIdx.x] = reinterpret_cast<const uint2*>(p.table)[threadIdx.x];   // 4 KiB
+  const int nst = (int)(p.nbins / BB), last = nst - 1;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) dma(p, g0, q0, s < last ? s : last, smem + s * STAGE);
+
+  f32x4 acc[NA][NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i)
+#pragma unroll
+    for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ra0 = wr * 128 + r16, rb0 = wc * QW + r16;   // + 16 i / + 16 c
+
+  for (int kt = 0; kt < nst; ++kt) {
+    f6t::wait_vm<IPW>();   // stage kt landed (kt + 1 may be in flight)
+    f6t::barrier();        // ... for every wave; and every wave is done with stage kt - 1's buffer
+    {
+      const int nx = kt + NST - 1;
+      dma(p, g0, q0, nx < last ? nx : last, smem + (nx % NST) * STAGE);
+    }
+    const char* st = smem + (kt % NST) * STAGE;
+#pragma unroll
+    for (int g = 0; g < BB / 16; ++g) {
+      // counts of bins 16 g + 4 lq .. + 3 of every fragment row (one word per row; k-step s uses byte s)
+      uint32_t wa[NA], wb[NB];
+#pragma unroll
+      for (int i = 0; i < NA; ++i) wa[i] = *reinterpret_cast<const uint32_t*>(st + off(ra0 + 16 * i, g) + 4 * lq);
+#pragma unroll
+      for (int c = 0; c < NB; ++c) wb[c] = *reinterpret_cast<const uint32_t*>(st + PANEL + off(rb0 + 16 * c, g) + 4 * lq);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        h8 fa[NA], fb[NB];
+#pragma unroll
+        for (int i = 0; i < NA; ++i) fa[i] = *reinterpret_cast<const h8*>(tab + (((wa[i] >> (8 * s)) & 0xffu) << 4));
+#pragma unroll
+        for (int c = 0; c < NB; ++c) fb[c] = *reinterpret_cast<const h8*>(tab + (((wb[c] >> (8 * s)) & 0xffu) << 4));
+#pragma unroll
+        for (int i = 0; i < NA; ++i)
+#pragma unroll
+          for (int c = 0; c < NB; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[c], acc[i][c], 0, 0, 0);
+      }
+    }
+  }
+  f6t::wait_vm<0>();
+  f6t::barrier();
+
+  // epilogue: S~ = Tq + Tg - 4 acc -> keys; per lane the best KC of its 32 rows for each of its 4
+  // queries, merged over the 4 lane groups (shuffles), then over the two row-waves (LDS)
+  float* tq_l = reinterpret_cast<float*>(smem);                  // [256]
+  float* tg_l = tq_l + TQ;                                       // [256]
+  uint32_t* kbuf = reinterpret_cast<uint32_t*>(smem + 2048);     // [2][256][KC]
+  if (threadIdx.x < TQ) {
+    const int64_t q = q0 + threadIdx.x, g = g0 + threadIdx.x;
+    tq_l[threadIdx.x] = q < p.B ? p.tq[q] : 0.f;
+    tg_l[threadIdx.x] = g < p.N ? p.tg[g] : 0.f;
+  }
+  __syncthreads();
+  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
+  auto epi = [&](auto ctc) {
+    constexpr int c = decltype(ctc)::value;
+    const int ql = wc * QW + 16 * c + r16;
+    const float tqv = tq_l[ql];
+    keys::KeyList L;
+    L.init();
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gl = wr * 128 + 16 * i + 4 * lq + r;   // C/D of 16x16: row 4 (lane / 16) + reg, column lane % 16
+        const float sc = (tqv + tg_l[gl]) - 4.0f * acc[i][c][r];
+        L.insert(gl < nvalid ? keys::score_key(sc, gl) : keys::KEY_NONE);
+      }
+    uint32_t o[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) o[j] = (uint32_t)__shfl_xor((int)L.k[j], 16);
+    L.merge(o);
+#pragma unroll
+    for (int j = 0; j < KC; ++j) o[j] = (uint32_t)__shfl_xor((int)L.k[j], 32);
+    L.merge(o);
+    if (lq == 0) {
+      uint32_t* dst = kbuf + ((size_t)wr * TQ + ql) * KC;
+#pragma unroll
+      for (int j = 0; j < KC; j += 4) *reinterpret_cast<uint4*>(dst + j) = make_uint4(L.k[j], L.k[j + 1], L.k[j + 2], L.k[j + 3]);
+    }
+  };
+  epi(std::integral_constant<int, 0>{});
+  epi(std::integral_constant<int, 1>{});
+  epi(std::integral_constant<int, 2>{});
+  epi(std::integral_constant<int, 3>{});
+  __syncthreads();
+  if ((int)threadIdx.x < TQ) {
+    const int ql = threadIdx.x;
+    const int64_t q = q0 + ql;
+    keys::KeyList L;
+    uint32_t o[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      L.k[j] = kbuf[(size_t)ql * KC + j];
+      o[j] = kbuf[((size_t)TQ + ql) * KC + j];
+    }
+    L.merge(o);
+    if (q < p.B) {
+      Cand* out = p.cand + ((size_t)gt * p.B + q) * KC;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        const uint32_t kk = L.k[j];
+        out[j] = kk == keys::KEY_NONE ? Cand{__builtin_inff(), CAND_EMPTY}
+                                      : Cand{keys::key_score(kk), (int)(g0 + (kk & 0xffu))};
+      }
+    }
+  }
+}
+
+// row totals (exact: < 2^24) and the gallery's largest (float bits are ordered like uints for >= 0)
+__global__ void __launch_bounds__(256) row_total_kernel(const uint8_t* X, int64_t rows, int64_t ld, int64_t nbins,
+                                                        float* tot, unsigned* maxbits) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const uint8_t* x = X + r * ld;
+  uint32_t s = 0;
+  for (int64_t b = (int64_t)lane * 16; b < nbins; b += 64 * 16) {
+    const uint4 v = *reinterpret_cast<const uint4*>(x + b);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += (w[j] & 0xff) + ((w[j] >> 8) & 0xff) + ((w[j] >> 16) & 0xff) + (w[j] >> 24);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) {
+    tot[r] = (float)s;
+    if (maxbits) atomicMax(maxbits, __float_as_uint((float)s));
+  }
+}
+
+}  // namespace c2m
+
+// The fp16 table and its error constants, built once on the host (deterministic): subspace iteration
+// for the 8 leading eigenpairs of Fw[a][c] = F(a, c) / sqrt((a+1)(c+1)), U = sqrt(a+1) V sqrt(L),
+// rounded to fp16, row 0 zero; eta and kappa evaluated exactly (fp64) over all 256 x 256 pairs.
+struct Chi2Table {
+  uint16_t bits[256 * 8];
+  double eta, kappa;
+  uint16_t* dev = nullptr;   // device copy (per process; one device at a time is enough for the table)
+  int dev_id = -1;
+};
+
+static void jacobi_eig(int n, std::vector<double>& A, std::vector<double>& V) {   // A symmetric n x n
+  V.assign((size_t)n * n, 0.0);
+  for (int i = 0; i < n; ++i) V[(size_t)i * n + i] = 1.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0;
+    for (int i = 0; i < n; ++i)
+      for (int j = i + 1; j < n; ++j) off += A[(size_t)i * n + j] * A[(size_t)i * n + j];
+    if (off < 1e-30) break;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = A[(size_t)p * n + q];
+        if (std::fabs(apq) < 1e-300) continue;
+        const double theta = (A[(size_t)q * n + q] - A[(size_t)p * n + p]) / (2 * apq);
+        const double tt = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1));
+        const double cs = 1 / std::sqrt(tt * tt + 1), sn = tt * cs;
+        for (int k = 0; k < n; ++k) {
+          const double akp = A[(size_t)k * n + p], akq = A[(size_t)k * n + q];
+          A[(size_t)k * n + p] = cs * akp - sn * akq;
+          A[(size_t)k * n + q] = sn * akp + cs * akq;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double apk = A[(size_t)p * n + k], aqk = A[(size_t)q * n + k];
+          A[(size_t)p * n + k] = cs * apk - sn * aqk;
+          A[(size_t)q * n + k] = sn * apk + cs * aqk;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double vkp = V[(size_t)k * n + p], vkq = V[(size_t)k * n + q];
+          V[(size_t)k * n + p] = cs * vkp - sn * vkq;
+          V[(size_t)k * n + q] = sn * vkp + cs * vkq;
+        }
+      }
+  }
+}
+
+static Chi2Table& chi2_table() {
+  static Chi2Table T = [] {
+    Chi2Table t{};
+    constexpr int n = 256, R = 8, M = 16;   // M: subspace width
+    std::vector<double> Fm((size_t)n * n);
+    for (int a = 0; a < n; ++a)
+      for (int c = 0; c < n; ++c) {
+        const double s = (double)a + c;
+        Fm[(size_t)a * n + c] = s > 0 ? (double)a * c / s / std::sqrt((a + 1.0) * (c + 1.0)) : 0.0;
+      }
+    auto Fw = [&](int a, int c) { return Fm[(size_t)a * n + c]; };
+    std::vector<double> X((size_t)n * M), Y((size_t)n * M);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < M; ++j) X[(size_t)i * M + j] = std::cos(0.37 * (i + 1) * (j + 1)) + (i == j ? 1.0 : 0.0);
+    std::vector<double> H, W;
+    for (int it = 0; it < 40; ++it) {
+      for (int i = 0; i < n; ++i)   // Y = Fw X
+        for (int j = 0; j < M; ++j) {
+          double acc = 0;
+          for (int k = 0; k < n; ++k) acc += Fw(i, k) * X[(size_t)k * M + j];
+          Y[(size_t)i * M + j] = acc;
+        }
+      for (int j = 0; j < M; ++j) {   // modified Gram-Schmidt on the columns of Y
+        for (int l = 0; l < j; ++l) {
+          double d = 0;
+          for (int i = 0; i < n; ++i) d += Y[(size_t)i * M + j] * Y[(size_t)i * M + l];
+          for (int i = 0; i < n; ++i) Y[(size_t)i * M + j] -= d * Y[(size_t)i * M + l];
+        }
+        double nn = 0;
+        for (int i = 0; i < n; ++i) nn += Y[(size_t)i * M + j] * Y[(size_t)i * M + j];
+        nn = std::sqrt(nn);
+        for (int i = 0; i < n; ++i) Y[(size_t)i * M + j] /= nn;
+      }
+      X.swap(Y);
+    }
+    // Rayleigh-Ritz: H = X^T Fw X, X <- X W (descending eigenvalues)
+    H.assign((size_t)M * M, 0.0);
+    std::vector<double> FX((size_t)n * M);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < M; ++j) {
+        double acc = 0;
+        for (int k = 0; k < n; ++k) acc += Fw(i, k) * X[(size_t)k * M + j];
+        FX[(size_t)i * M + j] = acc;
+      }
+    for (int a = 0; a < M; ++a)
+      for (int b = 0; b < M; ++b) {
+        double acc = 0;
+        for (int i = 0; i < n; ++i) acc += X[(size_t)i * M + a] * FX[(size_t)i * M + b];
+        H[(size_t)a * M + b] = acc;
+      }
+    for (int a = 0; a < M; ++a)
+      for (int b = a + 1; b < M; ++b) H[(size_t)a * M + b] = H[(size_t)b * M + a] = 0.5 * (H[(size_t)a * M + b] + H[(size_t)b * M + a]);
+    jacobi_eig(M, H, W);
+    std::vector<int> ord(M);
+    for (int j = 0; j < M; ++j) ord[j] = j;
+    std::sort(ord.begin(), ord.end(), [&](int x, int y) { return H[(size_t)x * M + x] > H[(size_t)y * M + y]; });
+    double U[n][R];
+    for (int r = 0; r < R; ++r) {
+      const int j = ord[r];
+      const double lam = std::max(H[(size_t)j * M + j], 0.0);
+      for (int i = 0; i < n; ++i) {
+        double v = 0;
+        for (int k = 0; k < M; ++k) v += X[(size_t)i * M + k] * W[(size_t)k * M + j];
+        U[i][r] = i == 0 ? 0.0 : std::sqrt(i + 1.0) * v * std::sqrt(lam);
+      }
+    }
+    double U16[n][R];
+    for (int i = 0; i < n; ++i)
+      for (int r = 0; r < R; ++r) {
+        const _Float16 h = (_Float16)U[i][r];
+        U16[i][r] = (double)h;
+        uint16_t b;
+        std::memcpy(&b, &h, 2);
+        t.bits[i * R + r] = b;
+      }
+    double eta = 0, kappa = 0;
+    for (int a = 0; a < n; ++a)
+      for (int c = 0; c < n; ++c) {
+        if (a + c == 0) continue;
+        double sum = 0, sabs = 0;
+        for (int r = 0; r < R; ++r) {
+          sum += U16[a][r] * U16[c][r];
+          sabs += std::fabs(U16[a][r] * U16[c][r]);
+        }
+        const double F = (double)a * c / ((double)a + c);
+        eta = std::max(eta, std::fabs(F - sum) / (a + c));
+        kappa = std::max(kappa, sabs / (a + c));
+      }
+    t.eta = eta * (1 + 1e-9) + 1e-15;     // fp64 evaluation slack
+    t.kappa = kappa * (1 + 1e-9);
+    return t;
+  }();
+  return T;
+}
+
+static bool chi2_engine_valu() {   // OFR_CHI2_ENGINE=valu: the VALU tile kernel for every dtype
+  static const bool v = [] {
+    const char* e = getenv("OFR_CHI2_ENGINE");
+    return e && std::string(e) == "valu";
+  }();
+  return v;
+}
+
 }  // namespace ofr
 
 using namespace ofr;
 
+// MFMA pass workspace: tile lists [ceil(N/256)][B][16], query / gallery row totals, the largest total
+struct Chi2MWs {
+  size_t lists, tq, tg, tgmax, bytes;
+};
+static Chi2MWs chi2m_ws(int64_t B, int64_t N) {
+  Chi2MWs w;
+  const int64_t T = cdiv(N > 0 ? N : 1, c2m::TG);
+  w.lists = 0;
+  w.tq = round_up((int64_t)((size_t)T * B * c2m::KC * sizeof(Cand)), 256);
+  w.tg = w.tq + round_up(B * 4, 256);
+  w.tgmax = w.tg + round_up((N > 0 ? N : 1) * 4, 256);
+  w.bytes = w.tgmax + 256;
+  return w;
+}
+
 extern "C" size_t ofr_chi2_workspace_bytes(int64_t B, int64_t N, int k) {
   const int kc = pick_kc(k);
   const int64_t T = cdiv(N > 0 ? N : 1, C2X_T);   // the exact pass's 32-row tiles (>= the 64-row ones)
-  return (size_t)T * (size_t)B * kc * sizeof(Cand) + 256;
+  return std::max((size_t)T * (size_t)B * kc * sizeof(Cand) + 256, chi2m_ws(B, N).bytes);
+}
+
+// the MFMA coarse pass (uint8 counts) + the exact re-rank with its absolute certificate
+static int chi2_mfma_run(hipStream_t st, const uint8_t* Q, int64_t B, int64_t ldq, const uint8_t* G, int64_t N,
+                         int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
+                         int64_t* out_i, void* workspace, int* cert) {
+  Chi2Table& tb = chi2_table();
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_status(e, "hipGetDevice");
+  static uint16_t* table_dev[64] = {};
+  static bool attr_done = false;
+  if (dev < 0 || dev >= 64) return fail(OFR_E_UNSUPPORTED, "ofr_chi2_knn: device index >= 64");
+  if (!table_dev[dev]) {   // once per device: 4 KiB, copied synchronously
+    e = hipMalloc((void**)&table_dev[dev], sizeof(tb.bits));
+    if (e == hipSuccess) e = hipMemcpy(table_dev[dev], tb.bits, sizeof(tb.bits), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_status(e, "ofr_chi2_knn: table upload");
+  }
+  if (!attr_done) {
+    e = hipFuncSetAttribute((const void*)c2m::chi2_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c2m::LDS);
+    if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(chi2_mfma)");
+    attr_done = true;
+  }
+  const Chi2MWs w = chi2m_ws(B, N);
+  char* wsb = reinterpret_cast<char*>(workspace);
+  float* tq = reinterpret_cast<float*>(wsb + w.tq);
+  float* tg = reinterpret_cast<float*>(wsb + w.tg);
+  unsigned* tgmax = reinterpret_cast<unsigned*>(wsb + w.tgmax);
+  e = hipMemsetAsync(tgmax, 0, 4, st);
+  if (e != hipSuccess) return hip_status(e, "hipMemsetAsync(tgmax)");
+  hipLaunchKernelGGL(c2m::row_total_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, Q, B, ldq, nbins, tq,
+                     (unsigned*)nullptr);
+  OFR_LAUNCH_CHECK("row_total_kernel");
+  hipLaunchKernelGGL(c2m::row_total_kernel, dim3((unsigned)cdiv(N, 4)), dim3(256), 0, st, G, N, ldg, nbins, tg, tgmax);
+  OFR_LAUNCH_CHECK("row_total_kernel");
+  c2m::Args a;
+  a.Q = Q; a.B = B; a.ldq = ldq; a.G = G; a.N = N; a.ldg = ldg; a.nbins = nbins;
+  a.table = table_dev[dev]; a.tq = tq; a.tg = tg;
+  a.cand = reinterpret_cast<Cand*>(wsb + w.lists);
+  a.ntq = cdiv(B, c2m::TQ);
+  a.ntg = cdiv(N, c2m::TG);
+  a.gg = a.ntg < 4 ? a.ntg : 4;
+  OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_chi2_knn: grid too large");
+  hipLaunchKernelGGL(c2m::chi2_mfma_kernel, dim3((unsigned)(a.ntq * a.ntg)), dim3(c2m::NT), c2m::LDS, st, a);
+  OFR_LAUNCH_CHECK("chi2_mfma_kernel");
+  const double n_mfma = (double)(nbins / 4);
+  const double gamma = (n_mfma + 64.0) * 0x1p-23;
+  Chi2MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, nbins, denom, k, index_base, out_d, out_i, cert, 0.0,
+                  1.0 / denom};
+  m.abs_c1 = 4.0 * (tb.eta + gamma * tb.kappa) + 0x1p-22;
+  m.tg_max = reinterpret_cast<const float*>(tgmax);
+  hipLaunchKernelGGL((chi2_merge_rerank_kernel<DT_U8, c2m::KC>), dim3((unsigned)B), dim3(256), 0, st, m);
+  OFR_LAUNCH_CHECK("chi2_merge_rerank_kernel");
+  return OFR_OK;
+}
+
+extern "C" double ofr_chi2_mfma_bound(int64_t nbins) {
+  Chi2Table& tb = chi2_table();
+  return 4.0 * (tb.eta + ((double)(nbins / 4) + 64.0) * 0x1p-23 * tb.kappa) + 0x1p-22;
 }
 
 static int chi2_run(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
@@ -354,9 +814,14 @@ static int chi2_run(void* stream, int dtype, const void* Q, int64_t B, int64_t l
   // the exact pass's key is its fp64 sum rounded to fp32 (1/2 ulp) plus the fp64 summation.
   const double gamma = exact ? 0x1p-23 + (double)nbins * 0x1p-52
                              : ((double)((nbins + 1) / 2) + 4.0) * 0x1p-24 + (dtype == DT_F32 ? 4.0 : 2.0) * 0x1p-23;
+  hipStream_t st = (hipStream_t)stream;
+  // uint8 counts (LBP spatial histograms): the low-rank MFMA coarse pass (OFR_CHI2_ENGINE=valu: the VALU kernel)
+  if (!exact && dtype == DT_U8 && N > 0 && nbins % c2m::BB == 0 && ldq % 16 == 0 && ldg % 16 == 0 &&
+      !chi2_engine_valu())
+    return chi2_mfma_run(st, (const uint8_t*)Q, B, ldq, (const uint8_t*)G, N, ldg, nbins, denom, k, index_base,
+                         out_d, out_i, workspace, cert);
   Chi2MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, nbins, denom, k, index_base, out_d, out_i, cert, gamma,
                   exact ? 1.0 : 1.0 / denom};
-  hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
     case DT_U8: return chi2_dispatch<DT_U8>(st, kc, a, m, exact);
     case DT_U16: return chi2_dispatch<DT_U16>(st, kc, a, m, exact);
