@@ -296,6 +296,8 @@ size_t ofr_chi2_workspace_bytes(int64_t B, int64_t N, int k);
  * Tq, Tg the rows' total counts; ofr_chi2_mfma_bound(nbins) returns that factor.
  * OFR_CHI2_ENGINE=valu keeps the VALU pass.                                    */
 double ofr_chi2_mfma_bound(int64_t nbins);
+/* the fp16 table U [256][8] (bits) of that pass, host memory (tests re-derive the bound from it) */
+void ofr_chi2_table(uint16_t* out);
 int ofr_chi2_knn(void* stream, int dtype, const void* Q, int64_t B, int64_t ldq, const void* G, int64_t N,
                  int64_t ldg, int64_t nbins, double denom, int k, int64_t index_base, double* out_d,
                  int64_t* out_i, void* workspace, size_t workspace_bytes, int* cert);

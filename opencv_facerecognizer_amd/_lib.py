@@ -80,6 +80,7 @@ SIGNATURES = {
     "ofr_elbp_hist": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "ofr_chi2_workspace_bytes": (c_sz, [c_i64, c_i64, c_int]),
     "ofr_chi2_mfma_bound": (c_dbl, [c_i64]),
+    "ofr_chi2_table": (None, [c_vp]),
     "ofr_chi2_knn": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_dbl, c_int, c_i64, c_vp,
                              c_vp, c_vp, c_sz, c_vp]),
     "ofr_chi2_knn_exact": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_dbl, c_int, c_i64,

@@ -690,12 +690,9 @@ static Chi2Table& chi2_table() {
   return T;
 }
 
-static bool chi2_engine_valu() {   // OFR_CHI2_ENGINE=valu: the VALU tile kernel for every dtype
-  static const bool v = [] {
-    const char* e = getenv("OFR_CHI2_ENGINE");
-    return e && std::string(e) == "valu";
-  }();
-  return v;
+static bool chi2_engine_valu() {   // OFR_CHI2_ENGINE=valu: the VALU tile kernel for every dtype (read per call)
+  const char* e = getenv("OFR_CHI2_ENGINE");
+  return e && std::string(e) == "valu";
 }
 
 }  // namespace ofr
@@ -776,6 +773,8 @@ static int chi2_mfma_run(hipStream_t st, const uint8_t* Q, int64_t B, int64_t ld
   OFR_LAUNCH_CHECK("chi2_merge_rerank_kernel");
   return OFR_OK;
 }
+
+extern "C" void ofr_chi2_table(uint16_t* out) { std::memcpy(out, chi2_table().bits, sizeof(chi2_table().bits)); }
 
 extern "C" double ofr_chi2_mfma_bound(int64_t nbins) {
   Chi2Table& tb = chi2_table();

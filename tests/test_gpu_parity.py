@@ -669,6 +669,45 @@ def test_chi2_certificate_forces_exact_pass():
     _check_search("ChiSquareDistance", Q / 225.0, G / 225.0, dd.cpu().numpy(), ii.cpu().numpy(), 3)
 
 
+@pytest.mark.parametrize("data", ["lbp", "wide"])
+def test_chi2_mfma_pass_equals_valu_pass_and_oracle(monkeypatch, data):
+    """uint8 counts take the low-rank MFMA coarse pass (ofr_chi2.hip, c2m): the exact fp64 re-rank and
+    its absolute certificate must give the oracle's top-k (distance.py:112-116 over the whole gallery),
+    the same as the VALU pass (OFR_CHI2_ENGINE=valu).  'lbp': spatial histograms of 128x128 faces
+    (tile edges: 700 rows, 300 queries); 'wide': counts spread over 0..255 with shared bins (the table's
+    whole range)."""
+    from ocvfacerec.facerec.feature import SpatialHistogram
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import Chi2Gallery, counts_numpy
+    r = _rng(15)
+    if data == "lbp":
+        protos = r.integers(0, 256, (30, 16, 16)).astype(np.float64)
+        up = np.kron(protos, np.ones((8, 8)))
+        gal = np.clip(up[np.arange(700) % 30] + r.normal(0, 20, (700, 128, 128)), 0, 255).astype(np.uint8)
+        qry = np.clip(up[r.integers(0, 30, 300)] + r.normal(0, 20, (300, 128, 128)), 0, 255).astype(np.uint8)
+        sh = SpatialHistogram()
+        gc, cell, cb = sh.counts_device(gal)
+        qc, _, _ = sh.counts_device(qry)
+        G = counts_numpy(gc, cb).reshape(700, -1).astype(np.int64)
+        Q = counts_numpy(qc, cb).reshape(300, -1).astype(np.int64)
+        denom = float(cell)
+    else:
+        base = r.integers(0, 256, (40, 1024))
+        G = np.clip(base[np.arange(600) % 40] + r.integers(-3, 4, (600, 1024)), 0, 255)
+        Q = np.clip(base[r.integers(0, 40, 257)] + r.integers(-3, 4, (257, 1024)), 0, 255)
+        denom = 255.0
+    g = Chi2Gallery.from_counts(G.astype(np.uint8), 1, denom)
+    Qd = torch.from_numpy(Q.astype(np.uint8)).cuda()
+    monkeypatch.delenv("OFR_CHI2_ENGINE", raising=False)
+    dm, im = g.search(Qd, 3)
+    fb_m = g.last_fallbacks
+    monkeypatch.setenv("OFR_CHI2_ENGINE", "valu")
+    dv, iv = g.search(Qd, 3)
+    assert torch.equal(im, iv) and torch.equal(dm, dv)
+    assert fb_m[0] <= len(Q) // 10, fb_m            # separated identities: the MFMA pass certifies
+    _check_search("ChiSquareDistance", Q / denom, G / denom, dm.cpu().numpy(), im.cpu().numpy(), 3)
+
+
 def test_chi2_float_search_vs_oracle():
     from opencv_facerecognizer_amd._device import Chi2Gallery
     r = _rng(13)
