@@ -379,6 +379,9 @@ struct Engine16 {
     };
     auto readA = [&](const char* st, int i) { a[i] = frag16(st, wr * 128 + i * 16 + r16); };
     auto readB = [&](const char* st, int c) { b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16); };
+    // probe MODE 16384: the k loop keeps its first fragments (no refills; wrong results): MFMAs + feed
+    auto readAk = [&](const char* st, int i) { if constexpr ((MODE & 16384) == 0) readA(st, i); };
+    auto readBk = [&](const char* st, int c) { if constexpr ((MODE & 16384) == 0) readB(st, c); };
     if constexpr (MODE == 1) wait_vm<0>();
     else wait_vm<2 * IPW>();
     barrier();
@@ -425,7 +428,7 @@ struct Engine16 {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               mm(a[i], b[c], acc[i][c]);
-              if (c == NB - 1) readA(nxt, i);
+              if (c == NB - 1) readAk(nxt, i);
             }
           __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
 #pragma unroll
@@ -438,7 +441,7 @@ struct Engine16 {
           for (int i = 0; i < RS; ++i) {
 #pragma unroll
             for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
-            readA(nxt, i);
+            readAk(nxt, i);
           }
 #pragma unroll
           for (int i = 0; i < RS; ++i) {
@@ -468,10 +471,10 @@ struct Engine16 {
           for (int c = 0; c < NB; ++c) {
 #pragma unroll
             for (int i = 4; i < NA; ++i) mm(a[i], b[c], acc[i][c]);
-            readB(nxt, c);   // b3 before a4..a7: the next stage needs b3 at its 13th MFMA, a4 at its 17th
+            readBk(nxt, c);   // b3 before a4..a7: the next stage needs b3 at its 13th MFMA, a4 at its 17th
           }
 #pragma unroll
-          for (int i = 4; i < NA; ++i) readA(nxt, i);
+          for (int i = 4; i < NA; ++i) readAk(nxt, i);
           __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
 #pragma unroll
           for (int c = 0; c < NB; ++c) {
@@ -485,14 +488,14 @@ struct Engine16 {
         for (int i = RS; i < NA - 1; ++i) {
 #pragma unroll
           for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
-          readA(nxt, i);
+          readAk(nxt, i);
         }
 #pragma unroll
         for (int c = 0; c < NB; ++c) {
           mm(a[NA - 1], b[c], acc[NA - 1][c]);
-          readB(nxt, c);
+          readBk(nxt, c);
         }
-        readA(nxt, NA - 1);
+        readAk(nxt, NA - 1);
         __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
 #pragma unroll
         for (int i = RS; i < NA - 1; ++i) {
@@ -532,14 +535,14 @@ struct Engine16 {
       for (int i = 0; i < NA - 1; ++i) {
 #pragma unroll
         for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
-        readA(nxt, i);
+        readAk(nxt, i);
       }
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
         mm(a[NA - 1], b[c], acc[NA - 1][c]);
-        readB(nxt, c);
+        readBk(nxt, c);
       }
-      readA(nxt, NA - 1);
+      readAk(nxt, NA - 1);
       // the stage's DMAs first (issuing them later in the stage, staggered between the two waves of
       // a SIMD, measured 8 % slower: tools/f6_probe.hip SHAPE16), then per row i its 4 MFMAs and
       // the 2 reads of its successor; row 7 refills B as each of its MFMAs retires its operand

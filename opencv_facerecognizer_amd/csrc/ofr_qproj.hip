@@ -28,7 +28,9 @@
 // tile = 64 features x 4 slices by 256 images, 8 waves (2 per SIMD) of 128x64,
 // k step 128, both operands by LDS-DMA (the images as raw uint8 rows; the
 // fragments become x - 128 by an XOR with 0x80 after the LDS read).
-#include "ofr_i8_tile.h"
+#include <string.h>
+
+#include "ofr_i8s_tile.h"
 
 namespace ofr {
 namespace q8 {
@@ -53,20 +55,10 @@ struct Args {
   int64_t ntf, ntb, gg;
 };
 
-__global__ void __launch_bounds__(S::NT, 1) project_q8_kernel(Args p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
-  int64_t ft, bt;
-  i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
-  const int64_t a0 = ft * i8t::TA, b0 = bt * S::TQ;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave / S::WQ, wc = wave % S::WQ, h = lane >> 5, r32 = lane & 31;
-
-  i32x16 acc[4][S::CT], unused[4][1];
-  i8t::mainloop<1, 0, true>(smem, p.Aq, p.ldk, p.arows, a0, reinterpret_cast<const int8_t*>(p.X), p.ldx, p.B, b0,
-                            p.ldx, p.nk, acc, unused);
-
-  // epilogue: rows (reg&3) + 8*(reg>>2) + 4*h of each 32-block are the same 32 features in all four slices
+// epilogue shared by both engines: rows (reg&3) + 8*(reg>>2) + 4*h of each 32-block are the same
+// 32 features in all four slices
+__device__ __forceinline__ void project_epilogue(const Args& p, const i32x16 (&acc)[4][S::CT], int64_t ft, int64_t b0,
+                                                 int wr, int wc, int h, int r32) {
   const int64_t fb = ft * 2 + wr;   // 32-feature block of this wave
 #pragma unroll
   for (int ct = 0; ct < S::CT; ++ct) {
@@ -110,6 +102,53 @@ __global__ void __launch_bounds__(S::NT, 1) project_q8_kernel(Args p) {
         }
       }
     }
+  }
+}
+
+// OFR_PROJ_ENGINE=i8: the previous engine (ofr_i8_tile.h, 2 x 128-feature stages, FLAT copies)
+__global__ void __launch_bounds__(S::NT, 1) project_q8_kernel(Args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t ft, bt;
+  i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
+  const int64_t a0 = ft * i8t::TA, b0 = bt * S::TQ;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave / S::WQ, wc = wave % S::WQ, h = lane >> 5, r32 = lane & 31;
+
+  i32x16 acc[4][S::CT], unused[4][1];
+  i8t::mainloop<1, 0, true>(smem, p.Aq, p.ldk, p.arows, a0, reinterpret_cast<const int8_t*>(p.X), p.ldx, p.B, b0,
+                            p.ldx, p.nk, acc, unused);
+  project_epilogue(p, acc, ft, b0, wr, wc, h, r32);
+}
+
+// The default engine (ofr_i8s_tile.h): 64-feature stages in NST buffers, MUBUF copies, mid-stage
+// hand-off.  The panels' buffer descriptors bound the reads: B rows past the batch read as zero
+// (their outputs are not stored); columns past D meet zero W columns.
+template <int NST, bool XB = true>
+__global__ void __launch_bounds__(i8s::NT, 1) project_q8s_kernel(Args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t ft, bt;
+  i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
+  const int64_t a0 = ft * i8s::TA, b0 = bt * i8s::TB;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave / i8s::WQ, wc = wave % i8s::WQ, h = lane >> 5, r32 = lane & 31;
+  const int64_t brows = p.B - b0 < i8s::TB ? p.B - b0 : i8s::TB;
+  __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)(p.Aq + a0 * p.ldk), 0,
+                                                                (int)(i8s::TA * p.ldk), 0x00020000);
+  __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(p.X + b0 * p.ldx), 0, (int)(brows * p.ldx),
+                                                                0x00020000);
+  i32x16 acc[4][S::CT];
+  i8s::mainloop<NST, XB>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
+  project_epilogue(p, acc, ft, b0, wr, wc, h, r32);
+}
+
+// x -> x - 128 as int8 (XOR 0x80), 16 bytes per thread: the staged engine's pre-shifted B operand
+__global__ void __launch_bounds__(256) shift_images_kernel(const uint4* X, uint4* Y, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+    uint4 v = X[i];
+    v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
+    Y[i] = v;
   }
 }
 
@@ -300,6 +339,22 @@ static bool getenv_flag_gemv() {
   return f;
 }
 
+// OFR_PROJ_ENGINE selects the tile engine: default ("i8") ofr_i8_tile.h (two 128-feature stages,
+// FLAT copies); "s4" / "s5" the staged engine of ofr_i8s_tile.h with 4 / 5 64-feature buffers;
+// "s5p" the staged engine on images shifted to int8 by a pre-pass (no XOR in the k loop).  All give
+// identical bits; the staged forms measured no faster at the bench shape (tools/bench_proj.py,
+// profiles/r03_proj_engines.json: 1.67 / 1.72 / 1.69 / 1.68 ms), so the default stays.
+static int proj_engine() {
+  static const int f = [] {
+    const char* e = getenv("OFR_PROJ_ENGINE");
+    if (e && strcmp(e, "s4") == 0) return 4;
+    if (e && strcmp(e, "s5") == 0) return 5;
+    if (e && strcmp(e, "s5p") == 0) return 6;
+    return 0;
+  }();
+  return f;
+}
+
 extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx, const int8_t* Aq,
                                     int64_t ldk, const double* scale, const double* K, int64_t d, const double* shift,
                                     void* Y, int64_t ldy, int y_dtype) {
@@ -315,6 +370,15 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   if (!attr_done) {
     hipError_t e = hipFuncSetAttribute((const void*)q8::project_q8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        q8::S::LDS);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              i8s::Lds<4>::BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              i8s::Lds<5>::BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8)");
     attr_done = true;
   }
@@ -342,15 +406,47 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   q8::Args p;
   p.X = X; p.B = B; p.D = D; p.ldx = ldx; p.Aq = Aq; p.ldk = ldk; p.scale = scale; p.K = K; p.shift = shift;
   p.d = d; p.Y = Y; p.ldy = ldy; p.y_f64 = y_dtype == OFR_DT_F64;
-  p.nk = (int)cdiv(D, q8::S::BK);
   p.ntf = cdiv(d, 64);
   p.arows = p.ntf * 256;
-  p.ntb = cdiv(B, q8::S::TQ);
   p.gg = p.ntf < q8::GROUP_F ? p.ntf : q8::GROUP_F;
+  const int engine = proj_engine();
+  if (engine == 0) {
+    p.nk = (int)cdiv(D, q8::S::BK);
+    p.ntb = cdiv(B, q8::S::TQ);
+    OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
+    hipLaunchKernelGGL(q8::project_q8_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(q8::S::NT), q8::S::LDS,
+                       (hipStream_t)stream, p);
+    OFR_LAUNCH_CHECK("project_q8_kernel");
+    return OFR_OK;
+  }
+  // the staged engine addresses a panel with 32-bit buffer offsets
+  OFR_CHECK_ARG((int64_t)i8s::TA * ldk < 0x7fffffffLL && (int64_t)i8s::TB * ldx < 0x7fffffffLL,
+                "ofr_project_u8_exact: rows too long for the staged engine");
+  p.nk = (int)cdiv(D, i8s::BK);
+  p.ntb = cdiv(B, i8s::TB);
   OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-  hipLaunchKernelGGL(q8::project_q8_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(q8::S::NT), q8::S::LDS,
-                     (hipStream_t)stream, p);
-  OFR_LAUNCH_CHECK("project_q8_kernel");
+  if (engine == 4) {
+    hipLaunchKernelGGL(q8::project_q8s_kernel<4>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT), i8s::Lds<4>::BYTES,
+                       (hipStream_t)stream, p);
+  } else if (engine == 6) {   // images shifted to int8 by a pre-pass: no XOR in the k loop
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t* xs = nullptr;
+    hipError_t e = hipMallocAsync((void**)&xs, (size_t)B * ldx, st);
+    if (e != hipSuccess) return hip_status(e, "ofr_project_u8_exact: shifted images");
+    const int64_t n16 = B * ldx / 16;
+    hipLaunchKernelGGL(q8::shift_images_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n16, 256), 4096)), dim3(256), 0,
+                       st, (const uint4*)X, (uint4*)xs, n16);
+    OFR_LAUNCH_CHECK("shift_images_kernel");
+    p.X = xs;
+    hipLaunchKernelGGL((q8::project_q8s_kernel<5, false>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
+                       i8s::Lds<5>::BYTES, st, p);
+    OFR_LAUNCH_CHECK("project_q8s_kernel");
+    e = hipFreeAsync(xs, st);
+    return e == hipSuccess ? OFR_OK : hip_status(e, "ofr_project_u8_exact: hipFreeAsync");
+  } else
+    hipLaunchKernelGGL(q8::project_q8s_kernel<5>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT), i8s::Lds<5>::BYTES,
+                       (hipStream_t)stream, p);
+  OFR_LAUNCH_CHECK("project_q8s_kernel");
   return OFR_OK;
 }
 

@@ -32,6 +32,8 @@ from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
 PEAK_HBM = 8.0e12
 PEAK_F64_VALU = 78.6e12     # MI355X fp64 vector (spec)
 PEAK_PAIR_BINS = 256 * 4 * 32 * 2.4e9 / 4   # chi2 terms/s at the VALU issue limit (4 lane-slots per term)
+PEAK_F16_MFMA = 2.5e15      # fp16 / bf16 dense MFMA (MI355X_MICROARCH.md)
+CHI2_RANK = 8               # components of the low-rank table (ofr_chi2.hip, c2m): 8 MACs per (pair, bin)
 
 
 def timed(fn, reps):
@@ -101,6 +103,7 @@ def main():
     gal = Chi2Gallery(gc.reshape(N, nb), dtype=_lib.DT_U8, denom=float(cell), nbins=nb)
     Qc = qc.reshape(B, nb).contiguous()
     ms_search, (dd, ii) = timed(lambda: gal.search(Qc, 1), args.reps)
+    engine = "valu" if os.environ.get("OFR_CHI2_ENGINE", "") == "valu" else "mfma"
     acc = float(((ii[:, 0] // args.per_id) == ids_q).double().mean().item())
 
     ncode = (H - 2) * (H - 2)
@@ -110,6 +113,20 @@ def main():
     t_h, t_c, nh = cpu_baseline(G_img[:64].cpu().numpy(), Q_img[:1].cpu().numpy(), args.cpu_seconds)
     cpu_total = N * t_h + B * (t_h + N * t_c)             # histograms of gallery + queries, per-item chi2 loop
     gpu_total = (ms_hist * (1 + B / N) + ms_search) * 1e-3
+    rate = pair_bins / (ms_search * 1e-3)
+    if engine == "mfma":   # uint8 counts: v_mfma_f32_16x16x32_f16 over 4 bins x 8 table components
+        roof = {"bound": "mfma", "kernel": "c2m::chi2_mfma_kernel (fp16 16x16x32, low-rank chi2 table)",
+                "achieved": rate * 2 * CHI2_RANK / 1e12, "peak": PEAK_F16_MFMA / 1e12, "unit": "TFLOP/s",
+                "frac": rate * 2 * CHI2_RANK / PEAK_F16_MFMA,
+                "note": f"{2 * CHI2_RANK} fp16 MFMA flops per (pair, bin); 4 x (Tq + Tg) bound certified, "
+                        "exact fp64 re-rank of the best 16"}
+    else:
+        roof = {"bound": "VALU issue", "kernel": "chi2_tile_kernel (packed fp32 VALU)",
+                "note": "per two (pair, bin) terms: v_pk_add (a-c), v_pk_add (a+c), 2 x v_rcp "
+                        "(half rate), v_pk_mul, v_pk_fma = 8 lane-slots; peak = 256 CU x 4 SIMD x "
+                        "32 lanes x 2.4 GHz / 4 slots per term",
+                "achieved": rate / 1e12, "peak": PEAK_PAIR_BINS / 1e12, "unit": "T (pair, bin)/s",
+                "frac": rate / PEAK_PAIR_BINS}
     out = {
         "metric": "faces/sec: ExtendedLBP + SpatialHistogram 8x8 + ChiSquare 1-NN (configs[3])",
         "config": {"gallery": N, "batch": B, "side": H, "lbp": "ExtendedLBP(radius=1, neighbors=8)",
@@ -124,13 +141,8 @@ def main():
                                   "flops_per_face": flops_face, "bytes_per_face": bytes_face}},
         "chi2_search": {"ms": ms_search, "queries_per_s": B / (ms_search * 1e-3),
                         "pair_bins_per_s": pair_bins / (ms_search * 1e-3),
-                        "roofline": {"bound": "VALU issue",
-                                     "note": "per two (pair, bin) terms: v_pk_add (a-c), v_pk_add (a+c), 2 x v_rcp "
-                                             "(half rate), v_pk_mul, v_pk_fma = 8 lane-slots; peak = 256 CU x 4 SIMD x "
-                                             "32 lanes x 2.4 GHz / 4 slots per term",
-                                     "achieved": pair_bins / (ms_search * 1e-3) / 1e12,
-                                     "peak": PEAK_PAIR_BINS / 1e12, "unit": "T (pair, bin)/s",
-                                     "frac": pair_bins / (ms_search * 1e-3) / PEAK_PAIR_BINS}},
+                        "engine": engine,
+                        "roofline": roof},
         "top1_identity_acc": acc,
         "chi2_uncertified_after_each_pass": list(gal.last_fallbacks),
         "end_to_end_queries_per_s": B / gpu_total,

@@ -347,6 +347,14 @@ int main(int argc, char** argv) {
         return 1;
     return 0;
   }
+  if (getenv("FEEDTEST")) {   // the library sieve pass without its epilogue, without its fragment refills
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (run16<13312>(a, reps, "lib") || run16<13312 + 4>(a, reps, "noepi") ||
+          run16<13312 + 4 + 16384>(a, reps, "noepi-norefill") || run16<5>(a, reps, "nodma-noepi"))
+        return 1;
+    return 0;
+  }
   if (getenv("QDIRECT")) {   // query operand straight to registers (f6t::EngineQ) vs Engine16
     a.gg = 4 < ntg ? 4 : ntg;
     for (int rep = 0; rep < 2; ++rep)

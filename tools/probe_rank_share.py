@@ -19,9 +19,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-import bench  # noqa: E402
 from opencv_facerecognizer_amd import _lib  # noqa: E402
-from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank  # noqa: E402
+from opencv_facerecognizer_amd._device import round_up  # noqa: E402
+from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_gallery, build_projection  # noqa: E402
 
 
 def timed(fn, reps):
@@ -45,10 +45,10 @@ def main():
     dev = _lib.device()
     side, d, per_id, B, k, G = 100, 9999, 10, a.batch, 1, a.gpus
     N = a.gallery // G
-    P, _ = bench.build_projection(side * side, d, dev)
+    P, _ = build_projection(side * side, d, dev)
     bank = IdentityBank(a.gallery // per_id, side, side, device=dev)
-    ld = bench.round_up(d, 32)
-    g = bench.build_gallery(P, bank, per_id, 0, N, a.gallery, d, ld, dev)          # rank 0's rows
+    ld = round_up(d, 32)
+    g = build_gallery(P, bank, per_id, 0, N, a.gallery, d, ld, dev)          # rank 0's rows
     g._tier_gallery("f6")
     gq = torch.Generator(device=dev)
     gq.manual_seed(SEED + 7)
@@ -88,10 +88,20 @@ def main():
 
     tiles()
     stage1()
-    ub.copy_(ub_loc[:, k - 1])            # this shard's own k-th bound (no other ranks here)
+    # the global bound at G ranks: for a query whose identity lives on this shard (rows 10 i .. 10 i + 9
+    # below N) this shard's own k-th bound; for the others the owner's k-th distance, far below this
+    # shard's candidates -- emulated by 0, which prunes every candidate (merge_sharded's stage 2 then
+    # re-ranks nothing for that query, as on a real foreign shard)
+    own = (ids * per_id + per_id - 1) < N
+    ub_own = ub_loc[:, k - 1].clone()
+    ub.copy_(torch.where(own, ub_own, torch.zeros_like(ub_own)) if G > 1 else ub_own)
     res = {"gpus": G, "rows_per_rank": N, "batch": B, "faces_projected_per_rank": b1,
+           "queries_owned_by_this_shard": int(own.sum()),
            "prep_ms": timed(prep, a.reps), "tiles_ms": timed(tiles, a.reps), "merge_stage1_ms": timed(stage1, a.reps),
            "merge_stage2_ms": timed(stage2, a.reps), "local_step_ms": timed(local_step, a.reps)}
+    # bench.py's pipelined step: the next batch's preparation runs on a side stream beside this batch's
+    # merge, so the critical path is the tile pass + max(merge, preparation) (collectives not included)
+    res["pipelined_step_ms"] = res["tiles_ms"] + max(res["merge_stage1_ms"] + res["merge_stage2_ms"], res["prep_ms"])
     full = {"prep_full_batch_ms": timed(lambda: (P.project(Xq, shift64=g.shift64, out=Qd),
                                                  g.quantize_queries(Qd, qq, tier="f6")), a.reps)}
     res.update(full)
