@@ -47,6 +47,13 @@ PEAK_F6_MFMA = 10.0e15      # fp6 (block-scaled f8f6f4 MFMA): ~10 PF dense, the 
 # operands in registers, at the clock it holds under that load (tools/f6_shape_probe.hip,
 # profiles/r02_f6_shape_probe.log): the ceiling of any fp6 kernel on this part
 SUSTAINED_F6_MFMA = 6.28e15
+# The sieve pass is bound by its LDS-DMA feed, not by the MFMAs: the same kernel issuing only its stage
+# copies (no MFMAs, no fragment reads) takes 22.55 ms at the bench shape, as long as the whole pass
+# without its epilogue, and equally long when every tile copies the same L2-resident panels
+# (tools/f6_probe.hip FEEDTEST, profiles/r03_f6_probe_feedtest_dmaonly.log, r03_f6_probe_feedtest_l2.log):
+# 3,907 x 16 tiles x 79 stages x 48 KiB = 242.7 GB in 22.55 ms = 10.76 TB/s chip-wide (42 GB/s per CU),
+# a per-CU ingest ceiling
+F6_DMA_CEILING_BPS = 10.76e12
 PEAK_HBM = 8.0e12           # HBM3E 8 TB/s (spec)
 
 
@@ -456,6 +463,8 @@ def main():
         peak, kname = PEAK_F6_MFMA, ("ofr_knn_f6 phase 1 (fp6 e2m3): q8s::tile_kernel_f6<8, 0> sample pass + "
                                      "sieve_threshold_kernel + " + sieve)
         alg_bytes_tiles = 0.75 * (nl * d + B * d)                    # 6 bits per feature, gallery + queries
+        ntg_, ntq_, nst_ = -(-nl // 256), -(-B // 256), -(-d // 128)
+        fed = (ntg_ + -(-ntg_ // 64)) * ntq_ * nst_ * 49152.0         # sieve pass + sample pass (every 64th panel)
         executed = flops_tiles
     elif use_q8:
         peak, kname = PEAK_I8_MFMA, "q8s::tile_kernel<1> (ofr_knn_q8 phase 1, one int8 slice)"
@@ -492,7 +501,14 @@ def main():
                          "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
                          "launch_ms": ms_tiles,
                          **({"sustained_peak": SUSTAINED_F6_MFMA / 1e12, "frac_of_sustained": achieved / SUSTAINED_F6_MFMA,
-                             "sustained_source": "tools/f6_shape_probe.hip (profiles/r02_f6_shape_probe.log)"}
+                             "sustained_source": "tools/f6_shape_probe.hip (profiles/r02_f6_shape_probe.log)",
+                             "feed": {"what": "bytes copied into the CUs' LDS by the sample + sieve passes (48 KiB per "
+                                              "256x256x128 stage)", "bytes_per_launch": fed,
+                                      "achieved_TBps": fed / (ms_tiles * 1e-3) / 1e12,
+                                      "ceiling_TBps": F6_DMA_CEILING_BPS / 1e12,
+                                      "frac": fed / (ms_tiles * 1e-3) / F6_DMA_CEILING_BPS,
+                                      "ceiling_source": "tools/f6_probe.hip FEEDTEST dma-only "
+                                                        "(profiles/r03_f6_probe_feedtest_dmaonly.log)"}}
                             if args.search == "f6" else {})},
             "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else "") + ("+all_gather" if shard_prep else ""):
                            ms_proj, "knn_tiles": ms_tiles,

@@ -189,6 +189,26 @@ struct Engine {
     }
   }
 
+  // probe only: the same copies issued by waves 0-3 alone (12 pieces each), waves 4-7 issue none
+  static __device__ __forceinline__ void dma_buf4(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst,
+                                                  int kt, char* st) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    if (wave >= 4) return;
+    const int pb = (int)(nst * PANEL);
+    __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(G + gp * nst * (int64_t)PANEL), 0, pb,
+                                                                  0x00020000);
+    __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * nst * (int64_t)PANEL), 0, pb,
+                                                                  0x00020000);
+#pragma unroll
+    for (int t = 0; t < 2 * IPW; ++t) {
+      const int ins = wave * 2 * IPW + t;
+      const bool gal = ins < DMA_INS / 2;
+      const int off = (gal ? ins : ins - DMA_INS / 2) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(gal ? rg : rq, (OFR_LDS void*)(st + (gal ? 0 : PANEL) + off), 16,
+                                               kt * PANEL + off + lane * 16, 0, 0, 0);
+    }
+  }
+
   // reads threaded through MFMAs: NFR reads over MF MFMAs, front-loaded (2 after each MFMA while
   // they last, then 1, then none)
   static __device__ __forceinline__ void interleave() {
@@ -364,7 +384,9 @@ struct Engine16 {
         const char *g, *q;
         int ks;
         seg_src<NSEG>(s < last ? s : last, nst, G, G2, Q, Q2, g, q, ks);
-        Engine<8>::dma_buf(g, gp, q, qp, nst, ks, smem + (s % NST) * STAGE);
+        // probe MODE 131072: every tile copies gallery panel 0 and query panel 0 (L2-resident feed)
+        if constexpr ((MODE & 262144) != 0) Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (s % NST) * STAGE);
+        else Engine<8>::dma_buf(g, (MODE & 131072) ? 0 : gp, q, (MODE & 131072) ? 0 : qp, nst, ks, smem + (s % NST) * STAGE);
       } else {
         issue(s < last ? s : last);
       }
@@ -374,6 +396,7 @@ struct Engine16 {
     if constexpr ((MODE & 256) != 0) asm volatile("" : "+v"(sc));
     int sa = SCALE_ONE, sb = SCALE_ONE;
     auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) {
+      if constexpr ((MODE & 65536) != 0) return;   // probe: no MFMAs (the feed alone; wrong results)
       if constexpr ((MODE & 256) != 0) mfma_agpr(x, y, c, sc);
       else c = mfma(x, y, c, sa, sb);
     };
@@ -383,6 +406,7 @@ struct Engine16 {
     auto readAk = [&](const char* st, int i) { if constexpr ((MODE & 16384) == 0) readA(st, i); };
     auto readBk = [&](const char* st, int c) { if constexpr ((MODE & 16384) == 0) readB(st, c); };
     if constexpr (MODE == 1) wait_vm<0>();
+    else if constexpr ((MODE & 262144) != 0) wait_vm<4 * IPW>();
     else wait_vm<2 * IPW>();
     barrier();
     if constexpr ((MODE & 2048) != 0) {   // the loop's read order, so that its waits stay counted
@@ -411,12 +435,14 @@ struct Engine16 {
         const char *g, *q;
         int ks;
         seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
-        Engine<8>::dma_buf(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+        if constexpr ((MODE & 262144) != 0) Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+        else Engine<8>::dma_buf(g, (MODE & 131072) ? 0 : gp, q, (MODE & 131072) ? 0 : qp, nst, ks, smem + (kt % NST) * STAGE);
       };
       for (int kt = 0; kt < last; ++kt) {
         seg_scales<NSEG>(kt, nst, sa, sb);
         __builtin_amdgcn_sched_barrier(0);
-        wait_vm<IPW>();   // stage kt+1 landed (kt+2 may be in flight)
+        if constexpr ((MODE & 262144) != 0) wait_vm<2 * IPW>();
+        else wait_vm<IPW>();   // stage kt+1 landed (kt+2 may be in flight)
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         const char* nxt = smem + ((kt + 1) % NST) * STAGE;

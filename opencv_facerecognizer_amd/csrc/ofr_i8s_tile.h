@@ -142,5 +142,82 @@ __device__ __forceinline__ void mainloop(char* smem, __amdgpu_buffer_rsrc_t ra, 
   wait_vm<0>();   // no copy may still target this workgroup's LDS when it retires
 }
 
+// Ping-pong main loop: the same tile, stages and copies, but the two waves of a SIMD never read
+// fragments and issue MFMAs at the same time.  The wave groups g = wr (waves 0-3 and 4-7; the
+// cyclic wave -> SIMD order puts one of each on every SIMD) run one s_barrier apart: per stage j a
+// wave has a LOAD phase (its copies of stage j + NST - 2, the 12 fragment reads of stage j, the wait
+// for its copies of stage j + 1, lgkmcnt(0) on its reads) and an MFMA phase (16 MFMAs at raised
+// priority), each ending in an s_barrier.  Barrier H(n) is the n-th barrier every wave passes;
+// group 0 ends LOAD(j) at H(2j+1) and MFMA(j) at H(2j+2), group 1 one barrier later, so while one
+// wave of a SIMD issues its 16 MFMAs the other fetches the next stage's operands.
+//   visibility: stage j+1's copies are waited for (own vmcnt) before LOAD(j)'s barrier, i.e. by
+//     H(2j+2) for every wave; its first reader (group 0, LOAD(j+1)) starts after H(2j+2);
+//   reuse: LOAD(j) copies into the buffer of stage j-2, whose last reads (group 1, LOAD(j-2),
+//     drained by lgkmcnt(0) before its barrier H(2j-1)) precede the earliest copy (group 0 after
+//     H(2j)).
+template <int NST, bool XB>
+__device__ __forceinline__ void mainloop_pp(char* smem, __amdgpu_buffer_rsrc_t ra, int lda, __amdgpu_buffer_rsrc_t rb,
+                                            int ldb, int nk, i32x16 (&acc)[4][CT]) {
+  static_assert(NST == 4 || NST == 5, "stages");
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
+  const bool late = __builtin_amdgcn_readfirstlane(wr) != 0;   // group 1: one barrier behind
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < CT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+
+  const int last = nk - 1;
+  auto issue = [&](int s) { dma(ra, lda, rb, ldb, s < last ? s : last, smem + (s % NST) * STAGE); };
+#pragma unroll
+  for (int s = 0; s < NST - 2; ++s) issue(s);
+  wait_vm<(NST - 3) * IPW>();   // own copies of stage 0 landed
+  __builtin_amdgcn_s_barrier();   // H(0): stage 0 visible to every wave
+  if (late) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  i32x4 ga[2][4], qb[2][CT];
+  for (int kt = 0; kt < nk; ++kt) {
+    // LOAD phase: the fragment reads first (their latency runs under the copies' issue)
+    const char* st = smem + (kt % NST) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = 2 * ks + h;
+#pragma unroll
+      for (int j = 0; j < CT; ++j) qb[ks][j] = *reinterpret_cast<const i32x4*>(st + PANEL + off(wc * QW + j * 32 + r32, c));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ga[ks][i] = *reinterpret_cast<const i32x4*>(st + off(wr * 128 + i * 32 + r32, c));
+    }
+    issue(kt + NST - 2);
+    wait_vm<(NST - 3) * IPW>();   // own copies of stage kt+1 landed (kt+2 .. kt+NST-2 may fly)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (XB) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) qb[ks][j] ^= (int)0x80808080;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // MFMA phase
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ga[ks][i], qb[ks][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (!late) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
+  wait_vm<0>();   // no copy may still target this workgroup's LDS when it retires
+}
+
 }  // namespace i8s
 }  // namespace ofr

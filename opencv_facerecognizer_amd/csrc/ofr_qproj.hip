@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(S::NT, 1) project_q8_kernel(Args p) {
 // The default engine (ofr_i8s_tile.h): 64-feature stages in NST buffers, MUBUF copies, mid-stage
 // hand-off.  The panels' buffer descriptors bound the reads: B rows past the batch read as zero
 // (their outputs are not stored); columns past D meet zero W columns.
-template <int NST, bool XB = true>
+template <int NST, bool XB = true, bool PP = false>
 __global__ void __launch_bounds__(i8s::NT, 1) project_q8s_kernel(Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
@@ -139,7 +139,8 @@ __global__ void __launch_bounds__(i8s::NT, 1) project_q8s_kernel(Args p) {
   __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(p.X + b0 * p.ldx), 0, (int)(brows * p.ldx),
                                                                 0x00020000);
   i32x16 acc[4][S::CT];
-  i8s::mainloop<NST, XB>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
+  if constexpr (PP) i8s::mainloop_pp<NST, XB>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
+  else i8s::mainloop<NST, XB>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
   project_epilogue(p, acc, ft, b0, wr, wc, h, r32);
 }
 
@@ -350,6 +351,8 @@ static int proj_engine() {
     if (e && strcmp(e, "s4") == 0) return 4;
     if (e && strcmp(e, "s5") == 0) return 5;
     if (e && strcmp(e, "s5p") == 0) return 6;
+    if (e && strcmp(e, "pp4") == 0) return 7;
+    if (e && strcmp(e, "pp5") == 0) return 8;
     return 0;
   }();
   return f;
@@ -378,6 +381,12 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
                               i8s::Lds<5>::BYTES);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<4, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<4>::BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, true, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8)");
     attr_done = true;
@@ -425,7 +434,13 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   p.nk = (int)cdiv(D, i8s::BK);
   p.ntb = cdiv(B, i8s::TB);
   OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-  if (engine == 4) {
+  if (engine == 7) {
+    hipLaunchKernelGGL((q8::project_q8s_kernel<4, true, true>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
+                       i8s::Lds<4>::BYTES, (hipStream_t)stream, p);
+  } else if (engine == 8) {
+    hipLaunchKernelGGL((q8::project_q8s_kernel<5, true, true>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
+                       i8s::Lds<5>::BYTES, (hipStream_t)stream, p);
+  } else if (engine == 4) {
     hipLaunchKernelGGL(q8::project_q8s_kernel<4>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT), i8s::Lds<4>::BYTES,
                        (hipStream_t)stream, p);
   } else if (engine == 6) {   // images shifted to int8 by a pre-pass: no XOR in the k loop

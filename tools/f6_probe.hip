@@ -347,11 +347,21 @@ int main(int argc, char** argv) {
         return 1;
     return 0;
   }
+  if (getenv("GGDMA")) {   // the DMA-only variant against the tile-group width
+    for (int g : {1, 2, 4, 8, 16}) {
+      a.gg = g < ntg ? g : ntg;
+      if (run16<13312 + 4 + 16384 + 65536>(a, reps, "dma-only-gg")) return 1;
+    }
+    return 0;
+  }
   if (getenv("FEEDTEST")) {   // the library sieve pass without its epilogue, without its fragment refills
     a.gg = 4 < ntg ? 4 : ntg;
     for (int rep = 0; rep < 2; ++rep)
       if (run16<13312>(a, reps, "lib") || run16<13312 + 4>(a, reps, "noepi") ||
-          run16<13312 + 4 + 16384>(a, reps, "noepi-norefill") || run16<5>(a, reps, "nodma-noepi"))
+          run16<13312 + 4 + 16384>(a, reps, "noepi-norefill") || run16<13312 + 4 + 16384 + 65536>(a, reps, "dma-only") ||
+          run16<13312 + 4 + 16384 + 65536 + 131072>(a, reps, "dma-only-L2") || run16<13312 + 4 + 131072>(a, reps, "noepi-L2") ||
+          run16<13312 + 4 + 16384 + 65536 + 262144>(a, reps, "dma-only-4w") || run16<13312 + 4 + 262144>(a, reps, "noepi-4w") ||
+          run16<5>(a, reps, "nodma-noepi"))
         return 1;
     return 0;
   }
