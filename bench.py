@@ -47,13 +47,11 @@ PEAK_F6_MFMA = 10.0e15      # fp6 (block-scaled f8f6f4 MFMA): ~10 PF dense, the 
 # operands in registers, at the clock it holds under that load (tools/f6_shape_probe.hip,
 # profiles/r02_f6_shape_probe.log): the ceiling of any fp6 kernel on this part
 SUSTAINED_F6_MFMA = 6.28e15
-# The sieve pass is bound by its LDS-DMA feed, not by the MFMAs: the same kernel issuing only its stage
-# copies (no MFMAs, no fragment reads) takes 22.55 ms at the bench shape, as long as the whole pass
-# without its epilogue, and equally long when every tile copies the same L2-resident panels
-# (tools/f6_probe.hip FEEDTEST, profiles/r03_f6_probe_feedtest_dmaonly.log, r03_f6_probe_feedtest_l2.log):
-# 3,907 x 16 tiles x 79 stages x 48 KiB = 242.7 GB in 22.55 ms = 10.76 TB/s chip-wide (42 GB/s per CU),
-# a per-CU ingest ceiling
-F6_DMA_CEILING_BPS = 10.76e12
+# The sieve pass's stage copies by themselves (no MFMAs, no fragment reads; the library's copy protocol)
+# move 3,907 x 16 tiles x 79 stages x 48 KiB = 242.7 GB in 11.8 ms = 20.6 TB/s (81 GB/s per CU;
+# tools/f6_probe.hip FEEDTEST dma-only, profiles/r03_f6_probe_feedtest.log).  The pass reaches a fraction
+# of that: the copies' and reads' issue serialises with the MFMAs, reported as roofline.feed.
+F6_DMA_CEILING_BPS = 20.6e12
 PEAK_HBM = 8.0e12           # HBM3E 8 TB/s (spec)
 
 
@@ -507,8 +505,8 @@ def main():
                                       "achieved_TBps": fed / (ms_tiles * 1e-3) / 1e12,
                                       "ceiling_TBps": F6_DMA_CEILING_BPS / 1e12,
                                       "frac": fed / (ms_tiles * 1e-3) / F6_DMA_CEILING_BPS,
-                                      "ceiling_source": "tools/f6_probe.hip FEEDTEST dma-only "
-                                                        "(profiles/r03_f6_probe_feedtest_dmaonly.log)"}}
+                                      "ceiling_source": "the copies alone: tools/f6_probe.hip FEEDTEST dma-only "
+                                                        "(profiles/r03_f6_probe_feedtest.log)"}}
                             if args.search == "f6" else {})},
             "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else "") + ("+all_gather" if shard_prep else ""):
                            ms_proj, "knn_tiles": ms_tiles,

@@ -326,15 +326,22 @@ struct Engine16 {
   static constexpr int IPW = DMA_INS / NW;   // 6
 
   // fragments live as 6 registers (the fp6 MFMA reads v[0:5] of its 8-register operand slot)
+  // P1 = false (probe only, wrong results): the part1 read skipped -- the cost of the second LDS read
+  template <bool P1 = true>
   static __device__ __forceinline__ i32x6 frag16(const char* st, int row) {
     const int q = (threadIdx.x & 63) >> 4;
     const char* sb = st + q * 6144;
-    const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + p1_slot(q, row) * 8);
-    asm volatile("" : "+v"(p1a));
-    const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
-    const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
     i32x6 f;
-    f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
+    if constexpr (P1) {
+      const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + p1_slot(q, row) * 8);
+      asm volatile("" : "+v"(p1a));
+      const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
+      const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
+      f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
+    } else {
+      const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
+      f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p0[0]; f[5] = p0[1];
+    }
     return f;
   }
   static __device__ __forceinline__ f32x4 mfma(const i32x6& a, const i32x6& b, const f32x4& c, int sa = SCALE_ONE,
@@ -348,6 +355,75 @@ struct Engine16 {
   static __device__ __forceinline__ void mfma_agpr(const i32x6& a, const i32x6& b, f32x4& c, int sc) {
     asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
                  : "+a"(c) : "v"(a), "v"(b), "v"(sc));
+  }
+
+  // Ping-pong main loop (probe MODE 524288).  The two waves of a SIMD (groups g = wr: waves 0-3 and
+  // 4-7; the cyclic wave -> SIMD order puts one of each on every SIMD) run one s_barrier apart, so one
+  // issues its 32 MFMAs (raised priority) while the other reads its 12 fragments of the next stage
+  // and issues its 6 stage copies.  Per stage j a wave runs LOAD(j) (fragment reads of stage j, the
+  // copy of stage j + 2 into the buffer of stage j - 1, the wait for its copies of stage j + 1,
+  // lgkmcnt(0)) and MFMA(j), each closed by an s_barrier.  H(n) = the n-th barrier: group 0 closes
+  // LOAD(j) at H(2j+1) and MFMA(j) at H(2j+2), group 1 one barrier later.
+  //   visibility: every wave waits for its copies of stage j+1 before closing LOAD(j), i.e. by
+  //     H(2j+2); the first reader of stage j+1 (group 0, LOAD(j+1)) starts after H(2j+2);
+  //   reuse: the last reads of stage j-1 (group 1, LOAD(j-1), drained by lgkmcnt(0) before H(2j))
+  //     precede the earliest copy into its buffer (group 0, LOAD(j), after H(2j)).
+  template <int NSEG = 1>
+  static __device__ __forceinline__ void mainloop_pp(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
+                                                     int nst, f32x4 (&acc)[NA][NB], const char* G2 = nullptr,
+                                                     const char* Q2 = nullptr) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr = wave / WQ, wc = wave % WQ, r16 = lane & 15;
+    const bool late = __builtin_amdgcn_readfirstlane(wr) != 0;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int last = NSEG * nst - 1;
+    auto issue = [&](int kt) {
+      const char *g, *q;
+      int ks;
+      const int s = kt < last ? kt : last;
+      seg_src<NSEG>(s, nst, G, G2, Q, Q2, g, q, ks);
+      Engine<8>::dma_buf(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+    };
+    static_assert(NST == 3, "ping-pong assumes 3 stages");
+    issue(0);
+    issue(1);
+    wait_vm<IPW>();                 // own copies of stage 0 landed (1 may fly)
+    __builtin_amdgcn_s_barrier();   // H(0)
+    if (late) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    i32x6 a[NA], b[NB];
+    int sa = SCALE_ONE, sb = SCALE_ONE;
+    for (int kt = 0; kt <= last; ++kt) {
+      // LOAD(kt)
+      const char* st = smem + (kt % NST) * STAGE;
+#pragma unroll
+      for (int c = 0; c < NB; ++c) b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) a[i] = frag16(st, wr * 128 + i * 16 + r16);
+      issue(kt + 2);                // into the buffer of stage kt - 1
+      seg_scales<NSEG>(kt, nst, sa, sb);
+      wait_vm<IPW>();               // own copies of stage kt+1 landed (kt+2 may fly)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // MFMA(kt)
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i], b[c], acc[i][c], sa, sb);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!late) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
+    wait_vm<0>();
+    barrier();
   }
 
   // MODE (probes): 1 = no k-loop DMA; 64 = DMA issued but never waited for (wrong results: isolates
@@ -400,8 +476,9 @@ struct Engine16 {
       if constexpr ((MODE & 256) != 0) mfma_agpr(x, y, c, sc);
       else c = mfma(x, y, c, sa, sb);
     };
-    auto readA = [&](const char* st, int i) { a[i] = frag16(st, wr * 128 + i * 16 + r16); };
-    auto readB = [&](const char* st, int c) { b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16); };
+    constexpr bool P1 = (MODE & 1048576) == 0;   // probe 1048576: no part1 reads (wrong results)
+    auto readA = [&](const char* st, int i) { a[i] = frag16<P1>(st, wr * 128 + i * 16 + r16); };
+    auto readB = [&](const char* st, int c) { b[c] = frag16<P1>(st + PANEL, wc * QW + c * 16 + r16); };
     // probe MODE 16384: the k loop keeps its first fragments (no refills; wrong results): MFMAs + feed
     auto readAk = [&](const char* st, int i) { if constexpr ((MODE & 16384) == 0) readA(st, i); };
     auto readBk = [&](const char* st, int c) { if constexpr ((MODE & 16384) == 0) readB(st, c); };

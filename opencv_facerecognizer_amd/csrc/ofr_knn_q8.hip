@@ -380,7 +380,8 @@ __device__ __forceinline__ void sieve_epilogue16(char* smem, const TileArgs& p, 
   sieve_flush<f6t::TQ>(smem, p, g0, q0);
 }
 
-// fp6 sieve pass on the 16x16x128 engine.  MODE probe bits: 1 = no k-loop DMA, 4 = no epilogue.
+// fp6 sieve pass on the 16x16x128 engine.  MODE probe bits: 1 = no k-loop DMA, 4 = no epilogue; the
+// main loop's own bits (f6t::Engine16::mainloop) pass through the mask below.
 template <int MODE, int NSEG = 1>
 __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   using E = f6t::Engine16;
@@ -391,9 +392,13 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
   f6t::f32x4 acc[8][4];
-  E::mainloop<MODE & 15809, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
-                                p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
-                                reinterpret_cast<const char*>(p.Q2));
+  if constexpr ((MODE & 524288) != 0)   // ping-pong main loop (f6t::Engine16::mainloop_pp)
+    E::mainloop_pp<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+                         p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
+  else
+    E::mainloop<MODE & 1539521, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+                                  p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
+                                  reinterpret_cast<const char*>(p.Q2));
   // sieve operands after the main loop (the 16x16 engine needs every register in it)
   float ga = __builtin_inff(), gs = 0.f, sq2[4], th[4];
   if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
@@ -1266,8 +1271,11 @@ constexpr int F6_NW = 8;
 // (after the first rows); 4096 / 8192 / both: that barrier after rows 0-1 / 0-5 / row 0 (default 0-3);
 // 2048 = column-major halves.  0 = the FLAT global_load_lds loop with one draining barrier per stage.
 // tools/f6_probe.hip times them: 1024 + 4096 + 8192 (re-fill barrier after row 0: 1.9 stages of
-// copy lead) is the fastest, 22.5 against 23.3 ms for 0.
-constexpr int F6S_MODE = 1024 + 4096 + 8192;
+// copy lead) is the fastest, 22.5 against 23.3 ms for 0.  262144: the stage copies issued by waves 0-3
+// alone (12 pieces each, one wave per SIMD) while waves 4-7 issue none, so one wave of every SIMD
+// keeps issuing MFMAs while the other pays the copies' issue cost (round 3: 23.11 -> 22.63 ms,
+// profiles/r03_f6_probe_feed4w.log).
+constexpr int F6S_MODE = 1024 + 4096 + 8192 + 262144;
 
 // name of the fp6 sieve kernel ofr_knn_f6 launches for B > 32, as rocprofv3 reports it (bench.py
 // labels its roofline entry with it, so the record names the variant that actually ran)

@@ -347,11 +347,30 @@ int main(int argc, char** argv) {
         return 1;
     return 0;
   }
-  if (getenv("GGDMA")) {   // the DMA-only variant against the tile-group width
+  if (getenv("GGDMA")) {   // the DMA-only variant and the 4-issuing-wave pass against the tile-group width
     for (int g : {1, 2, 4, 8, 16}) {
       a.gg = g < ntg ? g : ntg;
-      if (run16<13312 + 4 + 16384 + 65536>(a, reps, "dma-only-gg")) return 1;
+      if (run16<13312 + 4 + 16384 + 65536>(a, reps, "dma-only-gg") || run16<13312 + 4 + 262144>(a, reps, "noepi-4w-gg"))
+        return 1;
     }
+    return 0;
+  }
+  if (getenv("NOP1")) {   // the library pass with / without the part1 reads (b64) of every fragment
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (run16<275456>(a, reps, "lib4w") || run16<275456 + 1048576>(a, reps, "lib4w-nop1") ||
+          run16<275456 + 4>(a, reps, "noepi4w") || run16<275456 + 4 + 1048576>(a, reps, "noepi4w-nop1"))
+        return 1;
+    return 0;
+  }
+  if (getenv("FEED4W")) {   // copies issued by waves 0-3 only: with / without refills, epilogue; ping-pong
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (run16<13312>(a, reps, "lib") || run16<13312 + 262144>(a, reps, "lib-4w") || run16<524288>(a, reps, "pingpong") ||
+          run16<524288 + 4>(a, reps, "pingpong-noepi") || run16<13312 + 4>(a, reps, "noepi") ||
+          run16<13312 + 4 + 262144>(a, reps, "noepi-4w") || run16<13312 + 4 + 16384>(a, reps, "noepi-norefill") ||
+          run16<13312 + 4 + 16384 + 262144>(a, reps, "noepi-norefill-4w"))
+        return 1;
     return 0;
   }
   if (getenv("FEEDTEST")) {   // the library sieve pass without its epilogue, without its fragment refills
