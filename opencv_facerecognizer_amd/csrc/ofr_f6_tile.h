@@ -56,19 +56,8 @@ __host__ __device__ constexpr int64_t tiles_bytes(int64_t rows, int64_t d) {
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-  else if constexpr (N == 21) asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else static_assert(N == 0 || N == 3 || N == 4 || N == 10 || N == 6 || N == 7 || N == 8 || N == 12 || N == 14 || N == 21 || N == 24,
-                     "vmcnt");
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 __device__ __forceinline__ void barrier() {
@@ -190,6 +179,7 @@ struct Engine {
   }
 
   // probe only: the same copies issued by waves 0-3 alone (12 pieces each), waves 4-7 issue none
+  template <int T0 = 0, int T1 = 2 * IPW>
   static __device__ __forceinline__ void dma_buf4(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst,
                                                   int kt, char* st) {
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
@@ -200,7 +190,7 @@ struct Engine {
     __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * nst * (int64_t)PANEL), 0, pb,
                                                                   0x00020000);
 #pragma unroll
-    for (int t = 0; t < 2 * IPW; ++t) {
+    for (int t = T0; t < T1; ++t) {
       const int ins = wave * 2 * IPW + t;
       const bool gal = ins < DMA_INS / 2;
       const int off = (gal ? ins : ins - DMA_INS / 2) * 1024;
@@ -226,6 +216,123 @@ struct Engine {
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     if constexpr (MF - two - one > 0) __builtin_amdgcn_sched_group_barrier(0x008, MF - two - one, 0);
+  }
+
+  // Deep-staged main loop (NW = 8; tile_kernel_f6 MODE bit 32).  The buffers hold 64-feature
+  // half-stages (one MFMA k-step: 12 KiB of each panel block, 24 KiB per buffer), six of them, so a
+  // half-stage's copy is issued five half-stages (120 KiB) ahead of its reads; a 16x16x128 fragment
+  // spans 128 features and could not start before both halves of its stage landed, the 32x32x64
+  // fragment of this engine needs one half.  The 24 copy pieces of a half-stage: 3 per wave (MUBUF,
+  // branch-free, so the k loop stays one scheduling region).  Per
+  // half-stage u: wait for the own copies of u+1, s_barrier (every wave has consumed the fragments
+  // of u-1 and read those of u: buffers u-1 and u are free), copy u+5 into buffer (u+5) % 6 =
+  // (u-1) % 6, then u's 8 MFMAs with u+1's 6 fragments read between them (fragments double-buffered
+  // by parity).
+  template <int NSEG = 1>
+  static __device__ __forceinline__ void mainloop_deep(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
+                                                       int nst, f32x16 (&acc)[4][CT], const char* G2 = nullptr,
+                                                       const char* Q2 = nullptr) {
+    static_assert(NW == 8, "deep-staged loop: 8 waves");
+    constexpr int HB = PANEL / 2;                   // one operand's half-stage
+    constexpr int DST = 2 * HB;                     // 24 KiB per buffer
+    constexpr int NBUF = 6, LEAD = NBUF - 1;        // 144 KiB
+    constexpr int HPW = DST / 1024 / NW;            // copy pieces per wave (3)
+    static_assert(NBUF * DST <= LDS, "fits the kernel's LDS");
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
+    const int wu = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < CT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int last = 2 * NSEG * nst - 1;            // half-stages
+    const int pb = (int)(nst * PANEL);
+    auto issue = [&](int u) {
+      const int uu = u < last ? u : last;
+      const char *g, *q;
+      int ks;
+      seg_src<NSEG>(uu >> 1, nst, G, G2, Q, Q2, g, q, ks);
+      __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(g + gp * nst * (int64_t)PANEL), 0, pb,
+                                                                    0x00020000);
+      __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)(q + qp * nst * (int64_t)PANEL), 0, pb,
+                                                                    0x00020000);
+      char* st = smem + (u % NBUF) * DST;
+      const int src = ks * PANEL + (uu & 1) * HB;
+#pragma unroll
+      for (int t = 0; t < HPW; ++t) {
+        const int ins = wu * HPW + t;               // waves 0-3: gallery, 4-7: queries
+        const bool gal = ins < DST / 2048;
+        const int off = (gal ? ins : ins - DST / 2048) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(gal ? rg : rq, (OFR_LDS void*)(st + (gal ? 0 : HB) + off), 16,
+                                                 src + off + lane * 16, 0, 0, 0);
+      }
+    };
+#pragma unroll
+    for (int u = 0; u < LEAD; ++u) issue(u);
+    i32x6 ga[2][4], qb[2][CT];
+    auto frag6 = [&](const char* blk, int row) {    // sub-block h of the half-stage image
+      const char* sb = blk + h * 6144;
+      const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + p1_slot(h, row) * 8);
+      asm volatile("" : "+v"(p1a));
+      const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
+      const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
+      i32x6 f;
+      f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
+      return f;
+    };
+    auto frags = [&](int u, int set) {
+      const char* st = smem + (u % NBUF) * DST;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) qb[set][c] = frag6(st + HB, wc * QW + c * 32 + r32);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ga[set][i] = frag6(st, wr * 128 + i * 32 + r32);
+    };
+    int sa = SCALE_ONE, sb = SCALE_ONE;
+    auto mfmas = [&](int set) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const i32x8 a8 = __builtin_shufflevector(ga[set][i], ga[set][i], 0, 1, 2, 3, 4, 5, -1, -1);
+          const i32x8 b8 = __builtin_shufflevector(qb[set][c], qb[set][c], 0, 1, 2, 3, 4, 5, -1, -1);
+          acc[i][c] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[i][c], 2, 2, 0, sa, 0, sb);
+        }
+    };
+    wait_vm<(LEAD - 1) * HPW>();                    // own copies of half-stage 0 landed
+    barrier();
+    frags(0, 0);
+    // one half-stage; SET (compile time: register arrays indexed by constants) = u & 1
+    auto step = [&](int u, auto setc) {
+      constexpr int SET = decltype(setc)::value;
+      seg_scales<NSEG>(u >> 1, nst, sa, sb);
+      wait_vm<(LEAD - 2) * HPW>();                  // own copies of u+1 landed (u+2 .. u+4 may fly)
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      issue(u + LEAD);
+      __builtin_amdgcn_sched_barrier(0);
+      frags(u + 1, SET ^ 1);                        // u = last: unused reads of a stale buffer
+      mfmas(SET);
+      // 8 MFMAs with the 12 fragment reads between them: two after each of the first four, one after the next four
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int u = 0; u <= last; u += 2) {            // last + 1 = 2 NSEG nst half-stages: even
+      step(u, std::integral_constant<int, 0>{});
+      step(u + 1, std::integral_constant<int, 1>{});
+    }
+    wait_vm<0>();
+    barrier();
   }
 
   // Main loop, stage hand-off in the middle of a stage.  Per stage kt:
@@ -508,12 +615,23 @@ struct Engine16 {
       // 4 by default, 2 (MODE 4096), 6 (MODE 8192) or 1 (both) in the probe
       constexpr int RS = (MODE & 4096) && (MODE & 8192) ? 1 : ((MODE & 4096) ? 2 : ((MODE & 8192) ? 6 : 4));
       static_assert((MODE & 2048) == 0 || RS == 4, "column-major halves split at row 4");
+      // probe 2097152 (with 262144): the 12 pieces of an issuing wave in three chunks of 4, after the
+      // re-fill barrier and after the next two fragment rows, instead of one burst
+      constexpr bool SPREAD = (MODE & 2097152) != 0 && (MODE & 262144) != 0;
       auto issue_b = [&](int kt) {
         const char *g, *q;
         int ks;
         seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
-        if constexpr ((MODE & 262144) != 0) Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+        if constexpr (SPREAD) Engine<8>::dma_buf4<0, 4>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+        else if constexpr ((MODE & 262144) != 0) Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
         else Engine<8>::dma_buf(g, (MODE & 131072) ? 0 : gp, q, (MODE & 131072) ? 0 : qp, nst, ks, smem + (kt % NST) * STAGE);
+      };
+      auto issue_rest = [&](int kt, auto chunk) {   // SPREAD: pieces 4 chunk .. 4 chunk + 3
+        constexpr int C = decltype(chunk)::value;
+        const char *g, *q;
+        int ks;
+        seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
+        Engine<8>::dma_buf4<4 * C, 4 * C + 4>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
       };
       for (int kt = 0; kt < last; ++kt) {
         seg_scales<NSEG>(kt, nst, sa, sb);
@@ -592,6 +710,11 @@ struct Engine16 {
 #pragma unroll
           for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
           readAk(nxt, i);
+          if constexpr (SPREAD) {
+            const int nx = kt + NST;
+            if (i == RS) issue_rest(nx < last ? nx : last, std::integral_constant<int, 1>{});
+            if (i == RS + 1) issue_rest(nx < last ? nx : last, std::integral_constant<int, 2>{});
+          }
         }
 #pragma unroll
         for (int c = 0; c < NB; ++c) {

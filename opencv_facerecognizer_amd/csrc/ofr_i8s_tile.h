@@ -51,9 +51,25 @@ __device__ __forceinline__ void wait_vm() {
 
 // Stage kt of both panels into st.  ra / rb: buffer descriptors of the tile's A / B row panels
 // (base = first row of the panel, num_records = its readable bytes); lda / ldb their row pitch.
+// W4: the 32 pieces issued by waves 0-3 alone (8 each: 4 of A, 4 of B), waves 4-7 issue none.
+template <bool W4 = false>
 __device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t ra, int lda, __amdgpu_buffer_rsrc_t rb, int ldb, int kt,
                                     char* st) {
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  if constexpr (W4) {
+    if (wave >= 4) return;
+#pragma unroll
+    for (int t = 0; t < 2 * IPW; ++t) {
+      const bool a_side = t < IPW;
+      const int ins = wave * IPW + (t % IPW);
+      const int row = ins * 16 + (lane >> 2);
+      const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+      const int voff = row * (a_side ? lda : ldb) + kt * BK + chunk * 16;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_side ? ra : rb,
+                                               (OFR_LDS void*)(st + (a_side ? 0 : PANEL) + ins * 1024), 16, voff, 0, 0, 0);
+    }
+    return;
+  }
   const bool a_side = wave < NW / 2;   // uniform per wave
 #pragma unroll
   for (int t = 0; t < IPW; ++t) {
@@ -69,7 +85,7 @@ __device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t ra, int lda, __amdgpu
 
 // Main loop over nk stages.  XB: B holds uint8 (images), fragments become x - 128 by XOR 0x80.
 // acc[i][j]: A block i (rows wr*128 + 32 i + C/D row map) x B block j (rows wc*64 + 32 j + lane&31).
-template <int NST, bool XB>
+template <int NST, bool XB, bool W4 = false>
 __device__ __forceinline__ void mainloop(char* smem, __amdgpu_buffer_rsrc_t ra, int lda, __amdgpu_buffer_rsrc_t rb,
                                          int ldb, int nk, i32x16 (&acc)[4][CT]) {
   static_assert(NST == 4 || NST == 5, "stages");
@@ -84,7 +100,8 @@ __device__ __forceinline__ void mainloop(char* smem, __amdgpu_buffer_rsrc_t ra, 
 
   // branch-free: a stage past the end re-loads the last stage into a buffer nobody reads any more
   const int last = nk - 1;
-  auto issue = [&](int s) { dma(ra, lda, rb, ldb, s < last ? s : last, smem + (s % NST) * STAGE); };
+  auto issue = [&](int s) { dma<W4>(ra, lda, rb, ldb, s < last ? s : last, smem + (s % NST) * STAGE); };
+  constexpr int PW = W4 ? 2 * IPW : IPW;   // pieces per issuing wave and stage
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s) issue(s);
 
@@ -119,7 +136,7 @@ __device__ __forceinline__ void mainloop(char* smem, __amdgpu_buffer_rsrc_t ra, 
     __builtin_amdgcn_sched_group_barrier(0x008, 4 * CT - (4 + CT) - 1, 0);
   };
 
-  wait_vm<(NST - 2) * IPW>();   // stage 0 landed (own copies); 1 .. NST-2 may be in flight
+  wait_vm<(NST - 2) * PW>();   // stage 0 landed (own copies); 1 .. NST-2 may be in flight
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   frags(smem, 0);
@@ -129,13 +146,13 @@ __device__ __forceinline__ void mainloop(char* smem, __amdgpu_buffer_rsrc_t ra, 
     mfmas(0);
     interleave();
     __builtin_amdgcn_sched_barrier(0);
-    wait_vm<(NST - 3) * IPW>();   // stage kt+1 landed; kt+2 .. kt+NST-2 may be in flight
+    wait_vm<(NST - 3) * PW>();   // stage kt+1 landed; kt+2 .. kt+NST-2 may be in flight
     __builtin_amdgcn_s_barrier();   // ... for every wave; and every wave has consumed stage kt-1
     __builtin_amdgcn_sched_barrier(0);
     issue(kt + NST - 1);            // into stage kt-1's buffer
     frags(smem + ((kt + 1) % NST) * STAGE, 0);   // kt = last: unused reads of a stale buffer
     mfmas(1);
-    __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
+    if constexpr (!W4) __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
     interleave();
     __builtin_amdgcn_sched_barrier(0);
   }

@@ -295,9 +295,10 @@ __global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
-  // sieve operands, loaded under the main loop
+  // sieve operands, loaded under the main loop (after it for the deep-staged loop: ordinary loads in
+  // flight beside its LDS-DMA make the compiler wait vmcnt(0) inside the loop)
   float ga = __builtin_inff(), gs = 0.f, sq2[CT], th[CT];
-  if constexpr (SIEVE) {
+  auto sieve_operands = [&]() {
     static_assert(E::NT >= TG, "one gallery row per thread");
     if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
       ga = p.aux[g0 + threadIdx.x];
@@ -311,11 +312,18 @@ __global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
       sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
       th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
     }
-  }
+  };
+  if constexpr (SIEVE && (MODE & 32) == 0) sieve_operands();
   f6t::f32x16 acc[4][CT];
-  E::template mainloop<MODE & 19, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp,
-                                       reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG, acc,
-                                       reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
+  if constexpr ((MODE & 32) != 0)   // deep-staged loop: 64-feature half-stages in 6 buffers (f6t::Engine::mainloop_deep)
+    E::template mainloop_deep<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+                                    p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
+                                    reinterpret_cast<const char*>(p.Q2));
+  else
+    E::template mainloop<MODE & 19, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp,
+                                         reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG, acc,
+                                         reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
+  if constexpr (SIEVE && (MODE & 32) != 0) sieve_operands();
   if constexpr ((MODE & 4) != 0) {   // probe: no epilogue (the accumulators kept alive)
     float s = 0.f;
 #pragma unroll
@@ -396,7 +404,7 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
     E::mainloop_pp<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
                          p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
   else
-    E::mainloop<MODE & 1539521, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+    E::mainloop<MODE & 3636673, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
                                   p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
                                   reinterpret_cast<const char*>(p.Q2));
   // sieve operands after the main loop (the 16x16 engine needs every register in it)

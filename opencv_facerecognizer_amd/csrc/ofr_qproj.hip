@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(S::NT, 1) project_q8_kernel(Args p) {
 // The default engine (ofr_i8s_tile.h): 64-feature stages in NST buffers, MUBUF copies, mid-stage
 // hand-off.  The panels' buffer descriptors bound the reads: B rows past the batch read as zero
 // (their outputs are not stored); columns past D meet zero W columns.
-template <int NST, bool XB = true, bool PP = false>
+template <int NST, bool XB = true, bool PP = false, bool W4 = false>
 __global__ void __launch_bounds__(i8s::NT, 1) project_q8s_kernel(Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(i8s::NT, 1) project_q8s_kernel(Args p) {
                                                                 0x00020000);
   i32x16 acc[4][S::CT];
   if constexpr (PP) i8s::mainloop_pp<NST, XB>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
-  else i8s::mainloop<NST, XB>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
+  else i8s::mainloop<NST, XB, W4>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
   project_epilogue(p, acc, ft, b0, wr, wc, h, r32);
 }
 
@@ -353,6 +353,7 @@ static int proj_engine() {
     if (e && strcmp(e, "s5p") == 0) return 6;
     if (e && strcmp(e, "pp4") == 0) return 7;
     if (e && strcmp(e, "pp5") == 0) return 8;
+    if (e && strcmp(e, "s5w") == 0) return 9;
     return 0;
   }();
   return f;
@@ -387,6 +388,9 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
                               hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<4>::BYTES);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, true, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8)");
     attr_done = true;
@@ -434,7 +438,10 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   p.nk = (int)cdiv(D, i8s::BK);
   p.ntb = cdiv(B, i8s::TB);
   OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-  if (engine == 7) {
+  if (engine == 9) {
+    hipLaunchKernelGGL((q8::project_q8s_kernel<5, true, false, true>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
+                       i8s::Lds<5>::BYTES, (hipStream_t)stream, p);
+  } else if (engine == 7) {
     hipLaunchKernelGGL((q8::project_q8s_kernel<4, true, true>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
                        i8s::Lds<4>::BYTES, (hipStream_t)stream, p);
   } else if (engine == 8) {

@@ -355,11 +355,20 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (getenv("DEEP32")) {   // the 32x32x64 engine with 64-feature half-stages in 6 buffers vs the library pass
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (run16<275456>(a, reps, "lib4w") || run<8, 8>(a, reps, "sieve32") || run<8, 40>(a, reps, "sieve32-deep") ||
+          run<8, 44>(a, reps, "deep-noepi") || run<8, 13>(a, reps, "nodma-noepi32"))
+        return 1;
+    return 0;
+  }
   if (getenv("NOP1")) {   // the library pass with / without the part1 reads (b64) of every fragment
     a.gg = 4 < ntg ? 4 : ntg;
     for (int rep = 0; rep < 2; ++rep)
       if (run16<275456>(a, reps, "lib4w") || run16<275456 + 1048576>(a, reps, "lib4w-nop1") ||
-          run16<275456 + 4>(a, reps, "noepi4w") || run16<275456 + 4 + 1048576>(a, reps, "noepi4w-nop1"))
+          run16<275456 + 4>(a, reps, "noepi4w") || run16<275456 + 4 + 1048576>(a, reps, "noepi4w-nop1") ||
+          run16<275456 + 2097152>(a, reps, "lib4w-spread") || run16<275456 + 4 + 2097152>(a, reps, "noepi4w-spread"))
         return 1;
     return 0;
   }
