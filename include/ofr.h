@@ -434,6 +434,18 @@ int ofr_knn_sharded(ofr_comm* comm, const ofr_knn_shard* shards, int64_t B, int6
  * certificate (bound -inf / NaN never certifies; +inf always does).             */
 int ofr_topk_merge_certify(void* stream, const double* lists, int P, int64_t B, int k, double* out_d,
                            int64_t* out_i, int* cert);
+/* The pieces of that exchange for callers with their own transport (the package's
+ * torch.distributed path, parallel.py):
+ * ofr_topk_pack: d [B][k] fp64, i [B][k] int64, bound [B] (NULL: +inf) -> out [B][2k+1]
+ * (the layout ofr_topk_merge_certify reads, one rank's block);
+ * ofr_kth_bound: all [P][B][k] fp64, each rank's k upper bounds ascending -> ub [B] = the
+ * k-th smallest of the P*k (the pruned merge's global bound, classifier.py:113-119 across
+ * shards);
+ * ofr_open_rows: cert [B] int -> rows[0..count) = the b with cert[b] == 0, ascending, and
+ * count[0] (device; the caller reads count to size the next tier).                    */
+int ofr_topk_pack(void* stream, const double* d, const int64_t* i, const double* bound, int64_t B, int k, double* out);
+int ofr_kth_bound(void* stream, const double* all, int P, int64_t B, int k, double* ub);
+int ofr_open_rows(void* stream, const int* cert, int64_t B, int64_t* rows, int* count);
 
 /* Face-tensor ingestion ------------------------------------
  * Replaces cv2.imread(IMREAD_GRAYSCALE) + cv2.resize(im, size) [INTER_LINEAR] of

@@ -475,7 +475,7 @@ class FloatGallery:
         Returns the number of first-tier failures (host sync); self.last_fallbacks = the number of
         uncertified queries after each quantized tier that ran.  timings (a list, optional)
         receives (tier, queries, ms) per stage that ran (HIP events on the current stream)."""
-        bad = torch.nonzero(qq["cert"] == 0).reshape(-1)
+        bad = open_rows(qq["cert"])
         counts = [int(bad.numel())]
         pending = {}                    # tier -> indices into the original batch waiting for it
         self.last_skipped = {}
@@ -501,7 +501,7 @@ class FloatGallery:
                 d2, i2 = self.search_q8_phase(3, sub, q2, k, index_base)
                 out[0].index_copy_(0, rows, d2)
                 out[1].index_copy_(0, rows, i2)
-                still = torch.nonzero(q2["cert"] == 0).reshape(-1)
+                still = open_rows(q2["cert"])
                 counts.append(int(still.numel()))
                 self._route(tier, rows.index_select(0, still), Qd, q2["stats"].index_select(0, still),
                             q2["bound"].index_select(0, still), out, k, pending)
@@ -722,7 +722,7 @@ class Chi2Gallery:
         ws = self.ws.get(lib.ofr_chi2_workspace_bytes(B, self.N, k), Qd.device)
         call("ofr_chi2_knn", stream(), self.dtype, ptr(Qd), B, Qd.shape[1], ptr(self.G), self.N, self.G.shape[1],
              self.nbins, self.denom, k, index_base, ptr(out_d), ptr(out_i), ptr(ws), ws.numel(), ptr(cert))
-        rows = torch.nonzero(cert == 0).reshape(-1)
+        rows = open_rows(cert)
         counts = [int(rows.numel())]
         if rows.numel():
             sub = Qd.index_select(0, rows).contiguous()
@@ -746,6 +746,42 @@ class Chi2Gallery:
         if self.dtype != _lib.DT_F32:
             return self.counts_rows(arr)
         return f32_rows(np.asarray(arr, np.float64), ld=self.G.shape[1])
+
+
+def topk_pack(d, i, bound=None):
+    """(B x k) distances, indices and the per-query bound -> one [B][2k+1] fp64 block (ofr_topk_pack)."""
+    B, k = d.shape
+    out = torch.empty((B, 2 * k + 1), dtype=torch.float64, device=d.device)
+    call("ofr_topk_pack", stream(), ptr(d.contiguous()), ptr(i.contiguous()),
+         None if bound is None else ptr(bound.contiguous()), B, k, ptr(out))
+    return out
+
+
+def topk_merge_certify(lists, P, B, k, certify=True):
+    """Gathered blocks [P][B][2k+1] -> (best k distances, indices, certificate int32 or None)
+    (ofr_topk_merge_certify)."""
+    out_d = torch.empty((B, k), dtype=torch.float64, device=lists.device)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=lists.device)
+    cert = torch.empty(B, dtype=torch.int32, device=lists.device) if certify else None
+    call("ofr_topk_merge_certify", stream(), ptr(lists.contiguous()), P, B, k, ptr(out_d), ptr(out_i), ptr(cert))
+    return out_d, out_i, cert
+
+
+def kth_bound(allb, P, B, k):
+    """[P][B][k] ascending upper bounds -> [B] k-th smallest over the P*k (ofr_kth_bound)."""
+    ub = torch.empty(B, dtype=torch.float64, device=allb.device)
+    call("ofr_kth_bound", stream(), ptr(allb.contiguous()), P, B, k, ptr(ub))
+    return ub
+
+
+def open_rows(cert):
+    """int32 certificate [B] -> int64 device indices of the uncertified queries, ascending
+    (ofr_open_rows; one host read of their count)."""
+    B = cert.shape[0]
+    rows = torch.empty(max(B, 1), dtype=torch.int64, device=cert.device)
+    cnt = torch.empty(1, dtype=torch.int32, device=cert.device)
+    call("ofr_open_rows", stream(), ptr(cert.contiguous()), B, ptr(rows), ptr(cnt))
+    return rows[:int(cnt.item())]
 
 
 def topk_merge(in_d, in_i, P, kin, k):

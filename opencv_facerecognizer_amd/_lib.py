@@ -106,6 +106,9 @@ SIGNATURES = {
     "ofr_knn_sharded_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_int, c_int]),
     "ofr_knn_sharded": (c_int, [c_vp, c_vp, c_i64, c_i64, c_int]),
     "ofr_topk_merge_certify": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp]),
+    "ofr_topk_pack": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "ofr_kth_bound": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp]),
+    "ofr_open_rows": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "ofr_eig_workspace_bytes": (c_sz, [c_i64, c_i64]),
     "ofr_ctx_create": (c_int, [c_int, c_vp]),
     "ofr_ctx_destroy": (c_int, [c_vp]),

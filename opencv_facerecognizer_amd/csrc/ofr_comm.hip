@@ -160,6 +160,35 @@ __global__ void kth_bound_kernel(const double* all, int P, int64_t B, int k, dou
   ub[q] = best[k - 1];
 }
 
+// rows[0 .. count) = the b with cert[b] == 0, ascending (one workgroup: a block-wide prefix sum per
+// 1024-query chunk); count[0] = their number
+__global__ void __launch_bounds__(1024) open_rows_kernel(const int* cert, int64_t B, int64_t* rows, int* count) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) base = 0;
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < B; c0 += 1024) {
+    const int64_t b = c0 + t;
+    const int open = b < B && cert[b] == 0;
+    const unsigned long long m = __ballot(open);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int j = 0; j < w; ++j) off += wsum[j];
+    if (open) rows[off + before] = b;
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+      for (int j = 0; j < 16; ++j) tot += wsum[j];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  if (t == 0) count[0] = base;
+}
+
 __global__ void gather_rows_kernel(const float* Q, int64_t ldq, const int64_t* rows, int64_t n, float* out) {
   const int64_t r = blockIdx.x;
   if (r >= n) return;
@@ -254,6 +283,35 @@ extern "C" int ofr_comm_size(const ofr_comm* c) { return c ? c->ndev : 0; }
 
 extern "C" size_t ofr_knn_sharded_workspace_bytes(int64_t B, int64_t N, int64_t ldq, int k, int ndev) {
   return comm::layout(B, N, ldq, k, ndev).total;
+}
+
+extern "C" int ofr_topk_pack(void* stream, const double* d, const int64_t* i, const double* bound, int64_t B, int k,
+                             double* out) {
+  OFR_CHECK_ARG(B >= 0 && k >= 1 && k <= OFR_MAX_K, "ofr_topk_pack: bad sizes");
+  if (B == 0) return OFR_OK;
+  OFR_CHECK_ARG(d && i && out, "ofr_topk_pack: null pointer");
+  hipLaunchKernelGGL(comm::pack_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream, d, i, bound, B,
+                     k, out);
+  OFR_LAUNCH_CHECK("pack_kernel");
+  return OFR_OK;
+}
+
+extern "C" int ofr_kth_bound(void* stream, const double* all, int P, int64_t B, int k, double* ub) {
+  OFR_CHECK_ARG(P >= 1 && B >= 0 && k >= 1 && k <= OFR_MAX_K, "ofr_kth_bound: bad sizes");
+  if (B == 0) return OFR_OK;
+  OFR_CHECK_ARG(all && ub, "ofr_kth_bound: null pointer");
+  hipLaunchKernelGGL(comm::kth_bound_kernel, dim3((unsigned)cdiv(B, 128)), dim3(128), 0, (hipStream_t)stream, all, P, B,
+                     k, ub);
+  OFR_LAUNCH_CHECK("kth_bound_kernel");
+  return OFR_OK;
+}
+
+extern "C" int ofr_open_rows(void* stream, const int* cert, int64_t B, int64_t* rows, int* count) {
+  OFR_CHECK_ARG(B >= 0 && B < 0x7fffffffLL, "ofr_open_rows: bad size");
+  OFR_CHECK_ARG(cert && rows && count, "ofr_open_rows: null pointer");
+  hipLaunchKernelGGL(comm::open_rows_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, cert, B, rows, count);
+  OFR_LAUNCH_CHECK("open_rows_kernel");
+  return OFR_OK;
 }
 
 extern "C" int ofr_topk_merge_certify(void* stream, const double* lists, int P, int64_t B, int k, double* out_d,

@@ -83,6 +83,30 @@ def exchange_topk(d, i, group=None):
     return gd, gi
 
 
+def topk_pack(d, i, bound=None):
+    """This rank's (B x k) lists + bound -> one [B][2k+1] fp64 block (device kernel)."""
+    from ._device import topk_pack as _pack
+    return _pack(d, i, bound)
+
+
+def topk_merge_certify(lists, P, B, k, certify=True):
+    """Gathered [P][B][2k+1] blocks -> merged (d, i) and the global certificate (device kernel)."""
+    from ._device import topk_merge_certify as _mc
+    return _mc(lists, P, B, k, certify)
+
+
+def kth_bound(allb, P, B, k):
+    """[P][B][k] ascending per-rank upper bounds -> [B] k-th smallest over the ranks (device kernel)."""
+    from ._device import kth_bound as _kb
+    return _kb(allb, P, B, k)
+
+
+def open_rows(cert):
+    """int32 certificate -> int64 indices of the uncertified queries (device compaction, one count read)."""
+    from ._device import open_rows as _or
+    return _or(cert)
+
+
 def merge_topk(gd, gi, nlists, kin, k):
     """Device merge of the gathered lists (ofr_topk_merge)."""
     if nlists == 1 and kin == k:
@@ -134,8 +158,7 @@ def merge_sharded(gallery, Qd, qq, k, index_base, out, group=None):
     B = Qd.shape[0]
     ub_local = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
     gallery.merge_pruned(1, Qd, qq, k, ub_local, index_base)
-    allb = gather_rows(ub_local, group).reshape(ws, B, k).permute(1, 0, 2).reshape(B, ws * k)
-    ub = allb.kthvalue(k, dim=1).values.contiguous()
+    ub = kth_bound(gather_rows(ub_local, group), ws, B, k)     # [ws][B][k] rank-major -> [B]
     return gallery.merge_pruned(2, Qd, qq, k, ub, index_base, out)
 
 
@@ -168,14 +191,14 @@ def certify_sharded(gallery, Qd, qq, k, out, index_base, group=None):
     _, ws = world(group)
 
     def merged(d, i, bound):
-        gd, gi, minb = exchange_lists(d, i, bound, group)
-        md, mi = merge_topk(gd, gi, ws, k, k)
-        if bound is None:
-            return md, mi, None
-        return md, mi, global_certificate(md[:, k - 1], minb)
+        # one [B][2k+1] block per rank (ofr_topk_pack), ONE all-gather, then the merge and the global
+        # certificate in one kernel (ofr_topk_merge_certify; bound None: +inf, the certificate unused)
+        B = d.shape[0]
+        lists = gather_rows(topk_pack(d.to(torch.float64), i.to(torch.int64), bound), group)
+        return topk_merge_certify(lists, ws, B, k, certify=bound is not None)
 
     md, mi, cert = merged(out[0], out[1], qq["bound"])
-    rows = torch.nonzero(~cert).reshape(-1)
+    rows = open_rows(cert)
     counts = [int(rows.numel())]
     tier = qq["tier"]
     while rows.numel():
@@ -192,7 +215,7 @@ def certify_sharded(gallery, Qd, qq, k, out, index_base, group=None):
         mi.index_copy_(0, rows, mi2)
         if tier == "fp32":
             break
-        still = torch.nonzero(~c2).reshape(-1)
+        still = open_rows(c2)
         counts.append(int(still.numel()))
         rows = rows.index_select(0, still)
     return (md, mi), counts

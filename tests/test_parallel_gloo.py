@@ -151,7 +151,7 @@ def _cert_worker(rank, ws, port, k, out, overflow=False):
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
         import opencv_facerecognizer_amd.parallel as par
-        par.merge_topk = _host_merge                      # the device merge kernel needs a GPU
+        _patch_host_kernels(par)                          # the device kernels need a GPU
         Q, G = _data()
         n0, n1 = shard_range(len(G), rank, ws)
         # rank 1 overflows on the queries that are copies of its own rows (their true neighbours)
@@ -175,6 +175,48 @@ def _overflow_queries(Q, G):
     Q = Q.copy()
     Q[_OVERFLOW_Q] = G[700:708]          # rows of rank 1's shard [500, 1001)
     return Q
+
+
+# host restatements of the device kernels the sharded path calls (csrc/ofr_comm.hip: pack_kernel,
+# merge_certify_kernel, kth_bound_kernel, open_rows_kernel), for workers without a GPU
+def _host_pack(d, i, bound=None):
+    B, k = d.shape
+    out = np.empty((B, 2 * k + 1))
+    out[:, :k] = d.numpy()
+    out[:, k:2 * k] = i.numpy().astype(np.int64).view(np.float64)
+    out[:, 2 * k] = np.inf if bound is None else bound.numpy()
+    return torch.from_numpy(out)
+
+
+def _host_merge_certify(lists, P, B, k, certify=True):
+    g = lists.numpy().reshape(P, B, 2 * k + 1)
+    gd = g[:, :, :k].transpose(1, 0, 2).reshape(B, P * k)
+    gi = np.ascontiguousarray(g[:, :, k:2 * k]).view(np.int64).transpose(1, 0, 2).reshape(B, P * k)
+    md, mi = _host_merge(torch.from_numpy(gd.copy()), torch.from_numpy(gi.copy()), P, k, k)
+    if not certify:
+        return md, mi, None
+    bnd = g[:, :, 2 * k]
+    minb = np.where(np.isnan(bnd).any(0), -np.inf, bnd.min(0))
+    kth = md.numpy()[:, k - 1]
+    cert = ((kth * kth < minb) | np.isposinf(minb)).astype(np.int32)
+    return md, mi, torch.from_numpy(cert)
+
+
+def _host_kth_bound(allb, P, B, k):
+    a = allb.numpy().reshape(P, B, k).transpose(1, 0, 2).reshape(B, P * k)
+    return torch.from_numpy(np.sort(a, axis=1)[:, k - 1].copy())
+
+
+def _host_open_rows(cert):
+    return torch.from_numpy(np.nonzero(cert.numpy() == 0)[0].astype(np.int64))
+
+
+def _patch_host_kernels(par):
+    par.merge_topk = _host_merge
+    par.topk_pack = _host_pack
+    par.topk_merge_certify = _host_merge_certify
+    par.kth_bound = _host_kth_bound
+    par.open_rows = _host_open_rows
 
 
 def _host_merge(gd, gi, nlists, kin, k):
@@ -317,7 +359,9 @@ def _pruned_worker(rank, ws, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
+        import opencv_facerecognizer_amd.parallel as par
         from opencv_facerecognizer_amd.parallel import merge_sharded
+        _patch_host_kernels(par)
         g = _PrunedMock(rank)
         B, k = 4, 3
         merge_sharded(g, torch.zeros((B, 8)), {"tier": "f6"}, k, 0, None)
