@@ -890,6 +890,33 @@ def _merge_certify_ref(lists, P, B, k):
     return od, oi, cert
 
 
+@pytest.mark.parametrize("B", [1, 1000, 4096, 70001])
+def test_exchange_kernels_pack_kth_open_rows(B):
+    """The sharded step's exchange kernels against numpy: ofr_topk_pack (one rank's [B][2k+1] block,
+    NULL bound = +inf), ofr_kth_bound (k-th smallest of P ascending lists of k bounds, +inf rows) and
+    ofr_open_rows (ascending indices of cert == 0, across the 1024-query chunks of its scan)."""
+    from opencv_facerecognizer_amd import _device as D_
+    r = _rng(37 + B)
+    k, P = 3, 4
+    d = np.sort(r.random((B, k)), axis=1)
+    i = r.integers(-1, 10 ** 9, (B, k)).astype(np.int64)
+    bnd = r.random(B)
+    for bound in (None, bnd):
+        out = D_.topk_pack(torch.from_numpy(d).cuda(), torch.from_numpy(i).cuda(),
+                           None if bound is None else torch.from_numpy(bound).cuda()).cpu().numpy()
+        assert np.array_equal(out[:, :k], d) and np.array_equal(out[:, k:2 * k].copy().view(np.int64), i)
+        assert np.array_equal(out[:, 2 * k], np.full(B, np.inf) if bound is None else bound)
+    allb = np.sort(r.random((P, B, k)) * 10, axis=2)
+    allb[1, ::7] = np.inf                                  # a rank with no candidate for some queries
+    ub = D_.kth_bound(torch.from_numpy(allb).cuda(), P, B, k).cpu().numpy()
+    ref = np.sort(allb.transpose(1, 0, 2).reshape(B, P * k), axis=1)[:, k - 1]
+    assert np.array_equal(ub, ref)
+    cert = (r.random(B) < 0.7).astype(np.int32)
+    rows = D_.open_rows(torch.from_numpy(cert).cuda()).cpu().numpy()
+    assert np.array_equal(rows, np.nonzero(cert == 0)[0])
+    assert D_.open_rows(torch.ones(B, dtype=torch.int32, device="cuda")).numel() == 0
+
+
 def test_topk_merge_certify_kernel():
     """In-library global certificate (ofr_topk_merge_certify): P = 3 ranks' lists with ties across
     ranks, empty slots, and bounds -inf (an overflowed rank: never certifies), +inf, NaN, finite."""
