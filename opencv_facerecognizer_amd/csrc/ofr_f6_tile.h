@@ -66,6 +66,13 @@ __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+#ifdef OFR_F6_STAMPS
+// probe only (tools/f6_probe.hip, MODE 8388608): per (workgroup < STAMP_WG, wave) the summed cycles
+// of the sieve pass's stage phases (s_memtime), and the number of stages summed
+constexpr int STAMP_WG = 512, STAMP_N = 6;
+__device__ unsigned long long g_f6_stamps[STAMP_WG * 8 * STAMP_N];
+#endif
+
 // ---- passes over several segments of stages (the two-slice tier f6x2) -----------------------
 // NSEG = 1: stages [0, nst) of the gallery tiles G against the query tiles Q (tier f6).
 // NSEG = 3: stages [0, 3 nst) = the segments [x1 | x1 | x2] . [y1 | y2 | y1] of the two-slice rows
@@ -464,6 +471,80 @@ struct Engine16 {
                  : "+a"(c) : "v"(a), "v"(b), "v"(sc));
   }
 
+  // Asymmetric main loop (tile_kernel_f6s MODE bit 16777216).  Stamped timelines of the library
+  // loop (profiles/r03_f6_probe_stamps.log) show the wave of a SIMD that issues the stage copies
+  // blocked ~650-840 cycles per stage in their issue (the per-CU copy path back-pressures), while the
+  // other wave runs out of MFMAs and waits ~530 cycles at the next barrier.  Here the two waves of
+  // SIMD p (p and p + 4) share the 256-gallery-row x 64-query strip p unevenly: the copy-issuing wave
+  // p takes gallery row blocks 0 .. NIA-1, wave p + 4 the other 16 - NIA, so the matrix pipe has the
+  // second wave's MFMAs to run while the first issues copies.  The larger share does not fit the
+  // register file with a full fragment set, so both waves read their gallery fragments just in time
+  // through a ring of RING fragments (the query fragments, 4, for the whole stage); a stage's buffer
+  // is therefore read during that stage, and the copy of stage kt + 2 goes into the buffer of stage
+  // kt - 1 after the top barrier of stage kt (every wave drained its reads of kt - 1 before it):
+  // two stages of copy lead, 3 buffers.
+  //   top of stage kt: (issuing waves) own copies of kt landed -> s_barrier -> issuing waves: copy
+  //   kt + 2 -> query fragments of kt, ring prefill -> rows: per row the next ring read + 4 MFMAs ->
+  //   lgkmcnt(0).
+  template <int NI, bool ISSUE, int NSEG = 1>
+  static __device__ __forceinline__ void mainloop_as(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
+                                                     int nst, int row0, f32x4 (&acc)[NI][NB],
+                                                     const char* G2 = nullptr, const char* Q2 = nullptr) {
+    constexpr int RING = 4;
+    static_assert(NI >= RING, "ring");
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int p = wave & 3, r16 = lane & 15;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int last = NSEG * nst - 1;
+    auto issue = [&](int kt) {   // waves 0-3 (the ISSUE role): 12 pieces each
+      if constexpr (ISSUE) {
+        const char *g, *q;
+        int ks;
+        const int s = kt < last ? kt : last;
+        seg_src<NSEG>(s, nst, G, G2, Q, Q2, g, q, ks);
+        Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+      }
+    };
+    static_assert(NST == 3, "three stage buffers");
+    issue(0);
+    issue(1);
+    i32x6 a[RING], b[NB];
+    int sa = SCALE_ONE, sb = SCALE_ONE;
+    for (int kt = 0; kt <= last; ++kt) {
+      seg_scales<NSEG>(kt, nst, sa, sb);
+      if constexpr (ISSUE) wait_vm<2 * IPW>();   // own copies of stage kt landed (kt + 1 may fly)
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      const char* st = smem + (kt % NST) * STAGE;
+#pragma unroll
+      for (int c = 0; c < NB; ++c) b[c] = frag16(st + PANEL, p * QW + c * 16 + r16);
+#pragma unroll
+      for (int j = 0; j < RING - 1; ++j) a[j] = frag16(st, row0 + j * 16 + r16);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(kt + 2);                  // into the buffer of stage kt - 1 (its reads drained below)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        if (i + RING - 1 < NI) a[(i + RING - 1) % RING] = frag16(st, row0 + (i + RING - 1) * 16 + r16);
+#pragma unroll
+        for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i % RING], b[c], acc[i][c], sa, sb);
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i + RING - 1 < NI) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every read of stage kt done before the next barrier
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wait_vm<0>();
+    barrier();
+  }
+
   // Ping-pong main loop (probe MODE 524288).  The two waves of a SIMD (groups g = wr: waves 0-3 and
   // 4-7; the cyclic wave -> SIMD order puts one of each on every SIMD) run one s_barrier apart, so one
   // issues its 32 MFMAs (raised priority) while the other reads its 12 fragments of the next stage
@@ -633,13 +714,41 @@ struct Engine16 {
         seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
         Engine<8>::dma_buf4<4 * C, 4 * C + 4>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
       };
+#ifdef OFR_F6_STAMPS
+      constexpr bool ST = (MODE & 8388608) != 0;
+      unsigned long long st_sum[5] = {0, 0, 0, 0, 0}, st_t[6] = {0, 0, 0, 0, 0, 0};
+      unsigned long long st_n = 0;
+      auto stamp = [&](int j) {
+        if constexpr (ST) {
+          __builtin_amdgcn_sched_barrier(0);
+          st_t[j] = __builtin_amdgcn_s_memtime();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+#else
+      auto stamp = [&](int) {};
+#endif
       for (int kt = 0; kt < last; ++kt) {
         seg_scales<NSEG>(kt, nst, sa, sb);
         __builtin_amdgcn_sched_barrier(0);
+        stamp(0);
         if constexpr ((MODE & 262144) != 0) wait_vm<2 * IPW>();
         else wait_vm<IPW>();   // stage kt+1 landed (kt+2 may be in flight)
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        stamp(1);
+#ifdef OFR_F6_STAMPS
+        if constexpr (ST) {   // the previous stage's phases (its t5 = this t0)
+          if (kt > 8 && kt < last - 8) {
+            st_sum[0] += st_t[2] - st_t[1];   // rows before the re-fill barrier (previous stage)
+            st_sum[1] += st_t[3] - st_t[2];   // re-fill wait + barrier
+            st_sum[2] += st_t[4] - st_t[3];   // copy issue
+            st_sum[3] += st_t[0] - st_t[4];   // the remaining rows
+            st_sum[4] += st_t[1] - st_t[0];   // this stage's top wait (copies landed) + barrier
+            ++st_n;
+          }
+        }
+#endif
         const char* nxt = smem + ((kt + 1) % NST) * STAGE;
         if constexpr ((MODE & 2048) != 0) {
           // column-major halves: rows 0-3 against b[0], b[1], b[2], b[3] in turn; a[0..3] refilled
@@ -676,16 +785,19 @@ struct Engine16 {
         // 2 RS reads issued above may still be in flight and every read of the previous stage (all
         // from the buffer re-filled below) is done.  Scalar loads sharing the counter can only make the
         // wait stricter.  (More instructions per refill would also be safe; fewer would not.)
+        stamp(2);
         if constexpr (RS == 1) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
         else if constexpr (RS == 2) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
         else if constexpr (RS == 6) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
         else asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        stamp(3);
         {
           const int nx = kt + NST;
           issue_b(nx < last ? nx : last);
         }
+        stamp(4);
         if constexpr ((MODE & 2048) != 0) {
           // rows 4-7 column-major: b[c] refilled after its last MFMA (row 7), a[4..7] after column 3
 #pragma unroll
@@ -742,6 +854,16 @@ struct Engine16 {
         for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
       wait_vm<0>();
       barrier();
+#ifdef OFR_F6_STAMPS
+      if constexpr (ST) {
+        if (blockIdx.x < STAMP_WG && lane == 0) {
+          unsigned long long* o = g_f6_stamps + ((size_t)blockIdx.x * 8 + wave) * STAMP_N;
+#pragma unroll
+          for (int j = 0; j < 5; ++j) o[j] = st_sum[j];
+          o[5] = st_n;
+        }
+      }
+#endif
       return;
     }
     // Per stage kt: MFMAs of stage kt, each fragment replaced by stage kt+1's as soon as its last

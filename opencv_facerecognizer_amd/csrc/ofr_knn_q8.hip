@@ -388,6 +388,51 @@ __device__ __forceinline__ void sieve_epilogue16(char* smem, const TileArgs& p, 
   sieve_flush<f6t::TQ>(smem, p, g0, q0);
 }
 
+// The same epilogue for the asymmetric loop (f6t::Engine16::mainloop_as): NI gallery row blocks
+// from row0, the wave's 64 queries at (wave & 3) * 64.  Both roles of the kernel run it (one
+// __syncthreads before the compares, one in sieve_flush: equal counts).
+template <int NI>
+__device__ __forceinline__ void sieve_epilogue_as(char* smem, const TileArgs& p, int64_t g0, int64_t q0, float ga,
+                                                  float gs, const float (&sq2)[4], const float (&th)[4],
+                                                  const f6t::f32x4 (&acc)[NI][4], int row0) {
+  using E = f6t::Engine16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wc = wave & 3, g4 = (lane >> 4) * 4, r16 = lane & 15;
+  float* gtab = reinterpret_cast<float*>(smem);                                  // [TG][2]
+  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + TG * 8);
+  uint2* hits = reinterpret_cast<uint2*>(smem + TG * 8 + 16);                    // [SIEVE_HCAP]
+  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
+  if (threadIdx.x < TG) {
+    gtab[2 * threadIdx.x + 0] = ga;
+    gtab[2 * threadIdx.x + 1] = gs;
+  }
+  if (threadIdx.x == 0) *nhit = 0;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int gl0 = row0 + i * 16 + g4;            // this lane's 4 consecutive gallery rows
+    const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
+    const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
+    const float av[4] = {t0.x, t0.z, t1.x, t1.z}, sv[4] = {t0.y, t0.w, t1.y, t1.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gl = gl0 + r;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float sc = av[r] - sq2[c] * sv[r] * acc[i][c][r];
+        if (!(sc > th[c]) && gl < nvalid) {
+          const int ql = wc * E::QW + c * 16 + r16;
+          const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
+          const uint32_t slot = atomicAdd(nhit, 1u);
+          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)gl);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  sieve_flush<f6t::TQ>(smem, p, g0, q0);
+}
+
 // fp6 sieve pass on the 16x16x128 engine.  MODE probe bits: 1 = no k-loop DMA, 4 = no epilogue; the
 // main loop's own bits (f6t::Engine16::mainloop) pass through the mask below.
 template <int MODE, int NSEG = 1>
@@ -399,12 +444,48 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
+  if constexpr ((MODE & 16777216) != 0) {   // asymmetric loop (f6t::Engine16::mainloop_as)
+    constexpr int NIA = 6;                   // gallery row blocks of the copy-issuing waves 0-3
+    auto operands = [&](float& ga, float& gs, float (&sq2)[4], float (&th)[4]) {
+      ga = __builtin_inff();
+      gs = 0.f;
+      if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
+        ga = p.aux[g0 + threadIdx.x];
+        gs = p.gscale[g0 + threadIdx.x];
+      }
+      const int wc = (threadIdx.x >> 6) & 3, r16 = threadIdx.x & 15;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t q = q0 + wc * E::QW + c * 16 + r16;
+        const bool ok = q < p.B;
+        sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
+        th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
+      }
+    };
+    float ga, gs, sq2[4], th[4];
+    if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) < 4) {
+      f6t::f32x4 acc[NIA][4];
+      E::mainloop_as<NIA, true, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q),
+                                      qt, p.nk / NSEG, 0, acc, reinterpret_cast<const char*>(p.G2),
+                                      reinterpret_cast<const char*>(p.Q2));
+      operands(ga, gs, sq2, th);
+      sieve_epilogue_as<NIA>(smem, p, g0, q0, ga, gs, sq2, th, acc, 0);
+    } else {
+      f6t::f32x4 acc[16 - NIA][4];
+      E::mainloop_as<16 - NIA, false, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp,
+                                            reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG, NIA * 16, acc,
+                                            reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
+      operands(ga, gs, sq2, th);
+      sieve_epilogue_as<16 - NIA>(smem, p, g0, q0, ga, gs, sq2, th, acc, NIA * 16);
+    }
+    return;
+  }
   f6t::f32x4 acc[8][4];
   if constexpr ((MODE & 524288) != 0)   // ping-pong main loop (f6t::Engine16::mainloop_pp)
     E::mainloop_pp<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
                          p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
   else
-    E::mainloop<MODE & 3636673, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+    E::mainloop<MODE & 12025281, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
                                   p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
                                   reinterpret_cast<const char*>(p.Q2));
   // sieve operands after the main loop (the 16x16 engine needs every register in it)

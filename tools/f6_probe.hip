@@ -3,6 +3,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/f6_probe.hip \
 //         opencv_facerecognizer_amd/csrc/ofr_api.hip -o tools/f6_probe
 //   ./tools/f6_probe [N] [B] [d] [reps]
+#define OFR_F6_STAMPS 1
 #include "../opencv_facerecognizer_amd/csrc/ofr_knn_q8.hip"
 #include <cstdio>
 #include <cstdlib>
@@ -352,6 +353,36 @@ int main(int argc, char** argv) {
       a.gg = g < ntg ? g : ntg;
       if (run16<13312 + 4 + 16384 + 65536>(a, reps, "dma-only-gg") || run16<13312 + 4 + 262144>(a, reps, "noepi-4w-gg"))
         return 1;
+    }
+    return 0;
+  }
+  if (getenv("ASYM")) {   // the asymmetric loop against the library pass
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (run16<275456>(a, reps, "lib4w") || run16<16777216>(a, reps, "asym") || run16<16777216 + 4>(a, reps, "asym-noepi"))
+        return 1;
+    return 0;
+  }
+  if (getenv("STAMPS")) {   // phases of a stage of the library pass (s_memtime, waves 0-3 vs 4-7)
+    a.gg = 4 < ntg ? 4 : ntg;
+    if (run16<275456>(a, reps, "lib4w") || run16<275456 + 8388608>(a, reps, "lib4w-stamped")) return 1;
+    std::vector<unsigned long long> h(f6t::STAMP_WG * 8 * f6t::STAMP_N);
+    CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(f6t::g_f6_stamps), h.size() * 8));
+    const char* names[5] = {"rows before re-fill barrier", "re-fill wait+barrier", "copy issue", "remaining rows",
+                            "top wait (copies landed)+barrier"};
+    for (int role = 0; role < 2; ++role) {
+      double sum[5] = {0, 0, 0, 0, 0}, n = 0;
+      for (int b = 0; b < f6t::STAMP_WG; ++b)
+        for (int w = role * 4; w < role * 4 + 4; ++w) {
+          const unsigned long long* o = h.data() + ((size_t)b * 8 + w) * f6t::STAMP_N;
+          for (int j = 0; j < 5; ++j) sum[j] += (double)o[j];
+          n += (double)o[5];
+        }
+      printf("waves %d-%d (%s), cycles per stage:", role * 4, role * 4 + 3, role ? "no copies" : "issue the copies");
+      double tot = 0;
+      for (int j = 0; j < 5; ++j) tot += sum[j] / n;
+      for (int j = 0; j < 5; ++j) printf("  %s %.0f", names[j], sum[j] / n);
+      printf("  | total %.0f\n", tot);
     }
     return 0;
   }
