@@ -5,9 +5,13 @@ gallery is 40 GB of the 288 GB HBM): synthetic 100x100 uint8 faces (D=10000),
 a Fisherfaces projection to d=9999 (= c-1 for 10k identities, thetrainer.py
 get_model defaults), a 1M-row gallery (100k identities x 10 images), batches of
 B=4096 query faces, k=1, Euclidean distance.  One step = project the batch
-(ofr_project_u8_exact: int8-slice MFMA, exact) + fp32-MFMA search pass
-(ofr_knn_tiles_f32) + merge / exact fp64 re-rank (ofr_knn_merge_f32)
-[+ all-gather + ofr_topk_merge when sharded].
+(ofr_project_u8_exact: int8-slice MFMA, exact) + quantize it to fp6 + the fp6
+sample and sieve passes (ofr_knn_f6 phase 1) + merge / exact fp64 re-rank /
+certificate (phase 2) + the fallback tiers of the uncertified queries
+[+ the RCCL exchanges of DESIGN.md §6 when sharded].  --search fp32 runs the
+fp32-MFMA pass (ofr_knn_tiles_f32) instead.  The steps are pipelined over three
+query buffers (StepPipeline): the tile pass owns the main stream, the next
+batch's preparation and this batch's merge follow it on a side stream.
 Inputs are resident in HBM before the timed region.  W is random (no trained
 checkpoint exists at this scale), gallery/queries are synthetic (see
 opencv_facerecognizer_amd/synthetic.py).
@@ -35,7 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from opencv_facerecognizer_amd import _lib  # noqa: E402
-from opencv_facerecognizer_amd._device import FloatGallery, round_up  # noqa: E402
+from opencv_facerecognizer_amd._device import FloatGallery, Workspace, round_up  # noqa: E402
 from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, gather_rows_async,  # noqa: E402
                                                 merge_sharded, merge_topk, shard_range)
 from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_gallery, build_projection  # noqa: E402
@@ -141,6 +145,89 @@ def committed_traffic(cfg):
     return best
 
 
+class StepPipeline:
+    """The timed step's schedule over a sequence of query batches:
+
+      main stream  tile pass of batch s (behind its preparation);
+      side stream  behind tile pass s: batch s+1's preparation (projection, quantization, its
+                   all-gathers), then batch s's merge (exact re-rank + certificate) -- the projection
+                   runs alone and the merge runs under tile pass s+1;
+      host         batch s-1's certificate read (one sync, on the side stream up to merge s-1,
+                   which finished under tile pass s) and its fallback tiers, enqueued on the side
+                   stream before batch s+1's preparation.
+
+    Three query buffers (preparation s+1 / merge s / fallback s-1), two search workspaces (tile
+    pass s writes one while merge s-1 reads the other).  Callbacks, each enqueueing on the current
+    stream: prep(j) fills buffer j; tiles(j, w) and merge(j, w) run phase 1 / phase 2 of buffer j
+    on workspace w; finish(j) reads the certificate (host sync) and runs the fallback, returning
+    the batch's result.  overlap=False: one stream, the same order."""
+
+    NBUF, NWS = 3, 2
+
+    def __init__(self, device, prep, tiles, merge, finish, overlap=True):
+        self.prep_fn, self.tiles_fn, self.merge_fn, self.finish_fn = prep, tiles, merge, finish
+        self.main = torch.cuda.current_stream(device)
+        self.side = torch.cuda.Stream(device=device) if overlap else self.main
+        self.ws = [Workspace() for _ in range(self.NWS)]
+        self.ev_ready = [torch.cuda.Event() for _ in range(self.NBUF)]    # buffer prepared (side)
+        self.ev_merged = [torch.cuda.Event() for _ in range(self.NWS)]    # workspace's merge done (side)
+        self.ev_tiles = torch.cuda.Event()                                # latest tile pass done (main)
+        # the side stream starts behind everything the main stream has queued (gallery and tier builds,
+        # the query images, buffer fills): an unrecorded event is no dependency, and once the caching
+        # allocator stops calling hipMalloc (which synchronises) nothing else would order the first
+        # preparations (without this, a second run in one process projected stale queries)
+        if self.side is not self.main:
+            self.side.wait_stream(self.main)
+
+    def _prep(self, s, ev):
+        with torch.cuda.stream(self.side):
+            if ev:
+                ev[0].record()
+            self.prep_fn(s % self.NBUF)
+            if ev:
+                ev[1].record()
+            self.ev_ready[s % self.NBUF].record(self.side)
+
+    def _finish(self, s):
+        with torch.cuda.stream(self.side):
+            return self.finish_fn(s % self.NBUF)
+
+    def run(self, steps, events=None):
+        """Exactly `steps` preparations, tile passes, merges and fallbacks; returns the last batch's
+        result.  events[s]: 6 timing events (prep start/end on the side stream, tile pass end and start
+        on the main stream, merge end and start on the side stream)."""
+        ev = events or [None] * steps
+        res = None
+        self._prep(0, ev[0])
+        for s in range(steps):
+            j, w = s % self.NBUF, s % self.NWS
+            self.main.wait_event(self.ev_ready[j])
+            self.main.wait_event(self.ev_merged[w])         # merge s-2 done with this workspace
+            if ev[s]:
+                ev[s][4].record(self.main)
+            self.tiles_fn(j, self.ws[w])
+            if ev[s]:
+                ev[s][2].record(self.main)
+            self.ev_tiles.record(self.main)
+            if s >= 1:
+                res = self._finish(s - 1)
+            self.side.wait_event(self.ev_tiles)
+            if s + 1 < steps:
+                self._prep(s + 1, ev[s + 1])
+            with torch.cuda.stream(self.side):
+                if ev[s]:
+                    ev[s][5].record()
+                self.merge_fn(j, self.ws[w])
+                if ev[s]:
+                    ev[s][3].record()
+                self.ev_merged[w].record(self.side)
+        if steps:
+            res = self._finish(steps - 1)
+        # the caller's stream sees everything the side stream did
+        self.main.wait_stream(self.side)
+        return res
+
+
 def certificate_margin(gallery, Qd, qq, nsample=64):
     """(d_16^2 - d_1^2) / dS of the fp6 tier for a sample of queries: the certificate needs about 2
     (the 16th coarse candidate must clear the k-th exact distance by the bound on both sides).
@@ -174,53 +261,38 @@ def stress_run(P, bank, args, noise, device, N=None):
     gq.manual_seed(SEED + 7)
     ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
     Xq = bank.images(ids_q, seed=SEED + 99, noise=noise)
-    out = (torch.empty((B, k), dtype=torch.float64, device=device), torch.empty((B, k), dtype=torch.int64, device=device))
-    tiers, counts = [], None
-    # the headline's pipelined step (main()): batch s+1 prepared on a side stream behind batch s's
-    # tile pass, two query buffers, exactly K preparations and K searches in the timed region
-    bufs = [dict(Qd=torch.zeros((B, ld), dtype=torch.float32, device=device), qq=None) for _ in range(2)]
-    main_stream = torch.cuda.current_stream(device)
-    side = torch.cuda.Stream(device=device)
-    ev_ready, ev_free, ev_tiles = [torch.cuda.Event() for _ in range(2)], [torch.cuda.Event() for _ in range(2)], \
-        torch.cuda.Event()
-    # the side stream starts behind everything the main stream has queued (gallery and tier builds, the
-    # query images, the buffers' zero fills): an unrecorded event is no dependency, and once the caching
-    # allocator stops calling hipMalloc (which synchronises) nothing else would order the first preps
-    # (without this, a second stress_run in one process projected stale / half-generated queries)
-    side.wait_stream(main_stream)
+    tiers = []
+    # the headline's step pipeline (main()), exactly K preparations and K searches in the timed region
+    bufs = [dict(Qd=torch.zeros((B, ld), dtype=torch.float32, device=device), qq=None,
+                 out=(torch.empty((B, k), dtype=torch.float64, device=device),
+                      torch.empty((B, k), dtype=torch.int64, device=device)))
+            for _ in range(StepPipeline.NBUF)]
+    timed = []
 
     def prep(j):
-        b = bufs[j]
-        side.wait_event(ev_free[j])
-        side.wait_event(ev_tiles)
-        with torch.cuda.stream(side):
-            P.project(Xq, shift64=gallery.shift64, out=b["Qd"])
-            b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier="f6")
-            ev_ready[j].record(side)
+        P.project(Xq, shift64=gallery.shift64, out=bufs[j]["Qd"])
+        bufs[j]["qq"] = gallery.quantize_queries(bufs[j]["Qd"], bufs[j]["qq"], tier="f6")
 
-    def search(j, timings=None, then=None):
+    def finish(j):
         b = bufs[j]
-        main_stream.wait_event(ev_ready[j])
-        gallery.search_q8_phase(1, b["Qd"], b["qq"], k)
-        ev_tiles.record(main_stream)
-        if then is not None:
-            then()
-        gallery.search_q8_phase(2, b["Qd"], b["qq"], k, out=out)
-        gallery.fallback(b["Qd"], b["qq"], k, out, timings=timings)
-        ev_free[j].record(main_stream)
+        gallery.fallback(b["Qd"], b["qq"], k, b["out"], timings=tiers if timed else None)
+        return b["out"]
 
-    for j in range(2):
-        prep(j)
-        search(j)
+    pipe = StepPipeline(device, prep,
+                        lambda j, w: gallery.search_q8_phase(1, bufs[j]["Qd"], bufs[j]["qq"], k, workspace=w),
+                        lambda j, w: gallery.search_q8_phase(2, bufs[j]["Qd"], bufs[j]["qq"], k, out=bufs[j]["out"],
+                                                             workspace=w),
+                        finish)
+    pipe.run(StepPipeline.NBUF)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     K = args.stress_steps
-    prep(0)
-    for s in range(K):
-        search(s % 2, tiers, then=(lambda s=s: prep((s + 1) % 2)) if s + 1 < K else None)
+    timed.append(True)
+    out = pipe.run(K)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / K
-    Qd, qq = bufs[(K - 1) % 2]["Qd"], bufs[(K - 1) % 2]["qq"]
+    last = (K - 1) % StepPipeline.NBUF
+    Qd, qq = bufs[last]["Qd"], bufs[last]["qq"]
     counts = list(gallery.last_fallbacks)
     per_tier = {}
     for t, n, m in tiers:
@@ -273,7 +345,7 @@ def main():
     torch.cuda.synchronize()
     log(rank, f"setup {time.perf_counter() - t0:.1f}s: gallery rows {nl}/{N} per rank, d={d}, D={D}, B={B}")
 
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
     use_q8 = args.search in ("f6", "q8")
     tier0 = "f6" if args.search == "f6" else 1
     if use_q8:
@@ -285,103 +357,72 @@ def main():
     # all-gathered (fp6 panels need whole 256-row blocks per rank)
     b0, b1 = shard_range(B, rank, world)
     shard_prep = world > 1 and B % world == 0 and (tier0 != "f6" or (B // world) % 256 == 0)
-    # two query buffers: batch s+1 is prepared (projection, quantization, its all-gathers) on a side
-    # stream once batch s's tile pass is done, so it overlaps batch s's merge / certificate / host sync
-    # instead of following them (the tile pass itself keeps the whole chip)
+    # the step pipeline (StepPipeline): three query buffers, each with its own result lists
     bufs = [dict(Qd=Qd if j == 0 else torch.zeros_like(Qd), qq=None, pending=None, qq_loc=None,
+                 out=out if j == 0 else tuple(torch.empty_like(t) for t in out),
                  Qd_loc=torch.zeros((b1 - b0, ld), dtype=torch.float32, device=device) if shard_prep else None)
-            for j in range(2)]
-    main_stream = torch.cuda.current_stream(device)
-    # OFR_BENCH_OVERLAP=0: the preparation on the main stream (behind the tile pass, before the merge)
-    side = torch.cuda.Stream(device=device) if os.environ.get("OFR_BENCH_OVERLAP", "1") == "1" else main_stream
-    ev_ready = [torch.cuda.Event() for _ in range(2)]   # buffer j prepared (side stream)
-    ev_free = [torch.cuda.Event() for _ in range(2)]    # buffer j's last reader done (main stream)
-    ev_tiles = torch.cuda.Event()                        # the latest tile pass done (main stream)
-    if side is not main_stream:
-        side.wait_stream(main_stream)                    # first preps behind the setup work (see stress_run)
+            for j in range(StepPipeline.NBUF)]
 
-    def prep(j, events=None):
+    def prep(j):
         """Query batch -> centred fp32 search rows (+ the first tier's quantized rows) in buffer j."""
         b = bufs[j]
-        side.wait_event(ev_free[j])
-        side.wait_event(ev_tiles)
-        with torch.cuda.stream(side):
-            if events:
-                events[0].record()
-            if shard_prep:
-                P.project(Xq[b0:b1], shift64=gallery.shift64, out=b["Qd_loc"])   # this rank's faces
-                if use_q8:
-                    b["qq_loc"] = gallery.quantize_queries(b["Qd_loc"], b["qq_loc"], tier=tier0)
-                    b["qq"] = gallery.gather_queries(b["qq_loc"])
-                    # the fp32 rows are read from phase 2 on: their all-gather overlaps the tile pass
-                    b["pending"] = gather_rows_async(b["Qd_loc"])
-                    b["Qd"] = b["pending"].out
-                else:
-                    b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
+        if shard_prep:
+            P.project(Xq[b0:b1], shift64=gallery.shift64, out=b["Qd_loc"])   # this rank's faces
+            if use_q8:
+                b["qq_loc"] = gallery.quantize_queries(b["Qd_loc"], b["qq_loc"], tier=tier0)
+                b["qq"] = gallery.gather_queries(b["qq_loc"])
+                # the fp32 rows are read from phase 2 on: their all-gather overlaps the tile pass
+                b["pending"] = gather_rows_async(b["Qd_loc"])
+                b["Qd"] = b["pending"].out
             else:
-                P.project(Xq, shift64=gallery.shift64, out=b["Qd"])          # fp32(W^T x - c), exact int8 MFMA
-                if use_q8:
-                    b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier0)
-            if events:
-                events[1].record()
-            ev_ready[j].record(side)
-
-    def search(j, events=None, then=None):
-        """Tile pass, merge, certificate (+ fallback tiers) of the batch in buffer j.  then(): the next
-        batch's prep, enqueued right after this tile pass (it runs on the side stream)."""
-        b = bufs[j]
-        main_stream.wait_event(ev_ready[j])
-        if events:
-            events[4].record()
-        Qd_, qq_ = b["Qd"], b["qq"]
-        if use_q8:
-            gallery.search_q8_phase(1, Qd_, qq_, k)
+                b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
         else:
-            gallery.search_phase("tiles", Qd_, k)
-        if events:
-            events[2].record()
-        ev_tiles.record(main_stream)
-        if then is not None:
-            then()
+            P.project(Xq, shift64=gallery.shift64, out=b["Qd"])          # fp32(W^T x - c), exact int8 MFMA
+            if use_q8:
+                b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier0)
+
+    def tiles(j, w):
+        b = bufs[j]
+        if use_q8:
+            gallery.search_q8_phase(1, b["Qd"], b["qq"], k, workspace=w)
+        else:
+            gallery.search_phase("tiles", b["Qd"], k, workspace=w)
+
+    def merge(j, w):
+        b = bufs[j]
         if b["pending"] is not None:
-            Qd_ = b["pending"]()
+            b["Qd"] = b["pending"]()
             b["pending"] = None
         if use_q8:
-            merge_sharded(gallery, Qd_, qq_, k, n0, out)   # world 1: the plain phase 2
+            merge_sharded(gallery, b["Qd"], b["qq"], k, n0, b["out"], workspace=w)   # world 1: the plain phase 2
         else:
-            gallery.search_phase("merge", Qd_, k, index_base=n0, out=out)
-        if events:
-            events[3].record()
-        res = out
+            gallery.search_phase("merge", b["Qd"], k, index_base=n0, out=b["out"], workspace=w)
+
+    def finish(j):
+        b = bufs[j]
         if use_q8:
             if world > 1:      # global certificate: all-gather + merge + collective fallback
-                res, counts = certify_sharded(gallery, Qd_, qq_, k, out, n0)
+                res, counts = certify_sharded(gallery, b["Qd"], b["qq"], k, b["out"], n0)
                 fallbacks.append(counts[0])
                 last_counts[:] = counts
-            else:
-                fallbacks.append(gallery.fallback(Qd_, qq_, k, out, index_base=n0))
-                last_counts[:] = list(gallery.last_fallbacks)
-        elif world > 1:
-            gd, gi = exchange_topk(out[0], out[1])
-            res = merge_topk(gd, gi, world, k, k)
-        ev_free[j].record(main_stream)
-        return res
+                return res
+            fallbacks.append(gallery.fallback(b["Qd"], b["qq"], k, b["out"], index_base=n0))
+            last_counts[:] = list(gallery.last_fallbacks)
+            return b["out"]
+        if world > 1:
+            gd, gi = exchange_topk(*b["out"])
+            return merge_topk(gd, gi, world, k, k)
+        return b["out"]
 
-    for w in range(max(args.warmup, 2)):     # both buffers warmed (their quantized rows allocated)
-        prep(w % 2)
-        if w < args.warmup:
-            search(w % 2)
+    # OFR_BENCH_OVERLAP=0: everything on the main stream, in the same order
+    pipe = StepPipeline(device, prep, tiles, merge, finish, overlap=os.environ.get("OFR_BENCH_OVERLAP", "1") == "1")
+    pipe.run(max(args.warmup, StepPipeline.NBUF))     # untimed; every buffer and workspace allocated
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    # exactly K preps and K searches inside the timed region: batch 0's prep first, batch s+1's
-    # enqueued behind batch s's tile pass, none after the last
-    prep(0, ev[0])
-    for s in range(args.steps):
-        nxt = (lambda s=s: prep((s + 1) % 2, ev[s + 1])) if s + 1 < args.steps else None
-        res = search(s % 2, ev[s], then=nxt)
+    res = pipe.run(args.steps, ev)                     # exactly K preparations and K searches
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -391,14 +432,16 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    Qd, qq = bufs[(args.steps - 1) % 2]["Qd"], bufs[(args.steps - 1) % 2]["qq"]
+    last = (args.steps - 1) % StepPipeline.NBUF
+    Qd, qq = bufs[last]["Qd"], bufs[last]["qq"]
 
     ms_proj = np.mean([e[0].elapsed_time(e[1]) for e in ev])
     ms_tiles = np.mean([e[4].elapsed_time(e[2]) for e in ev])     # the tile pass on the main stream
-    ms_merge = np.mean([e[2].elapsed_time(e[3]) for e in ev])
+    ms_merge = np.mean([e[5].elapsed_time(e[3]) for e in ev])     # merge + certificate on the side stream
     idx = res[1][:, 0]
     acc = float(((idx // args.per_id) == ids_q).double().mean().item())
-    kept = gallery.sieve_counts(B) if args.search == "f6" else None   # last step's fp6 sieve (this rank)
+    kept = (gallery.sieve_counts(B, pipe.ws[(args.steps - 1) % StepPipeline.NWS]) if args.search == "f6"
+            else None)                                                  # last step's fp6 sieve (this rank)
     kept = None if kept is None else {"mean": float(kept.double().mean()), "max": int(kept.max()),
                                       "cap": 32768, "expected": "~16 x OFR_SIEVE_STRIDE (64)"}
 

@@ -447,14 +447,14 @@ class FloatGallery:
                  ptr(qq["cert"]), ptr(qq["bound"]), ptr(ws), ws.numel())
         return out
 
-    def merge_pruned(self, stage, Qd, qq, k, ub, index_base=0, out=None):
-        """The split fp6 merge of a sharded gallery (ofr_knn_f6_merge_pruned, after phase 1 on this
-        gallery's workspace): stage 1 writes ub [B][k] (this shard's upper bounds), stage 2 re-ranks
-        pruned by ub [B] (the global bound) into out / qq["cert"] / qq["bound"]."""
+    def merge_pruned(self, stage, Qd, qq, k, ub, index_base=0, out=None, workspace=None):
+        """The split fp6 merge of a sharded gallery (ofr_knn_f6_merge_pruned, after phase 1 on the same
+        workspace -- the gallery's, or the caller's): stage 1 writes ub [B][k] (this shard's upper
+        bounds), stage 2 re-ranks pruned by ub [B] (the global bound) into out / qq["cert"] / qq["bound"]."""
         g = self._tier_gallery("f6")
         B = Qd.shape[0]
         lib = _lib.load()
-        ws = self.ws.get(lib.ofr_knn_f6_workspace_bytes(B, self.N), Qd.device)
+        ws = (workspace or self.ws).get(lib.ofr_knn_f6_workspace_bytes(B, self.N), Qd.device)
         o = out if out is not None else (None, None)
         call("ofr_knn_f6_merge_pruned", stream(), stage, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
              ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]), ptr(self.aux),
@@ -462,13 +462,15 @@ class FloatGallery:
              ws.numel())
         return out
 
-    def sieve_counts(self, B):
-        """Rows kept per query by the last fp6 sieve pass of a B-query batch (int32 device view of
-        the workspace, valid until the next search), or None when B <= 32 (no sieve)."""
+    def sieve_counts(self, B, workspace=None):
+        """Rows kept per query by the last fp6 sieve pass of a B-query batch on `workspace` (the
+        gallery's by default; int32 device view, valid until the next search on it), or None when
+        B <= 32 (no sieve)."""
         off = _lib.load().ofr_knn_f6_sieve_counts_offset(B, self.N)
-        if off == ctypes.c_size_t(-1).value or self.ws.buf is None:
+        w = workspace or self.ws
+        if off == ctypes.c_size_t(-1).value or w.buf is None:
             return None
-        return self.ws.buf[off:off + 4 * B].view(torch.int32)
+        return w.buf[off:off + 4 * B].view(torch.int32)
 
     def fallback(self, Qd, qq, k, out, index_base=0, timings=None):
         """Re-run the queries the first tier left uncertified down the tier chain (then fp32).
@@ -560,14 +562,15 @@ class FloatGallery:
         Q = Q64 if isinstance(Q64, torch.Tensor) else f64_dev(np.asarray(Q64, np.float64), device=self.G.device)
         return center_round(Q.to(torch.float64).contiguous(), self.shift64, self.ld)
 
-    def search_phase(self, phase, Qd, k, index_base=0, out=None):
-        """One pass of the search: phase "tiles" (MFMA pass) or "merge" (merge + exact re-rank)."""
+    def search_phase(self, phase, Qd, k, index_base=0, out=None, workspace=None):
+        """One pass of the search: phase "tiles" (MFMA pass) or "merge" (merge + exact re-rank), both
+        on the same workspace (the gallery's, or the caller's)."""
         B = Qd.shape[0]
         if out is None:
             out = (torch.empty((B, k), dtype=torch.float64, device=Qd.device),
                    torch.empty((B, k), dtype=torch.int64, device=Qd.device))
         lib = _lib.load()
-        ws = self.ws.get(lib.ofr_knn_workspace_bytes(B, self.N, k), Qd.device)
+        ws = (workspace or self.ws).get(lib.ofr_knn_workspace_bytes(B, self.N, k), Qd.device)
         name = "ofr_knn_tiles_f32" if phase == "tiles" else "ofr_knn_merge_f32"
         call(name, stream(), self.metric, ptr(Qd), B, Qd.shape[1], ptr(self.G), self.N, self.ld, self.d,
              ptr(self.aux), k, index_base, ptr(out[0]), ptr(out[1]), ptr(ws), ws.numel())

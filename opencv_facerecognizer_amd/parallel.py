@@ -143,7 +143,7 @@ def exchange_lists(d, i, bound=None, group=None):
     return gd, gi, minb
 
 
-def merge_sharded(gallery, Qd, qq, k, index_base, out, group=None):
+def merge_sharded(gallery, Qd, qq, k, index_base, out, group=None, workspace=None):
     """Phase 2 of the certified search on a sharded gallery, after phase 1 (the tile pass) on every
     rank.  fp6 tier: the split merge -- every rank selects its candidates and bounds the squared
     distance of its best k from above (ofr_knn_f6_merge_pruned stage 1), ONE all-gather of those
@@ -151,15 +151,16 @@ def merge_sharded(gallery, Qd, qq, k, index_base, out, group=None):
     squared distance, and each rank re-ranks only the candidates that can still fall below it
     (stage 2): a rank that holds none of a query's neighbours skips its exact re-rank (the rows it
     skips are farther than k rows of another rank, so the global top-k and the certificate of
-    certify_sharded are unchanged).  Other tiers: the local merge.  Returns out."""
+    certify_sharded are unchanged).  Other tiers: the local merge.  workspace: the one phase 1 ran
+    on (the gallery's by default).  Returns out."""
     _, ws = world(group)
     if ws == 1 or qq["tier"] != "f6":
-        return gallery.search_q8_phase(2, Qd, qq, k, index_base=index_base, out=out)
+        return gallery.search_q8_phase(2, Qd, qq, k, index_base=index_base, out=out, workspace=workspace)
     B = Qd.shape[0]
     ub_local = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
-    gallery.merge_pruned(1, Qd, qq, k, ub_local, index_base)
+    gallery.merge_pruned(1, Qd, qq, k, ub_local, index_base, workspace=workspace)
     ub = kth_bound(gather_rows(ub_local, group), ws, B, k)     # [ws][B][k] rank-major -> [B]
-    return gallery.merge_pruned(2, Qd, qq, k, ub, index_base, out)
+    return gallery.merge_pruned(2, Qd, qq, k, ub, index_base, out, workspace=workspace)
 
 
 def global_certificate(kth, minb):

@@ -1,0 +1,88 @@
+"""bench.py's StepPipeline (the timed step's schedule): the tile pass of batch s on the
+main stream, batch s+1's preparation and batch s's merge on a side stream, batch s-1's certificate
+read and fallback tiers enqueued before batch s+1's preparation, three query buffers and two search
+workspaces.  Every batch's final top-k must equal the one-shot search of the same batch
+(quantize, ofr_knn_f6 phases 1+2, fallback tiers) on the default stream -- bit for bit: the schedule
+changes only which stream runs a kernel and which buffer it reads."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(noise, N=20_000, d=512, side=32, per=10, B=512, batches=5):
+    from opencv_facerecognizer_amd._device import round_up
+    from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_gallery, build_projection
+    dev = torch.device("cuda", 0)
+    n_ids = N // per
+    P, _ = build_projection(side * side, d, dev)
+    bank = IdentityBank(n_ids, side, side, device=dev)
+    g = build_gallery(P, bank, per, 0, N, N, d, max(32, round_up(d, 32)), dev, noise=noise)
+    gq = torch.Generator(device=dev)
+    gq.manual_seed(SEED + 11)
+    X = [bank.images(torch.randint(0, n_ids, (B,), generator=gq, device=dev), seed=SEED + 100 + s, noise=noise)
+         for s in range(batches)]
+    return P, g, X
+
+
+@pytest.mark.parametrize("noise", [12.0, 40.0])
+def test_step_pipeline_matches_one_shot(noise):
+    """noise 40: crowded identities, so the fallback tiers run inside finish() while the next tile
+    pass and the next preparation are in flight."""
+    from bench import StepPipeline
+    P, g, X = _setup(noise)
+    k, dev = 3, torch.device("cuda", 0)
+    for t in g.tier_path("f6")[:-1]:
+        g._tier_gallery(t)
+
+    # one-shot, serial, default stream
+    want, fell = [], 0
+    for Xs in X:
+        Qd = P.project(Xs, shift64=g.shift64)
+        qq = g.quantize_queries(Qd, tier="f6")
+        out = g.search_q8_phase(3, Qd, qq, k)
+        fell += g.fallback(Qd, qq, k, out)
+        want.append((out[0].cpu(), out[1].cpu()))
+
+    B, ld = X[0].shape[0], g.ld
+    bufs = [dict(Qd=torch.zeros((B, ld), dtype=torch.float32, device=dev), qq=None,
+                 out=(torch.empty((B, k), dtype=torch.float64, device=dev),
+                      torch.empty((B, k), dtype=torch.int64, device=dev))) for _ in range(StepPipeline.NBUF)]
+    order = []           # batch index per preparation, in enqueue order
+    got = []
+
+    def prep(j):
+        s = len(order)
+        order.append(s)
+        bufs[j]["batch"] = s
+        P.project(X[s], shift64=g.shift64, out=bufs[j]["Qd"])
+        bufs[j]["qq"] = g.quantize_queries(bufs[j]["Qd"], bufs[j]["qq"], tier="f6")
+
+    def tiles(j, w):
+        g.search_q8_phase(1, bufs[j]["Qd"], bufs[j]["qq"], k, workspace=w)
+
+    def merge(j, w):
+        g.search_q8_phase(2, bufs[j]["Qd"], bufs[j]["qq"], k, out=bufs[j]["out"], workspace=w)
+
+    def finish(j):
+        b = bufs[j]
+        g.fallback(b["Qd"], b["qq"], k, b["out"])
+        got.append((b["batch"], b["out"][0].clone(), b["out"][1].clone()))
+        return b["out"]
+
+    pipe = StepPipeline(dev, prep, tiles, merge, finish)
+    assert pipe.side is not pipe.main
+    pipe.run(len(X))
+    torch.cuda.synchronize()
+    assert order == list(range(len(X)))
+    assert [s for s, _, _ in got] == list(range(len(X)))
+    for s, d_, i_ in got:
+        assert torch.equal(i_.cpu(), want[s][1]), f"batch {s}: indices differ"
+        assert torch.equal(d_.cpu(), want[s][0]), f"batch {s}: distances differ"
+    print(f"noise {noise}: {fell} first-tier failures over {len(X)} batches")

@@ -343,7 +343,7 @@ class _PrunedMock:
         self.rank = rank
         self.seen = None
 
-    def merge_pruned(self, stage, Qd, qq, k, ub, index_base=0, out=None):
+    def merge_pruned(self, stage, Qd, qq, k, ub, index_base=0, out=None, workspace=None):
         if stage == 1:
             B = ub.shape[0]
             base = torch.arange(B, dtype=torch.float64)[:, None] * 10.0
