@@ -269,9 +269,14 @@ def stress_run(P, bank, args, noise, device, N=None):
             for _ in range(StepPipeline.NBUF)]
     timed = []
 
+    starts = []
+
     def prep(j):
         P.project(Xq, shift64=gallery.shift64, out=bufs[j]["Qd"])
-        bufs[j]["qq"] = gallery.quantize_queries(bufs[j]["Qd"], bufs[j]["qq"], tier="f6")
+        tier = gallery.start_tier(B)          # adaptive start (FloatGallery.start_tier): f6 unless it keeps failing
+        if timed:
+            starts.append(str(tier))
+        bufs[j]["qq"] = gallery.quantize_queries(bufs[j]["Qd"], bufs[j]["qq"], tier=tier)
 
     def finish(j):
         b = bufs[j]
@@ -300,6 +305,7 @@ def stress_run(P, bank, args, noise, device, N=None):
         e["ms"] += m / args.stress_steps
     acc = float(((out[1][:, 0] // args.per_id) == ids_q).double().mean().item())
     res = {"pixel_noise": noise, "queries_per_s": B / (ms * 1e-3), "ms_per_step": ms,
+           "start_tiers": {t: starts.count(t) for t in sorted(set(starts))},
            "uncertified_after_each_tier": counts, "skipped_tier": dict(gallery.last_skipped),
            "fallback_ms_per_step": per_tier,
            "certificate_margin_fp6": certificate_margin(gallery, Qd, qq), "top1_identity_acc": acc}
@@ -357,6 +363,7 @@ def main():
     # all-gathered (fp6 panels need whole 256-row blocks per rank)
     b0, b1 = shard_range(B, rank, world)
     shard_prep = world > 1 and B % world == 0 and (tier0 != "f6" or (B // world) % 256 == 0)
+    starts = []              # the first tier of every batch (one device)
     # the step pipeline (StepPipeline): three query buffers, each with its own result lists
     bufs = [dict(Qd=Qd if j == 0 else torch.zeros_like(Qd), qq=None, pending=None, qq_loc=None,
                  out=out if j == 0 else tuple(torch.empty_like(t) for t in out),
@@ -378,8 +385,10 @@ def main():
                 b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
         else:
             P.project(Xq, shift64=gallery.shift64, out=b["Qd"])          # fp32(W^T x - c), exact int8 MFMA
-            if use_q8:
-                b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier0)
+            if use_q8:       # one device: the adaptive start tier (FloatGallery.start_tier; f6 here)
+                tier = gallery.start_tier(B) if tier0 == "f6" and world == 1 else tier0
+                starts.append(str(tier))
+                b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier)
 
     def tiles(j, w):
         b = bufs[j]
@@ -555,6 +564,8 @@ def main():
                            ms_proj, "knn_tiles": ms_tiles,
                            "knn_merge_rerank" + ("+certificate" if use_q8 else ""): ms_merge},
             "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
+            "start_tiers": ({t: starts[-args.steps:].count(t) for t in sorted(set(starts[-args.steps:]))}
+                            if starts else None),
             "uncertified_after_each_tier": (list(last_counts) if use_q8 else None),
             "sieve_kept_rows_per_query": kept,
             "top1_identity_acc": acc,

@@ -207,6 +207,8 @@ class FloatGallery:
         self.q8 = None
         self._twin = None
         self.last_fallbacks = 0
+        self.tier_failures = {}                  # tier -> recent uncertified fraction (start_tier)
+        self._starts = 0
 
     def capacity(self):
         return int(self._Gbuf.shape[0])
@@ -238,6 +240,7 @@ class FloatGallery:
         center_round(F, self.shift64, self.ld, out=self._Gbuf[N0:N1])
         call("ofr_row_aux", stream(), self.metric, ptr(self._Gbuf[N0:]), n, self.d, self.ld, ptr(self._auxbuf[N0:]))
         self.N, self.G, self.aux = N1, self._Gbuf[:N1], self._auxbuf[:N1]
+        self.tier_failures = {}                    # new rows: the certificate statistics start over
         if self._twin is not None:                 # Cosine: the unit-row twin grows with it
             self._twin.append(self.unit_rows(self.G[N0:N1])[:, :self.d])
         for tier, g in (self.q8 or {}).items():     # "f6" before "f6x2": insertion order
@@ -338,6 +341,37 @@ class FloatGallery:
     @staticmethod
     def first_tier():
         return {"q8": 1, "q8x2": 2}.get(os.environ.get("OFR_SEARCH", "auto"), "f6")
+
+    # Adaptive start tier (serving, one device).  On a crowded gallery nearly every query fails the
+    # fp6 certificate and pays the fp6 pass for nothing before the f6x2 pass rescues it.  start_tier
+    # skips a quantized tier while its recent uncertified fraction (tier_failures: the latest batch of
+    # >= ADAPT_MIN_BATCH queries, averaged with the one before) is >= SKIP_FAIL, never skipping to
+    # the fp32 pass, and returns the configured first tier every REPROBE-th batch so a gallery that
+    # stops being crowded is noticed.  A routing choice only: every stage certifies or hands on, the
+    # results do not depend on it (tests/test_gpu_pipeline.py).  OFR_ADAPTIVE_TIER=0 disables it.
+    SKIP_FAIL = 0.9
+    REPROBE = 16
+    ADAPT_MIN_BATCH = 256
+
+    def start_tier(self, B):
+        """First tier for a batch of B queries (see above); counts the batch."""
+        first = self.first_tier()
+        if B < self.ADAPT_MIN_BATCH or os.environ.get("OFR_ADAPTIVE_TIER", "1") != "1":
+            return first
+        self._starts += 1
+        if self._starts % self.REPROBE == 0:
+            return first
+        t = first
+        while self.tier_failures.get(t, 0.0) >= self.SKIP_FAIL and self.NEXT.get(t, "fp32") != "fp32":
+            t = self.NEXT[t]
+        return t
+
+    def note_failures(self, tier, B, failed):
+        """Record that `failed` of B queries that ran tier `tier` (from its start) stayed uncertified."""
+        if B >= self.ADAPT_MIN_BATCH and tier != "fp32":
+            f = failed / B
+            prev = self.tier_failures.get(tier)
+            self.tier_failures[tier] = f if prev is None else 0.5 * (prev + f)
 
     @staticmethod
     def _q8_ld(d, slices):
@@ -479,6 +513,7 @@ class FloatGallery:
         receives (tier, queries, ms) per stage that ran (HIP events on the current stream)."""
         bad = open_rows(qq["cert"])
         counts = [int(bad.numel())]
+        self.note_failures(qq["tier"], int(qq["B"]), counts[0])
         pending = {}                    # tier -> indices into the original batch waiting for it
         self.last_skipped = {}
         self._route(qq["tier"], bad, Qd, qq["stats"].index_select(0, bad), qq["bound"].index_select(0, bad), out, k,
@@ -505,6 +540,7 @@ class FloatGallery:
                 out[1].index_copy_(0, rows, i2)
                 still = open_rows(q2["cert"])
                 counts.append(int(still.numel()))
+                self.note_failures(tier, int(rows.numel()), counts[-1])
                 self._route(tier, rows.index_select(0, still), Qd, q2["stats"].index_select(0, still),
                             q2["bound"].index_select(0, still), out, k, pending)
             if timings is not None:
@@ -584,7 +620,8 @@ class FloatGallery:
         if self.use_cos_cert(B, k):
             return self._search_cosine(Qd, k, index_base)
         if self.use_q8(B, k):
-            qq = self.quantize_queries(Qd, tier=self.first_tier())
+            self.last_start_tier = self.start_tier(B)
+            qq = self.quantize_queries(Qd, tier=self.last_start_tier)
             out = self.search_q8_phase(3, Qd, qq, k, index_base)
             self.fallback(Qd, qq, k, out, index_base)
             return out

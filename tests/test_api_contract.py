@@ -128,3 +128,32 @@ def test_certified_tier_paths():
     assert g.next_tier("f6", SMALL_BATCH) == "fp32" and g.next_tier(2, 4096) == "fp32"
     for t in FloatGallery.TIER_CHAIN[:-1]:
         assert FloatGallery.tier_path(t)[-1] == "fp32"
+
+
+def test_start_tier_policy_host_logic(monkeypatch):
+    """FloatGallery.start_tier / note_failures without a device: skip a tier at >= SKIP_FAIL recent
+    failures (never to fp32), small batches and OFR_ADAPTIVE_TIER=0 keep the first tier, the
+    average of the last two batches decides, every REPROBE-th batch probes the first tier."""
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    monkeypatch.delenv("OFR_ADAPTIVE_TIER", raising=False)
+    g = FloatGallery.__new__(FloatGallery)
+    g.tier_failures, g._starts = {}, 0
+    assert g.start_tier(4096) == "f6"
+    g.note_failures("f6", 4096, 4096)
+    assert g.start_tier(4096) == "f6x2"
+    assert g.start_tier(32) == "f6"                      # small batches: no statistics, no skipping
+    g.note_failures("f6x2", 4096, 4000)
+    assert g.start_tier(4096) == 2                        # f6x2 fails too: int8 x2
+    g.note_failures(2, 4096, 4096)
+    assert g.start_tier(4096) == 2                        # never skipped to the fp32 pass
+    g.note_failures("f6", 4096, 0)                        # (1.0 + 0.0) / 2 < SKIP_FAIL
+    g.tier_failures.pop("f6x2")
+    assert g.start_tier(4096) == "f6"
+    g.note_failures("f6", 100, 100)                       # batches below ADAPT_MIN_BATCH are not counted
+    assert g.tier_failures["f6"] == 0.5
+    g.tier_failures["f6"] = 1.0
+    seen = [g.start_tier(4096) for _ in range(2 * FloatGallery.REPROBE)]
+    assert seen.count("f6") == 2 and seen.count("f6x2") == 2 * FloatGallery.REPROBE - 2
+    monkeypatch.setenv("OFR_ADAPTIVE_TIER", "0")
+    assert g.start_tier(4096) == "f6"

@@ -86,3 +86,34 @@ def test_step_pipeline_matches_one_shot(noise):
         assert torch.equal(i_.cpu(), want[s][1]), f"batch {s}: indices differ"
         assert torch.equal(d_.cpu(), want[s][0]), f"batch {s}: distances differ"
     print(f"noise {noise}: {fell} first-tier failures over {len(X)} batches")
+
+
+def test_adaptive_start_tier_skips_failing_fp6(monkeypatch):
+    """FloatGallery.start_tier: on clusters the fp6 tier cannot certify (>= 90 % fail, the f6x2 test's
+    data), the second batch starts at f6x2; the results equal the fixed-start chain's bit for bit,
+    and every REPROBE-th batch starts at fp6 again."""
+    import numpy as np
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = np.random.default_rng(3)
+    d, K, per, B = 128, 200, 40, 300
+    mu = r.normal(0, 1, (K, d))
+    G = (mu[np.arange(K * per) % K] + r.normal(0, 0.5, (K * per, d))).astype(np.float32).astype(np.float64)
+    Q = (mu[r.integers(0, K, B)] + r.normal(0, 0.5, (B, d))).astype(np.float32).astype(np.float64)
+    monkeypatch.setenv("OFR_ADAPTIVE_TIER", "0")
+    fixed = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    want = fixed.search(fixed.query_rows(Q), 2)
+    assert fixed.last_fallbacks[0] >= 0.9 * B, fixed.last_fallbacks
+    monkeypatch.setenv("OFR_ADAPTIVE_TIER", "1")
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    starts = []
+    for it in range(FloatGallery.REPROBE + 1):
+        dd, ii = g.search(g.query_rows(Q), 2)
+        starts.append(g.last_start_tier)
+        assert torch.equal(ii, want[1]) and torch.equal(dd, want[0]), (it, starts)
+    assert starts[0] == "f6" and starts[1] == "f6x2", starts
+    assert starts[FloatGallery.REPROBE - 1] == "f6", starts          # the re-probe
+    assert starts.count("f6") == 2, starts
+    g.append(G[:3])                                                   # new rows: statistics start over
+    assert g.tier_failures == {} and g.start_tier(B) in ("f6",)
