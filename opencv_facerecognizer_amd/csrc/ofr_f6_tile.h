@@ -919,5 +919,213 @@ struct Engine16 {
   }
 };
 
+// ---- wide engine: 384 gallery x 256 query tiles, one wave per SIMD (round 3) -------------------
+// The 256 x 256 engines move 48 KiB into the CU per 256x256x128 stage and read 144 KiB of fragments
+// out of LDS for it; both streams cost SIMD issue time that does not overlap the MFMAs.
+// A 384 x 256 tile moves 60 KiB per 384x256x128 stage (-17 % per MAC), and one wave per SIMD with a
+// 192 x 128 wave tile (96 accumulators of 4 = 384 registers, the rest of the 512-entry file for
+// fragments) reads 20 fragments per wave and stage (-44 % per MAC against 8 waves of 128 x 64).
+// Wave w: gallery rows WR*192 + 16 i (i < 12), queries WC*128 + 16 c (c < 8), WR = w >> 1, WC = w & 1.
+//
+// LDS: gallery ring of 3 slots (36 KiB: the tile's three 128-row half panels of the stage), query
+// ring of 2 slots (24 KiB: the query panel's stage block, its global image).  A half-panel image keeps
+// the global sub-block structure at half size: sub-block q at q * 3 KiB, part0 (16 B per row) then
+// part1 (8 B per row at slot r ^ 16 (q & 1), the global p1_slot), so every piece of a copy is 1 KiB
+// contiguous on both sides and the fragment reads stay bank-conflict free.
+// Per stage s and row i (12 rows of 8 MFMAs, the gallery fragments through a ring of 3 read two rows
+// ahead, the 8 query fragments held and refilled for s + 1 after their last MFMA in row 11):
+//   row 1 start : barrier A (every wave's reads of Q(s), issued in row 11 of s - 1, done)
+//   rows 1 - 6  : one piece of Q(s + 2) per row into Q(s)'s slot (6 per wave, 24 per stage)
+//   rows 0 - 6  : one piece of G(s + 2) per row (pieces 2..8 of the wave's 9) into G(s - 1)'s slot
+//   row 10 start: own copies of G(s + 1), Q(s + 1) landed (vmcnt(15): only G(s + 2), Q(s + 2) may fly)
+//                 + barrier B (every wave's reads of G(s), the last in row 9, done)
+//   rows 10, 11 : pieces 0, 1 of G(s + 3) into G(s)'s slot; A[0], A[1] of s + 1 read
+// so every copy has >= 1.3 stages of lead and the CU's copy path sees ~1 KiB per SIMD per 8 MFMAs
+// instead of bursts.
+struct EngineW {
+  static constexpr int NW = 4, NT = 256;
+  static constexpr int TGW = 384;                    // gallery rows per tile
+  static constexpr int HPB = 12288;                  // a 128-row half panel of one stage
+  static constexpr int GSLOT = 3 * HPB, QSLOT = PANEL;
+  static constexpr int NGS = 3, NQS = 2;
+  static constexpr int LDS_BYTES = NGS * GSLOT + NQS * QSLOT;   // 159,744
+  static constexpr int NA = 12, NB = 8, RING = 3;
+  static constexpr int NAA = 8;                      // row blocks whose accumulators live in AGPRs (8 x 8 x 4 = 256)
+  static constexpr int GPW = 9, QPW = 6;             // copy pieces per wave and stage
+  static_assert(NA % RING == 0, "the ring index must repeat across stages");
+
+  // gallery tile gt: rows [384 gt, 384 gt + 384) = half panels 3 gt .. 3 gt + 2 of the 256-row panels,
+  // which lie in panels p0 = 3 gt / 2 and p0 + 1.  hb[k][part]: the byte offset of half panel k's
+  // sub-block 0 part (0: part0, 1: part1) in the gallery descriptor (stage 0).
+  struct Feed {
+    __amdgpu_buffer_rsrc_t rg, rq;
+    uint32_t hb[3][2];
+  };
+
+  static __device__ __forceinline__ void feed_init(Feed& f, const char* G, int64_t N, const char* Q, int64_t qp,
+                                                   int64_t nst, int64_t gt) {
+    const int64_t h0 = 3 * gt, p0 = h0 >> 1;
+    const int64_t pb = nst * (int64_t)PANEL;                 // bytes per 256-row panel
+    const int64_t rem = panels(N) * pb - p0 * pb;
+    const int64_t rec = rem < 2 * pb ? rem : 2 * pb;         // reads past the gallery return zeros
+    f.rg = __builtin_amdgcn_make_buffer_rsrc((void*)(G + p0 * pb), 0, (int)rec, 0x00020000);
+    f.rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * pb), 0, (int)pb, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int64_t h = h0 + k;
+      const uint32_t rel = (uint32_t)(((h >> 1) - p0) * pb), hh = (uint32_t)(h & 1);
+      f.hb[k][0] = rel + hh * 2048;
+      f.hb[k][1] = rel + 4096 + hh * 1024;
+    }
+  }
+  static __device__ __forceinline__ char* gslot(char* smem, int s) { return smem + (s % NGS) * GSLOT; }
+  static __device__ __forceinline__ char* qslot(char* smem, int s) { return smem + NGS * GSLOT + (s % NQS) * QSLOT; }
+  // piece J of wave W's share of stage ks of the gallery tile (9 of its 36) / query panel (6 of 24)
+  template <int W, int J>
+  static __device__ __forceinline__ void gcopy(const Feed& f, char* smem, int s, int ks) {
+    constexpr int g = W * GPW + J, k = g / 12, q = (g % 12) / 3, part = g % 3;
+    constexpr uint32_t cs = q * 6144 + (part == 1 ? 1024 : 0), cd = k * HPB + q * 3072 + (part < 2 ? part * 1024 : 2048);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(f.rg, (OFR_LDS void*)(gslot(smem, s) + cd), 16, (threadIdx.x & 63) * 16,
+                                             f.hb[k][part == 2] + cs + (uint32_t)ks * PANEL, 0, 0);
+  }
+  template <int W, int J>
+  static __device__ __forceinline__ void qcopy(const Feed& f, char* smem, int s, int ks) {
+    constexpr uint32_t o = (W * QPW + J) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(f.rq, (OFR_LDS void*)(qslot(smem, s) + o), 16, (threadIdx.x & 63) * 16,
+                                             o + (uint32_t)ks * PANEL, 0, 0);
+  }
+
+  // gallery fragment: local tile row R0 (a multiple of 16, compile time) of slot st
+  template <int R0>
+  static __device__ __forceinline__ i32x6 fragA(const char* st) {
+    constexpr int k = R0 / 128, rl = R0 % 128;
+    const int lane = threadIdx.x & 63, q = lane >> 4, l = lane & 15;
+    const char* sb = st + k * HPB + q * 3072;
+    const int slot = (rl + l) ^ ((q & 1) << 4);
+    const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 2048 + slot * 8);
+    asm volatile("" : "+v"(p1a));
+    const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + (rl + l) * 16);
+    const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
+    i32x6 f;
+    f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
+    return f;
+  }
+
+  // The accumulators are pinned by inline asm: 384 registers per lane exceed either register file,
+  // and the compiler gives every MFMA of a function the same form (all AGPR or all VGPR), shuffling
+  // the rest through v_accvgpr moves.  Row blocks i < NAA accumulate in AGPRs, the others in VGPRs.
+  // Hazards: an accumulator is re-read (as srcC) 96 MFMAs after it was written; the epilogue reads
+  // them after wait_drain().
+  template <bool AG>
+  static __device__ __forceinline__ void mfma(const i32x6& a, const i32x6& b, f32x4& c, int sc) {
+    if constexpr (AG)
+      asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
+                   : "+a"(c) : "v"(a), "v"(b), "v"(sc));
+    else
+      asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
+                   : "+v"(c) : "v"(a), "v"(b), "v"(sc));
+  }
+  static __device__ __forceinline__ void wait_drain() {   // the last MFMAs' results readable
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  }
+
+  // MODE (probes): 1 = no copies in the k loop (the prologue's stages re-read), 2 = no MFMAs
+  template <int W, int MODE>
+  static __device__ __forceinline__ void mainloop(char* smem, const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
+    constexpr int WR = W >> 1, WC = W & 1;
+    const int r16 = threadIdx.x & 15;
+    int sc = SCALE_ONE;
+    asm volatile("" : "+v"(sc));
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int last = nst - 1;
+    auto cl = [&](int s) { return s < last ? s : last; };
+    auto gall = [&](int s) {
+      gcopy<W, 0>(f, smem, s, cl(s)); gcopy<W, 1>(f, smem, s, cl(s)); gcopy<W, 2>(f, smem, s, cl(s));
+      gcopy<W, 3>(f, smem, s, cl(s)); gcopy<W, 4>(f, smem, s, cl(s)); gcopy<W, 5>(f, smem, s, cl(s));
+      gcopy<W, 6>(f, smem, s, cl(s)); gcopy<W, 7>(f, smem, s, cl(s)); gcopy<W, 8>(f, smem, s, cl(s));
+    };
+    auto qall = [&](int s) {
+      qcopy<W, 0>(f, smem, s, cl(s)); qcopy<W, 1>(f, smem, s, cl(s)); qcopy<W, 2>(f, smem, s, cl(s));
+      qcopy<W, 3>(f, smem, s, cl(s)); qcopy<W, 4>(f, smem, s, cl(s)); qcopy<W, 5>(f, smem, s, cl(s));
+    };
+    // prologue: G(0), Q(0), G(1), Q(1) and pieces 0, 1 of G(2)
+    gall(0); qall(0); gall(1); qall(1);
+    gcopy<W, 0>(f, smem, 2, cl(2));
+    gcopy<W, 1>(f, smem, 2, cl(2));
+    wait_vm<GPW + QPW + 2>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    i32x6 a[RING], b[NB];
+    {
+      const char* g0 = gslot(smem, 0);
+      a[0] = fragA<WR * 192 + 0>(g0);
+      a[1] = fragA<WR * 192 + 16>(g0);
+#pragma unroll
+      for (int c = 0; c < NB; ++c) b[c] = Engine16::frag16(qslot(smem, 0), WC * 128 + c * 16 + r16);
+    }
+    for (int s = 0; s <= last; ++s) {
+      const char* gc = gslot(smem, s);
+      const char* gn = gslot(smem, s + 1);
+      const char* qn = qslot(smem, s + 1);
+      auto row = [&](auto ii) {
+        constexpr int i = decltype(ii)::value;
+        constexpr bool AG = i < NAA;
+        auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) {
+          if constexpr ((MODE & 2) == 0) mfma<AG>(x, y, c, sc);
+        };
+        if constexpr (i == 1) {              // barrier A: Q(s) consumed by every wave
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (i == 10) {             // barrier B: G(s+1), Q(s+1) landed; G(s) consumed
+          if constexpr ((MODE & 1) == 0) wait_vm<GPW + QPW>();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr ((MODE & 1) == 0) {
+          if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(f, smem, s + 2, cl(s + 2));
+          if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(f, smem, s + 2, cl(s + 2));
+          if constexpr (i >= 10) gcopy<W, (i >= 10 ? i - 10 : 0)>(f, smem, s + 3, cl(s + 3));
+        }
+        mm(a[i % RING], b[0], acc[i][0]);
+        if constexpr (i + 2 < NA) a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? i + 2 : 0) * 16>(gc);
+        else a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? 0 : i + 2 - NA) * 16>(gn);
+        if constexpr (i == NA - 1) {
+#pragma unroll
+          for (int c = 1; c < NB; ++c) {
+            mm(a[i % RING], b[c], acc[i][c]);
+            b[c - 1] = Engine16::frag16(qn, WC * 128 + (c - 1) * 16 + r16);
+          }
+          b[NB - 1] = Engine16::frag16(qn, WC * 128 + (NB - 1) * 16 + r16);
+        } else {
+#pragma unroll
+          for (int c = 1; c < NB; ++c) mm(a[i % RING], b[c], acc[i][c]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      row(std::integral_constant<int, 0>{});
+      row(std::integral_constant<int, 1>{});
+      row(std::integral_constant<int, 2>{});
+      row(std::integral_constant<int, 3>{});
+      row(std::integral_constant<int, 4>{});
+      row(std::integral_constant<int, 5>{});
+      row(std::integral_constant<int, 6>{});
+      row(std::integral_constant<int, 7>{});
+      row(std::integral_constant<int, 8>{});
+      row(std::integral_constant<int, 9>{});
+      row(std::integral_constant<int, 10>{});
+      row(std::integral_constant<int, 11>{});
+    }
+    wait_vm<0>();
+    wait_drain();
+    barrier();
+  }
+};
+
 }  // namespace f6t
 }  // namespace ofr

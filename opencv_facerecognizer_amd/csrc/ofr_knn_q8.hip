@@ -181,7 +181,7 @@ constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
 // query block of this lane (th = key_float(theta | 0xff): truncated key <= theta  <=>
 // !(score > th); NaN for KEY_NONE keeps every row).  More than SIEVE_HCAP hits in one tile push
 // every query of the tile past its bucket cap (uncertified, no candidates read by the merge).
-template <int TQ>
+template <int TQ, int GB = 8, int TGR = TG>
 __device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64_t g0, int64_t q0);
 
 template <int CT, int TQ, int QW, int WQ, class CV>
@@ -235,11 +235,13 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
   sieve_flush<TQ>(smem, p, g0, q0);
 }
 
-// The tile's staged hits -> per-query buckets (after the compares and a barrier)
-template <int TQ>
+// The tile's staged hits -> per-query buckets (after the compares and a barrier).  A hit packs
+// (tile query << GB) | tile gallery row; TGR gallery rows per tile (the staging area follows their
+// [TGR][2] operand table).
+template <int TQ, int GB, int TGR>
 __device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
-  const uint32_t* nhit = reinterpret_cast<const uint32_t*>(smem + TG * 8);
-  const uint2* hits = reinterpret_cast<const uint2*>(smem + TG * 8 + 16);
+  const uint32_t* nhit = reinterpret_cast<const uint32_t*>(smem + TGR * 8);
+  const uint2* hits = reinterpret_cast<const uint2*>(smem + TGR * 8 + 16);
   const uint32_t nh = *nhit;
   if (nh > (uint32_t)SIEVE_HCAP) {   // hits lost: push every query of the tile past its cap (uncertified)
     // saturating (max, not add): any number of overflowing tiles leaves the count at cap + 1 plus
@@ -249,8 +251,8 @@ __device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64
   }
   for (uint32_t e = threadIdx.x; e < nh; e += blockDim.x) {
     const uint2 hv = hits[e];
-    const int64_t q = q0 + (int)(hv.y >> 8);
-    const int gl = (int)(hv.y & 0xffu);
+    const int64_t q = q0 + (int)(hv.y >> GB);
+    const int gl = (int)(hv.y & ((1u << GB) - 1u));
     if (q < p.B) {
       const int slot = atomicAdd(p.count + q, 1);
       if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(hv.x), (int)(g0 + gl)};
@@ -514,6 +516,93 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
     return;
   }
   sieve_epilogue16(smem, p, g0, q0, ga, gs, sq2, th, acc);
+}
+
+// fp6 sieve pass on the wide engine (f6t::EngineW): 384 gallery x 256 query tiles, 4 waves (one per
+// SIMD), p.ntg = ceil(N / 384) gallery tiles.  The epilogue is sieve_epilogue16's for the 192 x 128
+// wave tile: element r of acc[i][c] of lane l is gallery row WR*192 + 16 i + 4 (l / 16) + r, query
+// WC*128 + 16 c + l % 16.  MODE probe bits: 1 / 2 = no copies / no MFMAs in the k loop, 4 = no
+// epilogue (the accumulators kept alive).
+template <int W, int MODE>
+__device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, const f6t::EngineW::Feed& f, int64_t g0,
+                                         int64_t q0) {
+  using E = f6t::EngineW;
+  f6t::f32x4 acc[E::NA][E::NB];
+  constexpr int WR = W >> 1;
+  E::mainloop<W, MODE & 3>(smem, f, p.nk, acc);
+  float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
+  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
+  uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [SIEVE_HCAP]
+  const int nvalid = p.N - g0 < E::TGW ? (int)(p.N - g0) : E::TGW;
+  for (int r = threadIdx.x; r < E::TGW; r += E::NT) {
+    const bool ok = r < nvalid;
+    gtab[2 * r + 0] = ok ? p.aux[g0 + r] : __builtin_inff();
+    gtab[2 * r + 1] = ok ? p.gscale[g0 + r] : 0.f;
+  }
+  if (threadIdx.x == 0) *nhit = 0;
+  const int lane = threadIdx.x & 63, wc = W & 1, g4 = (lane >> 4) * 4, r16 = lane & 15;
+  float sq2[E::NB], th[E::NB];
+#pragma unroll
+  for (int c = 0; c < E::NB; ++c) {
+    const int64_t q = q0 + wc * 128 + c * 16 + r16;
+    const bool ok = q < p.B;
+    sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
+    th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
+  }
+  __syncthreads();
+  if constexpr ((MODE & 4) != 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < E::NA; ++i)
+#pragma unroll
+      for (int c = 0; c < E::NB; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += acc[i][c][r];
+    if (s == 1.2345f) p.cand[0].d = s;
+    __syncthreads();
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < E::NA; ++i) {
+    const int gl0 = WR * 192 + i * 16 + g4;        // this lane's 4 consecutive gallery rows
+    const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
+    const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
+    const float av[4] = {t0.x, t0.z, t1.x, t1.z}, sv[4] = {t0.y, t0.w, t1.y, t1.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gl = gl0 + r;
+#pragma unroll
+      for (int c = 0; c < E::NB; ++c) {
+        const float sc = av[r] - sq2[c] * sv[r] * acc[i][c][r];
+        if (!(sc > th[c]) && gl < nvalid) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
+          const int ql = wc * 128 + c * 16 + r16;
+          const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
+          const uint32_t slot = atomicAdd(nhit, 1u);
+          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)gl);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  sieve_flush<f6t::TQ, 9, E::TGW>(smem, p, g0, q0);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
+  using E = f6t::EngineW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t gt, qt;
+  i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
+  const int64_t g0 = gt * E::TGW, q0 = qt * f6t::TQ;
+  E::Feed f;
+  E::feed_init(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), qt, p.nk, gt);
+  switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
+    case 0: f6w_body<0, MODE>(smem, p, f, g0, q0); break;
+    case 1: f6w_body<1, MODE>(smem, p, f, g0, q0); break;
+    case 2: f6w_body<2, MODE>(smem, p, f, g0, q0); break;
+    default: f6w_body<3, MODE>(smem, p, f, g0, q0); break;
+  }
 }
 
 // ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
@@ -1370,18 +1459,22 @@ constexpr int F6S_MODE = 1024 + 4096 + 8192 + 262144;
 // labels its roofline entry with it, so the record names the variant that actually ran)
 static int f6_shape();
 extern "C" const char* ofr_f6_sieve_kernel(void) {
-  static const std::string names[2] = {
+  static const std::string names[3] = {
       "q8s::tile_kernel_f6s<" + std::to_string(F6S_MODE) + ", 1> (16x16x128 fp6 engine)",
-      "q8s::tile_kernel_f6<" + std::to_string(F6_NW) + ", 8> (32x32x64 fp6 engine)"};
-  return names[f6_shape() == 16 ? 0 : 1].c_str();
+      "q8s::tile_kernel_f6<" + std::to_string(F6_NW) + ", 8> (32x32x64 fp6 engine)",
+      "q8s::tile_kernel_f6w<0> (16x16x128 fp6 engine, 384x256 tiles, 1 wave per SIMD)"};
+  return names[f6_shape() == 16 ? 0 : (f6_shape() == 32 ? 1 : 2)].c_str();
 }
 
-// MFMA shape of the sieve pass: 16 = v_mfma_scale_f32_16x16x128 (f6t::Engine16, default),
-// 32 = the 32x32x64 engine (OFR_F6_SHAPE=32)
+// Engine of the sieve pass: 16 = v_mfma_scale_f32_16x16x128 on 256 x 256 tiles, 8 waves
+// (f6t::Engine16, default), 32 = the 32x32x64 engine (OFR_F6_SHAPE=32), 384 = the 16x16x128 engine on
+// 384 x 256 tiles, one wave per SIMD (f6t::EngineW, OFR_F6_SHAPE=384; one segment: the two-slice tier
+// keeps Engine16)
 static int f6_shape() {
   static const int s = [] {
     const char* e = getenv("OFR_F6_SHAPE");
-    return e && atoi(e) == 32 ? 32 : 16;
+    const int v = e ? atoi(e) : 0;
+    return v == 32 || v == 384 ? v : 16;
   }();
   return s;
 }
@@ -1522,6 +1615,9 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
         }
+        hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel_f6w<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           f6t::EngineW::LDS_BYTES);
+        if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 wide tile)");
         attr_done = true;
       }
       // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel -> thresholds
@@ -1544,10 +1640,17 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       a.count = count;
       a.bucket = bucket;
       a.cap = q8s::SIEVE_CAP;
-      if (f6_shape() == 16 && two)
+      if (f6_shape() == 384 && !two) {
+        q8s::TileArgs wa = a;   // 384-row gallery tiles over the same 256-row panel layout
+        wa.ntg = cdiv(N, f6t::EngineW::TGW);
+        wa.gg = wa.ntg < q8s::GROUP_G ? wa.ntg : q8s::GROUP_G;
+        OFR_CHECK_ARG(wa.ntq * wa.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
+        hipLaunchKernelGGL((q8s::tile_kernel_f6w<0>), dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),
+                           f6t::EngineW::LDS_BYTES, st, wa);
+      } else if (f6_shape() != 32 && two)
         hipLaunchKernelGGL((q8s::tile_kernel_f6s<F6S_MODE, 3>), dim3((unsigned)(a.ntq * a.ntg)),
                            dim3(f6t::Engine16::NT), f6t::LDS, st, a);
-      else if (f6_shape() == 16)
+      else if (f6_shape() != 32)
         hipLaunchKernelGGL((q8s::tile_kernel_f6s<F6S_MODE>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
                            f6t::LDS, st, a);
       else if (two)

@@ -256,6 +256,29 @@ static int run16(q8s::TileArgs a, int reps, const char* tag) {
   return 0;
 }
 
+template <int MODE>
+static int runw(q8s::TileArgs a, int reps, const char* tag) {
+  using E = f6t::EngineW;
+  a.ntg = (a.N + E::TGW - 1) / E::TGW;
+  const double ops = 2.0 * (double)a.N * a.ntq * f6t::TQ * a.nk * f6t::BK;
+  CK(hipFuncSetAttribute((const void*)q8s::tile_kernel_f6w<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, E::LDS_BYTES));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const unsigned grid = (unsigned)(a.ntq * a.ntg);
+  hipLaunchKernelGGL((q8s::tile_kernel_f6w<MODE>), dim3(grid), dim3(E::NT), E::LDS_BYTES, 0, a);
+  CK(hipGetLastError());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((q8s::tile_kernel_f6w<MODE>), dim3(grid), dim3(E::NT), E::LDS_BYTES, 0, a);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  printf("f6 wide384 %-12s mode=%-2d gg=%-3ld ms=%8.2f  executed=%7.1f TOPS (%.1f%% of 10000)\n", tag, MODE, (long)a.gg, ms,
+         ops / ms / 1e9, ops / ms / 1e9 / 100.0);
+  fflush(stdout);
+  return 0;
+}
+
 template <int MODE, int NSQ, int R, int D>
 static int runq(q8s::TileArgs a, int reps, const char* tag) {
   const double ops = 2.0 * (double)a.ntg * f6t::TA * a.ntq * f6t::TQ * a.nk * f6t::BK;
@@ -345,6 +368,14 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; ++rep)
       if (run16<0>(a, reps, "sieve16") || run16<1024>(a, reps, "mubuf2b16") || run16<1024 + 4096>(a, reps, "mubuf2b-rs2") ||
           run16<1024 + 4096 + 8192>(a, reps, "mubuf2b-rs1"))
+        return 1;
+    return 0;
+  }
+  if (getenv("WIDE")) {   // the 384 x 256 one-wave-per-SIMD engine (f6t::EngineW) vs the library pass
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (run16<275456>(a, reps, "lib4w") || run16<275456 + 4>(a, reps, "lib4w-noepi") || runw<0>(a, reps, "wide") ||
+          runw<4>(a, reps, "wide-noepi") || runw<5>(a, reps, "wide-nocopy") || runw<7>(a, reps, "wide-nomfma"))
         return 1;
     return 0;
   }
