@@ -148,19 +148,22 @@ def committed_traffic(cfg):
 class StepPipeline:
     """The timed step's schedule over a sequence of query batches:
 
-      main stream  tile pass of batch s (behind its preparation);
-      side stream  behind tile pass s: batch s+1's preparation (projection, quantization, its
-                   all-gathers), then batch s's merge (exact re-rank + certificate) -- the projection
-                   runs alone and the merge runs under tile pass s+1;
+      main stream  tile pass of batch s (behind its preparation): its sample pass + thresholds, then
+                   its sieve pass;
+      side stream  behind sample pass s: batch s-1's merge (exact re-rank + certificate), which so
+                   runs under sieve pass s and leaves the short sample pass alone; behind tile pass s:
+                   batch s+1's preparation (projection, quantization, its all-gathers), which runs
+                   alone;
       host         batch s-1's certificate read (one sync, on the side stream up to merge s-1,
-                   which finished under tile pass s) and its fallback tiers, enqueued on the side
+                   which finishes early in sieve pass s) and its fallback tiers, enqueued on the side
                    stream before batch s+1's preparation.
 
     Three query buffers (preparation s+1 / merge s / fallback s-1), two search workspaces (tile
     pass s writes one while merge s-1 reads the other).  Callbacks, each enqueueing on the current
-    stream: prep(j) fills buffer j; tiles(j, w) and merge(j, w) run phase 1 / phase 2 of buffer j
-    on workspace w; finish(j) reads the certificate (host sync) and runs the fallback, returning
-    the batch's result.  overlap=False: one stream, the same order."""
+    stream: prep(j) fills buffer j; tiles(j, w, part) runs part "sample" (sample pass + thresholds)
+    or "sieve" of phase 1 of buffer j on workspace w, merge(j, w) phase 2; finish(j) reads the
+    certificate (host sync) and runs the fallback, returning the batch's result.  overlap=False: one
+    stream, the same order."""
 
     NBUF, NWS = 3, 2
 
@@ -172,6 +175,7 @@ class StepPipeline:
         self.ev_ready = [torch.cuda.Event() for _ in range(self.NBUF)]    # buffer prepared (side)
         self.ev_merged = [torch.cuda.Event() for _ in range(self.NWS)]    # workspace's merge done (side)
         self.ev_tiles = torch.cuda.Event()                                # latest tile pass done (main)
+        self.ev_sample = torch.cuda.Event()                               # latest sample pass done (main)
         # the side stream starts behind everything the main stream has queued (gallery and tier builds,
         # the query images, buffer fills): an unrecorded event is no dependency, and once the caching
         # allocator stops calling hipMalloc (which synchronises) nothing else would order the first
@@ -192,6 +196,17 @@ class StepPipeline:
         with torch.cuda.stream(self.side):
             return self.finish_fn(s % self.NBUF)
 
+    def _merge(self, s, ev):
+        j, w = s % self.NBUF, s % self.NWS
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.ev_sample)            # behind the next batch's sample pass
+            if ev:
+                ev[5].record()
+            self.merge_fn(j, self.ws[w])
+            if ev:
+                ev[3].record()
+            self.ev_merged[w].record(self.side)
+
     def run(self, steps, events=None):
         """Exactly `steps` preparations, tile passes, merges and fallbacks; returns the last batch's
         result.  events[s]: 6 timing events (prep start/end on the side stream, tile pass end and start
@@ -205,7 +220,11 @@ class StepPipeline:
             self.main.wait_event(self.ev_merged[w])         # merge s-2 done with this workspace
             if ev[s]:
                 ev[s][4].record(self.main)
-            self.tiles_fn(j, self.ws[w])
+            self.tiles_fn(j, self.ws[w], "sample")
+            self.ev_sample.record(self.main)
+            if s >= 1:                                      # merge s-1 under sieve pass s
+                self._merge(s - 1, ev[s - 1])
+            self.tiles_fn(j, self.ws[w], "sieve")
             if ev[s]:
                 ev[s][2].record(self.main)
             self.ev_tiles.record(self.main)
@@ -214,14 +233,8 @@ class StepPipeline:
             self.side.wait_event(self.ev_tiles)
             if s + 1 < steps:
                 self._prep(s + 1, ev[s + 1])
-            with torch.cuda.stream(self.side):
-                if ev[s]:
-                    ev[s][5].record()
-                self.merge_fn(j, self.ws[w])
-                if ev[s]:
-                    ev[s][3].record()
-                self.ev_merged[w].record(self.side)
         if steps:
+            self._merge(steps - 1, ev[steps - 1])
             res = self._finish(steps - 1)
         # the caller's stream sees everything the side stream did
         self.main.wait_stream(self.side)
@@ -284,7 +297,8 @@ def stress_run(P, bank, args, noise, device, N=None):
         return b["out"]
 
     pipe = StepPipeline(device, prep,
-                        lambda j, w: gallery.search_q8_phase(1, bufs[j]["Qd"], bufs[j]["qq"], k, workspace=w),
+                        lambda j, w, part: gallery.search_q8_phase(4 if part == "sample" else 8, bufs[j]["Qd"],
+                                                                   bufs[j]["qq"], k, workspace=w),
                         lambda j, w: gallery.search_q8_phase(2, bufs[j]["Qd"], bufs[j]["qq"], k, out=bufs[j]["out"],
                                                              workspace=w),
                         finish)
@@ -390,11 +404,11 @@ def main():
                 starts.append(str(tier))
                 b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier)
 
-    def tiles(j, w):
+    def tiles(j, w, part):
         b = bufs[j]
         if use_q8:
-            gallery.search_q8_phase(1, b["Qd"], b["qq"], k, workspace=w)
-        else:
+            gallery.search_q8_phase(4 if part == "sample" else 8, b["Qd"], b["qq"], k, workspace=w)
+        elif part == "sample":
             gallery.search_phase("tiles", b["Qd"], k, workspace=w)
 
     def merge(j, w):

@@ -184,7 +184,11 @@ int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, 
  * ofr_knn_f6_workspace_bytes(B, N) bytes, 16-byte aligned, kept between the
  * phase-1 and phase-2 calls; after phase 1 the int32 kept-row counts [B] sit
  * at byte ofr_knn_f6_sieve_counts_offset(B, N) of it (SIZE_MAX: no sieve,
- * B <= 32).  Env OFR_SIEVE_STRIDE (default 64) sets the sample stride.       */
+ * B <= 32).  Env OFR_SIEVE_STRIDE (default 64) sets the sample stride.
+ * Phase 1 in two calls (a pipelined caller overlaps other work with the second
+ * only): phases 4 = the sample pass + thresholds (B <= 32: the whole stream
+ * pass), 8 = the sieve pass (after a phases-4 call on the same workspace);
+ * 1 = 4 + 8.  Phase bits combine (e.g. 10 = sieve, then merge).             */
 size_t ofr_f6_tiles_bytes(int64_t R, int64_t d);
 /* Append support (NearestNeighbor.update, classifier.py:65-70): quantize X's R rows
  * into rows row0 .. row0+R-1 of an existing tiled buffer (scale/stats indexed by

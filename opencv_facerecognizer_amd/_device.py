@@ -453,8 +453,14 @@ class FloatGallery:
 
     def search_q8_phase(self, phases, Qd, qq, k, index_base=0, out=None, workspace=None):
         """phases 1 = quantized tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"]), 3 = both.
+        The fp6 tiers split phase 1 (ofr_knn_f6): 4 = sample pass + thresholds, 8 = the sieve pass; the
+        int8 tiers run all of phase 1 under bit 4 and nothing under bit 8.
         workspace: a Workspace of the caller's instead of the gallery's."""
         tier = qq["tier"]
+        if tier not in ("f6", "f6x2") and phases & 12:
+            phases = (phases & 3) | (1 if phases & 4 else 0)
+            if phases == 0:
+                return out
         g = self._tier_gallery(tier)
         B = Qd.shape[0]
         if out is None:

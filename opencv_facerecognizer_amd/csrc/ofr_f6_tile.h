@@ -948,6 +948,7 @@ struct EngineW {
   static constexpr int HPB = 12288;                  // a 128-row half panel of one stage
   static constexpr int GSLOT = 3 * HPB, QSLOT = PANEL;
   static constexpr int NGS = 3, NQS = 2;
+  static constexpr int QBASE = NGS * GSLOT;          // the query ring after the gallery ring
   static constexpr int LDS_BYTES = NGS * GSLOT + NQS * QSLOT;   // 159,744
   static constexpr int NA = 12, NB = 8, RING = 3;
   static constexpr int NAA = 8;                      // row blocks whose accumulators live in AGPRs (8 x 8 x 4 = 256)
@@ -955,13 +956,14 @@ struct EngineW {
   static_assert(NA % RING == 0, "the ring index must repeat across stages");
 
   // gallery tile gt: rows [384 gt, 384 gt + 384) = half panels 3 gt .. 3 gt + 2 of the 256-row panels,
-  // which lie in panels p0 = 3 gt / 2 and p0 + 1.  hb[k][part]: the byte offset of half panel k's
-  // sub-block 0 part (0: part0, 1: part1) in the gallery descriptor (stage 0).
+  // which lie in panels p0 = 3 gt / 2 and p0 + 1.  gsrc[j]: the byte offset (stage 0) in the gallery
+  // descriptor of the wave's gallery piece j.
   struct Feed {
     __amdgpu_buffer_rsrc_t rg, rq;
-    uint32_t hb[3][2];
+    uint32_t gsrc[GPW];
   };
 
+  template <int W>
   static __device__ __forceinline__ void feed_init(Feed& f, const char* G, int64_t N, const char* Q, int64_t qp,
                                                    int64_t nst, int64_t gt) {
     const int64_t h0 = 3 * gt, p0 = h0 >> 1;
@@ -971,44 +973,60 @@ struct EngineW {
     f.rg = __builtin_amdgcn_make_buffer_rsrc((void*)(G + p0 * pb), 0, (int)rec, 0x00020000);
     f.rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * pb), 0, (int)pb, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int j = 0; j < GPW; ++j) {
+      const int g = W * GPW + j, k = g / 12, q = (g % 12) / 3, part = g % 3;
       const int64_t h = h0 + k;
       const uint32_t rel = (uint32_t)(((h >> 1) - p0) * pb), hh = (uint32_t)(h & 1);
-      f.hb[k][0] = rel + hh * 2048;
-      f.hb[k][1] = rel + 4096 + hh * 1024;
+      f.gsrc[j] = rel + q * 6144 + (part < 2 ? hh * 2048 + part * 1024 : 4096 + hh * 1024);
     }
   }
-  static __device__ __forceinline__ char* gslot(char* smem, int s) { return smem + (s % NGS) * GSLOT; }
-  static __device__ __forceinline__ char* qslot(char* smem, int s) { return smem + NGS * GSLOT + (s % NQS) * QSLOT; }
-  // piece J of wave W's share of stage ks of the gallery tile (9 of its 36) / query panel (6 of 24)
+  // piece J of wave W's share of stage ks (kso = ks * PANEL) of the gallery tile (9 of its 36) / query
+  // panel (6 of 24) into the slot at LDS byte offset so
   template <int W, int J>
-  static __device__ __forceinline__ void gcopy(const Feed& f, char* smem, int s, int ks) {
+  static __device__ __forceinline__ void gcopy(const Feed& f, uint32_t so, uint32_t kso) {
     constexpr int g = W * GPW + J, k = g / 12, q = (g % 12) / 3, part = g % 3;
-    constexpr uint32_t cs = q * 6144 + (part == 1 ? 1024 : 0), cd = k * HPB + q * 3072 + (part < 2 ? part * 1024 : 2048);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(f.rg, (OFR_LDS void*)(gslot(smem, s) + cd), 16, (threadIdx.x & 63) * 16,
-                                             f.hb[k][part == 2] + cs + (uint32_t)ks * PANEL, 0, 0);
+    constexpr uint32_t cd = k * HPB + q * 3072 + (part < 2 ? part * 1024 : 2048);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(f.rg, (OFR_LDS void*)(uintptr_t)(so + cd), 16, (threadIdx.x & 63) * 16,
+                                             f.gsrc[J] + kso, 0, 0);
   }
   template <int W, int J>
-  static __device__ __forceinline__ void qcopy(const Feed& f, char* smem, int s, int ks) {
+  static __device__ __forceinline__ void qcopy(const Feed& f, uint32_t so, uint32_t kso) {
     constexpr uint32_t o = (W * QPW + J) * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(f.rq, (OFR_LDS void*)(qslot(smem, s) + o), 16, (threadIdx.x & 63) * 16,
-                                             o + (uint32_t)ks * PANEL, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(f.rq, (OFR_LDS void*)(uintptr_t)(so + o), 16, (threadIdx.x & 63) * 16,
+                                             o + kso, 0, 0);
   }
 
-  // gallery fragment: local tile row R0 (a multiple of 16, compile time) of slot st
-  template <int R0>
-  static __device__ __forceinline__ i32x6 fragA(const char* st) {
-    constexpr int k = R0 / 128, rl = R0 % 128;
-    const int lane = threadIdx.x & 63, q = lane >> 4, l = lane & 15;
-    const char* sb = st + k * HPB + q * 3072;
-    const int slot = (rl + l) ^ ((q & 1) << 4);
-    const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 2048 + slot * 8);
-    asm volatile("" : "+v"(p1a));
-    const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + (rl + l) * 16);
-    const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
+  // Fragment reads from per-lane base addresses of a slot plus compile-time offsets (one VALU add per
+  // base and stage; the reads carry the rest in their offset field).  Part1 slots (the p1_slot swizzle)
+  // of a 16-row block m are 16 m + l ^ 16 (q & 1) = 16 (m +- (q & 1)) + l: one base for even, one for
+  // odd m.  Volatile: two part1 reads must not fuse into a ds_read2_b64 (its halves belong to different
+  // fragments and would cost moves).
+  struct Bases {
+    uint32_t p0, p1e, p1o;
+  };
+  static __device__ __forceinline__ Bases abase(uint32_t slot) {   // gallery slot (half-panel images)
+    const uint32_t lane = threadIdx.x & 63, q = lane >> 4, l = lane & 15, qo = (q & 1) << 4;
+    return Bases{slot + q * 3072 + l * 16, slot + q * 3072 + 2048 + (l + qo) * 8, slot + q * 3072 + 2048 + (l - qo) * 8};
+  }
+  static __device__ __forceinline__ Bases bbase(uint32_t slot) {   // query slot (panel image)
+    const uint32_t lane = threadIdx.x & 63, q = lane >> 4, l = lane & 15, qo = (q & 1) << 4;
+    return Bases{slot + q * 6144 + l * 16, slot + q * 6144 + 4096 + (l + qo) * 8, slot + q * 6144 + 4096 + (l - qo) * 8};
+  }
+  static __device__ __forceinline__ i32x6 frag_at(uint32_t a0, uint32_t a1) {
+    const i32x4 p0 = *reinterpret_cast<volatile const OFR_LDS i32x4*>((uintptr_t)a0);
+    const i32x2 p1 = *reinterpret_cast<volatile const OFR_LDS i32x2*>((uintptr_t)a1);
     i32x6 f;
     f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
     return f;
+  }
+  template <int R0>   // gallery rows R0 .. R0 + 15 of the tile (R0 a multiple of 16)
+  static __device__ __forceinline__ i32x6 fragA(const Bases& b) {
+    constexpr int k = R0 / 128, rl = R0 % 128;
+    return frag_at(b.p0 + k * HPB + rl * 16, ((rl >> 4) & 1 ? b.p1o : b.p1e) + k * HPB + rl * 8);
+  }
+  template <int R0>   // query rows R0 .. R0 + 15 of the panel
+  static __device__ __forceinline__ i32x6 fragB(const Bases& b) {
+    return frag_at(b.p0 + R0 * 16, ((R0 >> 4) & 1 ? b.p1o : b.p1e) + R0 * 8);
   }
 
   // The accumulators are pinned by inline asm: 384 registers per lane exceed either register file,
@@ -1029,11 +1047,11 @@ struct EngineW {
     asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
   }
 
-  // MODE (probes): 1 = no copies in the k loop (the prologue's stages re-read), 2 = no MFMAs
+  // MODE (probes): 1 = no copies in the k loop (the prologue's stages re-read), 2 = no MFMAs,
+  // 8 = copies never waited for (wrong results)
   template <int W, int MODE>
-  static __device__ __forceinline__ void mainloop(char* smem, const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
+  static __device__ __forceinline__ void mainloop(const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
     constexpr int WR = W >> 1, WC = W & 1;
-    const int r16 = threadIdx.x & 15;
     int sc = SCALE_ONE;
     asm volatile("" : "+v"(sc));
 #pragma unroll
@@ -1041,35 +1059,37 @@ struct EngineW {
 #pragma unroll
       for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int last = nst - 1;
-    auto cl = [&](int s) { return s < last ? s : last; };
-    auto gall = [&](int s) {
-      gcopy<W, 0>(f, smem, s, cl(s)); gcopy<W, 1>(f, smem, s, cl(s)); gcopy<W, 2>(f, smem, s, cl(s));
-      gcopy<W, 3>(f, smem, s, cl(s)); gcopy<W, 4>(f, smem, s, cl(s)); gcopy<W, 5>(f, smem, s, cl(s));
-      gcopy<W, 6>(f, smem, s, cl(s)); gcopy<W, 7>(f, smem, s, cl(s)); gcopy<W, 8>(f, smem, s, cl(s));
+    auto kso = [&](int s) { return (uint32_t)(s < last ? s : last) * (uint32_t)PANEL; };
+    auto gall = [&](uint32_t so, uint32_t ko) {
+      gcopy<W, 0>(f, so, ko); gcopy<W, 1>(f, so, ko); gcopy<W, 2>(f, so, ko);
+      gcopy<W, 3>(f, so, ko); gcopy<W, 4>(f, so, ko); gcopy<W, 5>(f, so, ko);
+      gcopy<W, 6>(f, so, ko); gcopy<W, 7>(f, so, ko); gcopy<W, 8>(f, so, ko);
     };
-    auto qall = [&](int s) {
-      qcopy<W, 0>(f, smem, s, cl(s)); qcopy<W, 1>(f, smem, s, cl(s)); qcopy<W, 2>(f, smem, s, cl(s));
-      qcopy<W, 3>(f, smem, s, cl(s)); qcopy<W, 4>(f, smem, s, cl(s)); qcopy<W, 5>(f, smem, s, cl(s));
+    auto qall = [&](uint32_t so, uint32_t ko) {
+      qcopy<W, 0>(f, so, ko); qcopy<W, 1>(f, so, ko); qcopy<W, 2>(f, so, ko);
+      qcopy<W, 3>(f, so, ko); qcopy<W, 4>(f, so, ko); qcopy<W, 5>(f, so, ko);
     };
+    // ring slots (LDS byte offsets) of stages s, s + 1, s + 2 (gallery) and s, s + 1 (query)
+    uint32_t g0 = 0, g1 = GSLOT, g2 = 2 * GSLOT, q0 = QBASE, q1 = QBASE + QSLOT;
     // prologue: G(0), Q(0), G(1), Q(1) and pieces 0, 1 of G(2)
-    gall(0); qall(0); gall(1); qall(1);
-    gcopy<W, 0>(f, smem, 2, cl(2));
-    gcopy<W, 1>(f, smem, 2, cl(2));
+    gall(g0, kso(0)); qall(q0, kso(0)); gall(g1, kso(1)); qall(q1, kso(1));
+    gcopy<W, 0>(f, g2, kso(2));
+    gcopy<W, 1>(f, g2, kso(2));
     wait_vm<GPW + QPW + 2>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     i32x6 a[RING], b[NB];
     {
-      const char* g0 = gslot(smem, 0);
-      a[0] = fragA<WR * 192 + 0>(g0);
-      a[1] = fragA<WR * 192 + 16>(g0);
-#pragma unroll
-      for (int c = 0; c < NB; ++c) b[c] = Engine16::frag16(qslot(smem, 0), WC * 128 + c * 16 + r16);
+      const Bases ab = abase(g0), bb = bbase(q0);
+      a[0] = fragA<WR * 192 + 0>(ab);
+      a[1] = fragA<WR * 192 + 16>(ab);
+      b[0] = fragB<WC * 128 + 0>(bb); b[1] = fragB<WC * 128 + 16>(bb); b[2] = fragB<WC * 128 + 32>(bb);
+      b[3] = fragB<WC * 128 + 48>(bb); b[4] = fragB<WC * 128 + 64>(bb); b[5] = fragB<WC * 128 + 80>(bb);
+      b[6] = fragB<WC * 128 + 96>(bb); b[7] = fragB<WC * 128 + 112>(bb);
     }
     for (int s = 0; s <= last; ++s) {
-      const char* gc = gslot(smem, s);
-      const char* gn = gslot(smem, s + 1);
-      const char* qn = qslot(smem, s + 1);
+      const Bases ac = abase(g0), an = abase(g1), bn = bbase(q1);
+      const uint32_t k2 = kso(s + 2), k3 = kso(s + 3);
       auto row = [&](auto ii) {
         constexpr int i = decltype(ii)::value;
         constexpr bool AG = i < NAA;
@@ -1082,26 +1102,29 @@ struct EngineW {
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (i == 10) {             // barrier B: G(s+1), Q(s+1) landed; G(s) consumed
-          if constexpr ((MODE & 1) == 0) wait_vm<GPW + QPW>();
+          if constexpr ((MODE & 9) == 0) wait_vm<GPW + QPW>();
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr ((MODE & 1) == 0) {
-          if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(f, smem, s + 2, cl(s + 2));
-          if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(f, smem, s + 2, cl(s + 2));
-          if constexpr (i >= 10) gcopy<W, (i >= 10 ? i - 10 : 0)>(f, smem, s + 3, cl(s + 3));
+          // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0), G(s+3) into G(s)'s (g0)
+          if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(f, g2, k2);
+          if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(f, q0, k2);
+          if constexpr (i >= 10) gcopy<W, (i >= 10 ? i - 10 : 0)>(f, g0, k3);
         }
         mm(a[i % RING], b[0], acc[i][0]);
-        if constexpr (i + 2 < NA) a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? i + 2 : 0) * 16>(gc);
-        else a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? 0 : i + 2 - NA) * 16>(gn);
+        if constexpr (i + 2 < NA) a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? i + 2 : 0) * 16>(ac);
+        else a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? 0 : i + 2 - NA) * 16>(an);
         if constexpr (i == NA - 1) {
-#pragma unroll
-          for (int c = 1; c < NB; ++c) {
-            mm(a[i % RING], b[c], acc[i][c]);
-            b[c - 1] = Engine16::frag16(qn, WC * 128 + (c - 1) * 16 + r16);
-          }
-          b[NB - 1] = Engine16::frag16(qn, WC * 128 + (NB - 1) * 16 + r16);
+          mm(a[i % RING], b[1], acc[i][1]); b[0] = fragB<WC * 128 + 0>(bn);
+          mm(a[i % RING], b[2], acc[i][2]); b[1] = fragB<WC * 128 + 16>(bn);
+          mm(a[i % RING], b[3], acc[i][3]); b[2] = fragB<WC * 128 + 32>(bn);
+          mm(a[i % RING], b[4], acc[i][4]); b[3] = fragB<WC * 128 + 48>(bn);
+          mm(a[i % RING], b[5], acc[i][5]); b[4] = fragB<WC * 128 + 64>(bn);
+          mm(a[i % RING], b[6], acc[i][6]); b[5] = fragB<WC * 128 + 80>(bn);
+          mm(a[i % RING], b[7], acc[i][7]); b[6] = fragB<WC * 128 + 96>(bn);
+          b[7] = fragB<WC * 128 + 112>(bn);
         } else {
 #pragma unroll
           for (int c = 1; c < NB; ++c) mm(a[i % RING], b[c], acc[i][c]);
@@ -1120,6 +1143,10 @@ struct EngineW {
       row(std::integral_constant<int, 9>{});
       row(std::integral_constant<int, 10>{});
       row(std::integral_constant<int, 11>{});
+      const uint32_t gt_ = g0;   // rotate: s+1 -> current, s+2 -> next, s (now re-filled with s+3) -> s+2's
+      g0 = g1; g1 = g2; g2 = gt_;
+      const uint32_t qt_ = q0;
+      q0 = q1; q1 = qt_;
     }
     wait_vm<0>();
     wait_drain();

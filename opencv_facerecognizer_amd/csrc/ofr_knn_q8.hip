@@ -365,25 +365,37 @@ __device__ __forceinline__ void sieve_epilogue16(char* smem, const TileArgs& p, 
   }
   if (threadIdx.x == 0) *nhit = 0;
   __syncthreads();
+  // per row block the lane's 16 compares first (branch-free), then one wave-wide test: a block holds
+  // ~1 kept pair per wave on gallery data, so most blocks skip the staging (f6w_body, round 3)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int gl0 = wr * 128 + i * 16 + g4;        // this lane's 4 consecutive gallery rows
     const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
     const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
     const float av[4] = {t0.x, t0.z, t1.x, t1.z}, sv[4] = {t0.y, t0.w, t1.y, t1.w};
+    float sc[4][4];
+    uint32_t m = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gl = gl0 + r;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float sc = av[r] - sq2[c] * sv[r] * acc[i][c][r];
-        if (!(sc > th[c]) && gl < nvalid) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
-          const int ql = wc * E::QW + c * 16 + r16;
-          const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
-          const uint32_t slot = atomicAdd(nhit, 1u);
-          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)gl);
-        }
+        sc[r][c] = av[r] - sq2[c] * sv[r] * acc[i][c][r];
+        m |= (!(sc[r][c] > th[c]) && gl0 + r < nvalid) ? 1u << (r * 4 + c) : 0u;
       }
+    if (__builtin_amdgcn_ballot_w64(m != 0) == 0) continue;   // uniform
+    while (m) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
+      const int b = __builtin_ctz(m);
+      m &= m - 1;
+      const int r = b >> 2, c = b & 3;
+      float v = sc[0][0];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) v = (rr * 4 + cc == b) ? sc[rr][cc] : v;
+      const int ql = wc * E::QW + c * 16 + r16;
+      const uint32_t kb = __float_as_uint(key_score(score_key(v, 0)));
+      const uint32_t slot = atomicAdd(nhit, 1u);
+      if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)(gl0 + r));
     }
   }
   __syncthreads();
@@ -524,12 +536,14 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
 // WC*128 + 16 c + l % 16.  MODE probe bits: 1 / 2 = no copies / no MFMAs in the k loop, 4 = no
 // epilogue (the accumulators kept alive).
 template <int W, int MODE>
-__device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, const f6t::EngineW::Feed& f, int64_t g0,
-                                         int64_t q0) {
+__device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
   using E = f6t::EngineW;
   f6t::f32x4 acc[E::NA][E::NB];
   constexpr int WR = W >> 1;
-  E::mainloop<W, MODE & 3>(smem, f, p.nk, acc);
+  E::Feed f;
+  E::feed_init<W>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ, p.nk,
+                  g0 / E::TGW);
+  E::mainloop<W, MODE & 11>(f, p.nk, acc);
   float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
   uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
   uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [SIEVE_HCAP]
@@ -562,25 +576,47 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, const f6
     __syncthreads();
     return;
   }
+  // Per row block: the lane's 32 coarse scores sc = fma(-(sq2 sv), acc, a) in packed pairs (two rows
+  // of one query per v_pk_fma_f32), per query column the min over the 4 rows, one v_cmp_ngt per column
+  // (NaN th, "keep every row", passes) and a wave-wide OR: a block holds ~1 kept pair per wave on
+  // gallery data, so most blocks skip the staging.  A block that passes re-tests its 32 scores exactly
+  // (the padding rows, a = +inf, pass only a NaN th and are excluded there).
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int i = 0; i < E::NA; ++i) {
     const int gl0 = WR * 192 + i * 16 + g4;        // this lane's 4 consecutive gallery rows
     const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
     const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
-    const float av[4] = {t0.x, t0.z, t1.x, t1.z}, sv[4] = {t0.y, t0.w, t1.y, t1.w};
+    const f32x2 avp[2] = {f32x2{t0.x, t0.z}, f32x2{t1.x, t1.z}}, svp[2] = {f32x2{t0.y, t0.w}, f32x2{t1.y, t1.w}};
+    float sc[4][E::NB];
+    uint64_t col[E::NB];   // per query column: the lanes with a candidate hit (wave-uniform)
+    uint64_t any = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gl = gl0 + r;
+    for (int c = 0; c < E::NB; ++c) {
 #pragma unroll
-      for (int c = 0; c < E::NB; ++c) {
-        const float sc = av[r] - sq2[c] * sv[r] * acc[i][c][r];
-        if (!(sc > th[c]) && gl < nvalid) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
-          const int ql = wc * 128 + c * 16 + r16;
-          const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
-          const uint32_t slot = atomicAdd(nhit, 1u);
-          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)gl);
-        }
+      for (int rp = 0; rp < 2; ++rp) {
+        const f32x2 t = svp[rp] * sq2[c];
+        const f32x2 x = __builtin_elementwise_fma(-t, f32x2{acc[i][c][2 * rp], acc[i][c][2 * rp + 1]}, avp[rp]);
+        sc[2 * rp][c] = x.x;
+        sc[2 * rp + 1][c] = x.y;
       }
+      const float mn = fminf(fminf(sc[0][c], sc[1][c]), fminf(sc[2][c], sc[3][c]));
+      col[c] = __builtin_amdgcn_ballot_w64(!(mn > th[c]));
+      any |= col[c];
+    }
+    if (any == 0) continue;   // uniform
+    // ~2 kept pairs per block on gallery data, in one or two query columns: only those are examined
+#pragma unroll
+    for (int c = 0; c < E::NB; ++c) {
+      if (col[c] == 0) continue;   // uniform
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!(sc[r][c] > th[c]) && gl0 + r < nvalid) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
+          const int ql = wc * 128 + c * 16 + r16;
+          const uint32_t kb = __float_as_uint(key_score(score_key(sc[r][c], 0)));
+          const uint32_t slot = atomicAdd(nhit, 1u);
+          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
+        }
     }
   }
   __syncthreads();
@@ -595,13 +631,11 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   int64_t gt, qt;
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
   const int64_t g0 = gt * E::TGW, q0 = qt * f6t::TQ;
-  E::Feed f;
-  E::feed_init(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), qt, p.nk, gt);
   switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
-    case 0: f6w_body<0, MODE>(smem, p, f, g0, q0); break;
-    case 1: f6w_body<1, MODE>(smem, p, f, g0, q0); break;
-    case 2: f6w_body<2, MODE>(smem, p, f, g0, q0); break;
-    default: f6w_body<3, MODE>(smem, p, f, g0, q0); break;
+    case 0: f6w_body<0, MODE>(smem, p, g0, q0); break;
+    case 1: f6w_body<1, MODE>(smem, p, g0, q0); break;
+    case 2: f6w_body<2, MODE>(smem, p, g0, q0); break;
+    default: f6w_body<3, MODE>(smem, p, g0, q0); break;
   }
 }
 
@@ -1466,15 +1500,15 @@ extern "C" const char* ofr_f6_sieve_kernel(void) {
   return names[f6_shape() == 16 ? 0 : (f6_shape() == 32 ? 1 : 2)].c_str();
 }
 
-// Engine of the sieve pass: 16 = v_mfma_scale_f32_16x16x128 on 256 x 256 tiles, 8 waves
-// (f6t::Engine16, default), 32 = the 32x32x64 engine (OFR_F6_SHAPE=32), 384 = the 16x16x128 engine on
-// 384 x 256 tiles, one wave per SIMD (f6t::EngineW, OFR_F6_SHAPE=384; one segment: the two-slice tier
-// keeps Engine16)
+// Engine of the sieve pass: 384 = v_mfma_scale_f32_16x16x128 on 384 x 256 tiles, one wave per SIMD
+// (f6t::EngineW, default since round 3: 22.2 -> 20.1 ms, tools/f6_probe.hip WIDE); 16 = the same MFMA on
+// 256 x 256 tiles, 8 waves (f6t::Engine16, OFR_F6_SHAPE=16; also the two-slice tier's engine); 32 = the
+// 32x32x64 engine (OFR_F6_SHAPE=32)
 static int f6_shape() {
   static const int s = [] {
     const char* e = getenv("OFR_F6_SHAPE");
     const int v = e ? atoi(e) : 0;
-    return v == 32 || v == 384 ? v : 16;
+    return v == 32 || v == 16 ? v : 384;
   }();
   return s;
 }
@@ -1536,7 +1570,8 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
                           int64_t d, const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                           int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
                           void* workspace, size_t workspace_bytes) {
-  OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_f6: phases must be 1 (tiles), 2 (merge) or 3");
+  OFR_CHECK_ARG(phases >= 1 && phases <= 15,
+                "ofr_knn_f6: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
                      out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr);
 }
@@ -1546,7 +1581,8 @@ extern "C" int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B,
                             int64_t ldg, int64_t d, const void* Gt, const void* Gt2, const float* gscale,
                             const float* aux, const double* gmax, int k, int64_t index_base, double* out_d,
                             int64_t* out_i, int* cert, double* bound, void* workspace, size_t workspace_bytes) {
-  OFR_CHECK_ARG(phases >= 1 && phases <= 3, "ofr_knn_f6x2: phases must be 1 (tiles), 2 (merge) or 3");
+  OFR_CHECK_ARG(phases >= 1 && phases <= 15,
+                "ofr_knn_f6x2: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
   OFR_CHECK_ARG(Qt2 && Gt2, "ofr_knn_f6x2: null second-slice tiles");
   if (B >= 1 && B <= 32) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6x2: needs more than 32 queries (the sieve pass)");
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
@@ -1601,10 +1637,13 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   int* count = reinterpret_cast<int*>(wsb + w.count);
   Cand* bucket = reinterpret_cast<Cand*>(wsb + w.bucket);
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
-  if (phases & 1) {
+  if (phases & 1) phases |= 12;   // phase 1 = sample + thresholds (4), then the sieve (8)
+  if (phases & 12) {
     if (!sieve) {   // HBM regime: one 32-query block, gallery streamed straight to VGPRs
-      hipLaunchKernelGGL((q8s::stream_kernel_f6<q8s::SU, true>), dim3((unsigned)a.ntg), dim3(512), 0, st, a);
-      OFR_LAUNCH_CHECK("f6 stream_kernel");
+      if (phases & 4) {
+        hipLaunchKernelGGL((q8s::stream_kernel_f6<q8s::SU, true>), dim3((unsigned)a.ntg), dim3(512), 0, st, a);
+        OFR_LAUNCH_CHECK("f6 stream_kernel");
+      }
     } else {
       static bool attr_done = false;
       if (!attr_done) {
@@ -1626,21 +1665,27 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       s.ntg = cdiv(a.ntg, s.gstride);
       s.gg = s.ntg < q8s::GROUP_G ? s.ntg : q8s::GROUP_G;
       s.cand = reinterpret_cast<Cand*>(wsb + w.lists);
-      if (two)
+      if (!(phases & 4)) {
+        // sieve only: the thresholds of a preceding phases-4 call are in the workspace
+      } else if (two)
         hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0, 3>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
                            f6t::LDS, st, s);
       else
         hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
                            f6t::LDS, st, s);
-      OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
-      hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, s.cand, s.ntg,
-                         theta, count, B);
-      OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
+      if (phases & 4) {
+        OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
+        hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, s.cand, s.ntg,
+                           theta, count, B);
+        OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
+      }
       a.theta = theta;
       a.count = count;
       a.bucket = bucket;
       a.cap = q8s::SIEVE_CAP;
-      if (f6_shape() == 384 && !two) {
+      if (!(phases & 8)) {
+        // sample + thresholds only
+      } else if (f6_shape() == 384 && !two) {
         q8s::TileArgs wa = a;   // 384-row gallery tiles over the same 256-row panel layout
         wa.ntg = cdiv(N, f6t::EngineW::TGW);
         wa.gg = wa.ntg < q8s::GROUP_G ? wa.ntg : q8s::GROUP_G;

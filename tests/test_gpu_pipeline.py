@@ -1,7 +1,7 @@
 """bench.py's StepPipeline (the timed step's schedule): the tile pass of batch s on the
-main stream, batch s+1's preparation and batch s's merge on a side stream, batch s-1's certificate
-read and fallback tiers enqueued before batch s+1's preparation, three query buffers and two search
-workspaces.  Every batch's final top-k must equal the one-shot search of the same batch
+main stream (sample pass, then sieve pass), batch s-1's merge on a side stream behind sample pass s,
+batch s+1's preparation behind tile pass s, batch s-1's certificate read and fallback tiers enqueued
+before batch s+1's preparation, three query buffers and two search workspaces.  Every batch's final top-k must equal the one-shot search of the same batch
 (quantize, ofr_knn_f6 phases 1+2, fallback tiers) on the default stream -- bit for bit: the schedule
 changes only which stream runs a kernel and which buffer it reads."""
 import os
@@ -64,8 +64,8 @@ def test_step_pipeline_matches_one_shot(noise):
         P.project(X[s], shift64=g.shift64, out=bufs[j]["Qd"])
         bufs[j]["qq"] = g.quantize_queries(bufs[j]["Qd"], bufs[j]["qq"], tier="f6")
 
-    def tiles(j, w):
-        g.search_q8_phase(1, bufs[j]["Qd"], bufs[j]["qq"], k, workspace=w)
+    def tiles(j, w, part):
+        g.search_q8_phase(4 if part == "sample" else 8, bufs[j]["Qd"], bufs[j]["qq"], k, workspace=w)
 
     def merge(j, w):
         g.search_q8_phase(2, bufs[j]["Qd"], bufs[j]["qq"], k, out=bufs[j]["out"], workspace=w)

@@ -260,6 +260,7 @@ template <int MODE>
 static int runw(q8s::TileArgs a, int reps, const char* tag) {
   using E = f6t::EngineW;
   a.ntg = (a.N + E::TGW - 1) / E::TGW;
+  if (a.gg > a.ntg) a.gg = a.ntg;
   const double ops = 2.0 * (double)a.N * a.ntq * f6t::TQ * a.nk * f6t::BK;
   CK(hipFuncSetAttribute((const void*)q8s::tile_kernel_f6w<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, E::LDS_BYTES));
   hipEvent_t e0, e1;
@@ -371,12 +372,22 @@ int main(int argc, char** argv) {
         return 1;
     return 0;
   }
+  if (getenv("WIDE_DEPTH")) {   // per-tile fixed cost: the wide pass at this d (time = rounds x (fixed + nst x stage))
+    a.gg = 4 < ntg ? 4 : ntg;
+    for (int rep = 0; rep < 2; ++rep)
+      if (runw<0>(a, reps, "wide") || runw<4>(a, reps, "wide-noepi")) return 1;
+    return 0;
+  }
   if (getenv("WIDE")) {   // the 384 x 256 one-wave-per-SIMD engine (f6t::EngineW) vs the library pass
     a.gg = 4 < ntg ? 4 : ntg;
     for (int rep = 0; rep < 2; ++rep)
       if (run16<275456>(a, reps, "lib4w") || run16<275456 + 4>(a, reps, "lib4w-noepi") || runw<0>(a, reps, "wide") ||
-          runw<4>(a, reps, "wide-noepi") || runw<5>(a, reps, "wide-nocopy") || runw<7>(a, reps, "wide-nomfma"))
+          runw<4>(a, reps, "wide-noepi") || runw<5>(a, reps, "wide-nocopy"))
         return 1;
+    for (int g : {2, 4, 8}) {
+      a.gg = g;
+      if (runw<0>(a, reps, "wide-gg")) return 1;
+    }
     return 0;
   }
   if (getenv("GGDMA")) {   // the DMA-only variant and the 4-issuing-wave pass against the tile-group width
