@@ -51,11 +51,6 @@ PEAK_F6_MFMA = 10.0e15      # fp6 (block-scaled f8f6f4 MFMA): ~10 PF dense, the 
 # operands in registers, at the clock it holds under that load (tools/f6_shape_probe.hip,
 # profiles/r02_f6_shape_probe.log): the ceiling of any fp6 kernel on this part
 SUSTAINED_F6_MFMA = 6.28e15
-# The sieve pass's stage copies by themselves (no MFMAs, no fragment reads; the library's copy protocol)
-# move 3,907 x 16 tiles x 79 stages x 48 KiB = 242.7 GB in 11.8 ms = 20.6 TB/s (81 GB/s per CU;
-# tools/f6_probe.hip FEEDTEST dma-only, profiles/r03_f6_probe_feedtest.log).  The pass reaches a fraction
-# of that: the copies' and reads' issue serialises with the MFMAs, reported as roofline.feed.
-F6_DMA_CEILING_BPS = 20.6e12
 PEAK_HBM = 8.0e12           # HBM3E 8 TB/s (spec)
 
 
@@ -209,8 +204,8 @@ class StepPipeline:
 
     def run(self, steps, events=None):
         """Exactly `steps` preparations, tile passes, merges and fallbacks; returns the last batch's
-        result.  events[s]: 6 timing events (prep start/end on the side stream, tile pass end and start
-        on the main stream, merge end and start on the side stream)."""
+        result.  events[s]: 7 timing events (prep start/end on the side stream, tile pass end and start
+        on the main stream, merge end and start on the side stream, sample pass end on the main stream)."""
         ev = events or [None] * steps
         res = None
         self._prep(0, ev[0])
@@ -222,6 +217,8 @@ class StepPipeline:
                 ev[s][4].record(self.main)
             self.tiles_fn(j, self.ws[w], "sample")
             self.ev_sample.record(self.main)
+            if ev[s]:
+                ev[s][6].record(self.main)
             if s >= 1:                                      # merge s-1 under sieve pass s
                 self._merge(s - 1, ev[s - 1])
             self.tiles_fn(j, self.ws[w], "sieve")
@@ -365,7 +362,7 @@ def main():
     torch.cuda.synchronize()
     log(rank, f"setup {time.perf_counter() - t0:.1f}s: gallery rows {nl}/{N} per rank, d={d}, D={D}, B={B}")
 
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(7)] for _ in range(args.steps)]
     use_q8 = args.search in ("f6", "q8")
     tier0 = "f6" if args.search == "f6" else 1
     if use_q8:
@@ -460,6 +457,8 @@ def main():
 
     ms_proj = np.mean([e[0].elapsed_time(e[1]) for e in ev])
     ms_tiles = np.mean([e[4].elapsed_time(e[2]) for e in ev])     # the tile pass on the main stream
+    ms_sample = np.mean([e[4].elapsed_time(e[6]) for e in ev])    # its sample pass + thresholds
+    ms_sieve = np.mean([e[6].elapsed_time(e[2]) for e in ev])     # its sieve pass (fp6; else the rest)
     ms_merge = np.mean([e[5].elapsed_time(e[3]) for e in ev])     # merge + certificate on the side stream
     idx = res[1][:, 0]
     acc = float(((idx // args.per_id) == ids_q).double().mean().item())
@@ -523,12 +522,16 @@ def main():
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
     if args.search == "f6":
-        sieve = _lib.load().ofr_f6_sieve_kernel().decode() + " sieve pass"     # the variant the library launches
-        peak, kname = PEAK_F6_MFMA, ("ofr_knn_f6 phase 1 (fp6 e2m3): q8s::tile_kernel_f6<8, 0> sample pass + "
-                                     "sieve_threshold_kernel + " + sieve)
+        # the dominant kernel is the sieve pass: it alone does all 2 B N d of the algorithmic work (the
+        # sample pass before it re-does 1/64 of it to set the thresholds); its launch is timed by its own
+        # events on the main stream, phase 1 (sample + thresholds + sieve) is reported beside it
+        sieve = _lib.load().ofr_f6_sieve_kernel().decode()                    # the variant the library launches
+        peak, kname = PEAK_F6_MFMA, "ofr_knn_f6 sieve pass (fp6 e2m3): " + sieve
+        achieved = flops_tiles / (ms_sieve * 1e-3)
         alg_bytes_tiles = 0.75 * (nl * d + B * d)                    # 6 bits per feature, gallery + queries
         ntg_, ntq_, nst_ = -(-nl // 256), -(-B // 256), -(-d // 128)
-        fed = (ntg_ + -(-ntg_ // 64)) * ntq_ * nst_ * 49152.0         # sieve pass + sample pass (every 64th panel)
+        wide = "f6w" in sieve                                        # 384 x 256 tiles: 60 KiB per stage
+        fed = (-(-nl // 384) * 61440.0 if wide else ntg_ * 49152.0) * ntq_ * nst_   # copied into LDS per sieve pass
         executed = flops_tiles
     elif use_q8:
         peak, kname = PEAK_I8_MFMA, "q8s::tile_kernel<1> (ofr_knn_q8 phase 1, one int8 slice)"
@@ -560,19 +563,20 @@ def main():
             "roofline": {"kernel": kname, "bound": "mfma",
                          "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s" if not use_q8 else "TOPS",
                          "frac": achieved / peak, "traffic": tr[0] if tr else None,
-                         "executed_ops_per_launch": executed, "executed_frac": executed / (ms_tiles * 1e-3) / peak,
+                         "executed_ops_per_launch": executed,
+                         "executed_frac": executed / ((ms_sieve if args.search == "f6" else ms_tiles) * 1e-3) / peak,
                          "traffic_source": tr[1] if tr else None,
                          "algorithmic_flops_per_launch": flops_tiles, "algorithmic_bytes_per_launch": alg_bytes_tiles,
-                         "launch_ms": ms_tiles,
-                         **({"sustained_peak": SUSTAINED_F6_MFMA / 1e12, "frac_of_sustained": achieved / SUSTAINED_F6_MFMA,
+                         "launch_ms": ms_sieve if args.search == "f6" else ms_tiles,
+                         **({"phase1": {"what": "sample pass + thresholds + sieve pass (events on the main stream)",
+                                        "ms": ms_tiles, "sample_ms": ms_sample,
+                                        "frac": flops_tiles / (ms_tiles * 1e-3) / peak},
+                             "sustained_peak": SUSTAINED_F6_MFMA / 1e12, "frac_of_sustained": achieved / SUSTAINED_F6_MFMA,
                              "sustained_source": "tools/f6_shape_probe.hip (profiles/r02_f6_shape_probe.log)",
-                             "feed": {"what": "bytes copied into the CUs' LDS by the sample + sieve passes (48 KiB per "
-                                              "256x256x128 stage)", "bytes_per_launch": fed,
-                                      "achieved_TBps": fed / (ms_tiles * 1e-3) / 1e12,
-                                      "ceiling_TBps": F6_DMA_CEILING_BPS / 1e12,
-                                      "frac": fed / (ms_tiles * 1e-3) / F6_DMA_CEILING_BPS,
-                                      "ceiling_source": "the copies alone: tools/f6_probe.hip FEEDTEST dma-only "
-                                                        "(profiles/r03_f6_probe_feedtest.log)"}}
+                             "feed": {"what": "bytes copied into the CUs' LDS by the sieve pass (60 KiB per 384x256x128 "
+                                              "stage; 48 KiB per 256x256x128 stage on the 8-wave engine)",
+                                      "bytes_per_launch": fed,
+                                      "achieved_TBps": fed / (ms_sieve * 1e-3) / 1e12}}
                             if args.search == "f6" else {})},
             "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else "") + ("+all_gather" if shard_prep else ""):
                            ms_proj, "knn_tiles": ms_tiles,

@@ -1097,7 +1097,8 @@ struct EngineW {
           if constexpr ((MODE & 2) == 0) mfma<AG>(x, y, c, sc);
         };
         if constexpr (i == 1) {              // barrier A: Q(s) consumed by every wave
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          // Q(s)'s reads (row 11 of s - 1) are older than row 0's gallery read, the only one allowed in flight
+          asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -1111,21 +1112,29 @@ struct EngineW {
           // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0), G(s+3) into G(s)'s (g0)
           if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(f, g2, k2);
           if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(f, q0, k2);
-          if constexpr (i >= 10) gcopy<W, (i >= 10 ? i - 10 : 0)>(f, g0, k3);
+          if constexpr (i == 10) gcopy<W, 0>(f, g0, k3);   // piece 1: in the middle of rows 10 / 11
         }
-        mm(a[i % RING], b[0], acc[i][0]);
-        if constexpr (i + 2 < NA) a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? i + 2 : 0) * 16>(ac);
-        else a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? 0 : i + 2 - NA) * 16>(an);
         if constexpr (i == NA - 1) {
-          mm(a[i % RING], b[1], acc[i][1]); b[0] = fragB<WC * 128 + 0>(bn);
-          mm(a[i % RING], b[2], acc[i][2]); b[1] = fragB<WC * 128 + 16>(bn);
-          mm(a[i % RING], b[3], acc[i][3]); b[2] = fragB<WC * 128 + 32>(bn);
-          mm(a[i % RING], b[4], acc[i][4]); b[3] = fragB<WC * 128 + 48>(bn);
-          mm(a[i % RING], b[5], acc[i][5]); b[4] = fragB<WC * 128 + 64>(bn);
-          mm(a[i % RING], b[6], acc[i][6]); b[5] = fragB<WC * 128 + 80>(bn);
-          mm(a[i % RING], b[7], acc[i][7]); b[6] = fragB<WC * 128 + 96>(bn);
-          b[7] = fragB<WC * 128 + 112>(bn);
+          // rows 10 and 11 run together (below, i == 10)
+        } else if constexpr (i == NA - 2) {
+          // Rows 10 and 11 column by column, each query fragment refilled for s + 1 after its last use:
+          // b[c] then has 15 - c MFMAs before its first use in row 0 of s + 1 (row-major: 7).  Gallery
+          // ring: s + 1's A[0] into A[9]'s slot now, its A[1] into A[10]'s after the last pair.
+          static_assert(NA % RING == 0 && (NA - 2) % RING == 1, "ring slots of rows 10 / 11");
+          a[0] = fragA<WR * 192 + 0>(an);
+          mm(a[1], b[0], acc[10][0]); mm(a[2], b[0], acc[11][0]); b[0] = fragB<WC * 128 + 0>(bn);
+          mm(a[1], b[1], acc[10][1]); mm(a[2], b[1], acc[11][1]); b[1] = fragB<WC * 128 + 16>(bn);
+          mm(a[1], b[2], acc[10][2]); mm(a[2], b[2], acc[11][2]); b[2] = fragB<WC * 128 + 32>(bn);
+          mm(a[1], b[3], acc[10][3]); mm(a[2], b[3], acc[11][3]); b[3] = fragB<WC * 128 + 48>(bn);
+          if constexpr ((MODE & 1) == 0) gcopy<W, 1>(f, g0, k3);
+          mm(a[1], b[4], acc[10][4]); mm(a[2], b[4], acc[11][4]); b[4] = fragB<WC * 128 + 64>(bn);
+          mm(a[1], b[5], acc[10][5]); mm(a[2], b[5], acc[11][5]); b[5] = fragB<WC * 128 + 80>(bn);
+          mm(a[1], b[6], acc[10][6]); mm(a[2], b[6], acc[11][6]); b[6] = fragB<WC * 128 + 96>(bn);
+          mm(a[1], b[7], acc[10][7]); mm(a[2], b[7], acc[11][7]); b[7] = fragB<WC * 128 + 112>(bn);
+          a[1] = fragA<WR * 192 + 16>(an);
         } else {
+          mm(a[i % RING], b[0], acc[i][0]);
+          a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? i + 2 : 0) * 16>(ac);
 #pragma unroll
           for (int c = 1; c < NB; ++c) mm(a[i % RING], b[c], acc[i][c]);
         }

@@ -181,7 +181,7 @@ constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
 // query block of this lane (th = key_float(theta | 0xff): truncated key <= theta  <=>
 // !(score > th); NaN for KEY_NONE keeps every row).  More than SIEVE_HCAP hits in one tile push
 // every query of the tile past its bucket cap (uncertified, no candidates read by the merge).
-template <int TQ, int GB = 8, int TGR = TG>
+template <int TQ, int GB = 8, int TGR = TG, int HCAP = SIEVE_HCAP>
 __device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64_t g0, int64_t q0);
 
 template <int CT, int TQ, int QW, int WQ, class CV>
@@ -237,13 +237,13 @@ __device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, in
 
 // The tile's staged hits -> per-query buckets (after the compares and a barrier).  A hit packs
 // (tile query << GB) | tile gallery row; TGR gallery rows per tile (the staging area follows their
-// [TGR][2] operand table).
-template <int TQ, int GB, int TGR>
+// [TGR][2] operand table), HCAP staging slots.
+template <int TQ, int GB, int TGR, int HCAP>
 __device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
   const uint32_t* nhit = reinterpret_cast<const uint32_t*>(smem + TGR * 8);
   const uint2* hits = reinterpret_cast<const uint2*>(smem + TGR * 8 + 16);
   const uint32_t nh = *nhit;
-  if (nh > (uint32_t)SIEVE_HCAP) {   // hits lost: push every query of the tile past its cap (uncertified)
+  if (nh > (uint32_t)HCAP) {   // hits lost: push every query of the tile past its cap (uncertified)
     // saturating (max, not add): any number of overflowing tiles leaves the count at cap + 1 plus
     // at most one increment per gallery row, which the host bounds below 2^31 (ofr_knn_f6)
     if ((int)threadIdx.x < TQ && q0 + threadIdx.x < p.B) atomicMax(p.count + q0 + threadIdx.x, (int)p.cap + 1);
@@ -546,7 +546,10 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
   E::mainloop<W, MODE & 11>(f, p.nk, acc);
   float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
   uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
-  uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [SIEVE_HCAP]
+  uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [HCAPW]
+  // 2x SIEVE_HCAP: a 384-row tile collects 1.5x the hits of a 256-row one (loose thresholds, small d)
+  constexpr int HCAPW = 2 * SIEVE_HCAP;
+  static_assert(E::TGW * 8 + 16 + HCAPW * 8 <= E::LDS_BYTES, "hit staging fits the ring's LDS");
   const int nvalid = p.N - g0 < E::TGW ? (int)(p.N - g0) : E::TGW;
   for (int r = threadIdx.x; r < E::TGW; r += E::NT) {
     const bool ok = r < nvalid;
@@ -615,12 +618,12 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
           const int ql = wc * 128 + c * 16 + r16;
           const uint32_t kb = __float_as_uint(key_score(score_key(sc[r][c], 0)));
           const uint32_t slot = atomicAdd(nhit, 1u);
-          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
+          if (slot < (uint32_t)HCAPW) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
         }
     }
   }
   __syncthreads();
-  sieve_flush<f6t::TQ, 9, E::TGW>(smem, p, g0, q0);
+  sieve_flush<f6t::TQ, 9, E::TGW, HCAPW>(smem, p, g0, q0);
 }
 
 template <int MODE>
