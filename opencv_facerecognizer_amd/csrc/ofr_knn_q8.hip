@@ -531,25 +531,20 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
 }
 
 // fp6 sieve pass on the wide engine (f6t::EngineW): 384 gallery x 256 query tiles, 4 waves (one per
-// SIMD), p.ntg = ceil(N / 384) gallery tiles.  The epilogue is sieve_epilogue16's for the 192 x 128
-// wave tile: element r of acc[i][c] of lane l is gallery row WR*192 + 16 i + 4 (l / 16) + r, query
-// WC*128 + 16 c + l % 16.  MODE probe bits: 1 / 2 = no copies / no MFMAs in the k loop, 4 = no
-// epilogue (the accumulators kept alive).
+// SIMD), p.ntg = ceil(N / 384) gallery tiles.  Epilogue of wave W for the 192 x 128 wave tile: element r
+// of acc[i][c] of lane l is gallery row WR*192 + 16 i + 4 (l / 16) + r, query WC*128 + 16 c + l % 16.
+// LDS: the [384][2] operand table at `tab`, the hit count at tab + 3072, HCAP hit slots at `stage`; hits
+// past HCAP go straight to their query's bucket (one global atomic each) instead of the staging.
+// MODE probe bit 4 = no epilogue (the accumulators kept alive).
 template <int W, int MODE>
-__device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
+__device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int64_t g0, int64_t q0,
+                                             f6t::f32x4 (&acc)[f6t::EngineW::NA][f6t::EngineW::NB], uint32_t tab,
+                                             uint32_t stage, int hcap) {
   using E = f6t::EngineW;
-  f6t::f32x4 acc[E::NA][E::NB];
   constexpr int WR = W >> 1;
-  E::Feed f;
-  E::feed_init<W>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ, p.nk,
-                  g0 / E::TGW);
-  E::mainloop<W, MODE & 11>(f, p.nk, acc);
-  float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
-  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
-  uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [HCAPW]
-  // 2x SIEVE_HCAP: a 384-row tile collects 1.5x the hits of a 256-row one (loose thresholds, small d)
-  constexpr int HCAPW = 2 * SIEVE_HCAP;
-  static_assert(E::TGW * 8 + 16 + HCAPW * 8 <= E::LDS_BYTES, "hit staging fits the ring's LDS");
+  float* gtab = reinterpret_cast<float*>(smem + tab);                              // [384][2]
+  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + tab + E::TGW * 8);
+  uint2* hits = reinterpret_cast<uint2*>(smem + stage);                           // [hcap]
   const int nvalid = p.N - g0 < E::TGW ? (int)(p.N - g0) : E::TGW;
   for (int r = threadIdx.x; r < E::TGW; r += E::NT) {
     const bool ok = r < nvalid;
@@ -618,12 +613,42 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
           const int ql = wc * 128 + c * 16 + r16;
           const uint32_t kb = __float_as_uint(key_score(score_key(sc[r][c], 0)));
           const uint32_t slot = atomicAdd(nhit, 1u);
-          if (slot < (uint32_t)HCAPW) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
+          if (slot < (uint32_t)hcap) {
+            hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
+          } else if (q0 + ql < p.B) {   // staging full: straight to the query's bucket
+            const int64_t q = q0 + ql;
+            const int bs = atomicAdd(p.count + q, 1);
+            if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + gl0 + r)};
+          }
         }
     }
   }
   __syncthreads();
-  sieve_flush<f6t::TQ, 9, E::TGW, HCAPW>(smem, p, g0, q0);
+  // the staged hits -> per-query buckets
+  const uint32_t nh = *nhit < (uint32_t)hcap ? *nhit : (uint32_t)hcap;
+  for (uint32_t e = threadIdx.x; e < nh; e += E::NT) {
+    const uint2 hv = hits[e];
+    const int64_t q = q0 + (int)(hv.y >> 9);
+    if (q < p.B) {
+      const int bs = atomicAdd(p.count + q, 1);
+      if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(hv.x), (int)(g0 + (int)(hv.y & 511u))};
+    }
+  }
+}
+
+template <int W, int MODE>
+__device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
+  using E = f6t::EngineW;
+  f6t::f32x4 acc[E::NA][E::NB];
+  E::Feed f;
+  E::feed_init<W>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ, p.nk,
+                  g0 / E::TGW);
+  E::mainloop<W, MODE & 11>(f, p.nk, acc);
+  // the whole ring is free after the main loop: 2 x SIEVE_HCAP staging slots (a 384-row tile collects
+  // 1.5x the hits of a 256-row one)
+  constexpr int HCAPW = 2 * SIEVE_HCAP;
+  static_assert(E::TGW * 8 + 16 + HCAPW * 8 <= E::LDS_BYTES, "hit staging fits the ring's LDS");
+  f6w_epilogue<W, MODE>(smem, p, g0, q0, acc, 0, E::TGW * 8 + 16, HCAPW);
 }
 
 template <int MODE>
