@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include "ofr_i8s_tile.h"
+#include "ofr_i8w_tile.h"
 
 namespace ofr {
 namespace q8 {
@@ -142,6 +143,86 @@ __global__ void __launch_bounds__(i8s::NT, 1) project_q8s_kernel(Args p) {
   if constexpr (PP) i8s::mainloop_pp<NST, XB>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
   else i8s::mainloop<NST, XB, W4>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
   project_epilogue(p, acc, ft, b0, wr, wc, h, r32);
+}
+
+// The wide engine (ofr_i8w_tile.h, round 3): 384 slice rows (96 features x 4 slices) x 256 images, 4
+// waves, each all 384 rows x 64 images, so a feature's four slices meet in one wave.  Tile ft covers
+// projection blocks jb = 3 ft .. 3 ft + 2 (rows jb*128 + s*32 + j%32); element reg of acc[i][c] of lane
+// l: row 16 i + 4 (l / 16) + reg = block i / 8, slice (i % 8) / 2, feature (i % 2) * 16 + 4 (l / 16) + reg
+// of the block; image 64 W + 16 c + l % 16.  The epilogue combines the four slices exactly as
+// project_epilogue (the same fp64 operations in the same order: identical results).
+template <int W>
+__device__ __forceinline__ void project_w_body(const Args& p, int64_t ft, int64_t b0) {
+  i8w::i32x4 acc[i8w::NA][i8w::NB];
+  i8w::Feed f;
+  i8w::feed_init(f, p.Aq, p.ldk, p.arows, ft * i8w::TA, p.X, p.ldx, p.B, b0);
+  i8w::mainloop<W>(f, p.nk, acc);
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g = lane >> 4;
+  // features outer (their scale / K / shift loaded once), the wave's 4 image blocks inner; block 2 (the
+  // VGPR-resident accumulators) first, which frees its 128 registers for the AGPR blocks' conversions
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int jbl = (jj + 2) % 3;
+      const int i0 = jbl * 8 + h;
+      const int64_t j0 = (ft * 3 + jbl) * 32 + h * 16 + 4 * g;
+      double sj[4], kj[4], hj[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = j0 + e < p.d;
+        sj[e] = ok ? p.scale[j0 + e] : 0.0;
+        kj[e] = ok ? p.K[j0 + e] : 0.0;
+        hj[e] = ok && p.shift ? p.shift[j0 + e] : 0.0;
+      }
+#pragma unroll
+      for (int c = 0; c < i8w::NB; ++c) {
+        const int64_t b = b0 + W * 64 + c * 16 + l16;
+        if (b >= p.B) continue;
+        double v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          double tv = (double)acc[i0][c][e];
+          tv += (double)acc[i0 + 2][c][e] * 0x1p-7;
+          tv += (double)acc[i0 + 4][c][e] * 0x1p-14;
+          tv += (double)acc[i0 + 6][c][e] * 0x1p-21;
+          double y = sj[e] * (tv + kj[e]);   // exact: x . Wq[:, j]
+          if (p.shift) y -= hj[e];
+          v[e] = j0 + e < p.d ? y : 0.0;
+        }
+        if (p.y_f64) {
+          double* yr = (double*)p.Y + b * p.ldy;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (j0 + e < p.d) yr[j0 + e] = v[e];
+        } else {
+          float* yr = (float*)p.Y + b * p.ldy;
+          if (j0 + 4 <= p.d && (((uintptr_t)(yr + j0)) & 15) == 0) {
+            f32x4 o;
+            o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+            *reinterpret_cast<f32x4*>(yr + j0) = o;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (j0 + e < p.d) yr[j0 + e] = (float)v[e];
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+__global__ void __launch_bounds__(i8w::NT, 1) project_q8w_kernel(Args p) {
+  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  int64_t ft, bt;
+  i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
+  const int64_t b0 = bt * i8w::TB;
+  switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
+    case 0: project_w_body<0>(p, ft, b0); break;
+    case 1: project_w_body<1>(p, ft, b0); break;
+    case 2: project_w_body<2>(p, ft, b0); break;
+    default: project_w_body<3>(p, ft, b0); break;
+  }
 }
 
 // x -> x - 128 as int8 (XOR 0x80), 16 bytes per thread: the staged engine's pre-shifted B operand
@@ -354,6 +435,7 @@ static int proj_engine() {
     if (e && strcmp(e, "pp4") == 0) return 7;
     if (e && strcmp(e, "pp5") == 0) return 8;
     if (e && strcmp(e, "s5w") == 0) return 9;
+    if (e && strcmp(e, "w") == 0) return 10;
     return 0;
   }();
   return f;
@@ -392,6 +474,9 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, true, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)q8::project_q8w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              i8w::LDS_BYTES);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8)");
     attr_done = true;
   }
@@ -423,6 +508,19 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   p.arows = p.ntf * 256;
   p.gg = p.ntf < q8::GROUP_F ? p.ntf : q8::GROUP_F;
   const int engine = proj_engine();
+  if (engine == 10) {   // the wide engine: tiles of 384 slice rows (3 projection blocks) x 256 images
+    OFR_CHECK_ARG((int64_t)i8w::TA * ldk < 0x7fffffffLL && (int64_t)i8w::TB * ldx < 0x7fffffffLL,
+                  "ofr_project_u8_exact: rows too long for the wide engine");
+    p.ntf = cdiv(p.arows, i8w::TA);
+    p.gg = p.ntf < q8::GROUP_F ? p.ntf : q8::GROUP_F;
+    p.nk = (int)cdiv(D, i8w::BK);
+    p.ntb = cdiv(B, i8w::TB);
+    OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
+    hipLaunchKernelGGL(q8::project_q8w_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), i8w::LDS_BYTES,
+                       (hipStream_t)stream, p);
+    OFR_LAUNCH_CHECK("project_q8w_kernel");
+    return OFR_OK;
+  }
   if (engine == 0) {
     p.nk = (int)cdiv(D, q8::S::BK);
     p.ntb = cdiv(B, q8::S::TQ);

@@ -86,6 +86,15 @@ def main():
         else:
             rec["identical_to_" + ref[0]] = bool(np.array_equal(y32, ref[1]) and np.array_equal(y64, ref[2]))
             rec["max_abs_diff_f64"] = float(np.max(np.abs(y64 - ref[2])))
+            bad = np.argwhere(y64 != ref[2])        # where the first rows differ: (image, feature) pattern
+            if len(bad):
+                rec["mismatch"] = {"count": int(len(bad)), "of": int(y64.size),
+                                   "images": sorted(set(int(x) for x in bad[:, 0]))[:16],
+                                   "features_mod_128": sorted(set(int(x) % 128 for x in bad[:, 1]))[:40],
+                                   "features_first": [int(x) for x in bad[:12, 1]],
+                                   "image0_features": [int(x) for x in bad[bad[:, 0] == 0][:64, 1]],
+                                   "image0_diffs": [float(y64[0, x] - ref[2][0, x]) for x in bad[bad[:, 0] == 0][:12, 1]],
+                                   "per_image": [int((bad[:, 0] == i).sum()) for i in range(16)]}
         res["engines"][eng] = rec
         print(eng, rec, file=sys.stderr, flush=True)
     ok = all(v.get("identical_to_" + ref[0], True) for v in res["engines"].values())

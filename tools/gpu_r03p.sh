@@ -1,9 +1,9 @@
 #!/bin/bash
-# GPU call: the whole -m gpu suite, smoke, the default bench line, then the 8-rank rehearsal.
-set -u
+# Round-3: projection engines (bit-identical check + timing), then the whole GPU suite + smoke.
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; mkdir -p gpurun_out
 T=${1:-r03p}
-BENCH_ARGS="--steps 10 --warmup 2" TEST_TIMEOUT=700 BENCH_TIMEOUT=500 bash tools/gpu_round.sh $T || exit $?
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${T}_smoke.txt 2>&1 || exit $?
-tail -1 gpurun_out/${T}_smoke.txt
-bash tools/gpu_rehearse_ranks.sh 8
+ok() { local rc=$1; [ $rc -eq 0 ] || { echo "step rc=$rc: stopping"; exit $rc; }; }
+timeout -k 10 300 python tools/bench_proj.py --engines ${ENGINES:-i8,w} > gpurun_out/${T}_proj.json 2> gpurun_out/${T}_proj.log; ok $?
+cat gpurun_out/${T}_proj.json
+[ -n "$NO_SUITE" ] && exit 0
+bash tools/gpu_suite.sh ${T}
