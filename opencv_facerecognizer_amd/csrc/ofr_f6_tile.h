@@ -1182,9 +1182,14 @@ struct EngineW {
     const int last = nst - 1;
     auto kso = [&](int s) { return (uint32_t)(s < last ? s : last) * (uint32_t)PANEL; };
     R.prologue(f, kso(0), kso(1), kso(2));
-    for (int s = 0; s <= last; ++s) R.stage(f, f, kso(s + 2), kso(s + 3), false, acc);
+    for (int s = 0; s <= last; ++s) {
+      R.stage(f, f, kso(s + 2), kso(s + 3), false, acc);
+      // the last stage drains the MFMA pipe inside the loop: hipcc pads nothing after an asm MFMA and
+      // places its loop-exit copies of the accumulators (moves, spills) right after the last one
+      if (s == last) wait_drain();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     wait_vm<0>();
-    wait_drain();
     barrier();
   }
 

@@ -191,13 +191,17 @@ __device__ __forceinline__ void mainloop(const Feed& f, int nk, i32x4 (&acc)[NA]
     };
     [&]<int... I>(std::integer_sequence<int, I...>) { (row(std::integral_constant<int, I>{}), ...); }
     (std::make_integer_sequence<int, NA>{});
+    // The last stage drains the MFMA pipe before leaving the loop: hipcc pads nothing after an asm MFMA
+    // and places its loop-exit copies of the accumulators (register moves, spills) right after the last
+    // one -- 8-pass XDL result -> any reader needs 12 wait states.
+    if (s == last) asm volatile("s_nop 7\n s_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     const uint32_t gt_ = g0;   // rotate: s+1 -> current, s+2 -> next, s (re-filled with s+3) -> s+2's
     g0 = g1; g1 = g2; g2 = gt_;
     const uint32_t qt_ = q0;
     q0 = q1; q1 = qt_;
   }
   wait_vm<0>();
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");   // the last MFMAs' results readable
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);

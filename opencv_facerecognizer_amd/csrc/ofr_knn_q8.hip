@@ -580,8 +580,12 @@ __device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int6
   // gallery data, so most blocks skip the staging.  A block that passes re-tests its 32 scores exactly
   // (the padding rows, a = +inf, pass only a NaN th and are excluded there).
   typedef float f32x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int i = 0; i < E::NA; ++i) {
+  // Row blocks unrolled structurally (a lambda per compile-time i), not by `#pragma unroll`: a loop the
+  // compiler leaves rolled indexes acc dynamically, which demotes the whole accumulator array to
+  // scratch -- stores right after the asm MFMAs, with none of their wait states (stale scores).
+  auto rowblock = [&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    __builtin_amdgcn_sched_barrier(0);             // one row block's temporaries live at a time
     const int gl0 = WR * 192 + i * 16 + g4;        // this lane's 4 consecutive gallery rows
     const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
     const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
@@ -602,7 +606,7 @@ __device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int6
       col[c] = __builtin_amdgcn_ballot_w64(!(mn > th[c]));
       any |= col[c];
     }
-    if (any == 0) continue;   // uniform
+    if (any == 0) return;   // uniform
     // ~2 kept pairs per block on gallery data, in one or two query columns: only those are examined
 #pragma unroll
     for (int c = 0; c < E::NB; ++c) {
@@ -622,7 +626,14 @@ __device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int6
           }
         }
     }
-  }
+  };
+  static_assert(E::NA == 12, "row blocks below");
+  rowblock(std::integral_constant<int, 0>{}); rowblock(std::integral_constant<int, 1>{});
+  rowblock(std::integral_constant<int, 2>{}); rowblock(std::integral_constant<int, 3>{});
+  rowblock(std::integral_constant<int, 4>{}); rowblock(std::integral_constant<int, 5>{});
+  rowblock(std::integral_constant<int, 6>{}); rowblock(std::integral_constant<int, 7>{});
+  rowblock(std::integral_constant<int, 8>{}); rowblock(std::integral_constant<int, 9>{});
+  rowblock(std::integral_constant<int, 10>{}); rowblock(std::integral_constant<int, 11>{});
   __syncthreads();
   // the staged hits -> per-query buckets
   const uint32_t nh = *nhit < (uint32_t)hcap ? *nhit : (uint32_t)hcap;
@@ -658,7 +669,14 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   int64_t gt, qt;
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
-  const int64_t g0 = gt * E::TGW, q0 = qt * f6t::TQ;
+  // the coordinates come out of VALU 64-bit divisions: made scalar again, or every descriptor built
+  // from them lands in VGPRs and each LDS-DMA copy becomes a readfirstlane waterfall loop
+  auto uni = [](int64_t v) {
+    const uint64_t u = (uint64_t)v;
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u));
+  };
+  const int64_t g0 = uni(gt) * E::TGW, q0 = uni(qt) * f6t::TQ;
   switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
     case 0: f6w_body<0, MODE>(smem, p, g0, q0); break;
     case 1: f6w_body<1, MODE>(smem, p, g0, q0); break;

@@ -421,22 +421,23 @@ static bool getenv_flag_gemv() {
   return f;
 }
 
-// OFR_PROJ_ENGINE selects the tile engine: default ("i8") ofr_i8_tile.h (two 128-feature stages,
-// FLAT copies); "s4" / "s5" the staged engine of ofr_i8s_tile.h with 4 / 5 64-feature buffers;
-// "s5p" the staged engine on images shifted to int8 by a pre-pass (no XOR in the k loop).  All give
-// identical bits; the staged forms measured no faster at the bench shape (tools/bench_proj.py,
-// profiles/r03_proj_engines.json: 1.67 / 1.72 / 1.69 / 1.68 ms), so the default stays.
+// OFR_PROJ_ENGINE selects the tile engine: default ("w") the wide engine of ofr_i8w_tile.h (384 x 256
+// tiles, one wave per SIMD: 1.51 against 1.67 ms at the bench shape, profiles/r03_proj_wide.json);
+// "i8" ofr_i8_tile.h (two 128-feature stages, FLAT copies; the default until round 3); "s4" / "s5" the
+// staged engine of ofr_i8s_tile.h with 4 / 5 64-feature buffers; "s5p" the staged engine on images
+// shifted to int8 by a pre-pass (no XOR in the k loop).  All give identical bits (tools/bench_proj.py;
+// the staged forms: 1.72 / 1.69 / 1.68 ms, profiles/r03_proj_engines.json).
 static int proj_engine() {
   static const int f = [] {
     const char* e = getenv("OFR_PROJ_ENGINE");
+    if (e && strcmp(e, "i8") == 0) return 0;
     if (e && strcmp(e, "s4") == 0) return 4;
     if (e && strcmp(e, "s5") == 0) return 5;
     if (e && strcmp(e, "s5p") == 0) return 6;
     if (e && strcmp(e, "pp4") == 0) return 7;
     if (e && strcmp(e, "pp5") == 0) return 8;
     if (e && strcmp(e, "s5w") == 0) return 9;
-    if (e && strcmp(e, "w") == 0) return 10;
-    return 0;
+    return 10;
   }();
   return f;
 }
