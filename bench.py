@@ -162,8 +162,12 @@ class StepPipeline:
 
     NBUF, NWS = 3, 2
 
-    def __init__(self, device, prep, tiles, merge, finish, overlap=True):
+    def __init__(self, device, prep, tiles, merge, finish, overlap=True, prep_behind=None):
         self.prep_fn, self.tiles_fn, self.merge_fn, self.finish_fn = prep, tiles, merge, finish
+        # prep_behind "tiles" (default): batch s+1's preparation waits for tile pass s and runs alone;
+        # "sample": it waits only for sample pass s and shares the chip with sieve pass s
+        self.prep_behind = prep_behind or os.environ.get("OFR_BENCH_PREP", "tiles")
+        assert self.prep_behind in ("tiles", "sample"), self.prep_behind
         self.main = torch.cuda.current_stream(device)
         self.side = torch.cuda.Stream(device=device) if overlap else self.main
         self.ws = [Workspace() for _ in range(self.NWS)]
@@ -227,7 +231,7 @@ class StepPipeline:
             self.ev_tiles.record(self.main)
             if s >= 1:
                 res = self._finish(s - 1)
-            self.side.wait_event(self.ev_tiles)
+            self.side.wait_event(self.ev_tiles if self.prep_behind == "tiles" else self.ev_sample)
             if s + 1 < steps:
                 self._prep(s + 1, ev[s + 1])
         if steps:

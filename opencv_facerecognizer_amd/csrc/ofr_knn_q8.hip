@@ -28,6 +28,9 @@
 // (strictly: no excluded row can reach or tie the k-th).  cert[q] = 1 then;
 // otherwise 0 and the caller re-runs that query on the fp32 path.
 #include <cstdlib>
+#ifndef OFR_F6W_EPI_SB
+#define OFR_F6W_EPI_SB 1   // one row block of the wide epilogue scheduled at a time
+#endif
 #include <type_traits>
 
 #include "ofr_f6_tile.h"
@@ -585,7 +588,9 @@ __device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int6
   // scratch -- stores right after the asm MFMAs, with none of their wait states (stale scores).
   auto rowblock = [&](auto ii) {
     constexpr int i = decltype(ii)::value;
+#if OFR_F6W_EPI_SB
     __builtin_amdgcn_sched_barrier(0);             // one row block's temporaries live at a time
+#endif
     const int gl0 = WR * 192 + i * 16 + g4;        // this lane's 4 consecutive gallery rows
     const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
     const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
