@@ -1047,19 +1047,39 @@ struct EngineW {
     asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
   }
 
-  // The stages of one tile.  F2 / F3: the feeds of the stages s + 2 / s + 3 copied during stage s, k2 / k3
-  // their stage offsets; defer3: no G(s + 3) pieces in rows 10 / 11.  (A persistent form -- the ring run
-  // on across a workgroup's tiles, the next tile's first stages copied during this one's last stages and
-  // epilogue -- was built in round 3 and dropped: with the epilogue inside the tile loop the register
-  // allocator spills accumulators to scratch in the k loop and moves the feed offsets to VGPRs, which
-  // turns every copy into a waterfall loop)
+  // MODE (probes): 1 = no copies in the k loop (the prologue's stages re-read), 2 = no MFMAs,
+  // 8 = copies never waited for (wrong results)
   template <int W, int MODE>
-  struct Ring {
+  static __device__ __forceinline__ void mainloop(const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
+    constexpr int WR = W >> 1, WC = W & 1;
+    int sc = SCALE_ONE;
+    asm volatile("" : "+v"(sc));
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int last = nst - 1;
+    auto kso = [&](int s) { return (uint32_t)(s < last ? s : last) * (uint32_t)PANEL; };
+    auto gall = [&](uint32_t so, uint32_t ko) {
+      gcopy<W, 0>(f, so, ko); gcopy<W, 1>(f, so, ko); gcopy<W, 2>(f, so, ko);
+      gcopy<W, 3>(f, so, ko); gcopy<W, 4>(f, so, ko); gcopy<W, 5>(f, so, ko);
+      gcopy<W, 6>(f, so, ko); gcopy<W, 7>(f, so, ko); gcopy<W, 8>(f, so, ko);
+    };
+    auto qall = [&](uint32_t so, uint32_t ko) {
+      qcopy<W, 0>(f, so, ko); qcopy<W, 1>(f, so, ko); qcopy<W, 2>(f, so, ko);
+      qcopy<W, 3>(f, so, ko); qcopy<W, 4>(f, so, ko); qcopy<W, 5>(f, so, ko);
+    };
+    // ring slots (LDS byte offsets) of stages s, s + 1, s + 2 (gallery) and s, s + 1 (query)
     uint32_t g0 = 0, g1 = GSLOT, g2 = 2 * GSLOT, q0 = QBASE, q1 = QBASE + QSLOT;
+    // prologue: G(0), Q(0), G(1), Q(1) and pieces 0, 1 of G(2)
+    gall(g0, kso(0)); qall(q0, kso(0)); gall(g1, kso(1)); qall(q1, kso(1));
+    gcopy<W, 0>(f, g2, kso(2));
+    gcopy<W, 1>(f, g2, kso(2));
+    wait_vm<GPW + QPW + 2>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
     i32x6 a[RING], b[NB];
-    int sc;
-    __device__ __forceinline__ void read_first() {   // A[0], A[1], B of the stage in g0 / q0
-      constexpr int WR = W >> 1, WC = W & 1;
+    {
       const Bases ab = abase(g0), bb = bbase(q0);
       a[0] = fragA<WR * 192 + 0>(ab);
       a[1] = fragA<WR * 192 + 16>(ab);
@@ -1067,10 +1087,9 @@ struct EngineW {
       b[3] = fragB<WC * 128 + 48>(bb); b[4] = fragB<WC * 128 + 64>(bb); b[5] = fragB<WC * 128 + 80>(bb);
       b[6] = fragB<WC * 128 + 96>(bb); b[7] = fragB<WC * 128 + 112>(bb);
     }
-    __device__ __forceinline__ void stage(const Feed& F2, const Feed& F3, uint32_t k2, uint32_t k3, bool defer3,
-                                          f32x4 (&acc)[NA][NB]) {
-      constexpr int WR = W >> 1, WC = W & 1;
+    for (int s = 0; s <= last; ++s) {
       const Bases ac = abase(g0), an = abase(g1), bn = bbase(q1);
+      const uint32_t k2 = kso(s + 2), k3 = kso(s + 3);
       auto row = [&](auto ii) {
         constexpr int i = decltype(ii)::value;
         constexpr bool AG = i < NAA;
@@ -1091,10 +1110,9 @@ struct EngineW {
         }
         if constexpr ((MODE & 1) == 0) {
           // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0), G(s+3) into G(s)'s (g0)
-          if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(F2, g2, k2);
-          if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(F2, q0, k2);
-          if constexpr (i == 10)   // piece 1: in the middle of rows 10 / 11
-            if (!defer3) gcopy<W, 0>(F3, g0, k3);
+          if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(f, g2, k2);
+          if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(f, q0, k2);
+          if constexpr (i == 10) gcopy<W, 0>(f, g0, k3);   // piece 1: in the middle of rows 10 / 11
         }
         if constexpr (i == NA - 1) {
           // rows 10 and 11 run together (below, i == 10)
@@ -1108,8 +1126,7 @@ struct EngineW {
           mm(a[1], b[1], acc[10][1]); mm(a[2], b[1], acc[11][1]); b[1] = fragB<WC * 128 + 16>(bn);
           mm(a[1], b[2], acc[10][2]); mm(a[2], b[2], acc[11][2]); b[2] = fragB<WC * 128 + 32>(bn);
           mm(a[1], b[3], acc[10][3]); mm(a[2], b[3], acc[11][3]); b[3] = fragB<WC * 128 + 48>(bn);
-          if constexpr ((MODE & 1) == 0)
-            if (!defer3) gcopy<W, 1>(F3, g0, k3);
+          if constexpr ((MODE & 1) == 0) gcopy<W, 1>(f, g0, k3);
           mm(a[1], b[4], acc[10][4]); mm(a[2], b[4], acc[11][4]); b[4] = fragB<WC * 128 + 64>(bn);
           mm(a[1], b[5], acc[10][5]); mm(a[2], b[5], acc[11][5]); b[5] = fragB<WC * 128 + 80>(bn);
           mm(a[1], b[6], acc[10][6]); mm(a[2], b[6], acc[11][6]); b[6] = fragB<WC * 128 + 96>(bn);
@@ -1139,60 +1156,12 @@ struct EngineW {
       g0 = g1; g1 = g2; g2 = gt_;
       const uint32_t qt_ = q0;
       q0 = q1; q1 = qt_;
-    }
-    // prologue: G(0), Q(0), G(1), Q(1) and pieces 0, 1 of G(2) of f (stage offsets k0, k1, k2), then
-    // A/B of stage 0
-    __device__ __forceinline__ void prologue(const Feed& f, uint32_t k0, uint32_t k1, uint32_t k2) {
-      gall<W>(f, g0, k0); qall<W>(f, q0, k0); gall<W>(f, g1, k1); qall<W>(f, q1, k1);
-      gcopy<W, 0>(f, g2, k2);
-      gcopy<W, 1>(f, g2, k2);
-      wait_vm<GPW + QPW + 2>();
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      read_first();
-    }
-  };
-  template <int W>
-  static __device__ __forceinline__ void gall(const Feed& f, uint32_t so, uint32_t ko) {
-    gcopy<W, 0>(f, so, ko); gcopy<W, 1>(f, so, ko); gcopy<W, 2>(f, so, ko);
-    gcopy<W, 3>(f, so, ko); gcopy<W, 4>(f, so, ko); gcopy<W, 5>(f, so, ko);
-    gcopy<W, 6>(f, so, ko); gcopy<W, 7>(f, so, ko); gcopy<W, 8>(f, so, ko);
-  }
-  template <int W>
-  static __device__ __forceinline__ void qall(const Feed& f, uint32_t so, uint32_t ko) {
-    qcopy<W, 0>(f, so, ko); qcopy<W, 1>(f, so, ko); qcopy<W, 2>(f, so, ko);
-    qcopy<W, 3>(f, so, ko); qcopy<W, 4>(f, so, ko); qcopy<W, 5>(f, so, ko);
-  }
-  static __device__ __forceinline__ void zero(f32x4 (&acc)[NA][NB]) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i)
-#pragma unroll
-      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-
-  // One tile (nst >= 3), the copies of stages past the last clamped to it (into free slots, never read).
-  // MODE (probes): 1 = no copies in the k loop (the prologue's stages re-read), 2 = no MFMAs,
-  // 8 = copies never waited for (wrong results)
-  template <int W, int MODE>
-  static __device__ __forceinline__ void mainloop(const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
-    Ring<W, MODE> R;
-    R.sc = SCALE_ONE;
-    asm volatile("" : "+v"(R.sc));
-    zero(acc);
-    const int last = nst - 1;
-    auto kso = [&](int s) { return (uint32_t)(s < last ? s : last) * (uint32_t)PANEL; };
-    R.prologue(f, kso(0), kso(1), kso(2));
-    for (int s = 0; s <= last; ++s) {
-      R.stage(f, f, kso(s + 2), kso(s + 3), false, acc);
-      // the last stage drains the MFMA pipe inside the loop: hipcc pads nothing after an asm MFMA and
-      // places its loop-exit copies of the accumulators (moves, spills) right after the last one
       if (s == last) wait_drain();
       __builtin_amdgcn_sched_barrier(0);
     }
     wait_vm<0>();
     barrier();
   }
-
 };
 
 }  // namespace f6t

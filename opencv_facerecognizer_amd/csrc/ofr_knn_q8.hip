@@ -28,9 +28,6 @@
 // (strictly: no excluded row can reach or tie the k-th).  cert[q] = 1 then;
 // otherwise 0 and the caller re-runs that query on the fp32 path.
 #include <cstdlib>
-#ifndef OFR_F6W_EPI_SB
-#define OFR_F6W_EPI_SB 1   // one row block of the wide epilogue scheduled at a time
-#endif
 #include <type_traits>
 
 #include "ofr_f6_tile.h"
@@ -534,20 +531,25 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
 }
 
 // fp6 sieve pass on the wide engine (f6t::EngineW): 384 gallery x 256 query tiles, 4 waves (one per
-// SIMD), p.ntg = ceil(N / 384) gallery tiles.  Epilogue of wave W for the 192 x 128 wave tile: element r
-// of acc[i][c] of lane l is gallery row WR*192 + 16 i + 4 (l / 16) + r, query WC*128 + 16 c + l % 16.
-// LDS: the [384][2] operand table at `tab`, the hit count at tab + 3072, HCAP hit slots at `stage`; hits
-// past HCAP go straight to their query's bucket (one global atomic each) instead of the staging.
-// MODE probe bit 4 = no epilogue (the accumulators kept alive).
+// SIMD), p.ntg = ceil(N / 384) gallery tiles.  The epilogue is sieve_epilogue16's for the 192 x 128
+// wave tile: element r of acc[i][c] of lane l is gallery row WR*192 + 16 i + 4 (l / 16) + r, query
+// WC*128 + 16 c + l % 16.  MODE probe bits: 1 / 2 = no copies / no MFMAs in the k loop, 4 = no
+// epilogue (the accumulators kept alive).
 template <int W, int MODE>
-__device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int64_t g0, int64_t q0,
-                                             f6t::f32x4 (&acc)[f6t::EngineW::NA][f6t::EngineW::NB], uint32_t tab,
-                                             uint32_t stage, int hcap) {
+__device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
   using E = f6t::EngineW;
+  f6t::f32x4 acc[E::NA][E::NB];
   constexpr int WR = W >> 1;
-  float* gtab = reinterpret_cast<float*>(smem + tab);                              // [384][2]
-  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + tab + E::TGW * 8);
-  uint2* hits = reinterpret_cast<uint2*>(smem + stage);                           // [hcap]
+  E::Feed f;
+  E::feed_init<W>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ, p.nk,
+                  g0 / E::TGW);
+  E::mainloop<W, MODE & 11>(f, p.nk, acc);
+  float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
+  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
+  uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [HCAPW]
+  // 2x SIEVE_HCAP: a 384-row tile collects 1.5x the hits of a 256-row one (loose thresholds, small d)
+  constexpr int HCAPW = 2 * SIEVE_HCAP;
+  static_assert(E::TGW * 8 + 16 + HCAPW * 8 <= E::LDS_BYTES, "hit staging fits the ring's LDS");
   const int nvalid = p.N - g0 < E::TGW ? (int)(p.N - g0) : E::TGW;
   for (int r = threadIdx.x; r < E::TGW; r += E::NT) {
     const bool ok = r < nvalid;
@@ -583,14 +585,8 @@ __device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int6
   // gallery data, so most blocks skip the staging.  A block that passes re-tests its 32 scores exactly
   // (the padding rows, a = +inf, pass only a NaN th and are excluded there).
   typedef float f32x2 __attribute__((ext_vector_type(2)));
-  // Row blocks unrolled structurally (a lambda per compile-time i), not by `#pragma unroll`: a loop the
-  // compiler leaves rolled indexes acc dynamically, which demotes the whole accumulator array to
-  // scratch -- stores right after the asm MFMAs, with none of their wait states (stale scores).
-  auto rowblock = [&](auto ii) {
-    constexpr int i = decltype(ii)::value;
-#if OFR_F6W_EPI_SB
-    __builtin_amdgcn_sched_barrier(0);             // one row block's temporaries live at a time
-#endif
+#pragma unroll
+  for (int i = 0; i < E::NA; ++i) {
     const int gl0 = WR * 192 + i * 16 + g4;        // this lane's 4 consecutive gallery rows
     const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
     const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
@@ -611,7 +607,7 @@ __device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int6
       col[c] = __builtin_amdgcn_ballot_w64(!(mn > th[c]));
       any |= col[c];
     }
-    if (any == 0) return;   // uniform
+    if (any == 0) continue;   // uniform
     // ~2 kept pairs per block on gallery data, in one or two query columns: only those are examined
 #pragma unroll
     for (int c = 0; c < E::NB; ++c) {
@@ -622,49 +618,12 @@ __device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int6
           const int ql = wc * 128 + c * 16 + r16;
           const uint32_t kb = __float_as_uint(key_score(score_key(sc[r][c], 0)));
           const uint32_t slot = atomicAdd(nhit, 1u);
-          if (slot < (uint32_t)hcap) {
-            hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
-          } else if (q0 + ql < p.B) {   // staging full: straight to the query's bucket
-            const int64_t q = q0 + ql;
-            const int bs = atomicAdd(p.count + q, 1);
-            if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + gl0 + r)};
-          }
+          if (slot < (uint32_t)HCAPW) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
         }
     }
-  };
-  static_assert(E::NA == 12, "row blocks below");
-  rowblock(std::integral_constant<int, 0>{}); rowblock(std::integral_constant<int, 1>{});
-  rowblock(std::integral_constant<int, 2>{}); rowblock(std::integral_constant<int, 3>{});
-  rowblock(std::integral_constant<int, 4>{}); rowblock(std::integral_constant<int, 5>{});
-  rowblock(std::integral_constant<int, 6>{}); rowblock(std::integral_constant<int, 7>{});
-  rowblock(std::integral_constant<int, 8>{}); rowblock(std::integral_constant<int, 9>{});
-  rowblock(std::integral_constant<int, 10>{}); rowblock(std::integral_constant<int, 11>{});
-  __syncthreads();
-  // the staged hits -> per-query buckets
-  const uint32_t nh = *nhit < (uint32_t)hcap ? *nhit : (uint32_t)hcap;
-  for (uint32_t e = threadIdx.x; e < nh; e += E::NT) {
-    const uint2 hv = hits[e];
-    const int64_t q = q0 + (int)(hv.y >> 9);
-    if (q < p.B) {
-      const int bs = atomicAdd(p.count + q, 1);
-      if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(hv.x), (int)(g0 + (int)(hv.y & 511u))};
-    }
   }
-}
-
-template <int W, int MODE>
-__device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
-  using E = f6t::EngineW;
-  f6t::f32x4 acc[E::NA][E::NB];
-  E::Feed f;
-  E::feed_init<W>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ, p.nk,
-                  g0 / E::TGW);
-  E::mainloop<W, MODE & 11>(f, p.nk, acc);
-  // the whole ring is free after the main loop: 2 x SIEVE_HCAP staging slots (a 384-row tile collects
-  // 1.5x the hits of a 256-row one)
-  constexpr int HCAPW = 2 * SIEVE_HCAP;
-  static_assert(E::TGW * 8 + 16 + HCAPW * 8 <= E::LDS_BYTES, "hit staging fits the ring's LDS");
-  f6w_epilogue<W, MODE>(smem, p, g0, q0, acc, 0, E::TGW * 8 + 16, HCAPW);
+  __syncthreads();
+  sieve_flush<f6t::TQ, 9, E::TGW, HCAPW>(smem, p, g0, q0);
 }
 
 template <int MODE>
@@ -674,14 +633,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   int64_t gt, qt;
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
-  // the coordinates come out of VALU 64-bit divisions: made scalar again, or every descriptor built
-  // from them lands in VGPRs and each LDS-DMA copy becomes a readfirstlane waterfall loop
-  auto uni = [](int64_t v) {
-    const uint64_t u = (uint64_t)v;
-    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
-                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u));
-  };
-  const int64_t g0 = uni(gt) * E::TGW, q0 = uni(qt) * f6t::TQ;
+  const int64_t g0 = gt * E::TGW, q0 = qt * f6t::TQ;
   switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
     case 0: f6w_body<0, MODE>(smem, p, g0, q0); break;
     case 1: f6w_body<1, MODE>(smem, p, g0, q0); break;
