@@ -1516,6 +1516,19 @@ static int f6_shape() {
   return s;
 }
 
+// gallery tiles per tile group of the wide sieve pass (i8t::tile_coords): 2, so the ~32 workgroups
+// resident on one XCD cover 2 gallery x 16 query tiles (every query panel of a 4096 batch) -- same-box
+// A/B (profiles/r03_f6w_group_ab.log): 20.57-20.76 ms per pass at 2, 20.70 at 4, 21.2-21.4 at 3,
+// 21.6-21.7 at 8, 23.1-23.2 at 16.  OFR_F6W_GROUP overrides (probe)
+static int f6w_group() {
+  static const int g = [] {
+    const char* e = getenv("OFR_F6W_GROUP");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 64 ? v : 2;
+  }();
+  return g;
+}
+
 // f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
 // thresholds, counts and buckets (each 256-byte aligned)
 struct SieveWs {
@@ -1691,7 +1704,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       } else if (f6_shape() == 384 && !two) {
         q8s::TileArgs wa = a;   // 384-row gallery tiles over the same 256-row panel layout
         wa.ntg = cdiv(N, f6t::EngineW::TGW);
-        wa.gg = wa.ntg < q8s::GROUP_G ? wa.ntg : q8s::GROUP_G;
+        wa.gg = wa.ntg < f6w_group() ? wa.ntg : f6w_group();
         OFR_CHECK_ARG(wa.ntq * wa.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
         hipLaunchKernelGGL((q8s::tile_kernel_f6w<0>), dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),
                            f6t::EngineW::LDS_BYTES, st, wa);
