@@ -329,10 +329,42 @@ def stress_run(P, bank, args, noise, device, N=None):
     return res
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT) and wait for them.  Runs before anything
+    touches the GPU; the children are new processes (no exec of this one).  Returns the exit status:
+    the first non-zero child status, else 0.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    for p in procs:
+        rc = p.wait()
+        if rc and not status:
+            status = rc
+            for q in procs:            # one rank failed: the others would wait in a collective forever
+                if q.poll() is None:
+                    q.terminate()
+    return status
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU, e.g. "
+              f"torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus})", file=sys.stderr)
+        sys.exit(2)
     local = 0 if os.environ.get("OFR_ONE_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)

@@ -305,10 +305,46 @@ def lda_eigen(Sw, Sb, num_components, solver=None, device_out=False):
             V = V[:, order]
             V = V / np.linalg.norm(V, axis=0)
             return lam[order], (_device.f64_dev(np.ascontiguousarray(V)) if device_out else V)
-    evals, evecs = np.linalg.eig(np.linalg.inv(Sw) @ Sb)
-    idx = np.argsort(-evals.real)
-    V = evecs[:, idx][:, :m].real
-    return evals[idx][:m].real, (_device.f64_dev(np.ascontiguousarray(V)) if device_out else V)
+    try:
+        iSw = np.linalg.inv(Sw)
+    except np.linalg.LinAlgError:
+        lam, V = _lda_singular_sw(Sw, Sb, m)
+    else:
+        evals, evecs = np.linalg.eig(iSw @ Sb)
+        idx = np.argsort(-evals.real)
+        lam, V = evals[idx][:m].real, evecs[:, idx][:, :m].real
+    return lam, (_device.f64_dev(np.ascontiguousarray(V)) if device_out else V)
+
+
+def _lda_singular_sw(Sw, Sb, m):
+    """feature.py:170 when inv(Sw) hits an exactly zero pivot.
+
+    Sw is singular whenever the within-class deviations span fewer than the PCA(n - c) dimensions
+    it lives in -- e.g. two identical images in one class: the bundled data set holds one such pair
+    (steve_crop0.jpg == steve_crop5.jpg), so the reference's own inv(Sw) there inverts rounding noise
+    (its last LU pivot is ~1 ulp of the matrix), and whether that noise is exactly zero depends on
+    the last bits of the PCA features.  The reference's result with a vanishing POSITIVE pivot is
+    the generalized problem Sb v = lambda Sw v: the null directions of Sw come first with an
+    infinite eigenvalue, the rest are the finite generalized eigenpairs -- the same columns the
+    reference's inv + eig converge to.  Solved by QZ (scipy.linalg.eig(Sb, Sw), LAPACK dggev);
+    |beta| below 1e3 n eps ||Sw|| counts as zero (infinite eigenvalue, ranked first).  Columns at
+    unit 2-norm like numpy's eig."""
+    import scipy.linalg
+    Sw = np.asarray(Sw, np.float64)
+    Sb = np.asarray(Sb, np.float64)
+    n = Sw.shape[0]
+    (alpha, beta), V = scipy.linalg.eig(Sb, Sw, homogeneous_eigvals=True)
+    tol = 1e3 * n * np.finfo(np.float64).eps * max(np.linalg.norm(Sw), np.finfo(np.float64).tiny)
+    inf = np.abs(beta) <= tol
+    with np.errstate(divide="ignore", invalid="ignore"):
+        lam = np.where(inf, np.inf, (alpha / np.where(inf, 1.0, beta)).real)
+    idx = np.argsort(-lam, kind="stable")[:m]
+    V = V[:, idx].real
+    nrm = np.linalg.norm(V, axis=0)
+    V = V / np.where(nrm > 0, nrm, 1.0)
+    warnings.warn("LDA: Sw is singular (inv(Sw) failed, feature.py:170); %d null direction(s) of Sw ranked "
+                  "first (generalized eigenproblem, QZ)" % int(inf.sum()))
+    return lam[idx], V
 
 
 class LDA(_DeviceProjMixin, AbstractFeature):
@@ -405,15 +441,17 @@ class Fisherfaces(_DeviceProjMixin, AbstractFeature):
         if k >= D:
             # PCA keeps every pixel dimension (a rotation): LDA in pixel space, W = V directly
             self._regime = "pixel"
-            Sw, Sb = training.pixel_scatter(training.pixel_pieces(Xd, D, lay), lay.counts, n)
+            Sw, Sb = training.finite("pixel_scatter", *training.pixel_scatter(training.pixel_pieces(Xd, D, lay),
+                                                                              lay.counts, n))
             evals, Wd = lda_eigen(Sw, Sb, m, device_out=True)
             del Sw, Sb
         elif n <= D:
             # n x n Gram of the centred faces: U_k = XC^T V_k / sigma_k, features V_k sigma_k
             self._regime = "gram"
-            lam, V = training.eigh_desc(training.centred_gram(Xd, D, lay), k)
+            lam, V = training.finite("eigh_desc", *training.eigh_desc(
+                training.finite("centred_gram", training.centred_gram(Xd, D, lay)), k))
             sig = lam.clamp_min(0.0).sqrt()
-            Sw, Sb = training.feature_scatter((V * sig).contiguous(), y)
+            Sw, Sb = training.finite("feature_scatter", *training.feature_scatter((V * sig).contiguous(), y))
             evals, L = lda_eigen(Sw, Sb, m)
             L32 = _device.f64_dev(np.asarray(L, dtype=np.float32).astype(np.float64))   # feature.py:176
             inv = torch.where(sig > 0, 1.0 / sig, torch.zeros_like(sig))
@@ -423,13 +461,14 @@ class Fisherfaces(_DeviceProjMixin, AbstractFeature):
             # D x D covariance: P = leading k eigenvectors, features XC P, W = P L
             self._regime = "cov"
             pieces = training.pixel_pieces(Xd, D, lay)
-            lam, Pd = training.eigh_desc(training.covariance(pieces, n), k)
+            lam, Pd = training.finite("eigh_desc", *training.eigh_desc(
+                training.finite("covariance", training.covariance(pieces, n)), k))
             del pieces
             Pd = Pd.contiguous()
             mu = training.mean_image(Xd, D, lay)
             shift = _device.gemm_f64(mu.reshape(1, -1).contiguous(), Pd).reshape(-1)
             Fd = _device.Projection(Wt_device=Pd.t().contiguous(), D=D).project(Xd, shift64=shift, f64=True)
-            Sw, Sb = training.feature_scatter(Fd, y)
+            Sw, Sb = training.finite("feature_scatter", *training.feature_scatter(Fd, y))
             del Fd
             evals, L = lda_eigen(Sw, Sb, m)
             L32 = np.asarray(L, dtype=np.float32).astype(np.float64)          # feature.py:176

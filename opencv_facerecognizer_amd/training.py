@@ -41,6 +41,16 @@ from . import _device
 from ._lib import call, ptr, stream
 
 
+def finite(stage, *ts):
+    """Raise OfrError naming the stage when a device intermediate holds a NaN / inf (one reduction
+    and one host read per tensor: training only)."""
+    from ._lib import OfrError
+    for t in ts:
+        if not bool(torch.isfinite(t).all()):
+            raise OfrError(f"Fisherfaces training: non-finite values after {stage}")
+    return ts[0] if len(ts) == 1 else ts
+
+
 def _i64(t, device):
     return torch.from_numpy(np.ascontiguousarray(np.asarray(t, dtype=np.int64))).to(device)
 

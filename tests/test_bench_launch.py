@@ -1,0 +1,40 @@
+"""bench.py --gpus N (VERDICT r3 "missing" #2): the flag decides the world size.
+
+* CPU: a --gpus that disagrees with a launcher's WORLD_SIZE exits non-zero before touching a GPU.
+* GPU: ``bench.py --gpus 2`` without a launcher starts the two rank processes itself; with
+  OFR_DIST_BACKEND=gloo OFR_ONE_DEVICE=1 both ranks share the box's one GPU, and rank 0's JSON line
+  reports n_gpus 2 with every query certified and the identities found.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def test_gpus_flag_must_match_launcher_world_size():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
+    assert "--gpus 2 but WORLD_SIZE=1" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_spawns_two_ranks():
+    env = dict(os.environ, OFR_DIST_BACKEND="gloo", OFR_ONE_DEVICE="1")
+    for key in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(key, None)
+    cmd = [sys.executable, BENCH, "--gpus", "2", "--gallery", "40000", "--batch", "1024", "--steps", "2",
+           "--warmup", "1", "--no-cpu", "--stress", "", "--config1", "0", "--small-batches", ""]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["steps"] == 2
+    assert r["uncertified_queries_per_step"] == 0.0
+    assert r["top1_identity_acc"] == 1.0
