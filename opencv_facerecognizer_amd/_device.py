@@ -659,8 +659,8 @@ def counts_of(F, denom, count_bytes=None):
     if F.size and (C.min() < 0 or not np.array_equal(C / denom, F)):
         return None
     top = C.max() if C.size else 0
-    cb = count_bytes or next(b for b in (1, 2, 4) if top <= _COUNT_DT[b][3])
-    if top > _COUNT_DT[cb][3]:
+    cb = count_bytes or next((b for b in (1, 2, 4) if top <= _COUNT_DT[b][3]), None)
+    if cb is None or top > _COUNT_DT[cb][3]:       # wider than 32-bit counts: not a counts gallery
         return None
     return C.astype(_COUNT_DT[cb][2]), cb
 

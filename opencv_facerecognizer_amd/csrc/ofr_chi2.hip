@@ -13,7 +13,9 @@
 // kernel then re-evaluates the reference formula EXACTLY in fp64 on the
 // survivors, with p = value/denom (denom = cell pixel count for counts, the
 // reference histogram being count/(py*px)) and eps = 2^-52.
+#include <atomic>
 #include <cmath>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -728,18 +730,32 @@ static int chi2_mfma_run(hipStream_t st, const uint8_t* Q, int64_t B, int64_t ld
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_status(e, "hipGetDevice");
-  static uint16_t* table_dev[64] = {};
-  static bool attr_done = false;
+  // per-device fp16 table (4 KiB): uploaded once under a lock and published only after the copy
+  // completed, so a caller on another thread (one context per thread) never sees an unfilled table
+  static std::atomic<uint16_t*> table_dev[64] = {};
+  static std::mutex table_mu;
+  static std::atomic<bool> attr_done{false};
   if (dev < 0 || dev >= 64) return fail(OFR_E_UNSUPPORTED, "ofr_chi2_knn: device index >= 64");
-  if (!table_dev[dev]) {   // once per device: 4 KiB, copied synchronously
-    e = hipMalloc((void**)&table_dev[dev], sizeof(tb.bits));
-    if (e == hipSuccess) e = hipMemcpy(table_dev[dev], tb.bits, sizeof(tb.bits), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_status(e, "ofr_chi2_knn: table upload");
+  uint16_t* table = table_dev[dev].load(std::memory_order_acquire);
+  if (!table) {
+    std::lock_guard<std::mutex> g(table_mu);
+    table = table_dev[dev].load(std::memory_order_acquire);
+    if (!table) {
+      uint16_t* t = nullptr;
+      e = hipMalloc((void**)&t, sizeof(tb.bits));
+      if (e == hipSuccess) e = hipMemcpy(t, tb.bits, sizeof(tb.bits), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        if (t) (void)hipFree(t);
+        return hip_status(e, "ofr_chi2_knn: table upload");
+      }
+      table_dev[dev].store(t, std::memory_order_release);
+      table = t;
+    }
   }
-  if (!attr_done) {
+  if (!attr_done.load(std::memory_order_acquire)) {
     e = hipFuncSetAttribute((const void*)c2m::chi2_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c2m::LDS);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(chi2_mfma)");
-    attr_done = true;
+    attr_done.store(true, std::memory_order_release);
   }
   const Chi2MWs w = chi2m_ws(B, N);
   char* wsb = reinterpret_cast<char*>(workspace);
@@ -755,7 +771,7 @@ static int chi2_mfma_run(hipStream_t st, const uint8_t* Q, int64_t B, int64_t ld
   OFR_LAUNCH_CHECK("row_total_kernel");
   c2m::Args a;
   a.Q = Q; a.B = B; a.ldq = ldq; a.G = G; a.N = N; a.ldg = ldg; a.nbins = nbins;
-  a.table = table_dev[dev]; a.tq = tq; a.tg = tg;
+  a.table = table; a.tq = tq; a.tg = tg;
   a.cand = reinterpret_cast<Cand*>(wsb + w.lists);
   a.ntq = cdiv(B, c2m::TQ);
   a.ntg = cdiv(N, c2m::TG);

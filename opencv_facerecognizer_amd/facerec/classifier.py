@@ -61,6 +61,38 @@ def vote(sorted_y):
     return int(vals[np.argmax(counts)])
 
 
+def vote_rows(labels):
+    """``vote`` of every row of a non-negative label matrix [B][k] at once: each row sorted, the
+    count of every entry's value, the first maximum of the sorted row (= the smallest of the most
+    frequent labels)."""
+    s = np.sort(labels, axis=1)
+    if s.shape[1] == 1:
+        return s[:, 0]
+    counts = (s[:, :, None] == s[:, None, :]).sum(axis=2)
+    return s[np.arange(len(s)), np.argmax(counts, axis=1)]
+
+
+def results(d_all, i_all, y):
+    """classifier.py:113-129 for a batch: host top-k (distances [B][k], gallery rows [B][k], -1 =
+    no row) -> the reference's per-query ``[label, {'labels': sorted_y, 'distances': ...}]``.  The
+    labels and the vote are formed for the whole batch at once; each query's arrays are row views
+    of the two batch arrays."""
+    y = np.asarray(y)
+    i_all = np.asarray(i_all)
+    d_all = np.asarray(d_all)
+    valid = i_all >= 0
+    if len(i_all) and valid.all() and len(y):
+        lab = y[i_all]
+        if lab.size == 0 or lab.min() >= 0:
+            votes = vote_rows(lab).tolist() if lab.shape[1] else [vote(r) for r in lab]
+            return [[v, {"labels": l, "distances": d}] for v, l, d in zip(votes, lab, d_all)]
+    out = []
+    for dist, idx, ok in zip(d_all, i_all, valid):      # ragged rows (k > N) or labels that raise
+        sorted_y = y[idx[ok]]
+        out.append([vote(sorted_y), {"labels": sorted_y, "distances": dist[ok]}])
+    return out
+
+
 class NearestNeighbor(AbstractClassifier):
     """classifier.py:53-132 on the GPU."""
 
@@ -91,14 +123,7 @@ class NearestNeighbor(AbstractClassifier):
     def predict_batch(self, Q):
         """Predict a batch: Q is a list of features or a 2-D array [B, d]."""
         d_all, i_all = self.search(Q)
-        y = np.asarray(self.y)
-        out = []
-        for dist, idx in zip(d_all, i_all):
-            valid = idx >= 0
-            sorted_y = y[idx[valid]]
-            sorted_distances = dist[valid]
-            out.append([vote(sorted_y), {"labels": sorted_y, "distances": sorted_distances}])
-        return out
+        return results(d_all, i_all, self.y)
 
     def search(self, Q, k=None):
         """Top-k gallery rows of every query: (distances fp64 [B,k], gallery indices int64 [B,k]) on host."""

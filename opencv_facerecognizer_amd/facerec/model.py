@@ -15,7 +15,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from .classifier import AbstractClassifier, NearestNeighbor, vote
+from .. import _lib
+from .classifier import AbstractClassifier, NearestNeighbor, results
 from .feature import AbstractFeature, Fisherfaces, SpatialHistogram
 from .lbp import ExtendedLBP
 
@@ -94,17 +95,20 @@ class PredictableModel(object):
         if len(groups) == 1:
             C, cell, cb = self.feature.counts_batch(groups[0][1])
             return self.classifier.search_counts(C, cell, cb, k)
+        # a group whose cell size differs from the counts gallery's comes back on the host
+        # (search_counts' float path): every group's result goes to the gallery device
         B = len(X)
+        dev = _lib.device()
         d_all = i_all = None
         for sel, xs in groups:
             C, cell, cb = self.feature.counts_batch(xs)
             d, i = self.classifier.search_counts(C, cell, cb, k)
             if d_all is None:
-                d_all = torch.empty((B,) + tuple(d.shape[1:]), dtype=d.dtype, device=d.device)
-                i_all = torch.empty((B,) + tuple(i.shape[1:]), dtype=i.dtype, device=i.device)
-            idx = torch.tensor(sel, device=d.device)
-            d_all.index_copy_(0, idx, d.to(d_all.device))
-            i_all.index_copy_(0, idx, i.to(i_all.device))
+                d_all = torch.empty((B,) + tuple(d.shape[1:]), dtype=d.dtype, device=dev)
+                i_all = torch.empty((B,) + tuple(i.shape[1:]), dtype=i.dtype, device=dev)
+            idx = torch.tensor(sel, dtype=torch.int64, device=dev)
+            d_all.index_copy_(0, idx, d.to(dev, d_all.dtype))
+            i_all.index_copy_(0, idx, i.to(dev, i_all.dtype))
         return d_all, i_all
 
     def predict_batch(self, X):
@@ -119,13 +123,7 @@ class PredictableModel(object):
         if len(X) == 0:
             return []
         d_all, i_all = self.search_batch(X)
-        y = np.asarray(self.classifier.y)
-        out = []
-        for dist, idx in zip(d_all, i_all):
-            valid = idx >= 0
-            sorted_y = y[idx[valid]]
-            out.append([vote(sorted_y), {"labels": sorted_y, "distances": dist[valid]}])
-        return out
+        return results(d_all, i_all, self.classifier.y)
 
     def __repr__(self):
         feature_repr = repr(self.feature)

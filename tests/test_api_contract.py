@@ -157,3 +157,24 @@ def test_start_tier_policy_host_logic(monkeypatch):
     assert seen.count("f6") == 2 and seen.count("f6x2") == 2 * FloatGallery.REPROBE - 2
     monkeypatch.setenv("OFR_ADAPTIVE_TIER", "0")
     assert g.start_tier(4096) == "f6"
+
+
+def test_results_batch_equals_per_row_reference_vote():
+    """classifier.results (the batched classifier.py:113-129): the vectorised vote equals the
+    reference's per-query vote (most frequent label, ties -> smallest), ragged rows keep the loop."""
+    import numpy as np
+    from opencv_facerecognizer_amd.facerec.classifier import results, vote
+    r = np.random.default_rng(4)
+    y = r.integers(0, 5, 300)
+    for k in (1, 2, 3, 8, 16):
+        i_all = r.integers(0, 300, (200, k))
+        d_all = np.sort(r.random((200, k)), axis=1)
+        out = results(d_all, i_all, y)
+        for o, idx, dist in zip(out, i_all, d_all):
+            ref = max(dict((key, val) for key, val in enumerate(np.bincount(y[idx])) if val).items(),
+                      key=lambda kv: kv[1])[0]                      # classifier.py:121-123
+            assert o[0] == ref == vote(y[idx])
+            assert np.array_equal(o[1]["labels"], y[idx]) and np.array_equal(o[1]["distances"], dist)
+    i_all = np.array([[3, -1], [5, 7]])
+    out = results(np.ones((2, 2)), i_all, y)
+    assert np.array_equal(out[0][1]["labels"], y[[3]]) and len(out[0][1]["distances"]) == 1

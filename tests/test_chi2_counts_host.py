@@ -32,3 +32,6 @@ def test_non_count_rows_are_refused():
     C, cb = counts_of(np.array([[70000.0, 1.0]]), 1.0)
     assert cb == 4 and C.dtype == np.uint32
     assert counts_of(np.array([[300.0]]), 1.0, count_bytes=1) is None
+    # integer values past 32-bit counts are not a counts gallery (was StopIteration)
+    assert counts_of(np.array([[2.0 ** 33, 1.0]]), 1.0) is None
+    assert infer_count_denom(np.array([[2.0 ** 33, 1.0]])) is None

@@ -152,3 +152,24 @@ def test_lbph_model_pickle_update_and_float_queries(golden, tmp_path):
     Qf = Qh * (1.0 + 1e-3)
     d, i = m2.classifier.search(Qf)
     _check_search("ChiSquareDistance", Qf, Gh, d, i, K)
+
+
+def test_lbph_model_mixed_size_batch(golden):
+    """a batch of faces of two sizes (the reference predicts any size, one face at a time)
+    is grouped by size; the 136 x 136 group has 17 x 17-pixel cells (a different count width and
+    denominator than the counts gallery: the float path on the host) -- results equal per-face
+    predict, in the batch's order."""
+    X, y, qry, gimg, ghist = _faces(golden)
+    model = _model()
+    model.compute(list(X), y)
+    r = np.random.Generator(np.random.PCG64(5))
+    big = [np.clip(np.kron(q[::16, ::16].astype(np.float64), np.ones((17, 17))) + r.normal(0, 8, (136, 136)),
+                   0, 255).astype(np.uint8) for q in qry[:6]]
+    batch = [qry[0], big[0], qry[1], big[1], big[2], qry[2], gimg[0], big[3]]
+    got = model.predict_batch(batch)
+    assert len(got) == len(batch)
+    for g, f in zip(got, batch):
+        w = model.predict(f)
+        assert g[0] == w[0]
+        assert np.array_equal(g[1]["labels"], w[1]["labels"])
+        assert np.allclose(g[1]["distances"], w[1]["distances"], rtol=1e-12, atol=0)
