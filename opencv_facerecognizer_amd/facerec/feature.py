@@ -306,8 +306,10 @@ def lda_eigen(Sw, Sb, num_components, solver=None, device_out=False):
             V = V / np.linalg.norm(V, axis=0)
             return lam[order], (_device.f64_dev(np.ascontiguousarray(V)) if device_out else V)
     try:
-        iSw = np.linalg.inv(Sw)
+        iSw = None if _numerically_singular(Sw) else np.linalg.inv(Sw)
     except np.linalg.LinAlgError:
+        iSw = None
+    if iSw is None:
         lam, V = _lda_singular_sw(Sw, Sb, m)
     else:
         evals, evecs = np.linalg.eig(iSw @ Sb)
@@ -316,14 +318,22 @@ def lda_eigen(Sw, Sb, num_components, solver=None, device_out=False):
     return lam, (_device.f64_dev(np.ascontiguousarray(V)) if device_out else V)
 
 
+def _numerically_singular(Sw):
+    """sigma_min(Sw) <= 16 n eps sigma_max(Sw): inv(Sw) is then rounding noise (2-norm condition
+    beyond 1 / (16 n eps))."""
+    sv = np.linalg.svd(np.asarray(Sw, np.float64), compute_uv=False)
+    return sv.size > 0 and not (sv[-1] > 16 * sv.size * np.finfo(np.float64).eps * sv[0])
+
+
 def _lda_singular_sw(Sw, Sb, m):
-    """feature.py:170 when inv(Sw) hits an exactly zero pivot.
+    """feature.py:170 when Sw is singular to working precision (``_numerically_singular``, or inv(Sw)
+    meets an exactly zero pivot).
 
     Sw is singular whenever the within-class deviations span fewer than the PCA(n - c) dimensions
     it lives in -- e.g. two identical images in one class: the bundled data set holds one such pair
     (steve_crop0.jpg == steve_crop5.jpg), so the reference's own inv(Sw) there inverts rounding noise
-    (its last LU pivot is ~1 ulp of the matrix), and whether that noise is exactly zero depends on
-    the last bits of the PCA features.  The reference's result with a vanishing POSITIVE pivot is
+    (its last LU pivot is ~1 ulp of the matrix): its non-dominant columns are set by that noise, and
+    whether the noise is exactly zero (inv raises) depends on the last bits of the PCA features.  The reference's result with a vanishing POSITIVE pivot is
     the generalized problem Sb v = lambda Sw v: the null directions of Sw come first with an
     infinite eigenvalue, the rest are the finite generalized eigenpairs -- the same columns the
     reference's inv + eig converge to.  Solved by QZ (scipy.linalg.eig(Sb, Sw), LAPACK dggev);
@@ -342,7 +352,7 @@ def _lda_singular_sw(Sw, Sb, m):
     V = V[:, idx].real
     nrm = np.linalg.norm(V, axis=0)
     V = V / np.where(nrm > 0, nrm, 1.0)
-    warnings.warn("LDA: Sw is singular (inv(Sw) failed, feature.py:170); %d null direction(s) of Sw ranked "
+    warnings.warn("LDA: Sw is singular to working precision (feature.py:170); %d null direction(s) of Sw ranked "
                   "first (generalized eigenproblem, QZ)" % int(inf.sum()))
     return lam[idx], V
 

@@ -53,8 +53,10 @@ def stream_churn():
         del s
 
 
-def run_chain(imgs, y):
+def run_chain(imgs, y, perm=None):
     from opencv_facerecognizer_amd import ingest, training
+    if perm is not None:
+        imgs, y = [imgs[i] for i in perm], y[perm]
     X = ingest.faces(imgs, (70, 70), ingest.INTER_LINEAR)
     Xh = X.cpu().numpy().reshape(len(imgs), -1)
     Xd = torch.from_numpy(Xh).cuda()
@@ -106,6 +108,18 @@ def main():
                "Sw_min_abs_pivot": float(np.abs(np.diag(lu)).min()), "Sw_eig_min_max": [float(ev[0]), float(ev[-1])],
                "inv_ok_by_alignment": inv_trials(cur["Sw"])}
         print(json.dumps(rec), flush=True)
+    # row orders (TheTrainer.read_images follows os.walk / os.listdir, which differ between file
+    # systems): does the reference's inv(Sw) meet an exactly zero pivot for some order?
+    r = np.random.default_rng(0)
+    fails = []
+    for t in range(32):
+        perm = r.permutation(len(y))
+        Sw = run_chain(imgs, y, perm)["Sw"]
+        try:
+            np.linalg.inv(Sw)
+        except np.linalg.LinAlgError:
+            fails.append(t)
+    print(json.dumps({"row_orders": 32, "inv_raised_for_orders": fails}), flush=True)
 
 
 if __name__ == "__main__":
