@@ -512,6 +512,24 @@ class FloatGallery:
             return None
         return w.buf[off:off + 4 * B].view(torch.int32)
 
+    SIEVE_CAP = 32768          # q8s::SIEVE_CAP: bucket slots per query
+
+    def sieve_state(self, B, workspace=None):
+        """The last fp6 sieve pass's per-query state on `workspace` (device views, B > 32): thresholds
+        theta (uint32 order keys as int32 [B]; the kernel keeps a row iff !(score > key_float(theta |
+        0xff))), counts [B] (rows that passed; > cap = overflow) and buckets [B][cap] of (truncated
+        score fp32, row int32) pairs.  Layout of ofr_knn_f6's workspace (theta, count, bucket regions,
+        each 256-byte aligned)."""
+        off = _lib.load().ofr_knn_f6_sieve_counts_offset(B, self.N)
+        w = workspace or self.ws
+        if off == ctypes.c_size_t(-1).value or w.buf is None:
+            return None
+        step = round_up(4 * B, 256)
+        theta = w.buf[off - step:off - step + 4 * B].view(torch.int32)
+        count = w.buf[off:off + 4 * B].view(torch.int32)
+        raw = w.buf[off + step:off + step + B * self.SIEVE_CAP * 8].view(torch.int32).view(B, self.SIEVE_CAP, 2)
+        return theta, count, raw[:, :, 0].view(torch.float32), raw[:, :, 1]
+
     def fallback(self, Qd, qq, k, out, index_base=0, timings=None):
         """Re-run the queries the first tier left uncertified down the tier chain (then fp32).
         Returns the number of first-tier failures (host sync); self.last_fallbacks = the number of

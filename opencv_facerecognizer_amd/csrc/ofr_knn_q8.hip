@@ -1506,14 +1506,12 @@ extern "C" const char* ofr_f6_sieve_kernel(void) {
 // Engine of the sieve pass: 384 = v_mfma_scale_f32_16x16x128 on 384 x 256 tiles, one wave per SIMD
 // (f6t::EngineW, default since round 3: 22.2 -> 20.1 ms, tools/f6_probe.hip WIDE); 16 = the same MFMA on
 // 256 x 256 tiles, 8 waves (f6t::Engine16, OFR_F6_SHAPE=16; also the two-slice tier's engine); 32 = the
-// 32x32x64 engine (OFR_F6_SHAPE=32)
+// 32x32x64 engine (OFR_F6_SHAPE=32).  Read at every call (the workspace does not depend on it), so a
+// test can run both sieve engines in one process.
 static int f6_shape() {
-  static const int s = [] {
-    const char* e = getenv("OFR_F6_SHAPE");
-    const int v = e ? atoi(e) : 0;
-    return v == 32 || v == 16 ? v : 384;
-  }();
-  return s;
+  const char* e = getenv("OFR_F6_SHAPE");
+  const int v = e ? atoi(e) : 0;
+  return v == 32 || v == 16 ? v : 384;
 }
 
 // gallery tiles per tile group of the wide sieve pass (i8t::tile_coords): 2, so the ~32 workgroups

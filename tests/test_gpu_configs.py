@@ -460,3 +460,102 @@ def test_sharded_training_equals_single_process():
     assert np.array_equal(res[0][1], np.asarray(ff._eigenvalues))
     F = np.stack([np.asarray(f).reshape(-1) for f in feats])
     assert np.allclose(np.concatenate([res[0][2], res[1][2]]), F, rtol=0, atol=1e-9 * np.abs(F).max())
+
+
+@pytest.mark.timeout(300)
+def test_projection_bench_shape_vs_float64():
+    """the projection at the bench shape (B = 4,096 faces, D = 10,000, d = 9,999 --
+    the 1,680-tile grid of the wide int8 engine, feature.py:241-242) against float64 X @ W on the
+    host for 64 sampled faces (not the device's own f64 path), the shifted fp32 search rows (the
+    bench's form: W^T x - c rounded once) against the same float64 reference, and the batch's
+    faces being independent of their position in the batch (a slice projected alone)."""
+    from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_projection
+    dev = torch.device("cuda", 0)
+    D, d, B = 10000, 9999, 4096
+    P, Wt = build_projection(D, d, dev)
+    bank = IdentityBank(100_000, 100, 100, device=dev)
+    gq = torch.Generator(device=dev)
+    gq.manual_seed(SEED + 7)
+    X = bank.images(torch.randint(0, 100_000, (B,), generator=gq, device=dev), seed=SEED + 99)
+    X[17] = 255                                                  # saturated and empty faces
+    X[18] = 0
+    c = torch.from_numpy(np.random.default_rng(3).normal(0, 2, d)).to(dev)
+    Y64 = P.project(X, f64=True)
+    Y32 = P.project(X, shift64=c)
+    torch.cuda.synchronize()
+    s = np.unique(np.concatenate([[0, 17, 18, 255, 256, 4095], np.random.default_rng(8).choice(B, 58, replace=False)]))
+    W = Wt.double().cpu().numpy().T                              # D x d, the fp32 weights in float64
+    Xs = X[torch.from_numpy(s).to(dev)].cpu().numpy().reshape(len(s), -1).astype(np.float64)
+    ref = Xs @ W
+    got = Y64[torch.from_numpy(s).to(dev)].cpu().numpy()
+    nrm = np.maximum(np.linalg.norm(ref, axis=1), 1.0)
+    err = np.abs(got - ref).max(axis=1) / nrm
+    assert err.max() < 1e-7, (err.max(), s[np.argmax(err)])
+    ref32 = (ref - c.cpu().numpy()).astype(np.float32)
+    got32 = Y32[torch.from_numpy(s).to(dev)].cpu().numpy()[:, :d]
+    tol = 2.0 ** -23 * np.abs(ref - c.cpu().numpy()) + 1e-7 * nrm[:, None]
+    assert np.all(np.abs(got32.astype(np.float64) - ref32.astype(np.float64)) <= tol)
+    # a slice of the batch projected alone gives the same bits (no dependence on the tile position)
+    part = P.project(X[1000:1300], f64=True)
+    assert torch.equal(part, Y64[1000:1300])
+
+
+@pytest.mark.timeout(600)
+def test_config3_lbph_chi2_full_size():
+    """BASELINE configs[3] at its own size (VERDICT r3 missing #3): ExtendedLBP(1, 8) + SpatialHistogram
+    8x8 of 65,536 gallery faces at 128 x 128 and 4,096 query faces, ChiSquare 1-NN (feature.py:286-302,
+    distance.py:112-116, classifier.py:104-119).  Histograms bit-exact against the oracle for sampled
+    faces; every query certified by the fp16-MFMA pass; identity accuracy; 32 sampled queries against
+    the oracle's chi-square over the whole gallery (a device fp64 shortlist of the reference formula,
+    then the oracle on the shortlist and on the returned row), with the near-tie rule of _check_search."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import Chi2Gallery
+    from opencv_facerecognizer_amd.facerec.feature import SpatialHistogram
+    from opencv_facerecognizer_amd.facerec.lbp import ExtendedLBP
+    from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank
+    dev = torch.device("cuda", 0)
+    N, B, H, per = 65536, 4096, 128, 8
+    bank = IdentityBank(N // per, H, H, device=dev)
+    G_img = bank.images(torch.arange(N, device=dev) // per, seed=SEED + 11).reshape(N, H, H)
+    gq = torch.Generator(device=dev)
+    gq.manual_seed(SEED + 12)
+    ids_q = torch.randint(0, N // per, (B,), generator=gq, device=dev)
+    Q_img = bank.images(ids_q, seed=SEED + 13).reshape(B, H, H)
+    sh = SpatialHistogram(ExtendedLBP(1, 8), (8, 8))
+    gc, cell, cb = sh.counts_device(G_img)
+    qc, _, _ = sh.counts_device(Q_img)
+    assert cell == 225 and cb == 1
+    nb = gc.shape[1] * gc.shape[2]
+    for i in (0, 4097, 65535):                                   # bit-exact histograms (feature.py:298-299)
+        assert np.array_equal(gc[i].reshape(-1).cpu().numpy() / 225.0, O.spatial_histogram(G_img[i].cpu().numpy()))
+    assert np.array_equal(qc[7].reshape(-1).cpu().numpy() / 225.0, O.spatial_histogram(Q_img[7].cpu().numpy()))
+    gal = Chi2Gallery(gc.reshape(N, nb), dtype=_lib.DT_U8, denom=float(cell), nbins=nb)
+    Qc = qc.reshape(B, nb).contiguous()
+    dd, ii = gal.search(Qc, 1)
+    torch.cuda.synchronize()
+    assert list(gal.last_fallbacks)[0] == 0, gal.last_fallbacks        # every query certified by the MFMA pass
+    acc = float(((ii[:, 0] // per) == ids_q).double().mean().item())
+    assert acc >= 0.99, acc
+    s = np.sort(np.random.default_rng(17).choice(B, 32, replace=False))
+    Gf = gc.reshape(N, nb)
+    short = []
+    for b in s:                                                   # device fp64 shortlist: best 8 rows
+        q = Qc[b].double() / 225.0
+        best = []
+        for c0 in range(0, N, 8192):
+            g = Gf[c0:c0 + 8192].double() / 225.0
+            dist = ((g - q) ** 2 / (g + q + np.finfo(np.float64).eps)).sum(1)
+            v, j = torch.topk(dist, 8, largest=False)
+            best.append(torch.stack([v, (j + c0).double()], 1))
+        allb = torch.cat(best)
+        short.append(allb[torch.argsort(allb[:, 0])[:8], 1].long().cpu().numpy())
+    dd_h, ii_h = dd.cpu().numpy()[:, 0], ii.cpu().numpy()[:, 0]
+    for b, cand in zip(s, short):
+        qh = Qc[b].cpu().numpy() / 225.0
+        rows = np.unique(np.append(cand, ii_h[b]))
+        ref = np.array([O.chisquare(Gf[j].cpu().numpy() / 225.0, qh) for j in rows])
+        o = np.lexsort((rows, ref))
+        best_row, best_d = rows[o[0]], ref[o[0]]
+        mine = ref[np.searchsorted(rows, ii_h[b])]
+        assert abs(dd_h[b] - mine) <= 1e-9 * mine, (b, dd_h[b], mine)             # exact re-rank of its row
+        assert ii_h[b] == best_row or mine <= best_d * (1 + 1e-4), (b, ii_h[b], best_row, mine, best_d)
