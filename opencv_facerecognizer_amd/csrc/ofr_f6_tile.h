@@ -66,13 +66,6 @@ __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-#ifdef OFR_F6_STAMPS
-// probe only (tools/f6_probe.hip, MODE 8388608): per (workgroup < STAMP_WG, wave) the summed cycles
-// of the sieve pass's stage phases (s_memtime), and the number of stages summed
-constexpr int STAMP_WG = 512, STAMP_N = 6;
-__device__ unsigned long long g_f6_stamps[STAMP_WG * 8 * STAMP_N];
-#endif
-
 // ---- passes over several segments of stages (the two-slice tier f6x2) -----------------------
 // NSEG = 1: stages [0, nst) of the gallery tiles G against the query tiles Q (tier f6).
 // NSEG = 3: stages [0, 3 nst) = the segments [x1 | x1 | x2] . [y1 | y2 | y1] of the two-slice rows
@@ -139,11 +132,8 @@ struct Engine {
 
   // Stage kt of gallery panel gp and query panel qp -> LDS stage buffer st: DMA_INS
   // wave-instructions of 1 KiB, the first half the gallery block, the second the query block.
-  // SKIP (probes only): 2 = no gallery block, 16 = no query block
-  // 128 = the same bytes loaded into the VGPRs *sink instead of LDS (probe: intake without LDS writes)
-  template <int SKIP = 0>
   static __device__ __forceinline__ void dma(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst,
-                                             int kt, char* st, i32x4* sink = nullptr) {
+                                             int kt, char* st) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const char* gb = G + (gp * nst + kt) * (int64_t)PANEL;
     const char* qb = Q + (qp * nst + kt) * (int64_t)PANEL;
@@ -152,41 +142,18 @@ struct Engine {
       const int ins = wave * IPW + t;   // gallery: ins < 24 (a wave's instructions never straddle)
       const bool gal = ins < DMA_INS / 2;
       const int off = (gal ? ins : ins - DMA_INS / 2) * 1024;
-      if (((SKIP & 2) && gal) || ((SKIP & 16) && !gal)) continue;
-      if constexpr ((SKIP & 128) != 0) {
-        asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(*sink) : "v"((gal ? gb : qb) + off + lane * 16) : "memory");
-        continue;
-      }
       __builtin_amdgcn_global_load_lds((const OFR_GLOBAL void*)((gal ? gb : qb) + off + lane * 16),
                                        (OFR_LDS void*)(st + (gal ? 0 : PANEL) + off), 16, 0, 0);
     }
   }
 
-  // The same copy by MUBUF buffer_load ... lds (probe: Engine16 MODE 1024).  A FLAT global_load_lds in
-  // flight makes the compiler's waitcnt pass treat LDS reads as unordered (every first use of a fresh
-  // fragment then waits lgkmcnt(0)); the buffer form keeps them counted.  One descriptor per operand
-  // panel (nst stages, < 2^32 bytes), voffset = stage + instruction + lane.
-  static __device__ __forceinline__ void dma_buf(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst,
-                                                 int kt, char* st) {
-    // the wave index as a scalar: the descriptor choice below must be uniform (no waterfall loop)
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-    const int pb = (int)(nst * PANEL);
-    __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(G + gp * nst * (int64_t)PANEL), 0, pb,
-                                                                  0x00020000);
-    __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * nst * (int64_t)PANEL), 0, pb,
-                                                                  0x00020000);
-#pragma unroll
-    for (int t = 0; t < IPW; ++t) {
-      const int ins = wave * IPW + t;
-      const bool gal = ins < DMA_INS / 2;
-      const int off = (gal ? ins : ins - DMA_INS / 2) * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(gal ? rg : rq, (OFR_LDS void*)(st + (gal ? 0 : PANEL) + off), 16,
-                                               kt * PANEL + off + lane * 16, 0, 0, 0);
-    }
-  }
-
-  // probe only: the same copies issued by waves 0-3 alone (12 pieces each), waves 4-7 issue none
-  template <int T0 = 0, int T1 = 2 * IPW>
+  // The same copies by MUBUF buffer_load ... lds, issued by waves 0-3 alone (12 pieces each; waves
+  // 4-7 issue none, so one wave of every SIMD keeps the matrix pipe fed while the other pays the
+  // copies' issue cost: Engine16's loop).  A FLAT global_load_lds in flight makes the compiler's
+  // waitcnt pass treat LDS reads as unordered (every first use of a fresh fragment then waits
+  // lgkmcnt(0)); the buffer form keeps them counted.  One descriptor per operand panel (nst stages,
+  // < 2^32 bytes), voffset = stage + instruction + lane; the wave index is scalar, so the
+  // descriptor choice stays uniform (no waterfall loop).
   static __device__ __forceinline__ void dma_buf4(const char* G, int64_t gp, const char* Q, int64_t qp, int64_t nst,
                                                   int kt, char* st) {
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
@@ -197,7 +164,7 @@ struct Engine {
     __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * nst * (int64_t)PANEL), 0, pb,
                                                                   0x00020000);
 #pragma unroll
-    for (int t = T0; t < T1; ++t) {
+    for (int t = 0; t < 2 * IPW; ++t) {
       const int ins = wave * 2 * IPW + t;
       const bool gal = ins < DMA_INS / 2;
       const int off = (gal ? ins : ins - DMA_INS / 2) * 1024;
@@ -225,123 +192,6 @@ struct Engine {
     if constexpr (MF - two - one > 0) __builtin_amdgcn_sched_group_barrier(0x008, MF - two - one, 0);
   }
 
-  // Deep-staged main loop (NW = 8; tile_kernel_f6 MODE bit 32).  The buffers hold 64-feature
-  // half-stages (one MFMA k-step: 12 KiB of each panel block, 24 KiB per buffer), six of them, so a
-  // half-stage's copy is issued five half-stages (120 KiB) ahead of its reads; a 16x16x128 fragment
-  // spans 128 features and could not start before both halves of its stage landed, the 32x32x64
-  // fragment of this engine needs one half.  The 24 copy pieces of a half-stage: 3 per wave (MUBUF,
-  // branch-free, so the k loop stays one scheduling region).  Per
-  // half-stage u: wait for the own copies of u+1, s_barrier (every wave has consumed the fragments
-  // of u-1 and read those of u: buffers u-1 and u are free), copy u+5 into buffer (u+5) % 6 =
-  // (u-1) % 6, then u's 8 MFMAs with u+1's 6 fragments read between them (fragments double-buffered
-  // by parity).
-  template <int NSEG = 1>
-  static __device__ __forceinline__ void mainloop_deep(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
-                                                       int nst, f32x16 (&acc)[4][CT], const char* G2 = nullptr,
-                                                       const char* Q2 = nullptr) {
-    static_assert(NW == 8, "deep-staged loop: 8 waves");
-    constexpr int HB = PANEL / 2;                   // one operand's half-stage
-    constexpr int DST = 2 * HB;                     // 24 KiB per buffer
-    constexpr int NBUF = 6, LEAD = NBUF - 1;        // 144 KiB
-    constexpr int HPW = DST / 1024 / NW;            // copy pieces per wave (3)
-    static_assert(NBUF * DST <= LDS, "fits the kernel's LDS");
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
-    const int wu = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < CT; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const int last = 2 * NSEG * nst - 1;            // half-stages
-    const int pb = (int)(nst * PANEL);
-    auto issue = [&](int u) {
-      const int uu = u < last ? u : last;
-      const char *g, *q;
-      int ks;
-      seg_src<NSEG>(uu >> 1, nst, G, G2, Q, Q2, g, q, ks);
-      __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(g + gp * nst * (int64_t)PANEL), 0, pb,
-                                                                    0x00020000);
-      __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)(q + qp * nst * (int64_t)PANEL), 0, pb,
-                                                                    0x00020000);
-      char* st = smem + (u % NBUF) * DST;
-      const int src = ks * PANEL + (uu & 1) * HB;
-#pragma unroll
-      for (int t = 0; t < HPW; ++t) {
-        const int ins = wu * HPW + t;               // waves 0-3: gallery, 4-7: queries
-        const bool gal = ins < DST / 2048;
-        const int off = (gal ? ins : ins - DST / 2048) * 1024;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(gal ? rg : rq, (OFR_LDS void*)(st + (gal ? 0 : HB) + off), 16,
-                                                 src + off + lane * 16, 0, 0, 0);
-      }
-    };
-#pragma unroll
-    for (int u = 0; u < LEAD; ++u) issue(u);
-    i32x6 ga[2][4], qb[2][CT];
-    auto frag6 = [&](const char* blk, int row) {    // sub-block h of the half-stage image
-      const char* sb = blk + h * 6144;
-      const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + p1_slot(h, row) * 8);
-      asm volatile("" : "+v"(p1a));
-      const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
-      const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
-      i32x6 f;
-      f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
-      return f;
-    };
-    auto frags = [&](int u, int set) {
-      const char* st = smem + (u % NBUF) * DST;
-#pragma unroll
-      for (int c = 0; c < CT; ++c) qb[set][c] = frag6(st + HB, wc * QW + c * 32 + r32);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ga[set][i] = frag6(st, wr * 128 + i * 32 + r32);
-    };
-    int sa = SCALE_ONE, sb = SCALE_ONE;
-    auto mfmas = [&](int set) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          const i32x8 a8 = __builtin_shufflevector(ga[set][i], ga[set][i], 0, 1, 2, 3, 4, 5, -1, -1);
-          const i32x8 b8 = __builtin_shufflevector(qb[set][c], qb[set][c], 0, 1, 2, 3, 4, 5, -1, -1);
-          acc[i][c] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[i][c], 2, 2, 0, sa, 0, sb);
-        }
-    };
-    wait_vm<(LEAD - 1) * HPW>();                    // own copies of half-stage 0 landed
-    barrier();
-    frags(0, 0);
-    // one half-stage; SET (compile time: register arrays indexed by constants) = u & 1
-    auto step = [&](int u, auto setc) {
-      constexpr int SET = decltype(setc)::value;
-      seg_scales<NSEG>(u >> 1, nst, sa, sb);
-      wait_vm<(LEAD - 2) * HPW>();                  // own copies of u+1 landed (u+2 .. u+4 may fly)
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      issue(u + LEAD);
-      __builtin_amdgcn_sched_barrier(0);
-      frags(u + 1, SET ^ 1);                        // u = last: unused reads of a stale buffer
-      mfmas(SET);
-      // 8 MFMAs with the 12 fragment reads between them: two after each of the first four, one after the next four
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    for (int u = 0; u <= last; u += 2) {            // last + 1 = 2 NSEG nst half-stages: even
-      step(u, std::integral_constant<int, 0>{});
-      step(u + 1, std::integral_constant<int, 1>{});
-    }
-    wait_vm<0>();
-    barrier();
-  }
-
   // Main loop, stage hand-off in the middle of a stage.  Per stage kt:
   //   A: fragments (kt, j=1) read between the MFMAs of (kt, j=0)
   //   wait for stage kt+1 to land, barrier (every wave has read all of stage kt)
@@ -351,9 +201,8 @@ struct Engine {
   // the matrix pipe still drains the previous block (2 % faster than a hand-off at the stage
   // boundary, which exposes the step-0 reads after every barrier: tools/f6_probe.hip).
   // Fragments double-buffered by j; 3 LDS stages (kt+1 read next, kt+2 and kt+3 in flight).
-  // MODE (probes): 1 = no k-loop DMA, 2 / 16 = no gallery / query block in the DMA.
   // NSEG: segments of nst stages each (seg_src); G2 / Q2 only for NSEG = 3
-  template <int MODE, int NSEG = 1>
+  template <int NSEG = 1>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
                                                   int nst, f32x16 (&acc)[4][CT], const char* G2 = nullptr,
                                                   const char* Q2 = nullptr) {
@@ -370,7 +219,7 @@ struct Engine {
       const char *g, *q;
       int ks;
       seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
-      dma<MODE & 18>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+      dma(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
     };
     // branch-free: a stage past the end re-loads the last one onto itself (same bytes)
     const int last = NSEG * nst - 1;
@@ -395,8 +244,7 @@ struct Engine {
                                                                       sa, 0, sb);
     };
 
-    if constexpr (MODE == 1) wait_vm<0>();
-    else wait_vm<2 * IPW>();   // stage 0 landed; 1 and 2 may be in flight
+    wait_vm<2 * IPW>();   // stage 0 landed; 1 and 2 may be in flight
     barrier();
     frags(smem, 0);
     for (int kt = 0; kt < last; ++kt) {
@@ -404,10 +252,9 @@ struct Engine {
       frags(smem + (kt % NST) * STAGE, 1);
       mfmas(0);
       interleave();
-      if constexpr (MODE == 1) wait_vm<0>();
-      else wait_vm<IPW>();     // stage kt+1 landed; kt+2 may be in flight
+      wait_vm<IPW>();     // stage kt+1 landed; kt+2 may be in flight
       barrier();
-      if constexpr (MODE != 1) {
+      {
         const int nx = kt + NST;
         issue(nx < last ? nx : last);
       }
@@ -440,22 +287,15 @@ struct Engine16 {
   static constexpr int IPW = DMA_INS / NW;   // 6
 
   // fragments live as 6 registers (the fp6 MFMA reads v[0:5] of its 8-register operand slot)
-  // P1 = false (probe only, wrong results): the part1 read skipped -- the cost of the second LDS read
-  template <bool P1 = true>
   static __device__ __forceinline__ i32x6 frag16(const char* st, int row) {
     const int q = (threadIdx.x & 63) >> 4;
     const char* sb = st + q * 6144;
     i32x6 f;
-    if constexpr (P1) {
-      const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + p1_slot(q, row) * 8);
-      asm volatile("" : "+v"(p1a));
-      const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
-      const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
-      f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
-    } else {
-      const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
-      f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p0[0]; f[5] = p0[1];
-    }
+    const OFR_LDS char* p1a = (const OFR_LDS char*)(sb + 4096 + p1_slot(q, row) * 8);
+    asm volatile("" : "+v"(p1a));
+    const i32x4 p0 = *reinterpret_cast<const i32x4*>(sb + row * 16);
+    const i32x2 p1 = *reinterpret_cast<const OFR_LDS i32x2*>(p1a);
+    f[0] = p0[0]; f[1] = p0[1]; f[2] = p0[2]; f[3] = p0[3]; f[4] = p1[0]; f[5] = p1[1];
     return f;
   }
   static __device__ __forceinline__ f32x4 mfma(const i32x6& a, const i32x6& b, const f32x4& c, int sa = SCALE_ONE,
@@ -464,439 +304,92 @@ struct Engine16 {
     const i32x8 b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, 4, 5, -1, -1);
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 2, 2, 0, sa, 0, sb);
   }
-  // probe only (MODE 256): the accumulators pinned to AGPRs through an asm MFMA (the compiler
-  // cannot see its latency: the probe drains the pipe with s_nops before reading them)
-  static __device__ __forceinline__ void mfma_agpr(const i32x6& a, const i32x6& b, f32x4& c, int sc) {
-    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
-                 : "+a"(c) : "v"(a), "v"(b), "v"(sc));
-  }
 
-  // Asymmetric main loop (tile_kernel_f6s MODE bit 16777216).  Stamped timelines of the library
-  // loop (profiles/r03_f6_probe_stamps.log) show the wave of a SIMD that issues the stage copies
-  // blocked ~650-840 cycles per stage in their issue (the per-CU copy path back-pressures), while the
-  // other wave runs out of MFMAs and waits ~530 cycles at the next barrier.  Here the two waves of
-  // SIMD p (p and p + 4) share the 256-gallery-row x 64-query strip p unevenly: the copy-issuing wave
-  // p takes gallery row blocks 0 .. NIA-1, wave p + 4 the other 16 - NIA, so the matrix pipe has the
-  // second wave's MFMAs to run while the first issues copies.  The larger share does not fit the
-  // register file with a full fragment set, so both waves read their gallery fragments just in time
-  // through a ring of RING fragments (the query fragments, 4, for the whole stage); a stage's buffer
-  // is therefore read during that stage, and the copy of stage kt + 2 goes into the buffer of stage
-  // kt - 1 after the top barrier of stage kt (every wave drained its reads of kt - 1 before it):
-  // two stages of copy lead, 3 buffers.
-  //   top of stage kt: (issuing waves) own copies of kt landed -> s_barrier -> issuing waves: copy
-  //   kt + 2 -> query fragments of kt, ring prefill -> rows: per row the next ring read + 4 MFMAs ->
-  //   lgkmcnt(0).
-  template <int NI, bool ISSUE, int NSEG = 1>
-  static __device__ __forceinline__ void mainloop_as(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
-                                                     int nst, int row0, f32x4 (&acc)[NI][NB],
-                                                     const char* G2 = nullptr, const char* Q2 = nullptr) {
-    constexpr int RING = 4;
-    static_assert(NI >= RING, "ring");
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int p = wave & 3, r16 = lane & 15;
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int last = NSEG * nst - 1;
-    auto issue = [&](int kt) {   // waves 0-3 (the ISSUE role): 12 pieces each
-      if constexpr (ISSUE) {
-        const char *g, *q;
-        int ks;
-        const int s = kt < last ? kt : last;
-        seg_src<NSEG>(s, nst, G, G2, Q, Q2, g, q, ks);
-        Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
-      }
-    };
-    static_assert(NST == 3, "three stage buffers");
-    issue(0);
-    issue(1);
-    i32x6 a[RING], b[NB];
-    int sa = SCALE_ONE, sb = SCALE_ONE;
-    for (int kt = 0; kt <= last; ++kt) {
-      seg_scales<NSEG>(kt, nst, sa, sb);
-      if constexpr (ISSUE) wait_vm<2 * IPW>();   // own copies of stage kt landed (kt + 1 may fly)
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      const char* st = smem + (kt % NST) * STAGE;
-#pragma unroll
-      for (int c = 0; c < NB; ++c) b[c] = frag16(st + PANEL, p * QW + c * 16 + r16);
-#pragma unroll
-      for (int j = 0; j < RING - 1; ++j) a[j] = frag16(st, row0 + j * 16 + r16);
-      __builtin_amdgcn_sched_barrier(0);
-      issue(kt + 2);                  // into the buffer of stage kt - 1 (its reads drained below)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        if (i + RING - 1 < NI) a[(i + RING - 1) % RING] = frag16(st, row0 + (i + RING - 1) * 16 + r16);
-#pragma unroll
-        for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i % RING], b[c], acc[i][c], sa, sb);
-      }
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (i + RING - 1 < NI) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every read of stage kt done before the next barrier
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    wait_vm<0>();
-    barrier();
-  }
-
-  // Ping-pong main loop (probe MODE 524288).  The two waves of a SIMD (groups g = wr: waves 0-3 and
-  // 4-7; the cyclic wave -> SIMD order puts one of each on every SIMD) run one s_barrier apart, so one
-  // issues its 32 MFMAs (raised priority) while the other reads its 12 fragments of the next stage
-  // and issues its 6 stage copies.  Per stage j a wave runs LOAD(j) (fragment reads of stage j, the
-  // copy of stage j + 2 into the buffer of stage j - 1, the wait for its copies of stage j + 1,
-  // lgkmcnt(0)) and MFMA(j), each closed by an s_barrier.  H(n) = the n-th barrier: group 0 closes
-  // LOAD(j) at H(2j+1) and MFMA(j) at H(2j+2), group 1 one barrier later.
-  //   visibility: every wave waits for its copies of stage j+1 before closing LOAD(j), i.e. by
-  //     H(2j+2); the first reader of stage j+1 (group 0, LOAD(j+1)) starts after H(2j+2);
-  //   reuse: the last reads of stage j-1 (group 1, LOAD(j-1), drained by lgkmcnt(0) before H(2j))
-  //     precede the earliest copy into its buffer (group 0, LOAD(j), after H(2j)).
+  // Main loop (round 2-3 measurements in DESIGN.md §5: 23.3 -> 22.5 ms for the split barrier and the
+  // MUBUF copies, 23.1 -> 22.6 ms for the copies issued by waves 0-3 alone).  The stage copies are
+  // MUBUF buffer_load ... lds pieces issued by waves 0-3 (Engine<8>::dma_buf4), so no FLAT instruction
+  // is ever in flight and the compiler counts the LDS reads.  Two barriers per stage kt:
+  //   top: stage kt+1 landed (own copies: vmcnt) and visible (s_barrier) -- no LDS drain;
+  //   after row 0 (whose refill a[0] is the only LDS read issued so far in the stage): lgkmcnt(2)
+  //   (every read of stage kt's buffer, all issued in stage kt-1, is done) + s_barrier, then stage
+  //   kt+3's copy into that buffer: 1.9 stages of copy lead out of three buffers.
+  // Per stage the MFMAs of stage kt, each fragment replaced by stage kt+1's as soon as its last MFMA
+  // is issued (A-major: a[i] after row i's 4 MFMAs, b[c] after row 7's MFMA c), so the fragments
+  // need no second register set (acc 128 + fragments 72 registers).
   template <int NSEG = 1>
-  static __device__ __forceinline__ void mainloop_pp(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
-                                                     int nst, f32x4 (&acc)[NA][NB], const char* G2 = nullptr,
-                                                     const char* Q2 = nullptr) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int wr = wave / WQ, wc = wave % WQ, r16 = lane & 15;
-    const bool late = __builtin_amdgcn_readfirstlane(wr) != 0;
-#pragma unroll
-    for (int i = 0; i < NA; ++i)
-#pragma unroll
-      for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int last = NSEG * nst - 1;
-    auto issue = [&](int kt) {
-      const char *g, *q;
-      int ks;
-      const int s = kt < last ? kt : last;
-      seg_src<NSEG>(s, nst, G, G2, Q, Q2, g, q, ks);
-      Engine<8>::dma_buf(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
-    };
-    static_assert(NST == 3, "ping-pong assumes 3 stages");
-    issue(0);
-    issue(1);
-    wait_vm<IPW>();                 // own copies of stage 0 landed (1 may fly)
-    __builtin_amdgcn_s_barrier();   // H(0)
-    if (late) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    i32x6 a[NA], b[NB];
-    int sa = SCALE_ONE, sb = SCALE_ONE;
-    for (int kt = 0; kt <= last; ++kt) {
-      // LOAD(kt)
-      const char* st = smem + (kt % NST) * STAGE;
-#pragma unroll
-      for (int c = 0; c < NB; ++c) b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16);
-#pragma unroll
-      for (int i = 0; i < NA; ++i) a[i] = frag16(st, wr * 128 + i * 16 + r16);
-      issue(kt + 2);                // into the buffer of stage kt - 1
-      seg_scales<NSEG>(kt, nst, sa, sb);
-      wait_vm<IPW>();               // own copies of stage kt+1 landed (kt+2 may fly)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      // MFMA(kt)
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < NA; ++i)
-#pragma unroll
-        for (int c = 0; c < NB; ++c) acc[i][c] = mfma(a[i], b[c], acc[i][c], sa, sb);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (!late) __builtin_amdgcn_s_barrier();   // equal barrier counts for both groups
-    wait_vm<0>();
-    barrier();
-  }
-
-  // MODE (probes): 1 = no k-loop DMA; 64 = DMA issued but never waited for (wrong results: isolates
-  // the cost of waiting for the DMA from that of moving its bytes); 128 = the k-loop's stage loads
-  // land in VGPRs, not LDS (wrong results: the feed's bytes without its LDS writes)
-  template <int MODE, int NSEG = 1>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
                                                   int nst, f32x4 (&acc)[NA][NB], const char* G2 = nullptr,
                                                   const char* Q2 = nullptr) {
-    static_assert(NSEG == 1 || (MODE & 256) == 0, "the AGPR probe runs one segment");
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr = wave / WQ, wc = wave % WQ, r16 = lane & 15;
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll
       for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    i32x4 sink = {0, 0, 0, 0};
+    const int last = NSEG * nst - 1;
     auto issue = [&](int kt) {
       const char *g, *q;
       int ks;
       seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
-      Engine<8>::dma<0>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
+      Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
     };
-    auto issue_k = [&](int kt) {
+#pragma unroll
+    for (int s = 0; s < NST; ++s) {   // buffer s takes stage min(s, last)
       const char *g, *q;
       int ks;
-      seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
-      Engine<8>::dma<MODE & 128>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE, &sink);
-    };
-    const int last = NSEG * nst - 1;
-#pragma unroll
-    for (int s = 0; s < NST; ++s) {
-      if constexpr ((MODE & 1024) != 0) {   // no FLAT DMA anywhere in the probe variant
-        const char *g, *q;
-        int ks;
-        seg_src<NSEG>(s < last ? s : last, nst, G, G2, Q, Q2, g, q, ks);
-        // probe MODE 131072: every tile copies gallery panel 0 and query panel 0 (L2-resident feed)
-        if constexpr ((MODE & 262144) != 0) Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (s % NST) * STAGE);
-        else Engine<8>::dma_buf(g, (MODE & 131072) ? 0 : gp, q, (MODE & 131072) ? 0 : qp, nst, ks, smem + (s % NST) * STAGE);
-      } else {
-        issue(s < last ? s : last);
-      }
+      seg_src<NSEG>(s < last ? s : last, nst, G, G2, Q, Q2, g, q, ks);
+      Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (s % NST) * STAGE);
     }
     i32x6 a[NA], b[NB];
-    int sc = 0x7f7f7f7f;
-    if constexpr ((MODE & 256) != 0) asm volatile("" : "+v"(sc));
     int sa = SCALE_ONE, sb = SCALE_ONE;
-    auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) {
-      if constexpr ((MODE & 65536) != 0) return;   // probe: no MFMAs (the feed alone; wrong results)
-      if constexpr ((MODE & 256) != 0) mfma_agpr(x, y, c, sc);
-      else c = mfma(x, y, c, sa, sb);
-    };
-    constexpr bool P1 = (MODE & 1048576) == 0;   // probe 1048576: no part1 reads (wrong results)
-    auto readA = [&](const char* st, int i) { a[i] = frag16<P1>(st, wr * 128 + i * 16 + r16); };
-    auto readB = [&](const char* st, int c) { b[c] = frag16<P1>(st + PANEL, wc * QW + c * 16 + r16); };
-    // probe MODE 16384: the k loop keeps its first fragments (no refills; wrong results): MFMAs + feed
-    auto readAk = [&](const char* st, int i) { if constexpr ((MODE & 16384) == 0) readA(st, i); };
-    auto readBk = [&](const char* st, int c) { if constexpr ((MODE & 16384) == 0) readB(st, c); };
-    if constexpr (MODE == 1) wait_vm<0>();
-    else if constexpr ((MODE & 262144) != 0) wait_vm<4 * IPW>();
-    else wait_vm<2 * IPW>();
+    auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) { c = mfma(x, y, c, sa, sb); };
+    auto readA = [&](const char* st, int i) { a[i] = frag16(st, wr * 128 + i * 16 + r16); };
+    auto readB = [&](const char* st, int c) { b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16); };
+    wait_vm<4 * IPW>();
     barrier();
-    if constexpr ((MODE & 2048) != 0) {   // the loop's read order, so that its waits stay counted
 #pragma unroll
-      for (int i = 0; i < 4; ++i) readA(smem, i);
+    for (int i = 0; i < NA; ++i) readA(smem, i);
 #pragma unroll
-      for (int c = 0; c < NB; ++c) readB(smem, c);
-#pragma unroll
-      for (int i = 4; i < NA; ++i) readA(smem, i);
-    } else {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) readA(smem, i);
-#pragma unroll
-      for (int c = 0; c < NB; ++c) readB(smem, c);
-    }
-    if constexpr ((MODE & 1024) != 0) {
-      // Probe: two barriers per stage.  Top of stage kt: stage kt+1 landed (own DMAs: vmcnt) and
-      // visible (s_barrier) -- no LDS drain.  Rows 0-3 with the refills of a[0..3] (8 LDS reads), then
-      // lgkmcnt(8) (every read of stage kt's buffer, all issued in stage kt-1, is done) + s_barrier,
-      // and only then stage kt+3's DMA into that buffer (1.5 stages of lead instead of 2).
-      // rows before the re-fill barrier (their refills are the only LDS reads it lets through):
-      // 4 by default, 2 (MODE 4096), 6 (MODE 8192) or 1 (both) in the probe
-      constexpr int RS = (MODE & 4096) && (MODE & 8192) ? 1 : ((MODE & 4096) ? 2 : ((MODE & 8192) ? 6 : 4));
-      static_assert((MODE & 2048) == 0 || RS == 4, "column-major halves split at row 4");
-      // probe 2097152 (with 262144): the 12 pieces of an issuing wave in three chunks of 4, after the
-      // re-fill barrier and after the next two fragment rows, instead of one burst
-      constexpr bool SPREAD = (MODE & 2097152) != 0 && (MODE & 262144) != 0;
-      auto issue_b = [&](int kt) {
-        const char *g, *q;
-        int ks;
-        seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
-        if constexpr (SPREAD) Engine<8>::dma_buf4<0, 4>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
-        else if constexpr ((MODE & 262144) != 0) Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
-        else Engine<8>::dma_buf(g, (MODE & 131072) ? 0 : gp, q, (MODE & 131072) ? 0 : qp, nst, ks, smem + (kt % NST) * STAGE);
-      };
-      auto issue_rest = [&](int kt, auto chunk) {   // SPREAD: pieces 4 chunk .. 4 chunk + 3
-        constexpr int C = decltype(chunk)::value;
-        const char *g, *q;
-        int ks;
-        seg_src<NSEG>(kt, nst, G, G2, Q, Q2, g, q, ks);
-        Engine<8>::dma_buf4<4 * C, 4 * C + 4>(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
-      };
-#ifdef OFR_F6_STAMPS
-      constexpr bool ST = (MODE & 8388608) != 0;
-      unsigned long long st_sum[5] = {0, 0, 0, 0, 0}, st_t[6] = {0, 0, 0, 0, 0, 0};
-      unsigned long long st_n = 0;
-      auto stamp = [&](int j) {
-        if constexpr (ST) {
-          __builtin_amdgcn_sched_barrier(0);
-          st_t[j] = __builtin_amdgcn_s_memtime();
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      };
-#else
-      auto stamp = [&](int) {};
-#endif
-      for (int kt = 0; kt < last; ++kt) {
-        seg_scales<NSEG>(kt, nst, sa, sb);
-        __builtin_amdgcn_sched_barrier(0);
-        stamp(0);
-        if constexpr ((MODE & 262144) != 0) wait_vm<2 * IPW>();
-        else wait_vm<IPW>();   // stage kt+1 landed (kt+2 may be in flight)
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        stamp(1);
-#ifdef OFR_F6_STAMPS
-        if constexpr (ST) {   // the previous stage's phases (its t5 = this t0)
-          if (kt > 8 && kt < last - 8) {
-            st_sum[0] += st_t[2] - st_t[1];   // rows before the re-fill barrier (previous stage)
-            st_sum[1] += st_t[3] - st_t[2];   // re-fill wait + barrier
-            st_sum[2] += st_t[4] - st_t[3];   // copy issue
-            st_sum[3] += st_t[0] - st_t[4];   // the remaining rows
-            st_sum[4] += st_t[1] - st_t[0];   // this stage's top wait (copies landed) + barrier
-            ++st_n;
-          }
-        }
-#endif
-        const char* nxt = smem + ((kt + 1) % NST) * STAGE;
-        if constexpr ((MODE & 2048) != 0) {
-          // column-major halves: rows 0-3 against b[0], b[1], b[2], b[3] in turn; a[0..3] refilled
-          // after their last MFMA (the half's last four)
-#pragma unroll
-          for (int c = 0; c < NB; ++c)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              mm(a[i], b[c], acc[i][c]);
-              if (c == NB - 1) readAk(nxt, i);
-            }
-          __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < RS; ++i) {
-#pragma unroll
-            for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
-            readAk(nxt, i);
-          }
-#pragma unroll
-          for (int i = 0; i < RS; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // lgkmcnt(2 RS): each refill is exactly two LDS instructions (frag16: ds_read_b128 + ds_read_b64,
-        // the part1 address opaque so they cannot be fused), and LDS returns in order, so at most the
-        // 2 RS reads issued above may still be in flight and every read of the previous stage (all
-        // from the buffer re-filled below) is done.  Scalar loads sharing the counter can only make the
-        // wait stricter.  (More instructions per refill would also be safe; fewer would not.)
-        stamp(2);
-        if constexpr (RS == 1) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-        else if constexpr (RS == 2) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-        else if constexpr (RS == 6) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        stamp(3);
-        {
-          const int nx = kt + NST;
-          issue_b(nx < last ? nx : last);
-        }
-        stamp(4);
-        if constexpr ((MODE & 2048) != 0) {
-          // rows 4-7 column-major: b[c] refilled after its last MFMA (row 7), a[4..7] after column 3
-#pragma unroll
-          for (int c = 0; c < NB; ++c) {
-#pragma unroll
-            for (int i = 4; i < NA; ++i) mm(a[i], b[c], acc[i][c]);
-            readBk(nxt, c);   // b3 before a4..a7: the next stage needs b3 at its 13th MFMA, a4 at its 17th
-          }
-#pragma unroll
-          for (int i = 4; i < NA; ++i) readAk(nxt, i);
-          __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
-#pragma unroll
-          for (int c = 0; c < NB; ++c) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-          continue;
-        }
-#pragma unroll
-        for (int i = RS; i < NA - 1; ++i) {
-#pragma unroll
-          for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
-          readAk(nxt, i);
-          if constexpr (SPREAD) {
-            const int nx = kt + NST;
-            if (i == RS) issue_rest(nx < last ? nx : last, std::integral_constant<int, 1>{});
-            if (i == RS + 1) issue_rest(nx < last ? nx : last, std::integral_constant<int, 2>{});
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
-          mm(a[NA - 1], b[c], acc[NA - 1][c]);
-          readBk(nxt, c);
-        }
-        readAk(nxt, NA - 1);
-        __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
-#pragma unroll
-        for (int i = RS; i < NA - 1; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
-      seg_scales<NSEG>(last, nst, sa, sb);
-#pragma unroll
-      for (int i = 0; i < NA; ++i)
-#pragma unroll
-        for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
-      wait_vm<0>();
-      barrier();
-#ifdef OFR_F6_STAMPS
-      if constexpr (ST) {
-        if (blockIdx.x < STAMP_WG && lane == 0) {
-          unsigned long long* o = g_f6_stamps + ((size_t)blockIdx.x * 8 + wave) * STAMP_N;
-#pragma unroll
-          for (int j = 0; j < 5; ++j) o[j] = st_sum[j];
-          o[5] = st_n;
-        }
-      }
-#endif
-      return;
-    }
-    // Per stage kt: MFMAs of stage kt, each fragment replaced by stage kt+1's as soon as its last
-    // MFMA is issued (A-major: A[i] after row i's 4 MFMAs, B[c] after row 7's MFMA c), so the
-    // fragments need no second register set (acc 128 + fragments 72 registers).
+    for (int c = 0; c < NB; ++c) readB(smem, c);
     for (int kt = 0; kt < last; ++kt) {
       seg_scales<NSEG>(kt, nst, sa, sb);
-      if constexpr ((MODE & 1) != 0) wait_vm<0>();
-      else if constexpr ((MODE & 64) == 0) wait_vm<IPW>();   // stage kt+1 landed; kt+2 may be in flight
-      barrier();                 // every wave has read stage kt: its buffer takes stage kt+3
-      if constexpr ((MODE & 1) == 0) {
-        const int nx = kt + NST;
-        issue_k(nx < last ? nx : last);
-      }
+      __builtin_amdgcn_sched_barrier(0);
+      wait_vm<2 * IPW>();   // stage kt+1 landed (kt+2 may be in flight)
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
       const char* nxt = smem + ((kt + 1) % NST) * STAGE;
 #pragma unroll
-      for (int i = 0; i < NA - 1; ++i) {
+      for (int c = 0; c < NB; ++c) mm(a[0], b[c], acc[0][c]);
+      readA(nxt, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      // lgkmcnt(2): the refill is exactly two LDS instructions (frag16: ds_read_b128 + ds_read_b64, the
+      // part1 address opaque so they cannot be fused), and LDS returns in order, so at most those two
+      // may still be in flight and every read of the previous stage (all from the buffer re-filled
+      // below) is done.  Scalar loads sharing the counter can only make the wait stricter.
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        const int nx = kt + NST;
+        issue(nx < last ? nx : last);
+      }
+#pragma unroll
+      for (int i = 1; i < NA - 1; ++i) {
 #pragma unroll
         for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
-        readAk(nxt, i);
+        readA(nxt, i);
       }
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
         mm(a[NA - 1], b[c], acc[NA - 1][c]);
-        readBk(nxt, c);
+        readB(nxt, c);
       }
-      readAk(nxt, NA - 1);
-      // the stage's DMAs first (issuing them later in the stage, staggered between the two waves of
-      // a SIMD, measured 8 % slower: tools/f6_probe.hip SHAPE16), then per row i its 4 MFMAs and
-      // the 2 reads of its successor; row 7 refills B as each of its MFMAs retires its operand
+      readA(nxt, NA - 1);
       __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
 #pragma unroll
-      for (int i = 0; i < NA - 1; ++i) {
+      for (int i = 1; i < NA - 1; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
@@ -913,8 +406,6 @@ struct Engine16 {
 #pragma unroll
       for (int c = 0; c < NB; ++c) mm(a[i], b[c], acc[i][c]);
     wait_vm<0>();
-    if constexpr ((MODE & 256) != 0) asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-    if constexpr ((MODE & 128) != 0) asm volatile("" : "+v"(sink));
     barrier();
   }
 };
@@ -1047,9 +538,7 @@ struct EngineW {
     asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
   }
 
-  // MODE (probes): 1 = no copies in the k loop (the prologue's stages re-read), 2 = no MFMAs,
-  // 8 = copies never waited for (wrong results)
-  template <int W, int MODE>
+  template <int W>
   static __device__ __forceinline__ void mainloop(const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
     constexpr int WR = W >> 1, WC = W & 1;
     int sc = SCALE_ONE;
@@ -1093,9 +582,7 @@ struct EngineW {
       auto row = [&](auto ii) {
         constexpr int i = decltype(ii)::value;
         constexpr bool AG = i < NAA;
-        auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) {
-          if constexpr ((MODE & 2) == 0) mfma<AG>(x, y, c, sc);
-        };
+        auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) { mfma<AG>(x, y, c, sc); };
         if constexpr (i == 1) {              // barrier A: Q(s) consumed by every wave
           // Q(s)'s reads (row 11 of s - 1) are older than row 0's gallery read, the only one allowed in flight
           asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
@@ -1103,17 +590,15 @@ struct EngineW {
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (i == 10) {             // barrier B: G(s+1), Q(s+1) landed; G(s) consumed
-          if constexpr ((MODE & 9) == 0) wait_vm<GPW + QPW>();
+          wait_vm<GPW + QPW>();
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
         }
-        if constexpr ((MODE & 1) == 0) {
-          // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0), G(s+3) into G(s)'s (g0)
-          if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(f, g2, k2);
-          if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(f, q0, k2);
-          if constexpr (i == 10) gcopy<W, 0>(f, g0, k3);   // piece 1: in the middle of rows 10 / 11
-        }
+        // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0), G(s+3) into G(s)'s (g0)
+        if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(f, g2, k2);
+        if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(f, q0, k2);
+        if constexpr (i == 10) gcopy<W, 0>(f, g0, k3);   // piece 1: in the middle of rows 10 / 11
         if constexpr (i == NA - 1) {
           // rows 10 and 11 run together (below, i == 10)
         } else if constexpr (i == NA - 2) {
@@ -1126,7 +611,7 @@ struct EngineW {
           mm(a[1], b[1], acc[10][1]); mm(a[2], b[1], acc[11][1]); b[1] = fragB<WC * 128 + 16>(bn);
           mm(a[1], b[2], acc[10][2]); mm(a[2], b[2], acc[11][2]); b[2] = fragB<WC * 128 + 32>(bn);
           mm(a[1], b[3], acc[10][3]); mm(a[2], b[3], acc[11][3]); b[3] = fragB<WC * 128 + 48>(bn);
-          if constexpr ((MODE & 1) == 0) gcopy<W, 1>(f, g0, k3);
+          gcopy<W, 1>(f, g0, k3);
           mm(a[1], b[4], acc[10][4]); mm(a[2], b[4], acc[11][4]); b[4] = fragB<WC * 128 + 64>(bn);
           mm(a[1], b[5], acc[10][5]); mm(a[2], b[5], acc[11][5]); b[5] = fragB<WC * 128 + 80>(bn);
           mm(a[1], b[6], acc[10][6]); mm(a[2], b[6], acc[11][6]); b[6] = fragB<WC * 128 + 96>(bn);

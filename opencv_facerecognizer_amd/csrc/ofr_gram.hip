@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(S::NT, 1) gram_u8_kernel(Args p) {
   const int8_t* base = reinterpret_cast<const int8_t*>(p.X) + p.k0;
   const int64_t cols = (int64_t)p.nk * i8t::ROWB;
   i32x16 acc[4][S::CT], unused[4][1];
-  i8t::mainloop<1, 0, true, true>(smem, base, p.ld, p.R, a0, base, p.ld, p.R, b0, cols, p.nk, acc, unused);
+  i8t::mainloop<1, true, true>(smem, base, p.ld, p.R, a0, base, p.ld, p.R, b0, cols, p.nk, acc, unused);
   // C/D map of v_mfma_i32_32x32x32_i8: A row (reg & 3) + 8 (reg >> 2) + 4 h of the 32-block, B row lane & 31
 #pragma unroll
   for (int ct = 0; ct < S::CT; ++ct) {

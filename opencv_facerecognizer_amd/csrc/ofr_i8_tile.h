@@ -98,8 +98,8 @@ __device__ __forceinline__ void barrier() {
 //   SL = 2: acc0 += A1 . B1,  acc1 += A2 . B1 + A1 . B2   (slices interleaved per 128-B line)
 // XB / XA: B / A hold uint8 (images); fragments are turned into x - 128 by an XOR with 0x80.
 // bcols: readable bytes per B row (DMA columns past it are clamped into the row; the
-// matching A columns are zero).  MODE 1/2: probe variants without k-loop DMA / MFMA.
-template <int SL, int MODE, bool XB, bool XA = false>
+// matching A columns are zero).
+template <int SL, bool XB, bool XA = false>
 __device__ __forceinline__ void mainloop(char* smem, const int8_t* A, int64_t lda, int64_t arows, int64_t a0,
                                          const int8_t* Bm, int64_t ldb, int64_t brows, int64_t b0, int64_t bcols,
                                          int nk, i32x16 (&acc0)[4][Shape<SL>::CT],
@@ -178,19 +178,18 @@ __device__ __forceinline__ void mainloop(char* smem, const int8_t* A, int64_t ld
   constexpr int MF = S::MF_PER_KS;            // MFMAs per k-half
   static_assert(MF >= NFR, "MFMA : read interleave");
   for (int kt = 0; kt < nk; ++kt) {
-    if constexpr (MODE == 1) wait_vm<0>();
-    else wait_vm<S::YOUNG>();   // step kt landed; younger steps may stay in flight
+    wait_vm<S::YOUNG>();   // step kt landed; younger steps may stay in flight
     barrier();
     const char* st = smem + (kt % S::NST) * S::STAGE;
     frags(st, 0);
-    if constexpr (MODE != 1) {
+    {
       const int nx = kt + S::NST - 1;
       issue(nx < last ? nx : last);
     }
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       if (ks + 1 < NKS) frags(st, ks + 1);
-      if constexpr (MODE != 2) mfmas(ks);
+      mfmas(ks);
     }
     // schedule: k-half-0 reads, the DMAs, then each k-half's MFMAs with the next
     // k-half's reads front-loaded between them (1 : 1, so they land before they are

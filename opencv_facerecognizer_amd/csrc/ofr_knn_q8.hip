@@ -184,57 +184,6 @@ constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
 template <int TQ, int GB = 8, int TGR = TG, int HCAP = SIEVE_HCAP>
 __device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64_t g0, int64_t q0);
 
-template <int CT, int TQ, int QW, int WQ, class CV>
-__device__ __forceinline__ void sieve_epilogue(char* smem, const TileArgs& p, int64_t g0, int64_t q0, float ga,
-                                               float gs, const float (&sq2)[CT], const float (&th)[CT], CV&& cval) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
-  float* gtab = reinterpret_cast<float*>(smem);                                  // [TG][2]
-  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + TG * 8);
-  uint2* hits = reinterpret_cast<uint2*>(smem + TG * 8 + 16);                    // [SIEVE_HCAP]
-  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
-  if (threadIdx.x < TG) {
-    gtab[2 * threadIdx.x + 0] = ga;
-    gtab[2 * threadIdx.x + 1] = gs;
-  }
-  if (threadIdx.x == 0) *nhit = 0;
-  __syncthreads();
-
-#pragma unroll
-  for (int rt = 0; rt < 4; ++rt) {
-    // the 16 rows of this row block first (one LDS wait), then the compares: a read per element
-    // would expose the LDS latency 64 times
-    float2 ag[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      ag[r] = reinterpret_cast<const float2*>(gtab)[wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int gl = wr * 128 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float a = ag[r].x, sg = ag[r].y;
-      auto one = [&](auto ctc) {
-        constexpr int ct = decltype(ctc)::value;
-        if constexpr (ct < CT) {
-          const float sc = a - sq2[ct] * sg * cval(rt, ctc, r);
-          if (!(sc > th[ct]) && gl < nvalid) {   // rare: ~16 * SIEVE_STRIDE of the N rows per query
-            const int ql = wc * QW + ct * 32 + r32;
-            const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
-            const uint32_t slot = atomicAdd(nhit, 1u);
-            if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)gl);
-          }
-        }
-      };
-      static_assert(CT <= 4, "sieve unroll");
-      one(std::integral_constant<int, 0>{});
-      one(std::integral_constant<int, 1>{});
-      one(std::integral_constant<int, 2>{});
-      one(std::integral_constant<int, 3>{});
-    }
-  }
-  __syncthreads();
-  sieve_flush<TQ>(smem, p, g0, q0);
-}
-
 // The tile's staged hits -> per-query buckets (after the compares and a barrier).  A hit packs
 // (tile query << GB) | tile gallery row; TGR gallery rows per tile (the staging area follows their
 // [TGR][2] operand table), HCAP staging slots.
@@ -260,9 +209,8 @@ __device__ __forceinline__ void sieve_flush(char* smem, const TileArgs& p, int64
   }
 }
 
-// MODE 0 is the search; 1 (no k-loop DMA) and 2 (no MFMA) exist only for the
-// feed/compute probe in tools/ and are never instantiated by the library.
-template <int SL, int MODE>
+// The int8 tiers' tile pass (SL int8 slices per row): per (query, tile) the best KC keys.
+template <int SL>
 __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
   using S = Shape<SL>;
   constexpr int CT = S::CT;
@@ -273,7 +221,7 @@ __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
   const int64_t g0 = gt * TG, q0 = qt * S::TQ;
 
   i32x16 acc0[4][CT], acc1[4][SL == 2 ? CT : 1];
-  i8t::mainloop<SL, MODE, false>(smem, p.G, p.ld, p.N, g0, p.Q, p.ld, p.B, q0, p.ld, p.nk, acc0, acc1);
+  i8t::mainloop<SL, false>(smem, p.G, p.ld, p.N, g0, p.Q, p.ld, p.B, q0, p.ld, p.nk, acc0, acc1);
   tile_epilogue<CT, S::TQ, S::QW, S::WQ>(smem, p, gt, g0, q0, [&](int rt, auto ctc, int r) {
     constexpr int ct = decltype(ctc)::value;
     float c = (float)acc0[rt][ct][r];
@@ -282,69 +230,28 @@ __global__ void __launch_bounds__(Shape<SL>::NT, 1) tile_kernel(TileArgs p) {
   });
 }
 
-// fp6 tier: p.G / p.Q are f6 tiled buffers (ofr_f6_tile.h), p.nk = stages, NW waves
-// (f6t::Engine).  MODE 0: tile lists (tile t = gallery panel t * gstride, the sieve's sample
-// pass); 8: the sieve.  Probe bits: 1 / 2 / 16 = no k-loop DMA / gallery DMA / query DMA,
-// 4 = no epilogue.
-template <int NW, int MODE, int NSEG = 1>
+// fp6 tier, the sieve's sample pass: p.G / p.Q are f6 tiled buffers (ofr_f6_tile.h), p.nk = stages,
+// NW waves (f6t::Engine, 32x32x64 MFMA); tile lists of the best KC keys per (query, tile), tile t =
+// gallery panel t * gstride.
+template <int NW, int NSEG = 1>
 __global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
   using E = f6t::Engine<NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr bool SIEVE = (MODE & 8) != 0;
   constexpr int CT = E::CT;
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   int64_t gt, qt;
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
-  // sieve operands, loaded under the main loop (after it for the deep-staged loop: ordinary loads in
-  // flight beside its LDS-DMA make the compiler wait vmcnt(0) inside the loop)
-  float ga = __builtin_inff(), gs = 0.f, sq2[CT], th[CT];
-  auto sieve_operands = [&]() {
-    static_assert(E::NT >= TG, "one gallery row per thread");
-    if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
-      ga = p.aux[g0 + threadIdx.x];
-      gs = p.gscale[g0 + threadIdx.x];
-    }
-    const int wc = (threadIdx.x >> 6) % E::WQ, r32 = threadIdx.x & 31;
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      const int64_t q = q0 + wc * E::QW + c * 32 + r32;
-      const bool ok = q < p.B;
-      sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
-      th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
-    }
-  };
-  if constexpr (SIEVE && (MODE & 32) == 0) sieve_operands();
   f6t::f32x16 acc[4][CT];
-  if constexpr ((MODE & 32) != 0)   // deep-staged loop: 64-feature half-stages in 6 buffers (f6t::Engine::mainloop_deep)
-    E::template mainloop_deep<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
-                                    p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
-                                    reinterpret_cast<const char*>(p.Q2));
-  else
-    E::template mainloop<MODE & 19, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp,
-                                         reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG, acc,
-                                         reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
-  if constexpr (SIEVE && (MODE & 32) != 0) sieve_operands();
-  if constexpr ((MODE & 4) != 0) {   // probe: no epilogue (the accumulators kept alive)
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < CT; ++c)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s += acc[i][c][r];
-    if (s == 1.2345f) p.cand[0].d = s;
-    return;
-  }
+  E::template mainloop<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
+                             p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
+                             reinterpret_cast<const char*>(p.Q2));
   auto cval = [&](int rt, auto ctc, int r) {
     constexpr int ct = decltype(ctc)::value;
     return acc[rt][ct][r];
   };
-  if constexpr (SIEVE)
-    sieve_epilogue<CT, f6t::TQ, E::QW, E::WQ>(smem, p, g0, q0, ga, gs, sq2, th, cval);
-  else
-    tile_epilogue<CT, f6t::TQ, E::QW, E::WQ>(smem, p, gt, g0, q0, cval);
+  tile_epilogue<CT, f6t::TQ, E::QW, E::WQ>(smem, p, gt, g0, q0, cval);
 }
 
 // Sieve epilogue of the 16x16x128 engine (f6t::Engine16): element reg r of accumulator (i, c) of
@@ -402,54 +309,9 @@ __device__ __forceinline__ void sieve_epilogue16(char* smem, const TileArgs& p, 
   sieve_flush<f6t::TQ>(smem, p, g0, q0);
 }
 
-// The same epilogue for the asymmetric loop (f6t::Engine16::mainloop_as): NI gallery row blocks
-// from row0, the wave's 64 queries at (wave & 3) * 64.  Both roles of the kernel run it (one
-// __syncthreads before the compares, one in sieve_flush: equal counts).
-template <int NI>
-__device__ __forceinline__ void sieve_epilogue_as(char* smem, const TileArgs& p, int64_t g0, int64_t q0, float ga,
-                                                  float gs, const float (&sq2)[4], const float (&th)[4],
-                                                  const f6t::f32x4 (&acc)[NI][4], int row0) {
-  using E = f6t::Engine16;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wc = wave & 3, g4 = (lane >> 4) * 4, r16 = lane & 15;
-  float* gtab = reinterpret_cast<float*>(smem);                                  // [TG][2]
-  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + TG * 8);
-  uint2* hits = reinterpret_cast<uint2*>(smem + TG * 8 + 16);                    // [SIEVE_HCAP]
-  const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
-  if (threadIdx.x < TG) {
-    gtab[2 * threadIdx.x + 0] = ga;
-    gtab[2 * threadIdx.x + 1] = gs;
-  }
-  if (threadIdx.x == 0) *nhit = 0;
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int gl0 = row0 + i * 16 + g4;            // this lane's 4 consecutive gallery rows
-    const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
-    const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
-    const float av[4] = {t0.x, t0.z, t1.x, t1.z}, sv[4] = {t0.y, t0.w, t1.y, t1.w};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gl = gl0 + r;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float sc = av[r] - sq2[c] * sv[r] * acc[i][c][r];
-        if (!(sc > th[c]) && gl < nvalid) {
-          const int ql = wc * E::QW + c * 16 + r16;
-          const uint32_t kb = __float_as_uint(key_score(score_key(sc, 0)));
-          const uint32_t slot = atomicAdd(nhit, 1u);
-          if (slot < (uint32_t)SIEVE_HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 8) | (uint32_t)gl);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  sieve_flush<f6t::TQ>(smem, p, g0, q0);
-}
-
-// fp6 sieve pass on the 16x16x128 engine.  MODE probe bits: 1 = no k-loop DMA, 4 = no epilogue; the
-// main loop's own bits (f6t::Engine16::mainloop) pass through the mask below.
-template <int MODE, int NSEG = 1>
+// fp6 sieve pass on the 16x16x128 engine (f6t::Engine16, 256 x 256 tiles, 8 waves): the two-slice
+// tier's engine (NSEG = 3) and the sieve pass under OFR_F6_SHAPE=16.
+template <int NSEG = 1>
 __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   using E = f6t::Engine16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -458,50 +320,9 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
   const int64_t gp = gt * p.gstride;
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
-  if constexpr ((MODE & 16777216) != 0) {   // asymmetric loop (f6t::Engine16::mainloop_as)
-    constexpr int NIA = 6;                   // gallery row blocks of the copy-issuing waves 0-3
-    auto operands = [&](float& ga, float& gs, float (&sq2)[4], float (&th)[4]) {
-      ga = __builtin_inff();
-      gs = 0.f;
-      if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
-        ga = p.aux[g0 + threadIdx.x];
-        gs = p.gscale[g0 + threadIdx.x];
-      }
-      const int wc = (threadIdx.x >> 6) & 3, r16 = threadIdx.x & 15;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int64_t q = q0 + wc * E::QW + c * 16 + r16;
-        const bool ok = q < p.B;
-        sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
-        th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
-      }
-    };
-    float ga, gs, sq2[4], th[4];
-    if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) < 4) {
-      f6t::f32x4 acc[NIA][4];
-      E::mainloop_as<NIA, true, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q),
-                                      qt, p.nk / NSEG, 0, acc, reinterpret_cast<const char*>(p.G2),
-                                      reinterpret_cast<const char*>(p.Q2));
-      operands(ga, gs, sq2, th);
-      sieve_epilogue_as<NIA>(smem, p, g0, q0, ga, gs, sq2, th, acc, 0);
-    } else {
-      f6t::f32x4 acc[16 - NIA][4];
-      E::mainloop_as<16 - NIA, false, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp,
-                                            reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG, NIA * 16, acc,
-                                            reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
-      operands(ga, gs, sq2, th);
-      sieve_epilogue_as<16 - NIA>(smem, p, g0, q0, ga, gs, sq2, th, acc, NIA * 16);
-    }
-    return;
-  }
   f6t::f32x4 acc[8][4];
-  if constexpr ((MODE & 524288) != 0)   // ping-pong main loop (f6t::Engine16::mainloop_pp)
-    E::mainloop_pp<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
-                         p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
-  else
-    E::mainloop<MODE & 12025281, NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
-                                  p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
-                                  reinterpret_cast<const char*>(p.Q2));
+  E::mainloop<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG,
+                    acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
   // sieve operands after the main loop (the 16x16 engine needs every register in it)
   float ga = __builtin_inff(), gs = 0.f, sq2[4], th[4];
   if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
@@ -516,26 +337,14 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
     sq2[c] = 2.0f * p.qscale[ok ? q : p.B - 1];
     th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
   }
-  if constexpr ((MODE & 4) != 0) {   // probe: no epilogue (the accumulators kept alive)
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s += acc[i][c][r];
-    if (s == 1.2345f) p.cand[0].d = s;
-    return;
-  }
   sieve_epilogue16(smem, p, g0, q0, ga, gs, sq2, th, acc);
 }
 
 // fp6 sieve pass on the wide engine (f6t::EngineW): 384 gallery x 256 query tiles, 4 waves (one per
 // SIMD), p.ntg = ceil(N / 384) gallery tiles.  The epilogue is sieve_epilogue16's for the 192 x 128
 // wave tile: element r of acc[i][c] of lane l is gallery row WR*192 + 16 i + 4 (l / 16) + r, query
-// WC*128 + 16 c + l % 16.  MODE probe bits: 1 / 2 = no copies / no MFMAs in the k loop, 4 = no
-// epilogue (the accumulators kept alive).
-template <int W, int MODE>
+// WC*128 + 16 c + l % 16.
+template <int W>
 __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
   using E = f6t::EngineW;
   f6t::f32x4 acc[E::NA][E::NB];
@@ -543,7 +352,7 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
   E::Feed f;
   E::feed_init<W>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ, p.nk,
                   g0 / E::TGW);
-  E::mainloop<W, MODE & 11>(f, p.nk, acc);
+  E::mainloop<W>(f, p.nk, acc);
   float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
   uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
   uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [HCAPW]
@@ -567,18 +376,6 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
     th[c] = ok ? key_float(p.theta[q] | 0xffu) : -__builtin_inff();
   }
   __syncthreads();
-  if constexpr ((MODE & 4) != 0) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < E::NA; ++i)
-#pragma unroll
-      for (int c = 0; c < E::NB; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s += acc[i][c][r];
-    if (s == 1.2345f) p.cand[0].d = s;
-    __syncthreads();
-    return;
-  }
   // Per row block: the lane's 32 coarse scores sc = fma(-(sq2 sv), acc, a) in packed pairs (two rows
   // of one query per v_pk_fma_f32), per query column the min over the 4 rows, one v_cmp_ngt per column
   // (NaN th, "keep every row", passes) and a wave-wide OR: a block holds ~1 kept pair per wave on
@@ -626,7 +423,6 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
   sieve_flush<f6t::TQ, 9, E::TGW, HCAPW>(smem, p, g0, q0);
 }
 
-template <int MODE>
 __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   using E = f6t::EngineW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -635,10 +431,10 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
   const int64_t g0 = gt * E::TGW, q0 = qt * f6t::TQ;
   switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
-    case 0: f6w_body<0, MODE>(smem, p, g0, q0); break;
-    case 1: f6w_body<1, MODE>(smem, p, g0, q0); break;
-    case 2: f6w_body<2, MODE>(smem, p, g0, q0); break;
-    default: f6w_body<3, MODE>(smem, p, g0, q0); break;
+    case 0: f6w_body<0>(smem, p, g0, q0); break;
+    case 1: f6w_body<1>(smem, p, g0, q0); break;
+    case 2: f6w_body<2>(smem, p, g0, q0); break;
+    default: f6w_body<3>(smem, p, g0, q0); break;
   }
 }
 
@@ -1352,12 +1148,12 @@ static int q8_tiles(hipStream_t st, q8s::TileArgs a) {
   using S = q8s::Shape<SL>;
   static bool attr_done = false;
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel<SL, 0>,
+    hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel<SL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(q8 tile)");
     attr_done = true;
   }
-  hipLaunchKernelGGL((q8s::tile_kernel<SL, 0>), dim3((unsigned)(a.ntq * a.ntg)), dim3(S::NT), S::LDS, st, a);
+  hipLaunchKernelGGL((q8s::tile_kernel<SL>), dim3((unsigned)(a.ntq * a.ntg)), dim3(S::NT), S::LDS, st, a);
   OFR_LAUNCH_CHECK("q8 tile_kernel");
   return OFR_OK;
 }
@@ -1478,40 +1274,26 @@ extern "C" int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, i
   return ofr_q8_maxima(stream, stats, aux, R, maxima);
 }
 
-// waves of the fp6 tile engine (f6t::Engine; tools/f6_probe.hip times both)
+// waves of the sample pass's fp6 engine (f6t::Engine<8>, 32x32x64 MFMA)
 constexpr int F6_NW = 8;
-// main-loop variant of the 16x16 sieve pass (f6t::Engine16::mainloop MODE bits): 1024 = the stage
-// copies by MUBUF buffer_load ... lds (LDS reads stay counted for the compiler) and the stage barrier
-// split into a visibility barrier (top, no LDS drain) and a counted-wait barrier before the re-fill
-// (after the first rows); 4096 / 8192 / both: that barrier after rows 0-1 / 0-5 / row 0 (default 0-3);
-// 2048 = column-major halves.  0 = the FLAT global_load_lds loop with one draining barrier per stage.
-// tools/f6_probe.hip times them: 1024 + 4096 + 8192 (re-fill barrier after row 0: 1.9 stages of
-// copy lead) is the fastest, 22.5 against 23.3 ms for 0.  262144: the stage copies issued by waves 0-3
-// alone (12 pieces each, one wave per SIMD) while waves 4-7 issue none, so one wave of every SIMD
-// keeps issuing MFMAs while the other pays the copies' issue cost (round 3: 23.11 -> 22.63 ms,
-// profiles/r03_f6_probe_feed4w.log).
-constexpr int F6S_MODE = 1024 + 4096 + 8192 + 262144;
 
 // name of the fp6 sieve kernel ofr_knn_f6 launches for B > 32, as rocprofv3 reports it (bench.py
 // labels its roofline entry with it, so the record names the variant that actually ran)
 static int f6_shape();
 extern "C" const char* ofr_f6_sieve_kernel(void) {
-  static const std::string names[3] = {
-      "q8s::tile_kernel_f6s<" + std::to_string(F6S_MODE) + ", 1> (16x16x128 fp6 engine)",
-      "q8s::tile_kernel_f6<" + std::to_string(F6_NW) + ", 8> (32x32x64 fp6 engine)",
-      "q8s::tile_kernel_f6w<0> (16x16x128 fp6 engine, 384x256 tiles, 1 wave per SIMD)"};
-  return names[f6_shape() == 16 ? 0 : (f6_shape() == 32 ? 1 : 2)].c_str();
+  static const std::string names[2] = {
+      "q8s::tile_kernel_f6s<1> (16x16x128 fp6 engine, 256x256 tiles, 8 waves)",
+      "q8s::tile_kernel_f6w (16x16x128 fp6 engine, 384x256 tiles, 1 wave per SIMD)"};
+  return names[f6_shape() == 16 ? 0 : 1].c_str();
 }
 
 // Engine of the sieve pass: 384 = v_mfma_scale_f32_16x16x128 on 384 x 256 tiles, one wave per SIMD
-// (f6t::EngineW, default since round 3: 22.2 -> 20.1 ms, tools/f6_probe.hip WIDE); 16 = the same MFMA on
-// 256 x 256 tiles, 8 waves (f6t::Engine16, OFR_F6_SHAPE=16; also the two-slice tier's engine); 32 = the
-// 32x32x64 engine (OFR_F6_SHAPE=32).  Read at every call (the workspace does not depend on it), so a
-// test can run both sieve engines in one process.
+// (f6t::EngineW, default since round 3: 22.2 -> 20.1 ms); 16 = the same MFMA on 256 x 256 tiles, 8
+// waves (f6t::Engine16, OFR_F6_SHAPE=16; also the two-slice tier's engine).  Read at every call (the
+// workspace does not depend on it), so a test can run both sieve engines in one process.
 static int f6_shape() {
   const char* e = getenv("OFR_F6_SHAPE");
-  const int v = e ? atoi(e) : 0;
-  return v == 32 || v == 16 ? v : 384;
+  return e && atoi(e) == 16 ? 16 : 384;
 }
 
 // gallery tiles per tile group of the wide sieve pass (i8t::tile_coords): 2, so the ~32 workgroups
@@ -1661,14 +1443,12 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
     } else {
       static bool attr_done = false;
       if (!attr_done) {
-        for (const void* f : {(const void*)q8s::tile_kernel_f6<F6_NW, 0>, (const void*)q8s::tile_kernel_f6<F6_NW, 8>,
-                              (const void*)q8s::tile_kernel_f6s<F6S_MODE>, (const void*)q8s::tile_kernel_f6<F6_NW, 0, 3>,
-                              (const void*)q8s::tile_kernel_f6<F6_NW, 8, 3>,
-                              (const void*)q8s::tile_kernel_f6s<F6S_MODE, 3>}) {
+        for (const void* f : {(const void*)q8s::tile_kernel_f6<F6_NW>, (const void*)q8s::tile_kernel_f6<F6_NW, 3>,
+                              (const void*)q8s::tile_kernel_f6s<1>, (const void*)q8s::tile_kernel_f6s<3>}) {
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
         }
-        hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel_f6w<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel_f6w, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            f6t::EngineW::LDS_BYTES);
         if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 wide tile)");
         attr_done = true;
@@ -1682,10 +1462,10 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       if (!(phases & 4)) {
         // sieve only: the thresholds of a preceding phases-4 call are in the workspace
       } else if (two)
-        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0, 3>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
+        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 3>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
                            f6t::LDS, st, s);
       else
-        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 0>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
+        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
                            f6t::LDS, st, s);
       if (phases & 4) {
         OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
@@ -1704,19 +1484,13 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         wa.ntg = cdiv(N, f6t::EngineW::TGW);
         wa.gg = wa.ntg < f6w_group() ? wa.ntg : f6w_group();
         OFR_CHECK_ARG(wa.ntq * wa.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
-        hipLaunchKernelGGL((q8s::tile_kernel_f6w<0>), dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),
+        hipLaunchKernelGGL(q8s::tile_kernel_f6w, dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),
                            f6t::EngineW::LDS_BYTES, st, wa);
-      } else if (f6_shape() != 32 && two)
-        hipLaunchKernelGGL((q8s::tile_kernel_f6s<F6S_MODE, 3>), dim3((unsigned)(a.ntq * a.ntg)),
-                           dim3(f6t::Engine16::NT), f6t::LDS, st, a);
-      else if (f6_shape() != 32)
-        hipLaunchKernelGGL((q8s::tile_kernel_f6s<F6S_MODE>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
-                           f6t::LDS, st, a);
-      else if (two)
-        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 8, 3>), dim3((unsigned)(a.ntq * a.ntg)), dim3(F6_NW * 64),
+      } else if (two)
+        hipLaunchKernelGGL((q8s::tile_kernel_f6s<3>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
                            f6t::LDS, st, a);
       else
-        hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 8>), dim3((unsigned)(a.ntq * a.ntg)), dim3(F6_NW * 64),
+        hipLaunchKernelGGL((q8s::tile_kernel_f6s<1>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
                            f6t::LDS, st, a);
       OFR_LAUNCH_CHECK("f6 tile_kernel (sieve)");
     }

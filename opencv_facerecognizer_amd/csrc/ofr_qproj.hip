@@ -23,21 +23,21 @@
 //
 // Layouts: Aq [ceil(d/64)*256][ldk] int8, ldk % 128 == 0, ldk >= round_up(D, 128);
 // the rows of feature block jb = j/32 are jb*128 + s*32 + j%32 (the four slices
-// of 32 features are the four 32-row MFMA blocks of one wave).  The product
-// runs on the int8 tile engine (ofr_i8_tile.h, one-slice shape): a 256x256
-// tile = 64 features x 4 slices by 256 images, 8 waves (2 per SIMD) of 128x64,
-// k step 128, both operands by LDS-DMA (the images as raw uint8 rows; the
-// fragments become x - 128 by an XOR with 0x80 after the LDS read).
+// of 32 features are four 32-row blocks).  The product runs on the wide int8
+// engine (ofr_i8w_tile.h): 384 slice rows (3 feature blocks x 4 slices) by 256
+// images per tile, both operands by LDS-DMA (the images as raw uint8 rows; the
+// fragments become x - 128 by an XOR with 0x80 after the LDS read); B <= 4 faces
+// take a split-K GEMV over the slices instead (same integers, same epilogue).
 #include <string.h>
 
-#include "ofr_i8s_tile.h"
+#include <atomic>
+
+#include "ofr_i8_tile.h"
 #include "ofr_i8w_tile.h"
 
 namespace ofr {
 namespace q8 {
 
-using i8t::i32x16;
-using S = i8t::Shape<1>;
 constexpr int GROUP_F = 4;   // feature tiles per tile group (i8t::tile_coords)
 
 struct Args {
@@ -55,95 +55,6 @@ struct Args {
   int nk;
   int64_t ntf, ntb, gg;
 };
-
-// epilogue shared by both engines: rows (reg&3) + 8*(reg>>2) + 4*h of each 32-block are the same
-// 32 features in all four slices
-__device__ __forceinline__ void project_epilogue(const Args& p, const i32x16 (&acc)[4][S::CT], int64_t ft, int64_t b0,
-                                                 int wr, int wc, int h, int r32) {
-  const int64_t fb = ft * 2 + wr;   // 32-feature block of this wave
-#pragma unroll
-  for (int ct = 0; ct < S::CT; ++ct) {
-    const int64_t b = b0 + wc * S::QW + ct * 32 + r32;
-    if (b >= p.B) continue;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      double v[4];
-      const int64_t j0 = fb * 32 + 8 * g + 4 * h;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 4 * g + e;
-        const int64_t j = j0 + e;
-        double tv = (double)acc[0][ct][r];
-        tv += (double)acc[1][ct][r] * 0x1p-7;
-        tv += (double)acc[2][ct][r] * 0x1p-14;
-        tv += (double)acc[3][ct][r] * 0x1p-21;
-        if (j < p.d) {
-          double y = p.scale[j] * (tv + p.K[j]);   // exact: x . Wq[:, j]
-          if (p.shift) y -= p.shift[j];
-          v[e] = y;
-        } else {
-          v[e] = 0.0;
-        }
-      }
-      if (p.y_f64) {
-        double* yr = (double*)p.Y + b * p.ldy;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (j0 + e < p.d) yr[j0 + e] = v[e];
-      } else {
-        float* yr = (float*)p.Y + b * p.ldy;
-        if (j0 + 4 <= p.d && (((uintptr_t)(yr + j0)) & 15) == 0) {
-          f32x4 f;
-          f[0] = (float)v[0]; f[1] = (float)v[1]; f[2] = (float)v[2]; f[3] = (float)v[3];
-          *reinterpret_cast<f32x4*>(yr + j0) = f;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (j0 + e < p.d) yr[j0 + e] = (float)v[e];
-        }
-      }
-    }
-  }
-}
-
-// OFR_PROJ_ENGINE=i8: the previous engine (ofr_i8_tile.h, 2 x 128-feature stages, FLAT copies)
-__global__ void __launch_bounds__(S::NT, 1) project_q8_kernel(Args p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
-  int64_t ft, bt;
-  i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
-  const int64_t a0 = ft * i8t::TA, b0 = bt * S::TQ;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave / S::WQ, wc = wave % S::WQ, h = lane >> 5, r32 = lane & 31;
-
-  i32x16 acc[4][S::CT], unused[4][1];
-  i8t::mainloop<1, 0, true>(smem, p.Aq, p.ldk, p.arows, a0, reinterpret_cast<const int8_t*>(p.X), p.ldx, p.B, b0,
-                            p.ldx, p.nk, acc, unused);
-  project_epilogue(p, acc, ft, b0, wr, wc, h, r32);
-}
-
-// The default engine (ofr_i8s_tile.h): 64-feature stages in NST buffers, MUBUF copies, mid-stage
-// hand-off.  The panels' buffer descriptors bound the reads: B rows past the batch read as zero
-// (their outputs are not stored); columns past D meet zero W columns.
-template <int NST, bool XB = true, bool PP = false, bool W4 = false>
-__global__ void __launch_bounds__(i8s::NT, 1) project_q8s_kernel(Args p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
-  int64_t ft, bt;
-  i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
-  const int64_t a0 = ft * i8s::TA, b0 = bt * i8s::TB;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave / i8s::WQ, wc = wave % i8s::WQ, h = lane >> 5, r32 = lane & 31;
-  const int64_t brows = p.B - b0 < i8s::TB ? p.B - b0 : i8s::TB;
-  __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)(p.Aq + a0 * p.ldk), 0,
-                                                                (int)(i8s::TA * p.ldk), 0x00020000);
-  __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(p.X + b0 * p.ldx), 0, (int)(brows * p.ldx),
-                                                                0x00020000);
-  i32x16 acc[4][S::CT];
-  if constexpr (PP) i8s::mainloop_pp<NST, XB>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
-  else i8s::mainloop<NST, XB, W4>(smem, ra, (int)p.ldk, rb, (int)p.ldx, (int)cdiv(p.D, i8s::BK), acc);
-  project_epilogue(p, acc, ft, b0, wr, wc, h, r32);
-}
 
 // The wide engine (ofr_i8w_tile.h, round 3): 384 slice rows (96 features x 4 slices) x 256 images, 4
 // waves, each all 384 rows x 64 images, so a feature's four slices meet in one wave.  Tile ft covers
@@ -222,15 +133,6 @@ __global__ void __launch_bounds__(i8w::NT, 1) project_q8w_kernel(Args p) {
     case 1: project_w_body<1>(p, ft, b0); break;
     case 2: project_w_body<2>(p, ft, b0); break;
     default: project_w_body<3>(p, ft, b0); break;
-  }
-}
-
-// x -> x - 128 as int8 (XOR 0x80), 16 bytes per thread: the staged engine's pre-shifted B operand
-__global__ void __launch_bounds__(256) shift_images_kernel(const uint4* X, uint4* Y, int64_t n16) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
-    uint4 v = X[i];
-    v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
-    Y[i] = v;
   }
 }
 
@@ -421,27 +323,6 @@ static bool getenv_flag_gemv() {
   return f;
 }
 
-// OFR_PROJ_ENGINE selects the tile engine: default ("w") the wide engine of ofr_i8w_tile.h (384 x 256
-// tiles, one wave per SIMD: 1.51 against 1.67 ms at the bench shape, profiles/r03_proj_wide.json);
-// "i8" ofr_i8_tile.h (two 128-feature stages, FLAT copies; the default until round 3); "s4" / "s5" the
-// staged engine of ofr_i8s_tile.h with 4 / 5 64-feature buffers; "s5p" the staged engine on images
-// shifted to int8 by a pre-pass (no XOR in the k loop).  All give identical bits (tools/bench_proj.py;
-// the staged forms: 1.72 / 1.69 / 1.68 ms, profiles/r03_proj_engines.json).
-static int proj_engine() {
-  static const int f = [] {
-    const char* e = getenv("OFR_PROJ_ENGINE");
-    if (e && strcmp(e, "i8") == 0) return 0;
-    if (e && strcmp(e, "s4") == 0) return 4;
-    if (e && strcmp(e, "s5") == 0) return 5;
-    if (e && strcmp(e, "s5p") == 0) return 6;
-    if (e && strcmp(e, "pp4") == 0) return 7;
-    if (e && strcmp(e, "pp5") == 0) return 8;
-    if (e && strcmp(e, "s5w") == 0) return 9;
-    return 10;
-  }();
-  return f;
-}
-
 extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx, const int8_t* Aq,
                                     int64_t ldk, const double* scale, const double* K, int64_t d, const double* shift,
                                     void* Y, int64_t ldy, int y_dtype) {
@@ -453,33 +334,12 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   OFR_CHECK_ARG(ldk >= round_up(D, 128) && ldk % 128 == 0 && ((uintptr_t)Aq % 16) == 0,
                 "ofr_project_u8_exact: bad Aq layout");
   OFR_CHECK_ARG(ldy >= d, "ofr_project_u8_exact: ldy < d");
-  static bool attr_done = false;
-  if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)q8::project_q8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       q8::S::LDS);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              i8s::Lds<4>::BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              i8s::Lds<5>::BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<4, true, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<4>::BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, true, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)q8::project_q8s_kernel<5, true, false, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, i8s::Lds<5>::BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)q8::project_q8w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              i8w::LDS_BYTES);
-    if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8)");
-    attr_done = true;
+  static std::atomic<bool> attr_done{false};
+  if (!attr_done.load(std::memory_order_acquire)) {
+    hipError_t e = hipFuncSetAttribute((const void*)q8::project_q8w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       i8w::LDS_BYTES);
+    if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8w)");
+    attr_done.store(true, std::memory_order_release);
   }
   if (B <= 4 && getenv_flag_gemv()) {
     hipStream_t st = (hipStream_t)stream;
@@ -508,66 +368,18 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   p.ntf = cdiv(d, 64);
   p.arows = p.ntf * 256;
   p.gg = p.ntf < q8::GROUP_F ? p.ntf : q8::GROUP_F;
-  const int engine = proj_engine();
-  if (engine == 10) {   // the wide engine: tiles of 384 slice rows (3 projection blocks) x 256 images
-    OFR_CHECK_ARG((int64_t)i8w::TA * ldk < 0x7fffffffLL && (int64_t)i8w::TB * ldx < 0x7fffffffLL,
-                  "ofr_project_u8_exact: rows too long for the wide engine");
-    p.ntf = cdiv(p.arows, i8w::TA);
-    p.gg = p.ntf < q8::GROUP_F ? p.ntf : q8::GROUP_F;
-    p.nk = (int)cdiv(D, i8w::BK);
-    p.ntb = cdiv(B, i8w::TB);
-    OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-    hipLaunchKernelGGL(q8::project_q8w_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), i8w::LDS_BYTES,
-                       (hipStream_t)stream, p);
-    OFR_LAUNCH_CHECK("project_q8w_kernel");
-    return OFR_OK;
-  }
-  if (engine == 0) {
-    p.nk = (int)cdiv(D, q8::S::BK);
-    p.ntb = cdiv(B, q8::S::TQ);
-    OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-    hipLaunchKernelGGL(q8::project_q8_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(q8::S::NT), q8::S::LDS,
-                       (hipStream_t)stream, p);
-    OFR_LAUNCH_CHECK("project_q8_kernel");
-    return OFR_OK;
-  }
-  // the staged engine addresses a panel with 32-bit buffer offsets
-  OFR_CHECK_ARG((int64_t)i8s::TA * ldk < 0x7fffffffLL && (int64_t)i8s::TB * ldx < 0x7fffffffLL,
-                "ofr_project_u8_exact: rows too long for the staged engine");
-  p.nk = (int)cdiv(D, i8s::BK);
-  p.ntb = cdiv(B, i8s::TB);
+  // the wide engine: tiles of 384 slice rows (3 projection blocks) x 256 images; its panels are
+  // addressed with 32-bit buffer offsets
+  OFR_CHECK_ARG((int64_t)i8w::TA * ldk < 0x7fffffffLL && (int64_t)i8w::TB * ldx < 0x7fffffffLL,
+                "ofr_project_u8_exact: rows too long for the wide engine");
+  p.ntf = cdiv(p.arows, i8w::TA);
+  p.gg = p.ntf < q8::GROUP_F ? p.ntf : q8::GROUP_F;
+  p.nk = (int)cdiv(D, i8w::BK);
+  p.ntb = cdiv(B, i8w::TB);
   OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-  if (engine == 9) {
-    hipLaunchKernelGGL((q8::project_q8s_kernel<5, true, false, true>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
-                       i8s::Lds<5>::BYTES, (hipStream_t)stream, p);
-  } else if (engine == 7) {
-    hipLaunchKernelGGL((q8::project_q8s_kernel<4, true, true>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
-                       i8s::Lds<4>::BYTES, (hipStream_t)stream, p);
-  } else if (engine == 8) {
-    hipLaunchKernelGGL((q8::project_q8s_kernel<5, true, true>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
-                       i8s::Lds<5>::BYTES, (hipStream_t)stream, p);
-  } else if (engine == 4) {
-    hipLaunchKernelGGL(q8::project_q8s_kernel<4>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT), i8s::Lds<4>::BYTES,
-                       (hipStream_t)stream, p);
-  } else if (engine == 6) {   // images shifted to int8 by a pre-pass: no XOR in the k loop
-    hipStream_t st = (hipStream_t)stream;
-    uint8_t* xs = nullptr;
-    hipError_t e = hipMallocAsync((void**)&xs, (size_t)B * ldx, st);
-    if (e != hipSuccess) return hip_status(e, "ofr_project_u8_exact: shifted images");
-    const int64_t n16 = B * ldx / 16;
-    hipLaunchKernelGGL(q8::shift_images_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n16, 256), 4096)), dim3(256), 0,
-                       st, (const uint4*)X, (uint4*)xs, n16);
-    OFR_LAUNCH_CHECK("shift_images_kernel");
-    p.X = xs;
-    hipLaunchKernelGGL((q8::project_q8s_kernel<5, false>), dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT),
-                       i8s::Lds<5>::BYTES, st, p);
-    OFR_LAUNCH_CHECK("project_q8s_kernel");
-    e = hipFreeAsync(xs, st);
-    return e == hipSuccess ? OFR_OK : hip_status(e, "ofr_project_u8_exact: hipFreeAsync");
-  } else
-    hipLaunchKernelGGL(q8::project_q8s_kernel<5>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8s::NT), i8s::Lds<5>::BYTES,
-                       (hipStream_t)stream, p);
-  OFR_LAUNCH_CHECK("project_q8s_kernel");
+  hipLaunchKernelGGL(q8::project_q8w_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), i8w::LDS_BYTES,
+                     (hipStream_t)stream, p);
+  OFR_LAUNCH_CHECK("project_q8w_kernel");
   return OFR_OK;
 }
 
