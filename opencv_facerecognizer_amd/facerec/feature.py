@@ -583,7 +583,8 @@ class SpatialHistogram(AbstractFeature):
             raise NotImplementedError("SpatialHistogram (MI355X build) runs ExtendedLBP operators only")
         from .lbp import as_u8_images
         if not hasattr(imgs, "device"):
-            imgs = as_u8_images(np.stack([np.asarray(x) for x in imgs]))
+            imgs = as_u8_images(np.ascontiguousarray(imgs) if isinstance(imgs, np.ndarray) and imgs.ndim == 3
+                                else np.stack([np.asarray(x) for x in imgs]))
         counts, cell, cb = _device.elbp_hist(_device.u8_images(imgs), self.lbp_operator.geometry(), tuple(self.sz))
         return counts, cell, cb
 
@@ -591,7 +592,8 @@ class SpatialHistogram(AbstractFeature):
         """Faces of one size (list, array [n][H][W] or a uint8 device tensor such as ``ingest.faces``
         returns) -> (counts [n][cells * 2^P] device tensor, cell pixel count, bytes per count), one
         launch.  The histogram of face i is counts[i] / cell."""
-        counts, cell, cb = self.counts_device(X if hasattr(X, "device") else list(X))
+        counts, cell, cb = self.counts_device(X if hasattr(X, "device") or (isinstance(X, np.ndarray) and X.ndim == 3)
+                                              else list(X))
         return counts.reshape(counts.shape[0], -1), cell, cb
 
     def histograms(self, X):

@@ -84,7 +84,7 @@ class PredictableModel(object):
     def _search_lbph(self, X, k):
         """LBPH batch: faces grouped by size, one histogram launch + one counts search per group."""
         import torch
-        if hasattr(X, "device"):
+        if hasattr(X, "device") or (isinstance(X, np.ndarray) and X.ndim == 3):   # one face size
             groups = [(None, X)]
         else:
             X = list(X)
