@@ -67,6 +67,7 @@ struct TileArgs {
   // two-slice fp6 tier (NSEG = 3 kernels): the second-slice tiles; nk = 3 x the stages of one slice
   const int8_t* G2;
   const int8_t* Q2;
+  int serp;   // wide sieve pass: odd tile groups walk the query tiles backwards (tile_kernel_f6w)
 };
 
 // ---- keys of the tile epilogue (ofr_keys.h: order-preserving u32 keys, med3 key lists) ----
@@ -175,6 +176,7 @@ __device__ __forceinline__ void tile_epilogue(char* smem, const TileArgs& p, int
 constexpr int64_t SIEVE_STRIDE = 64;   // sample: gallery tiles 0, 64, 128, ... (OFR_SIEVE_STRIDE overrides)
 constexpr int64_t SIEVE_CAP = 32768;   // kept rows per query (256 KiB; ~16 * SIEVE_STRIDE expected, heavy tail)
 constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
+constexpr int SIEVE_RANK = 16;         // theta = this-th best key of the sample (ofr_knn_f6's sieve_rank)
 
 // Hits of one 256 x 256 tile: (a, s) = (aux, gscale) of gallery row threadIdx.x (padding rows:
 // (+inf, 0); they are also excluded explicitly, since a NaN th passes everything), sq2 / th per
@@ -429,6 +431,8 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   int64_t gt, qt;
   i8t::tile_coords(t, p.gg, p.ntg, p.ntq, gt, qt);
+  // serpentine: the last query panels of a group are the first of the next, while still in L2
+  if (p.serp && ((t / (p.gg * p.ntq)) & 1)) qt = p.ntq - 1 - qt;
   const int64_t g0 = gt * E::TGW, q0 = qt * f6t::TQ;
   switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
     case 0: f6w_body<0>(smem, p, g0, q0); break;
@@ -632,13 +636,13 @@ __global__ void __launch_bounds__(256) premerge_kernel(const Cand* cand, int64_t
   if ((int)threadIdx.x < KC) out[(q * PM + blockIdx.x) * KC + threadIdx.x] = lists[threadIdx.x];
 }
 
-// Sieve thresholds from the sample pass's tile lists: theta[q] = the 16th best key (KEY_NONE
-// when the sample holds fewer than 16 rows); resets the bucket counts.  One wave per query (four
+// Sieve thresholds from the sample pass's tile lists: theta[q] = the rank-th best key (KEY_NONE
+// when the sample holds fewer than rank rows; rank <= KC); resets the bucket counts.  One wave per query (four
 // per block): each lane keeps the best 16 keys of its strided share (KeyList, one v_med3 per slot),
 // then six shuffle rounds merge the lanes' lists (the same value as sorting the whole list by
 // (score, index): only the 16th score is used, and score_key is monotone).
 __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists, int64_t T, uint32_t* theta,
-                                                              int* count, int64_t B) {
+                                                              int* count, int64_t B, int rank) {
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (q >= B) return;
@@ -665,7 +669,10 @@ __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists,
     L.merge(o);
   }
   if (lane == 0) {
-    theta[q] = L.k[KC - 1];
+    uint32_t t = L.k[KC - 1];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) t = j == rank - 1 ? L.k[j] : t;   // register array: constant indices
+    theta[q] = t;
     count[q] = 0;
   }
 }
@@ -1309,6 +1316,15 @@ static int f6w_group() {
   return g;
 }
 
+// serpentine query order across the wide sieve pass's tile groups: the query panels a group ends on
+// are the ones the next group starts on, while their stages are still in the XCD's L2 -- same-box
+// A/B (profiles/r04_f6w_order_ab.txt): 60.0 -> 51.9 GB of L2<->fabric traffic per launch (FETCH_SIZE
+// x 2), 21.56 -> 21.45 ms.  OFR_F6W_SERP=0 restores the plain order (probe).
+static int f6w_serp() {
+  const char* e = getenv("OFR_F6W_SERP");
+  return e && atoi(e) == 0 ? 0 : 1;
+}
+
 // f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
 // thresholds, counts and buckets (each 256-byte aligned)
 struct SieveWs {
@@ -1321,6 +1337,17 @@ static int64_t sieve_stride() {
     return v >= 1 && v <= 4096 ? (int64_t)v : q8s::SIEVE_STRIDE;
   }();
   return s;
+}
+
+// Rank of the sample's key that becomes the sieve threshold theta (at least k).  theta only steers
+// the volume: the certificate's tau = min(theta, 16th kept key) bounds every row left out whatever
+// theta is, and with >= 16 rows kept tau is the 16th kept key either way.  The 16th best of a 1/64
+// sample keeps ~16 x 64 rows per query on gallery data; a lower rank keeps proportionally fewer (fewer
+// sieve hits and a shorter bucket for the merge).  OFR_SIEVE_RANK overrides (read at every call).
+static int sieve_rank() {
+  const char* e = getenv("OFR_SIEVE_RANK");
+  const int v = e ? atoi(e) : 0;
+  return v >= 1 && v <= q8s::KC ? v : q8s::SIEVE_RANK;
 }
 
 static SieveWs sieve_ws(int64_t B, int64_t N) {
@@ -1470,7 +1497,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       if (phases & 4) {
         OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
         hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, s.cand, s.ntg,
-                           theta, count, B);
+                           theta, count, B, std::max(k, sieve_rank()));
         OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
       }
       a.theta = theta;
@@ -1483,6 +1510,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         q8s::TileArgs wa = a;   // 384-row gallery tiles over the same 256-row panel layout
         wa.ntg = cdiv(N, f6t::EngineW::TGW);
         wa.gg = wa.ntg < f6w_group() ? wa.ntg : f6w_group();
+        wa.serp = f6w_serp();
         OFR_CHECK_ARG(wa.ntq * wa.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
         hipLaunchKernelGGL(q8s::tile_kernel_f6w, dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),
                            f6t::EngineW::LDS_BYTES, st, wa);
