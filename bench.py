@@ -501,7 +501,9 @@ def main():
     kept = (gallery.sieve_counts(B, pipe.ws[(args.steps - 1) % StepPipeline.NWS]) if args.search == "f6"
             else None)                                                  # last step's fp6 sieve (this rank)
     kept = None if kept is None else {"mean": float(kept.double().mean()), "max": int(kept.max()),
-                                      "cap": 32768, "expected": "~16 x OFR_SIEVE_STRIDE (64)"}
+                                      "cap": 32768,
+                                      "expected": ("~4 x 64 (row sample)" if FloatGallery.row_sample()
+                                                   else "~16 x OFR_SIEVE_STRIDE (64) (panel sample)")}
 
     # ---- small-batch regime (the recognizers send one face per call): HBM-bound streaming of the gallery ----
     small = []

@@ -208,6 +208,25 @@ int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq,
                const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
                void* workspace, size_t workspace_bytes);
+/* ofr_knn_f6 with a ROW sample for the sieve thresholds (B > 32; new, same contract otherwise).
+ * St/sscale/saux: fp6 tiles (ofr_f6_tiles_bytes(Ns, d) bytes), row scales and aux terms of Ns <=
+ * ceil(N / 64) gallery rows, written by ofr_f6_sample_rows (rows 0, 64, 128, ...).  The threshold
+ * becomes the max(k, 4)-th best key of the sample instead of the 16th best of every 64th 256-row
+ * panel: ~4 x 64 rows kept per query instead of ~16 x 64, and a gallery stored identity by identity
+ * cannot put whole clusters of one face into the sample.  The sample only steers how many rows are
+ * kept: results and certificates are those of ofr_knn_f6 (any sample, any threshold).           */
+int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                       const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
+                       const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
+                       int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, const void* St,
+                       int64_t Ns, const float* sscale, const float* saux, void* workspace, size_t workspace_bytes);
+/* The row step of the sample (64) and its builder: gallery rows j * 64 for j in [j0, j1) (X = row 0
+ * of the fp32 gallery, ldx its leading dimension) are quantized into sample row j of tiles / scale /
+ * stats (as ofr_f6_quantize_rows_at) and saux[j] = aux[j * 64].  A gallery of N rows has j1 =
+ * ceil(N / 64); an append of rows [N0, N1) extends it with j0 = ceil(N0 / 64), j1 = ceil(N1 / 64). */
+int64_t ofr_f6_sample_step(void);
+int ofr_f6_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1, const float* aux,
+                       void* tiles, size_t tiles_bytes, float* scale, double* stats, float* saux);
 /* Phase 2 of ofr_knn_f6 split for a gallery sharded over ranks (new; replaces the
  * per-rank re-rank of classifier.py:104-119's loop at G > 1).  After phase 1 on every shard:
  *   stage 1 selects each query's 16 candidates into the workspace and writes ub[B][k] -- upper

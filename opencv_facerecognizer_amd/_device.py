@@ -247,6 +247,7 @@ class FloatGallery:
             if tier == "f6":
                 call("ofr_f6_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, ptr(g["Gs"]),
                      g["Gs"].numel(), ptr(g["scale"]), ptr(g["stats"]))
+                self._sample_rows(g, N0, N1)
             elif tier == "f6x2":                       # the first slice is the f6 tier's, extended above
                 call("ofr_f6x2_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, None,
                      ptr(g["Gs2"]), g["Gs2"].numel(), ptr(g["scale"]), ptr(g["stats"]))
@@ -389,10 +390,19 @@ class FloatGallery:
             gmax = torch.empty(4, dtype=torch.float64, device=dev_)
             extra = {}
             if tier == "f6":
-                nbytes = _lib.load().ofr_f6_tiles_bytes(cap, self.d)
+                lib = _lib.load()
+                nbytes = lib.ofr_f6_tiles_bytes(cap, self.d)
                 Gs = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
                 call("ofr_f6_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, ptr(Gs), nbytes,
                      ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
+                # the sieve's row sample (ofr_knn_f6_sampled): rows 0, 64, 128, ... in their own tiles
+                ns = -(-cap // lib.ofr_f6_sample_step())
+                sbytes = lib.ofr_f6_tiles_bytes(ns, self.d)
+                extra = dict(St=torch.empty(sbytes, dtype=torch.uint8, device=dev_),
+                             sscale=torch.empty(ns, dtype=torch.float32, device=dev_),
+                             sstats=torch.empty((ns, 3), dtype=torch.float64, device=dev_),
+                             saux=torch.empty(ns, dtype=torch.float32, device=dev_))
+                self._sample_rows(extra, 0, self.N)
                 ld = 0
             elif tier == "f6x2":                  # first slice = the f6 tier's tiles (same codes and scale)
                 Gs = self._tier_gallery("f6")["Gs"]
@@ -408,6 +418,19 @@ class FloatGallery:
                      ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
             self.q8[tier] = dict(Gs=Gs, scale=gs, stats=st, gmax=gmax, ld=ld, **extra)
         return self.q8[tier]
+
+    def _sample_rows(self, g, N0, N1):
+        """Extend the f6 tier's row sample over gallery rows [N0, N1) (ofr_f6_sample_rows)."""
+        step = _lib.load().ofr_f6_sample_step()
+        j0, j1 = -(-N0 // step), -(-N1 // step)
+        call("ofr_f6_sample_rows", stream(), ptr(self._Gbuf), self.ld, self.d, j0, j1, ptr(self._auxbuf), ptr(g["St"]),
+             g["St"].numel(), ptr(g["sscale"]), ptr(g["sstats"]), ptr(g["saux"]))
+
+    @staticmethod
+    def row_sample():
+        """The fp6 sieve's thresholds from the row sample (default) or, OFR_SIEVE_SAMPLE=panels, from every
+        64th 256-row panel (ofr_knn_f6; probe / A-B)."""
+        return os.environ.get("OFR_SIEVE_SAMPLE", "rows") != "panels"
 
     def quantize_queries(self, Qd, out=None, tier="f6"):
         """Centred fp32 query rows -> the tier's quantized rows, scales and stats (device)."""
@@ -475,6 +498,12 @@ class FloatGallery:
                  ptr(qq["scale"]), ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]),
                  ptr(g["Gs2"]), ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]),
                  ptr(out[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(ws), ws.numel())
+        elif tier == "f6" and self.row_sample():
+            ns = -(-self.N // lib.ofr_f6_sample_step())
+            call("ofr_knn_f6_sampled", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
+                 ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),
+                 ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
+                 ptr(qq["bound"]), ptr(g["St"]), ns, ptr(g["sscale"]), ptr(g["saux"]), ptr(ws), ws.numel())
         elif tier == "f6":
             call("ofr_knn_f6", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
                  ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),

@@ -65,6 +65,11 @@ SIGNATURES = {
     "ofr_f6_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp]),
     "ofr_knn_f6": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
                            c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz]),
+    "ofr_knn_f6_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
+                                   c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                   c_vp, c_sz]),
+    "ofr_f6_sample_step": (c_i64, []),
+    "ofr_f6_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp]),
     "ofr_knn_f6_merge_pruned": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp, c_sz]),

@@ -177,6 +177,10 @@ constexpr int64_t SIEVE_STRIDE = 64;   // sample: gallery tiles 0, 64, 128, ... 
 constexpr int64_t SIEVE_CAP = 32768;   // kept rows per query (256 KiB; ~16 * SIEVE_STRIDE expected, heavy tail)
 constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
 constexpr int SIEVE_RANK = 16;         // theta = this-th best key of the sample (ofr_knn_f6's sieve_rank)
+// ofr_knn_f6_sampled: the sample is a row sample (gallery rows 0, 64, 128, ...: ofr_f6_sample_rows)
+// instead of whole panels, theta its SIEVE_RANK_ROWS-th best key (~4 x 64 rows kept per query)
+constexpr int64_t SAMPLE_STEP = 64;
+constexpr int SIEVE_RANK_ROWS = 4;
 
 // Hits of one 256 x 256 tile: (a, s) = (aux, gscale) of gallery row threadIdx.x (padding rows:
 // (+inf, 0); they are also excluded explicitly, since a NaN th passes everything), sq2 / th per
@@ -1081,6 +1085,12 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
   }
 }
 
+// saux[j] = aux[j * step] for j in [j0, j1) (the row sample's aux terms)
+__global__ void sample_aux_kernel(const float* aux, int64_t j0, int64_t j1, int64_t step, float* saux) {
+  const int64_t j = j0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (j < j1) saux[j] = aux[j * step];
+}
+
 // zero rows of the last panel past R (they are never selected: the epilogue masks rows >= N)
 __global__ void f6_zero_tail(char* tiles, int64_t R, int64_t nst) {
   const int64_t p = R >> 8;
@@ -1281,6 +1291,24 @@ extern "C" int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, i
   return ofr_q8_maxima(stream, stats, aux, R, maxima);
 }
 
+extern "C" int64_t ofr_f6_sample_step(void) { return q8s::SAMPLE_STEP; }
+
+extern "C" int ofr_f6_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
+                                  const float* aux, void* tiles, size_t tiles_bytes, float* scale, double* stats,
+                                  float* saux) {
+  OFR_CHECK_ARG(j0 >= 0 && j1 >= j0 && d >= 1 && ldx >= d, "ofr_f6_sample_rows: bad sizes");
+  if (j1 == j0) return OFR_OK;
+  OFR_CHECK_ARG(X && aux && saux, "ofr_f6_sample_rows: null pointer");
+  OFR_CHECK_ARG(ldx < INT64_MAX / q8s::SAMPLE_STEP, "ofr_f6_sample_rows: leading dimension too large");
+  const int rc = ofr_f6_quantize_rows_at(stream, X + j0 * q8s::SAMPLE_STEP * ldx, j1 - j0, d,
+                                         ldx * q8s::SAMPLE_STEP, j0, tiles, tiles_bytes, scale, stats);
+  if (rc) return rc;
+  hipLaunchKernelGGL(q8s::sample_aux_kernel, dim3((unsigned)cdiv(j1 - j0, 256)), dim3(256), 0, (hipStream_t)stream,
+                     aux, j0, j1, q8s::SAMPLE_STEP, saux);
+  OFR_LAUNCH_CHECK("f6 sample_aux_kernel");
+  return OFR_OK;
+}
+
 // waves of the sample pass's fp6 engine (f6t::Engine<8>, 32x32x64 MFMA)
 constexpr int F6_NW = 8;
 
@@ -1343,15 +1371,22 @@ static int64_t sieve_stride() {
 // the volume: the certificate's tau = min(theta, 16th kept key) bounds every row left out whatever
 // theta is, and with >= 16 rows kept tau is the 16th kept key either way.  The 16th best of a 1/64
 // sample keeps ~16 x 64 rows per query on gallery data; a lower rank keeps proportionally fewer (fewer
-// sieve hits and a shorter bucket for the merge).  OFR_SIEVE_RANK overrides (read at every call).
-static int sieve_rank() {
+// sieve hits and a shorter bucket for the merge), but a panel sample of a gallery stored identity by
+// identity holds whole clusters of one face (profiles/r04_sieve_stride_rank_ab.txt: ranks 4 and 8
+// leave queries uncertified).  A row sample (ofr_knn_f6_sampled) holds at most a row or two of any
+// cluster, and its 4th best key keeps ~4 x 64 rows.  OFR_SIEVE_RANK overrides both (read at every call).
+static int sieve_rank(bool rows) {
   const char* e = getenv("OFR_SIEVE_RANK");
   const int v = e ? atoi(e) : 0;
-  return v >= 1 && v <= q8s::KC ? v : q8s::SIEVE_RANK;
+  return v >= 1 && v <= q8s::KC ? v : rows ? q8s::SIEVE_RANK_ROWS : q8s::SIEVE_RANK;
 }
 
+// sample rows of an N-row gallery (ofr_knn_f6_sampled: at most this many)
+static int64_t sample_rows(int64_t N) { return cdiv(N > 0 ? N : 1, q8s::SAMPLE_STEP); }
+
 static SieveWs sieve_ws(int64_t B, int64_t N) {
-  const int64_t ts = cdiv(cdiv(N > 0 ? N : 1, q8s::TG), sieve_stride());
+  // sample lists: panel sample (ofr_knn_f6) or row sample (ofr_knn_f6_sampled), whichever has more tiles
+  const int64_t ts = std::max(cdiv(cdiv(N > 0 ? N : 1, q8s::TG), sieve_stride()), cdiv(sample_rows(N), q8s::TG));
   SieveWs w;
   w.lists = 0;
   w.theta = round_up((int64_t)(B * ts * q8s::KC * sizeof(Cand)), 256);
@@ -1381,12 +1416,20 @@ extern "C" size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N) {
   return B <= 32 ? (size_t)-1 : sieve_ws(B, N).count;
 }
 
+// the row sample of ofr_knn_f6_sampled
+struct F6Sample {
+  const void* tiles;
+  int64_t n;
+  const float* scale;
+  const float* aux;
+};
+
 static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                        const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
                        size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2 = nullptr,
-                       const void* Gt2 = nullptr);
+                       const void* Gt2 = nullptr, const F6Sample* smp = nullptr);
 
 extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                           const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
@@ -1397,6 +1440,22 @@ extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, i
                 "ofr_knn_f6: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
                      out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr);
+}
+
+extern "C" int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                                  const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
+                                  int64_t d, const void* Gt, const float* gscale, const float* aux,
+                                  const double* gmax, int k, int64_t index_base, double* out_d, int64_t* out_i,
+                                  int* cert, double* bound, const void* St, int64_t Ns, const float* sscale,
+                                  const float* saux, void* workspace, size_t workspace_bytes) {
+  OFR_CHECK_ARG(phases >= 1 && phases <= 15,
+                "ofr_knn_f6_sampled: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
+  OFR_CHECK_ARG(St && sscale && saux, "ofr_knn_f6_sampled: null sample pointer");
+  OFR_CHECK_ARG(Ns >= 1 && Ns <= sample_rows(N), "ofr_knn_f6_sampled: sample rows must be in [1, ceil(N / 64)]");
+  OFR_CHECK_ARG((uintptr_t)St % 16 == 0, "ofr_knn_f6_sampled: sample tiles must be 16-byte aligned");
+  const F6Sample smp{St, Ns, sscale, saux};
+  return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, nullptr, nullptr, &smp);
 }
 
 extern "C" int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
@@ -1428,7 +1487,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                        const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
-                       size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2, const void* Gt2) {
+                       size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2, const void* Gt2,
+                       const F6Sample* smp) {
   const bool two = Gt2 != nullptr;   // the two-slice tier f6x2: three segments of stages (f6t::seg_src)
   OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_f6: bad sizes (empty galleries use ofr_knn_f32)");
   if (k < 1 || k > q8s::KC) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6: k must be in [1, 16]");
@@ -1480,10 +1540,19 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 wide tile)");
         attr_done = true;
       }
-      // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel -> thresholds
+      // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel, or of the row sample -> thresholds
       q8s::TileArgs s = a;
-      s.gstride = sieve_stride();
-      s.ntg = cdiv(a.ntg, s.gstride);
+      const bool rows = smp && !two;
+      if (rows) {
+        s.G = (const int8_t*)smp->tiles;
+        s.N = smp->n;
+        s.gscale = smp->scale;
+        s.aux = smp->aux;
+        s.ntg = f6t::panels(smp->n);
+      } else {
+        s.gstride = sieve_stride();
+        s.ntg = cdiv(a.ntg, s.gstride);
+      }
       s.gg = s.ntg < q8s::GROUP_G ? s.ntg : q8s::GROUP_G;
       s.cand = reinterpret_cast<Cand*>(wsb + w.lists);
       if (!(phases & 4)) {
@@ -1497,7 +1566,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       if (phases & 4) {
         OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
         hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, s.cand, s.ntg,
-                           theta, count, B, std::max(k, sieve_rank()));
+                           theta, count, B, std::max(k, sieve_rank(rows)));
         OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
       }
       a.theta = theta;

@@ -179,3 +179,72 @@ def test_sieve_complete_vs_exact_scores_headline_shape():
         wrong = np.intersect1d(np.concatenate(allowed_hi[j]), kept)
         assert wrong.size == 0, (j, s[j], wrong[:10])
     assert n_must >= 16 * 64                                           # the test is not vacuous
+
+
+def _clustered(n_id, per, d, B, seed):
+    """Gallery stored identity by identity (per rows each, as build_gallery and the reference's
+    read_images order them) and B queries near random identities."""
+    r = np.random.default_rng(seed)
+    C = r.normal(0, 20, (n_id, d))
+    G = (np.repeat(C, per, axis=0) + r.normal(0, 3, (n_id * per, d))).astype(np.float32).astype(np.float64)
+    Q = (C[r.integers(0, n_id, B)] + r.normal(0, 3, (B, d))).astype(np.float32).astype(np.float64)
+    return G, Q
+
+
+@pytest.mark.parametrize("k", [1, 5])
+def test_row_sample_same_results_fewer_rows(k, monkeypatch):
+    """ofr_knn_f6_sampled (row sample, 4th key: the default) against ofr_knn_f6 (every 64th panel, 16th
+    key; OFR_SIEVE_SAMPLE=panels): identical certified top-k -- both the exact fp64 top-k of the
+    gallery -- with fewer rows kept per query (the sample only steers the sieve's volume)."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    G, Q = _clustered(4000, 10, 192, 512, 77 + k)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    Qd = g.query_rows(Q)
+    res, kept = {}, {}
+    for mode in ("rows", "panels"):
+        monkeypatch.setenv("OFR_SIEVE_SAMPLE", mode)
+        qq = g.quantize_queries(Qd, tier="f6")
+        g.search_q8_phase(4 | 8, Qd, qq, k)
+        torch.cuda.synchronize()
+        kept[mode] = g.sieve_counts(len(Q)).cpu().numpy().copy()
+        d_, i_ = g.search(Qd, k)
+        torch.cuda.synchronize()
+        res[mode] = (d_.cpu().numpy(), i_.cpu().numpy())
+    assert np.array_equal(res["rows"][1], res["panels"][1])
+    assert np.array_equal(res["rows"][0], res["panels"][0])
+    Gt, Qt = torch.from_numpy(G).cuda(), torch.from_numpy(Q).cuda()
+    D2 = (Qt * Qt).sum(1)[:, None] + (Gt * Gt).sum(1)[None, :] - 2.0 * Qt @ Gt.t()
+    want = torch.topk(D2, k, dim=1, largest=False).indices.cpu().numpy()
+    assert np.array_equal(np.sort(res["rows"][1], 1), np.sort(want, 1))
+    assert np.all(kept["rows"] >= 1) and np.all(kept["rows"] <= g.SIEVE_CAP)
+    assert kept["rows"].mean() < 0.5 * kept["panels"].mean(), (kept["rows"].mean(), kept["panels"].mean())
+
+
+def test_row_sample_extended_by_append():
+    """An append extends the row sample exactly as a fresh build of all the rows writes it (rows
+    0, 64, ... of the grown gallery: tiles, scales and aux), and the grown gallery searches exactly."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    G, Q = _clustered(300, 10, 160, 64, 5)
+    N0 = 1000                                            # not a multiple of 64: the append starts mid-step
+    g = FloatGallery(G[:900], _lib.METRIC_EUCLIDEAN)
+    g.append(G[900:N0])                                  # grows the storage to 1,350 rows
+    cap0 = g.capacity()
+    assert cap0 > N0 + 300
+    g._tier_gallery("f6")                                # built before the next append, then extended in place
+    g.append(G[N0:cap0])                                 # fills the storage, no re-allocation
+    assert g.capacity() == cap0 and g.N == cap0 and g.q8 is not None
+    h = FloatGallery(G[:cap0], _lib.METRIC_EUCLIDEAN, shift64=g.shift64)
+    a, b = g._tier_gallery("f6"), h._tier_gallery("f6")
+    step = _lib.load().ofr_f6_sample_step()
+    ns = -(-g.N // step)
+    nb = _lib.load().ofr_f6_tiles_bytes(ns, g.d)
+    assert torch.equal(a["St"][:nb], b["St"][:nb])
+    assert torch.equal(a["sscale"][:ns], b["sscale"][:ns])
+    assert torch.equal(a["saux"][:ns], b["saux"][:ns])
+    assert torch.equal(a["saux"][:ns], g.aux[::step][:ns])
+    Qd = g.query_rows(Q)
+    d_, i_ = g.search(Qd, 3)
+    d2, i2 = h.search(h.query_rows(Q), 3)
+    assert torch.equal(i_, i2) and torch.allclose(d_, d2, rtol=1e-9)
