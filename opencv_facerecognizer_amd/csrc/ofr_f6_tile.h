@@ -451,18 +451,24 @@ struct EngineW {
   // descriptor of the wave's gallery piece j.
   struct Feed {
     __amdgpu_buffer_rsrc_t rg, rq;
+    __amdgpu_buffer_rsrc_t rg2, rq2;   // the second-slice tiles (NSEG = 3, the two-slice tier f6x2)
     uint32_t gsrc[GPW];
   };
 
-  template <int W>
+  template <int W, int NSEG = 1>
   static __device__ __forceinline__ void feed_init(Feed& f, const char* G, int64_t N, const char* Q, int64_t qp,
-                                                   int64_t nst, int64_t gt) {
+                                                   int64_t nst, int64_t gt, const char* G2 = nullptr,
+                                                   const char* Q2 = nullptr) {
     const int64_t h0 = 3 * gt, p0 = h0 >> 1;
     const int64_t pb = nst * (int64_t)PANEL;                 // bytes per 256-row panel
     const int64_t rem = panels(N) * pb - p0 * pb;
     const int64_t rec = rem < 2 * pb ? rem : 2 * pb;         // reads past the gallery return zeros
     f.rg = __builtin_amdgcn_make_buffer_rsrc((void*)(G + p0 * pb), 0, (int)rec, 0x00020000);
     f.rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * pb), 0, (int)pb, 0x00020000);
+    if constexpr (NSEG == 3) {
+      f.rg2 = __builtin_amdgcn_make_buffer_rsrc((void*)(G2 + p0 * pb), 0, (int)rec, 0x00020000);
+      f.rq2 = __builtin_amdgcn_make_buffer_rsrc((void*)(Q2 + qp * pb), 0, (int)pb, 0x00020000);
+    }
 #pragma unroll
     for (int j = 0; j < GPW; ++j) {
       const int g = W * GPW + j, k = g / 12, q = (g % 12) / 3, part = g % 3;
@@ -473,17 +479,19 @@ struct EngineW {
   }
   // piece J of wave W's share of stage ks (kso = ks * PANEL) of the gallery tile (9 of its 36) / query
   // panel (6 of 24) into the slot at LDS byte offset so
+  // (rg / rq: the descriptor of the stage's segment, f.rg / f.rq or f.rg2 / f.rq2)
   template <int W, int J>
-  static __device__ __forceinline__ void gcopy(const Feed& f, uint32_t so, uint32_t kso) {
+  static __device__ __forceinline__ void gcopy(const __amdgpu_buffer_rsrc_t rg, const Feed& f, uint32_t so,
+                                               uint32_t kso) {
     constexpr int g = W * GPW + J, k = g / 12, q = (g % 12) / 3, part = g % 3;
     constexpr uint32_t cd = k * HPB + q * 3072 + (part < 2 ? part * 1024 : 2048);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(f.rg, (OFR_LDS void*)(uintptr_t)(so + cd), 16, (threadIdx.x & 63) * 16,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (OFR_LDS void*)(uintptr_t)(so + cd), 16, (threadIdx.x & 63) * 16,
                                              f.gsrc[J] + kso, 0, 0);
   }
   template <int W, int J>
-  static __device__ __forceinline__ void qcopy(const Feed& f, uint32_t so, uint32_t kso) {
+  static __device__ __forceinline__ void qcopy(const __amdgpu_buffer_rsrc_t rq, uint32_t so, uint32_t kso) {
     constexpr uint32_t o = (W * QPW + J) * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(f.rq, (OFR_LDS void*)(uintptr_t)(so + o), 16, (threadIdx.x & 63) * 16,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (OFR_LDS void*)(uintptr_t)(so + o), 16, (threadIdx.x & 63) * 16,
                                              o + kso, 0, 0);
   }
 
@@ -534,11 +542,23 @@ struct EngineW {
       asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
                    : "+v"(c) : "v"(a), "v"(b), "v"(sc));
   }
+  template <bool AG>   // separate gallery (A) and query (B) block scales (NSEG = 3)
+  static __device__ __forceinline__ void mfma2(const i32x6& a, const i32x6& b, f32x4& c, int sa, int sb) {
+    if constexpr (AG)
+      asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
+                   : "+a"(c) : "v"(a), "v"(b), "v"(sa), "v"(sb));
+    else
+      asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
+                   : "+v"(c) : "v"(a), "v"(b), "v"(sa), "v"(sb));
+  }
   static __device__ __forceinline__ void wait_drain() {   // the last MFMAs' results readable
     asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
   }
 
-  template <int W>
+  // NSEG: segments of nst stages (seg_src): 1 = the fp6 tier; 3 = the two-slice tier f6x2, whose
+  // stages of segment 1 / 2 read the query / gallery second slices (f.rq2 / f.rg2) with block scale
+  // 2^-4 on that operand (seg_scales)
+  template <int W, int NSEG = 1>
   static __device__ __forceinline__ void mainloop(const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
     constexpr int WR = W >> 1, WC = W & 1;
     int sc = SCALE_ONE;
@@ -547,23 +567,43 @@ struct EngineW {
     for (int i = 0; i < NA; ++i)
 #pragma unroll
       for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int last = nst - 1;
-    auto kso = [&](int s) { return (uint32_t)(s < last ? s : last) * (uint32_t)PANEL; };
-    auto gall = [&](uint32_t so, uint32_t ko) {
-      gcopy<W, 0>(f, so, ko); gcopy<W, 1>(f, so, ko); gcopy<W, 2>(f, so, ko);
-      gcopy<W, 3>(f, so, ko); gcopy<W, 4>(f, so, ko); gcopy<W, 5>(f, so, ko);
-      gcopy<W, 6>(f, so, ko); gcopy<W, 7>(f, so, ko); gcopy<W, 8>(f, so, ko);
+    const int last = NSEG * nst - 1;
+    // byte offset of stage s (clamped to the last) inside its segment's tiles, and the segment's descriptors
+    auto kso = [&](int s) {
+      const int c = s < last ? s : last;
+      if constexpr (NSEG == 1) return (uint32_t)c * (uint32_t)PANEL;
+      else return (uint32_t)(c - (c >= 2 * nst ? 2 : (c >= nst ? 1 : 0)) * nst) * (uint32_t)PANEL;
     };
-    auto qall = [&](uint32_t so, uint32_t ko) {
-      qcopy<W, 0>(f, so, ko); qcopy<W, 1>(f, so, ko); qcopy<W, 2>(f, so, ko);
-      qcopy<W, 3>(f, so, ko); qcopy<W, 4>(f, so, ko); qcopy<W, 5>(f, so, ko);
+    auto rgs = [&](int s) {
+      if constexpr (NSEG == 1) return f.rg;
+      else return (s < last ? s : last) >= 2 * nst ? f.rg2 : f.rg;
+    };
+    auto rqs = [&](int s) {
+      if constexpr (NSEG == 1) return f.rq;
+      else {
+        const int c = s < last ? s : last;
+        return c >= nst && c < 2 * nst ? f.rq2 : f.rq;
+      }
+    };
+    auto gall = [&](uint32_t so, int st) {
+      const __amdgpu_buffer_rsrc_t r = rgs(st);
+      const uint32_t ko = kso(st);
+      gcopy<W, 0>(r, f, so, ko); gcopy<W, 1>(r, f, so, ko); gcopy<W, 2>(r, f, so, ko);
+      gcopy<W, 3>(r, f, so, ko); gcopy<W, 4>(r, f, so, ko); gcopy<W, 5>(r, f, so, ko);
+      gcopy<W, 6>(r, f, so, ko); gcopy<W, 7>(r, f, so, ko); gcopy<W, 8>(r, f, so, ko);
+    };
+    auto qall = [&](uint32_t so, int st) {
+      const __amdgpu_buffer_rsrc_t r = rqs(st);
+      const uint32_t ko = kso(st);
+      qcopy<W, 0>(r, so, ko); qcopy<W, 1>(r, so, ko); qcopy<W, 2>(r, so, ko);
+      qcopy<W, 3>(r, so, ko); qcopy<W, 4>(r, so, ko); qcopy<W, 5>(r, so, ko);
     };
     // ring slots (LDS byte offsets) of stages s, s + 1, s + 2 (gallery) and s, s + 1 (query)
     uint32_t g0 = 0, g1 = GSLOT, g2 = 2 * GSLOT, q0 = QBASE, q1 = QBASE + QSLOT;
     // prologue: G(0), Q(0), G(1), Q(1) and pieces 0, 1 of G(2)
-    gall(g0, kso(0)); qall(q0, kso(0)); gall(g1, kso(1)); qall(q1, kso(1));
-    gcopy<W, 0>(f, g2, kso(2));
-    gcopy<W, 1>(f, g2, kso(2));
+    gall(g0, 0); qall(q0, 0); gall(g1, 1); qall(q1, 1);
+    gcopy<W, 0>(rgs(2), f, g2, kso(2));
+    gcopy<W, 1>(rgs(2), f, g2, kso(2));
     wait_vm<GPW + QPW + 2>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -579,10 +619,19 @@ struct EngineW {
     for (int s = 0; s <= last; ++s) {
       const Bases ac = abase(g0), an = abase(g1), bn = bbase(q1);
       const uint32_t k2 = kso(s + 2), k3 = kso(s + 3);
+      const __amdgpu_buffer_rsrc_t rg2s = rgs(s + 2), rq2s = rqs(s + 2), rg3s = rgs(s + 3);
+      int sa = SCALE_ONE, sb = SCALE_ONE;
+      if constexpr (NSEG == 3) {
+        seg_scales<NSEG>(s, nst, sa, sb);
+        asm volatile("" : "+v"(sa), "+v"(sb));
+      }
       auto row = [&](auto ii) {
         constexpr int i = decltype(ii)::value;
         constexpr bool AG = i < NAA;
-        auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) { mfma<AG>(x, y, c, sc); };
+        auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) {
+          if constexpr (NSEG == 1) mfma<AG>(x, y, c, sc);
+          else mfma2<AG>(x, y, c, sa, sb);
+        };
         if constexpr (i == 1) {              // barrier A: Q(s) consumed by every wave
           // Q(s)'s reads (row 11 of s - 1) are older than row 0's gallery read, the only one allowed in flight
           asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
@@ -596,9 +645,9 @@ struct EngineW {
           __builtin_amdgcn_sched_barrier(0);
         }
         // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0), G(s+3) into G(s)'s (g0)
-        if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(f, g2, k2);
-        if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(f, q0, k2);
-        if constexpr (i == 10) gcopy<W, 0>(f, g0, k3);   // piece 1: in the middle of rows 10 / 11
+        if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(rg2s, f, g2, k2);
+        if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(rq2s, q0, k2);
+        if constexpr (i == 10) gcopy<W, 0>(rg3s, f, g0, k3);   // piece 1: in the middle of rows 10 / 11
         if constexpr (i == NA - 1) {
           // rows 10 and 11 run together (below, i == 10)
         } else if constexpr (i == NA - 2) {
@@ -611,7 +660,7 @@ struct EngineW {
           mm(a[1], b[1], acc[10][1]); mm(a[2], b[1], acc[11][1]); b[1] = fragB<WC * 128 + 16>(bn);
           mm(a[1], b[2], acc[10][2]); mm(a[2], b[2], acc[11][2]); b[2] = fragB<WC * 128 + 32>(bn);
           mm(a[1], b[3], acc[10][3]); mm(a[2], b[3], acc[11][3]); b[3] = fragB<WC * 128 + 48>(bn);
-          gcopy<W, 1>(f, g0, k3);
+          gcopy<W, 1>(rg3s, f, g0, k3);
           mm(a[1], b[4], acc[10][4]); mm(a[2], b[4], acc[11][4]); b[4] = fragB<WC * 128 + 64>(bn);
           mm(a[1], b[5], acc[10][5]); mm(a[2], b[5], acc[11][5]); b[5] = fragB<WC * 128 + 80>(bn);
           mm(a[1], b[6], acc[10][6]); mm(a[2], b[6], acc[11][6]); b[6] = fragB<WC * 128 + 96>(bn);

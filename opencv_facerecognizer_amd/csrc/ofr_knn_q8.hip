@@ -347,18 +347,20 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
 }
 
 // fp6 sieve pass on the wide engine (f6t::EngineW): 384 gallery x 256 query tiles, 4 waves (one per
-// SIMD), p.ntg = ceil(N / 384) gallery tiles.  The epilogue is sieve_epilogue16's for the 192 x 128
+// SIMD), p.ntg = ceil(N / 384) gallery tiles; NSEG = 3: the two-slice tier's three segments of p.nk / 3
+// stages (p.G2 / p.Q2 the second slices).  The epilogue is sieve_epilogue16's for the 192 x 128
 // wave tile: element r of acc[i][c] of lane l is gallery row WR*192 + 16 i + 4 (l / 16) + r, query
 // WC*128 + 16 c + l % 16.
-template <int W>
+template <int W, int NSEG>
 __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
   using E = f6t::EngineW;
   f6t::f32x4 acc[E::NA][E::NB];
   constexpr int WR = W >> 1;
   E::Feed f;
-  E::feed_init<W>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ, p.nk,
-                  g0 / E::TGW);
-  E::mainloop<W>(f, p.nk, acc);
+  E::feed_init<W, NSEG>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ,
+                        p.nk / NSEG, g0 / E::TGW, reinterpret_cast<const char*>(p.G2),
+                        reinterpret_cast<const char*>(p.Q2));
+  E::mainloop<W, NSEG>(f, p.nk / NSEG, acc);
   float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
   uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
   uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [HCAPW]
@@ -429,6 +431,7 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
   sieve_flush<f6t::TQ, 9, E::TGW, HCAPW>(smem, p, g0, q0);
 }
 
+template <int NSEG>
 __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   using E = f6t::EngineW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -439,10 +442,10 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   if (p.serp && ((t / (p.gg * p.ntq)) & 1)) qt = p.ntq - 1 - qt;
   const int64_t g0 = gt * E::TGW, q0 = qt * f6t::TQ;
   switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
-    case 0: f6w_body<0>(smem, p, g0, q0); break;
-    case 1: f6w_body<1>(smem, p, g0, q0); break;
-    case 2: f6w_body<2>(smem, p, g0, q0); break;
-    default: f6w_body<3>(smem, p, g0, q0); break;
+    case 0: f6w_body<0, NSEG>(smem, p, g0, q0); break;
+    case 1: f6w_body<1, NSEG>(smem, p, g0, q0); break;
+    case 2: f6w_body<2, NSEG>(smem, p, g0, q0); break;
+    default: f6w_body<3, NSEG>(smem, p, g0, q0); break;
   }
 }
 
@@ -1318,7 +1321,7 @@ static int f6_shape();
 extern "C" const char* ofr_f6_sieve_kernel(void) {
   static const std::string names[2] = {
       "q8s::tile_kernel_f6s<1> (16x16x128 fp6 engine, 256x256 tiles, 8 waves)",
-      "q8s::tile_kernel_f6w (16x16x128 fp6 engine, 384x256 tiles, 1 wave per SIMD)"};
+      "q8s::tile_kernel_f6w<1> (16x16x128 fp6 engine, 384x256 tiles, 1 wave per SIMD)"};
   return names[f6_shape() == 16 ? 0 : 1].c_str();
 }
 
@@ -1535,9 +1538,10 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::LDS);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 tile)");
         }
-        hipError_t e = hipFuncSetAttribute((const void*)q8s::tile_kernel_f6w, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           f6t::EngineW::LDS_BYTES);
-        if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 wide tile)");
+        for (const void* f : {(const void*)q8s::tile_kernel_f6w<1>, (const void*)q8s::tile_kernel_f6w<3>}) {
+          hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::EngineW::LDS_BYTES);
+          if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 wide tile)");
+        }
         attr_done = true;
       }
       // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel, or of the row sample -> thresholds
@@ -1575,14 +1579,18 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       a.cap = q8s::SIEVE_CAP;
       if (!(phases & 8)) {
         // sample + thresholds only
-      } else if (f6_shape() == 384 && !two) {
+      } else if (f6_shape() == 384) {
         q8s::TileArgs wa = a;   // 384-row gallery tiles over the same 256-row panel layout
         wa.ntg = cdiv(N, f6t::EngineW::TGW);
         wa.gg = wa.ntg < f6w_group() ? wa.ntg : f6w_group();
         wa.serp = f6w_serp();
         OFR_CHECK_ARG(wa.ntq * wa.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
-        hipLaunchKernelGGL(q8s::tile_kernel_f6w, dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),
-                           f6t::EngineW::LDS_BYTES, st, wa);
+        if (two)
+          hipLaunchKernelGGL(q8s::tile_kernel_f6w<3>, dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),
+                             f6t::EngineW::LDS_BYTES, st, wa);
+        else
+          hipLaunchKernelGGL(q8s::tile_kernel_f6w<1>, dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),
+                             f6t::EngineW::LDS_BYTES, st, wa);
       } else if (two)
         hipLaunchKernelGGL((q8s::tile_kernel_f6s<3>), dim3((unsigned)(a.ntq * a.ntg)), dim3(f6t::Engine16::NT),
                            f6t::LDS, st, a);

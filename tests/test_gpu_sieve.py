@@ -248,3 +248,42 @@ def test_row_sample_extended_by_append():
     d_, i_ = g.search(Qd, 3)
     d2, i2 = h.search(h.query_rows(Q), 3)
     assert torch.equal(i_, i2) and torch.allclose(d_, d2, rtol=1e-9)
+
+
+def test_f6x2_wide_engine_matches_8wave_engine(monkeypatch):
+    """The two-slice tier's sieve pass on the wide engine (tile_kernel_f6w<3>, default) keeps exactly the
+    rows, with exactly the keys, of the 8-wave engine (tile_kernel_f6s<3>, OFR_F6_SHAPE=16): both sum
+    the same 16x16x128 MFMAs stage by stage in the same order.  Crowded data (the tier's use), d = 320
+    (3 stages per segment, a partial last stage), a partial last gallery tile and query panel."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    G, Q = _clustered(2003, 9, 320, 300, 31)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    Qd = g.query_rows(Q)
+    state, res = {}, {}
+    for eng in ("wide", "8wave"):
+        if eng == "8wave":
+            monkeypatch.setenv("OFR_F6_SHAPE", "16")
+        else:
+            monkeypatch.delenv("OFR_F6_SHAPE", raising=False)
+        qq = g.quantize_queries(Qd, tier="f6x2")
+        out = g.search_q8_phase(4 | 8 | 2, Qd, qq, 4)
+        torch.cuda.synchronize()
+        theta, count, keys, rows = g.sieve_state(len(Q))
+        count = count.cpu().numpy().copy()
+        assert np.all((count >= 4) & (count <= g.SIEVE_CAP)), count
+        pairs = []
+        for b in range(len(Q)):
+            r = rows[b, :count[b]].cpu().numpy()
+            kk = keys[b, :count[b]].cpu().numpy()
+            o = np.argsort(r)
+            pairs.append((r[o], kk[o]))
+        state[eng] = (theta.cpu().numpy().copy(), count, pairs)
+        res[eng] = (out[0].cpu().numpy(), out[1].cpu().numpy(), qq["cert"].cpu().numpy().copy())
+    assert np.array_equal(state["wide"][0], state["8wave"][0])
+    assert np.array_equal(state["wide"][1], state["8wave"][1])
+    for b in range(len(Q)):
+        assert np.array_equal(state["wide"][2][b][0], state["8wave"][2][b][0]), b
+        assert np.array_equal(state["wide"][2][b][1].view(np.uint32), state["8wave"][2][b][1].view(np.uint32)), b
+    for j in range(3):
+        assert np.array_equal(res["wide"][j], res["8wave"][j])
