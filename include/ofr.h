@@ -446,6 +446,12 @@ typedef struct ofr_knn_shard {
   const float* gscale8;
   const double* gmax8;
   int64_t* tier_counts;     /* optional out [4] (read on shard 0) */
+  /* optional row sample of the shard's rows for the fp6 sieve thresholds (ofr_f6_sample_rows;
+     null St: the panel sample of ofr_knn_f6) -- round 4, appended */
+  const void* St;
+  int64_t Ns;
+  const float* sscale;
+  const float* saux;
 } ofr_knn_shard;
 int ofr_comm_init_all(int ndev, const int* devices, ofr_comm** comm);
 int ofr_comm_destroy(ofr_comm* comm);

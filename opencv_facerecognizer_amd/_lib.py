@@ -136,7 +136,7 @@ class KnnShard(ctypes.Structure):
                 ("gmax", c_vp), ("index_base", c_i64), ("workspace", c_vp), ("workspace_bytes", c_sz),
                 ("out_d", c_vp), ("out_i", c_vp), ("cert", c_vp),
                 ("Gt2", c_vp), ("gscale2", c_vp), ("gmax2", c_vp), ("G8", c_vp), ("ld8", c_i64), ("gscale8", c_vp),
-                ("gmax8", c_vp), ("tier_counts", c_vp)]
+                ("gmax8", c_vp), ("tier_counts", c_vp), ("St", c_vp), ("Ns", c_i64), ("sscale", c_vp), ("saux", c_vp)]
 
 
 class OfrError(RuntimeError):

@@ -348,9 +348,12 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
     L[p] = comm::layout(B, s.N, s.ldq, k, P);
     OFR_CHECK_ARG(s.workspace && s.workspace_bytes >= L[p].total, "ofr_knn_sharded: workspace too small");
     char* ws = (char*)s.workspace;
-    int rc = ofr_knn_f6(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt, s.gscale, s.aux,
-                        s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, ws + L[p].knn,
-                        ofr_knn_f6_workspace_bytes(B, s.N));
+    int rc = s.St ? ofr_knn_f6_sampled(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
+                                       s.gscale, s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
+                                       s.St, s.Ns, s.sscale, s.saux, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N))
+                  : ofr_knn_f6(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt, s.gscale,
+                               s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, ws + L[p].knn,
+                               ofr_knn_f6_workspace_bytes(B, s.N));
     if (rc) return rc;
     rc = ofr_knn_f6_merge_pruned(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
                                  s.gscale, s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,

@@ -351,6 +351,9 @@ class DeviceComm:
                 s.index_base = int(getattr(g, "index_base", 0))
                 s.workspace, s.workspace_bytes = ws.data_ptr(), nbytes
                 s.out_d, s.out_i, s.cert = out_d.data_ptr(), out_i.data_ptr(), cert.data_ptr()
+                if g.row_sample():                        # the sieve thresholds from the shard's row sample
+                    s.St, s.Ns = t["St"].data_ptr(), -(-g.N // lib.ofr_f6_sample_step())
+                    s.sscale, s.saux = t["sscale"].data_ptr(), t["saux"].data_ptr()
                 if "f6x2" in tiers:
                     t2 = g._tier_gallery("f6x2")
                     s.Gt2, s.gscale2, s.gmax2 = t2["Gs2"].data_ptr(), t2["scale"].data_ptr(), t2["gmax"].data_ptr()
