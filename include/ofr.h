@@ -262,6 +262,18 @@ int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, i
                            double* maxima);
 int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int64_t row0,
                               void* tiles1, void* tiles2, size_t tiles_bytes, float* scale, double* stats);
+/* ofr_knn_f6x2 with the sieve thresholds from the row sample (as ofr_knn_f6_sampled): St / sscale /
+ * saux the fp6 tier's sample (ofr_f6_sample_rows), St2 the second slices of the same rows
+ * (ofr_f6x2_sample_rows: rows j * 64 for j in [j0, j1) into sample row j of tiles2, with their scales
+ * and f6x2 stats).                                                                               */
+int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1, void* tiles2,
+                         size_t tiles_bytes, float* scale, double* stats);
+int ofr_knn_f6x2_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                         const void* Qt2, const float* qscale, const double* qstats, const float* G, int64_t N,
+                         int64_t ldg, int64_t d, const void* Gt, const void* Gt2, const float* gscale,
+                         const float* aux, const double* gmax, int k, int64_t index_base, double* out_d,
+                         int64_t* out_i, int* cert, double* bound, const void* St, const void* St2, int64_t Ns,
+                         const float* sscale, const float* saux, void* workspace, size_t workspace_bytes);
 int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt, const void* Qt2,
                  const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                  const void* Gt, const void* Gt2, const float* gscale, const float* aux, const double* gmax, int k,
@@ -452,6 +464,7 @@ typedef struct ofr_knn_shard {
   int64_t Ns;
   const float* sscale;
   const float* saux;
+  const void* St2;          /* optional: the second slices of the sample (ofr_f6x2_sample_rows) for f6x2 */
 } ofr_knn_shard;
 int ofr_comm_init_all(int ndev, const int* devices, ofr_comm** comm);
 int ofr_comm_destroy(ofr_comm* comm);

@@ -251,6 +251,7 @@ class FloatGallery:
             elif tier == "f6x2":                       # the first slice is the f6 tier's, extended above
                 call("ofr_f6x2_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, None,
                      ptr(g["Gs2"]), g["Gs2"].numel(), ptr(g["scale"]), ptr(g["stats"]))
+                self._sample_rows2(g, N0, N1)
             else:
                 call("ofr_q8_quantize_rows", stream(), tier, ptr(self.G[N0:]), n, self.d, self.ld, ptr(g["Gs"][N0:]),
                      g["ld"], ptr(g["scale"][N0:]), ptr(g["stats"][N0:]), None, None)
@@ -410,7 +411,15 @@ class FloatGallery:
                 Gs2 = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
                 call("ofr_f6x2_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, None, ptr(Gs2),
                      nbytes, ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
-                ld, extra = 0, dict(Gs2=Gs2)
+                # second slices of the f6 tier's row sample (ofr_knn_f6x2_sampled)
+                s1 = self._tier_gallery("f6")
+                ns = int(s1["sscale"].numel())
+                extra = dict(Gs2=Gs2, St2=torch.empty(_lib.load().ofr_f6_tiles_bytes(ns, self.d), dtype=torch.uint8,
+                                                      device=dev_),
+                             sscale2=torch.empty(ns, dtype=torch.float32, device=dev_),
+                             sstats2=torch.empty((ns, 3), dtype=torch.float64, device=dev_))
+                self._sample_rows2(extra, 0, self.N)
+                ld = 0
             else:
                 ld = self._q8_ld(self.d, tier)
                 Gs = torch.empty((cap, ld), dtype=torch.int8, device=dev_)
@@ -425,6 +434,13 @@ class FloatGallery:
         j0, j1 = -(-N0 // step), -(-N1 // step)
         call("ofr_f6_sample_rows", stream(), ptr(self._Gbuf), self.ld, self.d, j0, j1, ptr(self._auxbuf), ptr(g["St"]),
              g["St"].numel(), ptr(g["sscale"]), ptr(g["sstats"]), ptr(g["saux"]))
+
+    def _sample_rows2(self, g, N0, N1):
+        """Extend the f6x2 tier's second-slice row sample over gallery rows [N0, N1) (ofr_f6x2_sample_rows)."""
+        step = _lib.load().ofr_f6_sample_step()
+        j0, j1 = -(-N0 // step), -(-N1 // step)
+        call("ofr_f6x2_sample_rows", stream(), ptr(self._Gbuf), self.ld, self.d, j0, j1, ptr(g["St2"]),
+             g["St2"].numel(), ptr(g["sscale2"]), ptr(g["sstats2"]))
 
     @staticmethod
     def row_sample():
@@ -493,7 +509,15 @@ class FloatGallery:
         nbytes = (lib.ofr_knn_f6_workspace_bytes(B, self.N) if tier in ("f6", "f6x2")
                   else lib.ofr_knn_q8_workspace_bytes(B, self.N))
         ws = (workspace or self.ws).get(nbytes, Qd.device)
-        if tier == "f6x2":
+        if tier == "f6x2" and self.row_sample():
+            s1 = self._tier_gallery("f6")
+            ns = -(-self.N // lib.ofr_f6_sample_step())
+            call("ofr_knn_f6x2_sampled", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["Qs2"]),
+                 ptr(qq["scale"]), ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]),
+                 ptr(g["Gs2"]), ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]),
+                 ptr(out[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(s1["St"]), ptr(g["St2"]), ns,
+                 ptr(s1["sscale"]), ptr(s1["saux"]), ptr(ws), ws.numel())
+        elif tier == "f6x2":
             call("ofr_knn_f6x2", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["Qs2"]),
                  ptr(qq["scale"]), ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]),
                  ptr(g["Gs2"]), ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]),

@@ -77,6 +77,10 @@ SIGNATURES = {
     "ofr_f6x2_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp]),
     "ofr_knn_f6x2": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz]),
+    "ofr_f6x2_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp]),
+    "ofr_knn_f6x2_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                     c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_i64, c_vp, c_vp, c_vp, c_sz]),
     "ofr_topk_merge": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp]),
     "ofr_elbp_codes": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                c_vp]),
@@ -136,7 +140,8 @@ class KnnShard(ctypes.Structure):
                 ("gmax", c_vp), ("index_base", c_i64), ("workspace", c_vp), ("workspace_bytes", c_sz),
                 ("out_d", c_vp), ("out_i", c_vp), ("cert", c_vp),
                 ("Gt2", c_vp), ("gscale2", c_vp), ("gmax2", c_vp), ("G8", c_vp), ("ld8", c_i64), ("gscale8", c_vp),
-                ("gmax8", c_vp), ("tier_counts", c_vp), ("St", c_vp), ("Ns", c_i64), ("sscale", c_vp), ("saux", c_vp)]
+                ("gmax8", c_vp), ("tier_counts", c_vp), ("St", c_vp), ("Ns", c_i64), ("sscale", c_vp), ("saux", c_vp),
+                ("St2", c_vp)]
 
 
 class OfrError(RuntimeError):

@@ -493,9 +493,14 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
         rc = ofr_f6x2_quantize_rows(s.stream, sq, n, d, s.ldq, ws + L[p].qt1, ws + L[p].qt2, L[p].tiles_bytes, qs, qst,
                                     nullptr, nullptr);
         if (rc) return rc;
-        rc = ofr_knn_f6x2(s.stream, 3, sq, n, s.ldq, ws + L[p].qt1, ws + L[p].qt2, qs, qst, s.G, s.N, s.ldg, d, s.Gt,
-                          s.Gt2, s.gscale2, s.aux, s.gmax2, k, s.index_base, ld_, li_, lc_, lb_, ws + L[p].knn,
-                          ofr_knn_f6_workspace_bytes(n, s.N));
+        rc = s.St && s.St2
+                 ? ofr_knn_f6x2_sampled(s.stream, 3, sq, n, s.ldq, ws + L[p].qt1, ws + L[p].qt2, qs, qst, s.G, s.N,
+                                        s.ldg, d, s.Gt, s.Gt2, s.gscale2, s.aux, s.gmax2, k, s.index_base, ld_, li_,
+                                        lc_, lb_, s.St, s.St2, s.Ns, s.sscale, s.saux, ws + L[p].knn,
+                                        ofr_knn_f6_workspace_bytes(n, s.N))
+                 : ofr_knn_f6x2(s.stream, 3, sq, n, s.ldq, ws + L[p].qt1, ws + L[p].qt2, qs, qst, s.G, s.N, s.ldg, d,
+                                s.Gt, s.Gt2, s.gscale2, s.aux, s.gmax2, k, s.index_base, ld_, li_, lc_, lb_,
+                                ws + L[p].knn, ofr_knn_f6_workspace_bytes(n, s.N));
       } else if (stage == Q8X2) {
         // the query slices share the gallery's row layout (ofr_knn_q8 takes one ld for both)
         rc = ofr_q8_quantize_rows(s.stream, 2, sq, n, d, s.ldq, (int8_t*)(ws + L[p].q8), s.ld8, qs, qst, nullptr,

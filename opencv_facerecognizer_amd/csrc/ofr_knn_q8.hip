@@ -1296,6 +1296,16 @@ extern "C" int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, i
 
 extern "C" int64_t ofr_f6_sample_step(void) { return q8s::SAMPLE_STEP; }
 
+extern "C" int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
+                                    void* tiles2, size_t tiles_bytes, float* scale, double* stats) {
+  OFR_CHECK_ARG(j0 >= 0 && j1 >= j0 && d >= 1 && ldx >= d, "ofr_f6x2_sample_rows: bad sizes");
+  if (j1 == j0) return OFR_OK;
+  OFR_CHECK_ARG(X, "ofr_f6x2_sample_rows: null pointer");
+  OFR_CHECK_ARG(ldx < INT64_MAX / q8s::SAMPLE_STEP, "ofr_f6x2_sample_rows: leading dimension too large");
+  return ofr_f6x2_quantize_rows_at(stream, X + j0 * q8s::SAMPLE_STEP * ldx, j1 - j0, d, ldx * q8s::SAMPLE_STEP, j0,
+                                   nullptr, tiles2, tiles_bytes, scale, stats);
+}
+
 extern "C" int ofr_f6_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
                                   const float* aux, void* tiles, size_t tiles_bytes, float* scale, double* stats,
                                   float* saux) {
@@ -1425,6 +1435,7 @@ struct F6Sample {
   int64_t n;
   const float* scale;
   const float* aux;
+  const void* tiles2;   // second-slice tiles of the same rows (ofr_knn_f6x2_sampled)
 };
 
 static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
@@ -1456,9 +1467,29 @@ extern "C" int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int6
   OFR_CHECK_ARG(St && sscale && saux, "ofr_knn_f6_sampled: null sample pointer");
   OFR_CHECK_ARG(Ns >= 1 && Ns <= sample_rows(N), "ofr_knn_f6_sampled: sample rows must be in [1, ceil(N / 64)]");
   OFR_CHECK_ARG((uintptr_t)St % 16 == 0, "ofr_knn_f6_sampled: sample tiles must be 16-byte aligned");
-  const F6Sample smp{St, Ns, sscale, saux};
+  const F6Sample smp{St, Ns, sscale, saux, nullptr};
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
                      out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, nullptr, nullptr, &smp);
+}
+
+extern "C" int ofr_knn_f6x2_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                                    const void* Qt2, const float* qscale, const double* qstats, const float* G,
+                                    int64_t N, int64_t ldg, int64_t d, const void* Gt, const void* Gt2,
+                                    const float* gscale, const float* aux, const double* gmax, int k,
+                                    int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
+                                    const void* St, const void* St2, int64_t Ns, const float* sscale,
+                                    const float* saux, void* workspace, size_t workspace_bytes) {
+  OFR_CHECK_ARG(phases >= 1 && phases <= 15,
+                "ofr_knn_f6x2_sampled: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
+  OFR_CHECK_ARG(Qt2 && Gt2, "ofr_knn_f6x2_sampled: null second-slice tiles");
+  if (B >= 1 && B <= 32)
+    return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6x2_sampled: needs more than 32 queries (the sieve pass)");
+  OFR_CHECK_ARG(St && St2 && sscale && saux, "ofr_knn_f6x2_sampled: null sample pointer");
+  OFR_CHECK_ARG(Ns >= 1 && Ns <= sample_rows(N), "ofr_knn_f6x2_sampled: sample rows must be in [1, ceil(N / 64)]");
+  OFR_CHECK_ARG(((uintptr_t)St | (uintptr_t)St2) % 16 == 0, "ofr_knn_f6x2_sampled: sample tiles must be 16-byte aligned");
+  const F6Sample smp{St, Ns, sscale, saux, St2};
+  return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, Qt2, Gt2, &smp);
 }
 
 extern "C" int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
@@ -1546,9 +1577,10 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       }
       // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel, or of the row sample -> thresholds
       q8s::TileArgs s = a;
-      const bool rows = smp && !two;
+      const bool rows = smp && (!two || smp->tiles2);
       if (rows) {
         s.G = (const int8_t*)smp->tiles;
+        if (two) s.G2 = (const int8_t*)smp->tiles2;
         s.N = smp->n;
         s.gscale = smp->scale;
         s.aux = smp->aux;

@@ -357,6 +357,8 @@ class DeviceComm:
                 if "f6x2" in tiers:
                     t2 = g._tier_gallery("f6x2")
                     s.Gt2, s.gscale2, s.gmax2 = t2["Gs2"].data_ptr(), t2["scale"].data_ptr(), t2["gmax"].data_ptr()
+                    if g.row_sample():
+                        s.St2 = t2["St2"].data_ptr()
                 if 2 in tiers:
                     t8 = g._tier_gallery(2)
                     s.G8, s.ld8 = t8["Gs"].data_ptr(), t8["ld"]

@@ -233,6 +233,7 @@ def test_row_sample_extended_by_append():
     cap0 = g.capacity()
     assert cap0 > N0 + 300
     g._tier_gallery("f6")                                # built before the next append, then extended in place
+    g._tier_gallery("f6x2")
     g.append(G[N0:cap0])                                 # fills the storage, no re-allocation
     assert g.capacity() == cap0 and g.N == cap0 and g.q8 is not None
     h = FloatGallery(G[:cap0], _lib.METRIC_EUCLIDEAN, shift64=g.shift64)
@@ -244,6 +245,9 @@ def test_row_sample_extended_by_append():
     assert torch.equal(a["sscale"][:ns], b["sscale"][:ns])
     assert torch.equal(a["saux"][:ns], b["saux"][:ns])
     assert torch.equal(a["saux"][:ns], g.aux[::step][:ns])
+    a2, b2 = g._tier_gallery("f6x2"), h._tier_gallery("f6x2")
+    assert torch.equal(a2["St2"][:nb], b2["St2"][:nb])
+    assert torch.equal(a2["sscale2"][:ns], a["sscale"][:ns])
     Qd = g.query_rows(Q)
     d_, i_ = g.search(Qd, 3)
     d2, i2 = h.search(h.query_rows(Q), 3)
@@ -287,3 +291,30 @@ def test_f6x2_wide_engine_matches_8wave_engine(monkeypatch):
         assert np.array_equal(state["wide"][2][b][1].view(np.uint32), state["8wave"][2][b][1].view(np.uint32)), b
     for j in range(3):
         assert np.array_equal(res["wide"][j], res["8wave"][j])
+
+
+def test_f6x2_row_sample_certified_results_exact(monkeypatch):
+    """The two-slice tier with the row sample (ofr_knn_f6x2_sampled, default) and with the panel sample
+    (OFR_SIEVE_SAMPLE=panels): every query either mode certifies has the exact fp64 top-k, and the row
+    sample keeps fewer rows.  Crowded clusters (the tier's use)."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    G, Q = _clustered(3000, 10, 256, 384, 91)
+    G = G + np.random.default_rng(3).normal(0, 9, G.shape)           # crowd the identities
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    Qd = g.query_rows(Q)
+    Gt, Qt = torch.from_numpy(g.G[:, :g.d].double().cpu().numpy()).cuda(), Qd[:, :g.d].double()
+    D2 = (Qt * Qt).sum(1)[:, None] + (Gt * Gt).sum(1)[None, :] - 2.0 * Qt @ Gt.t()
+    want = torch.topk(D2, 3, dim=1, largest=False).indices.cpu().numpy()
+    kept = {}
+    for mode in ("rows", "panels"):
+        monkeypatch.setenv("OFR_SIEVE_SAMPLE", mode)
+        qq = g.quantize_queries(Qd, tier="f6x2")
+        out = g.search_q8_phase(1 | 2, Qd, qq, 3)
+        torch.cuda.synchronize()
+        kept[mode] = g.sieve_counts(len(Q)).cpu().numpy().copy()
+        cert = qq["cert"].cpu().numpy().astype(bool)
+        assert cert.sum() > len(Q) // 2, (mode, cert.sum())
+        got = out[1].cpu().numpy()
+        assert np.array_equal(np.sort(got[cert], 1), np.sort(want[cert], 1)), mode
+    assert kept["rows"].mean() < 0.5 * kept["panels"].mean(), (kept["rows"].mean(), kept["panels"].mean())
