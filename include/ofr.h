@@ -374,6 +374,17 @@ int ofr_class_center_f64(void* stream, const double* F, int64_t N, int64_t D, in
                          const int64_t* perm, const int64_t* offsets, int64_t c,
                          const double* total_mean, double* means, double* Fc, double* Mc,
                          double* Mc_n);
+/* The same statistics in pieces, for a training set sharded over ranks (round 4; the caller
+ * all-reduces the sums and counts in between): ofr_class_sums_f64 sums[c][D] = per-class sums of
+ * this rank's rows; ofr_class_between_f64 means = sums / counts (0 for an empty class), Mc, Mc_n
+ * as above from the global sums, counts [c] (fp64) and total_mean; ofr_class_sub_f64 Fc = F -
+ * means[y] for this rank's rows.                                                             */
+int ofr_class_sums_f64(void* stream, const double* F, int64_t D, int64_t ldf, const int64_t* perm,
+                       const int64_t* offsets, int64_t c, double* sums);
+int ofr_class_between_f64(void* stream, const double* sums, const double* counts, int64_t c, int64_t D,
+                          const double* total_mean, double* means, double* Mc, double* Mc_n);
+int ofr_class_sub_f64(void* stream, const double* F, int64_t N, int64_t D, int64_t ldf, const int64_t* perm,
+                      const int64_t* offsets, int64_t c, const double* means, double* Fc);
 
 /* Exact training products of uint8 face data (Fisherfaces.compute) -------------
  * Replaces the float64 products of PCA.compute feature.py:91-94 (Gram XC XC^T of

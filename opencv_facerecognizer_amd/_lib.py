@@ -81,6 +81,9 @@ SIGNATURES = {
     "ofr_knn_f6x2_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                      c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      c_vp, c_i64, c_vp, c_vp, c_vp, c_sz]),
+    "ofr_class_sums_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "ofr_class_between_f64": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "ofr_class_sub_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "ofr_topk_merge": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp]),
     "ofr_elbp_codes": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                c_vp]),

@@ -238,9 +238,69 @@ __global__ void class_center_kernel(const double* F, int64_t r_base, int64_t D, 
     Fc[row * D + j] = F[row * ldf + j] - means[lo * D + j];
 }
 
+// per-class column sums of fp64 rows (sequential in perm order, as class_mean_kernel)
+__global__ void class_sum_kernel(const double* F, int64_t D, int64_t ldf, const int64_t* perm, const int64_t* offsets,
+                                 double* sums) {
+  const int64_t c = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= D) return;
+  double acc = 0;
+  for (int64_t r = offsets[c]; r < offsets[c + 1]; ++r) acc += F[perm[r] * ldf + j];
+  sums[c * D + j] = acc;
+}
+
+// means / Mc / Mc_n of class_mean_kernel from class sums and counts (a sharded set's all-reduced pieces)
+__global__ void class_between_kernel(const double* sums, const double* counts, int64_t D, const double* total_mean,
+                                     double* means, double* Mc, double* Mc_n) {
+  const int64_t c = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= D) return;
+  const double cnt = counts[c];
+  const double mu = cnt > 0 ? sums[c * D + j] / cnt : 0.0;
+  means[c * D + j] = mu;
+  const double dm = mu - total_mean[j];
+  Mc[c * D + j] = dm;
+  Mc_n[c * D + j] = cnt * dm;
+}
+
 }  // namespace ofr
 
 using namespace ofr;
+
+extern "C" int ofr_class_sums_f64(void* stream, const double* F, int64_t D, int64_t ldf, const int64_t* perm,
+                                  const int64_t* offsets, int64_t c, double* sums) {
+  OFR_CHECK_ARG(D >= 1 && ldf >= D && c >= 1 && c < 65536, "ofr_class_sums_f64: bad sizes");
+  OFR_CHECK_ARG(F && perm && offsets && sums, "ofr_class_sums_f64: null pointer");
+  hipLaunchKernelGGL(class_sum_kernel, dim3((unsigned)cdiv(D, 256), (unsigned)c), dim3(256), 0, (hipStream_t)stream, F,
+                     D, ldf, perm, offsets, sums);
+  OFR_LAUNCH_CHECK("class_sum_kernel");
+  return OFR_OK;
+}
+
+extern "C" int ofr_class_between_f64(void* stream, const double* sums, const double* counts, int64_t c, int64_t D,
+                                     const double* total_mean, double* means, double* Mc, double* Mc_n) {
+  OFR_CHECK_ARG(D >= 1 && c >= 1 && c < 65536, "ofr_class_between_f64: bad sizes");
+  OFR_CHECK_ARG(sums && counts && total_mean && means && Mc && Mc_n, "ofr_class_between_f64: null pointer");
+  hipLaunchKernelGGL(class_between_kernel, dim3((unsigned)cdiv(D, 256), (unsigned)c), dim3(256), 0,
+                     (hipStream_t)stream, sums, counts, D, total_mean, means, Mc, Mc_n);
+  OFR_LAUNCH_CHECK("class_between_kernel");
+  return OFR_OK;
+}
+
+extern "C" int ofr_class_sub_f64(void* stream, const double* F, int64_t N, int64_t D, int64_t ldf, const int64_t* perm,
+                                 const int64_t* offsets, int64_t c, const double* means, double* Fc) {
+  OFR_CHECK_ARG(N >= 0 && D >= 1 && ldf >= D && c >= 1 && c < 65536, "ofr_class_sub_f64: bad sizes");
+  if (N == 0) return OFR_OK;
+  OFR_CHECK_ARG(F && perm && offsets && means && Fc, "ofr_class_sub_f64: null pointer");
+  const unsigned gx = (unsigned)std::min<int64_t>(cdiv(D, 256), 64);
+  for (int64_t done = 0; done < N; done += 65535) {
+    const int64_t chunk = std::min<int64_t>(N - done, 65535);
+    hipLaunchKernelGGL(class_center_kernel, dim3(gx, (unsigned)chunk), dim3(256), 0, (hipStream_t)stream, F, done, D,
+                       ldf, perm, offsets, c, means, Fc);
+    OFR_LAUNCH_CHECK("class_center_kernel");
+  }
+  return OFR_OK;
+}
 
 extern "C" int ofr_gemm_f64(void* stream, int transA, int transB, int64_t M, int64_t N, int64_t K, double alpha,
                             const double* A, int64_t lda, const double* B, int64_t ldb, double beta, double* C,

@@ -458,15 +458,7 @@ class Fisherfaces(_DeviceProjMixin, AbstractFeature):
         elif n <= D:
             # n x n Gram of the centred faces: U_k = XC^T V_k / sigma_k, features V_k sigma_k
             self._regime = "gram"
-            lam, V = training.finite("eigh_desc", *training.eigh_desc(
-                training.finite("centred_gram", training.centred_gram(Xd, D, lay)), k))
-            sig = lam.clamp_min(0.0).sqrt()
-            Sw, Sb = training.finite("feature_scatter", *training.feature_scatter((V * sig).contiguous(), y))
-            evals, L = lda_eigen(Sw, Sb, m)
-            L32 = _device.f64_dev(np.asarray(L, dtype=np.float32).astype(np.float64))   # feature.py:176
-            inv = torch.where(sig > 0, 1.0 / sig, torch.zeros_like(sig))
-            M = _device.gemm_f64((V * inv).contiguous(), L32)                       # V_k Sigma^-1 L
-            Wd = training.xct_times(Xd, D, lay, M, training.mean_image(Xd, D, lay))
+            evals, Wd = training.fisher_gram(Xd, D, lay, y, k, m)
         else:
             # D x D covariance: P = leading k eigenvectors, features XC P, W = P L
             self._regime = "cov"

@@ -237,49 +237,140 @@ def allreduce_exact(tensors, group=None):
     return tensors
 
 
+def allreduce_sum(tensors, group=None):
+    """Sum fp64 tensors over the ranks in place (not integer-valued: the result depends on the
+    reduction order at the last bit, but every rank receives the same values)."""
+    _, ws = world(group)
+    if ws > 1:
+        for t in tensors:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return tensors
+
+
+def gather_ragged_rows(x, group=None):
+    """All-gather row blocks of different lengths (dim 0), rank-major: pads every block to the longest
+    one for the collective and trims it again."""
+    _, ws = world(group)
+    if ws == 1:
+        return x
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    ns = gather_rows(n, group).cpu().numpy()
+    mx = int(ns.max())
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    pad[:x.shape[0]].copy_(x)
+    allr = gather_rows(pad, group)
+    return torch.cat([allr[r * mx:r * mx + int(ns[r])] for r in range(ws)], 0)
+
+
 def train_fisherfaces_sharded(feature, X_local, y_local, num_classes, group=None):
     """Fisherfaces.compute (feature.py:211-235) with the training faces sharded over the ranks.
 
-    Each rank holds its own faces (uint8) and their labels (global 0..c-1).  In the pixel regime
-    (PCA keeps every dimension: n - c >= D and n >= D, e.g. BASELINE configs[4]) the statistics are
-    sums over faces: rank r forms its exact pieces (X'^T X', class sums, column sums; int8 MFMA) and
-    ONE all-reduce (RCCL over xGMI; gloo in tests) combines them exactly; every rank then has the
-    same Sw, Sb.  Rank 0 solves the eigenproblem (host LAPACK, as the reference) and broadcasts W,
-    and each rank projects its own faces: the features come back as this rank's gallery shard.
-    Returns this rank's features (list of (d,1) matrices, the reference's return type)."""
+    Each rank holds its own faces (uint8) and their labels (global 0..c-1); the regime is chosen from
+    the global n, c, D exactly as Fisherfaces.compute chooses it:
+    * pixel (PCA keeps every dimension: n - c >= D and n >= D, e.g. BASELINE configs[4]): the
+      statistics are sums over faces -- rank r forms its exact pieces (X'^T X', class sums, column
+      sums; int8 MFMA) and ONE all-reduce (RCCL over xGMI; gloo in tests) combines them exactly;
+      rank 0 solves the pencil.  W equals the single-process model's bit for bit.
+    * cov (n > D, PCA(n - c) < D): X'^T X' and the column sums all-reduce exactly into the
+      covariance (the same bits on every rank), rank 0 takes its leading eigenvectors P and
+      broadcasts them, each rank projects its own faces, and the LDA scatter of the features is
+      all-reduced (training.feature_scatter_sharded: global class means, then per-rank centred
+      products); rank 0 solves LDA, W = P L.  Equal to the single-process model up to the order of
+      the fp64 feature sums.
+    * gram (n <= D: at most D faces of D pixels, <= D^2 bytes): the faces and labels are all-gathered
+      and rank 0 runs the single-process n x n Gram pipeline (training.fisher_gram); the same W.
+    W and the eigenvalues are broadcast, and each rank projects its own faces: the features come back
+    as this rank's gallery shard.  Returns this rank's features (list of (d,1) matrices, the
+    reference's return type)."""
     from . import _device, training
     from .facerec.feature import lda_eigen
     rank, ws = world(group)
     Xd, D, kind = _device_rows_u8(X_local)
     lay = training.Layout(y_local, Xd.device, c=num_classes)
     counts = torch.from_numpy(lay.counts.astype(np.float64)).to(Xd.device)
-    pieces = training.pixel_pieces(Xd, D, lay)
-    allreduce_exact([pieces["G"], pieces["S"], pieces["s"], counts], group)
+    allreduce_exact([counts], group)
     cnt = counts.cpu().numpy()
     n, c = int(cnt.sum()), int(num_classes)
-    if n - c < D or n < D:
-        raise NotImplementedError("sharded training needs the pixel regime (n - c >= D and n >= D)")
+    k = n - c                                              # PCA(n - c), as Fisherfaces.compute
+    if k <= 0 or k > n - 1:
+        k = n - 1
+    k = min(k, D, n)
     m = feature._num_components
     if m <= 0 or m > c - 1:
         m = c - 1
-    Sw, Sb = training.pixel_scatter(pieces, cnt, n)
-    del pieces
     W = torch.empty((D, m), dtype=torch.float64, device=Xd.device)
     ev = torch.empty(m, dtype=torch.float64, device=Xd.device)
-    if rank == 0:
+
+    def solve(Sw, Sb, P=None):            # rank 0: LDA (host, as the reference), W = P L (cov)
         evals, V = lda_eigen(Sw, Sb, m)
-        W.copy_(torch.from_numpy(np.ascontiguousarray(V, dtype=np.float64)))
+        if P is None:
+            W.copy_(torch.from_numpy(np.ascontiguousarray(V, dtype=np.float64)))
+        else:
+            L32 = np.asarray(V, dtype=np.float32).astype(np.float64)       # feature.py:176
+            W.copy_(_device.gemm_f64(P, _device.f64_dev(L32, device=P.device)))
         ev.copy_(torch.from_numpy(np.asarray(evals, dtype=np.float64)))
-    del Sw, Sb
+
+    if k >= D:
+        regime = "pixel"
+        pieces = training.pixel_pieces(Xd, D, lay)
+        allreduce_exact([pieces["G"], pieces["S"], pieces["s"]], group)
+        Sw, Sb = training.finite("pixel_scatter", *training.pixel_scatter(pieces, cnt, n))
+        del pieces
+        if rank == 0:
+            solve(Sw, Sb)
+        del Sw, Sb
+    elif n <= D:
+        regime = "gram"
+        Xall = gather_ragged_rows(Xd, group)
+        yall = gather_ragged_rows(torch.from_numpy(np.asarray(y_local, np.int64).reshape(-1)).to(Xd.device),
+                                  group).cpu().numpy()
+        if rank == 0:
+            evals, Wd = training.fisher_gram(Xall, D, training.Layout(yall, Xd.device, c=c), yall, k, m)
+            W.copy_(Wd)
+            ev.copy_(torch.from_numpy(np.asarray(evals, dtype=np.float64)))
+        del Xall
+    else:
+        regime = "cov"
+        pieces = training.pixel_pieces(Xd, D, lay)
+        del pieces["S"]
+        colsum = training.column_sums(Xd, D, lay, shift=0)[0].reshape(1, D).contiguous()   # exact sums of x
+        allreduce_exact([pieces["G"], pieces["s"], colsum], group)
+        mu = torch.empty_like(colsum)
+        nd = torch.tensor([float(n)], dtype=torch.float64, device=Xd.device)
+        _lib_call("ofr_row_div_f64", colsum, 1, D, D, nd, mu, D)                # mean image, rounded once
+        C = training.finite("covariance", training.covariance(pieces, n))
+        del pieces
+        P = torch.empty((D, k), dtype=torch.float64, device=Xd.device)
+        if rank == 0:
+            _, Pd = training.finite("eigh_desc", *training.eigh_desc(C, k))
+            P.copy_(Pd)
+            del Pd
+        del C
+        if ws > 1:
+            dist.broadcast(P, 0, group=group)
+        shift = _device.gemm_f64(mu, P).reshape(-1)
+        Fd = _device.Projection(Wt_device=P.t().contiguous(), D=D).project(Xd, shift64=shift, f64=True)
+        Sw, Sb = training.finite("feature_scatter", *training.feature_scatter_sharded(
+            Fd, lay, counts, n, lambda ts: allreduce_sum(ts, group)))
+        del Fd
+        if rank == 0:
+            solve(Sw, Sb, P)
+        del Sw, Sb, P
     if ws > 1:
         dist.broadcast(W, 0, group=group)
         dist.broadcast(ev, 0, group=group)
+    feature._regime = regime
     feature._eigenvalues = ev.cpu().numpy().astype(np.float32)
     feature._num_components = m
     feature._eigenvectors = np.asmatrix(W.cpu().numpy())
     feature.__dict__.pop("_dev_proj", None)
     Fd = feature.project_device(Xd, f64=True)
     return [np.asmatrix(r.reshape(-1, 1)) for r in Fd.cpu().numpy()]
+
+
+def _lib_call(name, *args):
+    from . import _lib
+    _lib.call(name, _lib.stream(), *[_lib.ptr(a) if isinstance(a, torch.Tensor) else a for a in args])
 
 
 def _device_rows_u8(X):

@@ -180,6 +180,47 @@ def feature_scatter(Fd, y):
     return _device.gemm_f64(Fc, Fc, transA=True), _device.gemm_f64(Mc, Mc_n, transA=True)
 
 
+def feature_scatter_sharded(Fd, lay, counts, n, allreduce):
+    """Sw, Sb [k][k] (feature.py:160-168) of fp64 features [n_r][k] sharded over ranks: the class sums of
+    every rank's rows are all-reduced into the global class means (``allreduce``: sums a list of
+    device tensors in place over the ranks), each rank centres its own rows on them and the
+    Fc^T Fc products are all-reduced into Sw; Sb = Mc^T (n_i Mc) from the global means, the same on
+    every rank.  counts: the global class sizes (device fp64 [c]), n their sum.  Equal to
+    feature_scatter of all the rows up to the order of the fp64 sums."""
+    k, c, dev_ = Fd.shape[1], lay.c, Fd.device
+    sums = torch.empty((c, k), dtype=torch.float64, device=dev_)
+    call("ofr_class_sums_f64", stream(), ptr(Fd), k, Fd.shape[1], ptr(lay.perm), ptr(lay.offsets), c, ptr(sums))
+    allreduce([sums])
+    tot = _col_sums_f64(sums).reshape(1, k).contiguous()
+    nd = torch.tensor([float(n)], dtype=torch.float64, device=dev_)
+    total = torch.empty_like(tot)
+    call("ofr_row_div_f64", stream(), ptr(tot), 1, k, k, ptr(nd), ptr(total), k)
+    means, Mc, Mc_n = (torch.empty((c, k), dtype=torch.float64, device=dev_) for _ in range(3))
+    call("ofr_class_between_f64", stream(), ptr(sums), ptr(counts), c, k, ptr(total), ptr(means), ptr(Mc), ptr(Mc_n))
+    Fc = torch.empty((Fd.shape[0], k), dtype=torch.float64, device=dev_)
+    call("ofr_class_sub_f64", stream(), ptr(Fd), Fd.shape[0], k, Fd.shape[1], ptr(lay.perm), ptr(lay.offsets), c,
+         ptr(means), ptr(Fc))
+    Sw = _device.gemm_f64(Fc, Fc, transA=True)
+    del Fc
+    allreduce([Sw])
+    return Sw, _device.gemm_f64(Mc, Mc_n, transA=True)
+
+
+def fisher_gram(Xd, D, lay, y, k, m):
+    """The gram regime of Fisherfaces.compute (n <= D): PCA(k) through the n x n Gram of the centred
+    faces, LDA(m) on its features V_k Sigma_k, W = XC^T (V_k Sigma_k^-1 L) -> (LDA eigenvalues, W
+    [D][m] device fp64)."""
+    from .facerec.feature import lda_eigen
+    lam, V = finite("eigh_desc", *eigh_desc(finite("centred_gram", centred_gram(Xd, D, lay)), k))
+    sig = lam.clamp_min(0.0).sqrt()
+    Sw, Sb = finite("feature_scatter", *feature_scatter((V * sig).contiguous(), y))
+    evals, L = lda_eigen(Sw, Sb, m)
+    L32 = _device.f64_dev(np.asarray(L, dtype=np.float32).astype(np.float64))   # feature.py:176
+    inv = torch.where(sig > 0, 1.0 / sig, torch.zeros_like(sig))
+    M = _device.gemm_f64((V * inv).contiguous(), L32)                       # V_k Sigma^-1 L
+    return evals, xct_times(Xd, D, lay, M, mean_image(Xd, D, lay))
+
+
 def xct_times(Xd, D, lay, M, mean):
     """XC^T M [D][m] for uint8 images X [n][D] and an fp64 device matrix M [n][m]:
     sum_n x_n[p] M[n][j] exactly on the int8-slice projection engine (X^T as the face rows, M as

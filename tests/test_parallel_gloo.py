@@ -109,6 +109,42 @@ def test_gather_rows_rank_major():
     assert np.array_equal(g, np.concatenate([base, base + 1000]))
 
 
+def _ragged_worker(rank, ws, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from opencv_facerecognizer_amd.parallel import allreduce_sum, gather_ragged_rows
+        x = (torch.arange((3 + 2 * rank) * 4, dtype=torch.int64).reshape(-1, 4) + 100 * rank).to(torch.uint8)
+        g = gather_ragged_rows(x)                  # the gram regime's face gather: 3 + 5 rows
+        v = torch.full((2, 3), 0.5 + rank, dtype=torch.float64)
+        allreduce_sum([v])
+        out.put((rank, g.numpy(), v.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_ragged_rows_and_allreduce_sum():
+    """Sharded training's collectives (parallel.gather_ragged_rows: row blocks of different lengths,
+    rank-major; parallel.allreduce_sum: fp64 sums, the same values on every rank)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ragged_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, g, v = q.get(timeout=120)
+        res[r] = (g, v)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = np.concatenate([np.arange(12).reshape(3, 4), np.arange(20).reshape(5, 4) + 100]).astype(np.uint8)
+    for r in (0, 1):
+        assert np.array_equal(res[r][0], want)
+        assert np.array_equal(res[r][1], np.full((2, 3), 2.0))
+
+
 class _MockShardGallery:
     """CPU stand-in for FloatGallery on one shard: every tier returns the exact local top-k (global
     indices) and, as its certificate bound, the squared distance of the 16th local candidate shrunk
