@@ -620,9 +620,6 @@ struct EngineW {
       const Bases ac = abase(g0), an = abase(g1), bn = bbase(q1);
       const uint32_t k2 = kso(s + 2), k3 = kso(s + 3);
       const __amdgpu_buffer_rsrc_t rg2s = rgs(s + 2), rq2s = rqs(s + 2), rg3s = rgs(s + 3);
-      // the last stages copy nothing ahead (the clamped copies of stage `last` again would only cost
-      // issue slots); the barrier-B wait then drains every copy (none of s + 2 is in flight)
-      const bool c2 = s + 2 <= last, c3 = s + 3 <= last;
       int sa = SCALE_ONE, sb = SCALE_ONE;
       if constexpr (NSEG == 3) {
         seg_scales<NSEG>(s, nst, sa, sb);
@@ -642,24 +639,15 @@ struct EngineW {
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (i == 10) {             // barrier B: G(s+1), Q(s+1) landed; G(s) consumed
-          if (c2)
-            wait_vm<GPW + QPW>();
-          else
-            wait_vm<0>();
+          wait_vm<GPW + QPW>();
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
         }
         // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0), G(s+3) into G(s)'s (g0)
-        if constexpr (i <= 6) {
-          if (c2) gcopy<W, (i <= 6 ? i + 2 : 0)>(rg2s, f, g2, k2);
-        }
-        if constexpr (i >= 1 && i <= 6) {
-          if (c2) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(rq2s, q0, k2);
-        }
-        if constexpr (i == 10) {
-          if (c3) gcopy<W, 0>(rg3s, f, g0, k3);   // piece 1: in the middle of rows 10 / 11
-        }
+        if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(rg2s, f, g2, k2);
+        if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(rq2s, q0, k2);
+        if constexpr (i == 10) gcopy<W, 0>(rg3s, f, g0, k3);   // piece 1: in the middle of rows 10 / 11
         if constexpr (i == NA - 1) {
           // rows 10 and 11 run together (below, i == 10)
         } else if constexpr (i == NA - 2) {
@@ -672,7 +660,7 @@ struct EngineW {
           mm(a[1], b[1], acc[10][1]); mm(a[2], b[1], acc[11][1]); b[1] = fragB<WC * 128 + 16>(bn);
           mm(a[1], b[2], acc[10][2]); mm(a[2], b[2], acc[11][2]); b[2] = fragB<WC * 128 + 32>(bn);
           mm(a[1], b[3], acc[10][3]); mm(a[2], b[3], acc[11][3]); b[3] = fragB<WC * 128 + 48>(bn);
-          if (c3) gcopy<W, 1>(rg3s, f, g0, k3);
+          gcopy<W, 1>(rg3s, f, g0, k3);
           mm(a[1], b[4], acc[10][4]); mm(a[2], b[4], acc[11][4]); b[4] = fragB<WC * 128 + 64>(bn);
           mm(a[1], b[5], acc[10][5]); mm(a[2], b[5], acc[11][5]); b[5] = fragB<WC * 128 + 80>(bn);
           mm(a[1], b[6], acc[10][6]); mm(a[2], b[6], acc[11][6]); b[6] = fragB<WC * 128 + 96>(bn);
