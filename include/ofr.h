@@ -187,8 +187,10 @@ int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, 
  * B <= 32).  Env OFR_SIEVE_STRIDE (default 64) sets the sample stride.
  * Phase 1 in two calls (a pipelined caller overlaps other work with the second
  * only): phases 4 = the sample pass + thresholds (B <= 32: the whole stream
- * pass), 8 = the sieve pass (after a phases-4 call on the same workspace);
- * 1 = 4 + 8.  Phase bits combine (e.g. 10 = sieve, then merge).             */
+ * pass), 8 = the sieve pass (after a phases-4 call on the same workspace;
+ * a second sieve pass on the same thresholds would append every kept row
+ * twice, so it marks every query's bucket overflowed instead: cert 0, bound
+ * -inf); 1 = 4 + 8.  Phase bits combine (e.g. 10 = sieve, then merge).       */
 size_t ofr_f6_tiles_bytes(int64_t R, int64_t d);
 /* Append support (NearestNeighbor.update, classifier.py:65-70): quantize X's R rows
  * into rows row0 .. row0+R-1 of an existing tiled buffer (scale/stats indexed by

@@ -649,7 +649,8 @@ __global__ void __launch_bounds__(256) premerge_kernel(const Cand* cand, int64_t
 // then six shuffle rounds merge the lanes' lists (the same value as sorting the whole list by
 // (score, index): only the 16th score is used, and score_key is monotone).
 __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists, int64_t T, uint32_t* theta,
-                                                              int* count, int64_t B, int rank) {
+                                                              int* count, int64_t B, int rank, uint32_t* armed) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *armed = 1u;   // the buckets are reset: one sieve pass may follow
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (q >= B) return;
@@ -682,6 +683,19 @@ __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists,
     theta[q] = t;
     count[q] = 0;
   }
+}
+
+// Before a sieve pass: it appends to the buckets, so it is valid once per sample pass (which resets them
+// and arms the flag).  A second sieve pass on the same thresholds (phases 8 called twice) would append
+// every kept row again, and duplicated candidates could certify a top-k that repeats one row: it is
+// made to overflow every bucket instead (uncertified, bound -inf).  One workgroup; disarms.
+__global__ void __launch_bounds__(256) sieve_arm_kernel(uint32_t* armed, int* count, int64_t B, int cap) {
+  __shared__ uint32_t a;
+  if (threadIdx.x == 0) a = __atomic_load_n(armed, __ATOMIC_RELAXED);
+  __syncthreads();
+  if (threadIdx.x == 0) *armed = 0u;
+  if (a != 1u)
+    for (int64_t q = threadIdx.x; q < B; q += blockDim.x) count[q] = cap + 1;
 }
 
 // One block per query.  (1) best KC of the tile lists (query-major: cand[q][t][KC], one
@@ -1369,7 +1383,7 @@ static int f6w_serp() {
 // f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
 // thresholds, counts and buckets (each 256-byte aligned)
 struct SieveWs {
-  size_t lists, theta, count, bucket, bytes;
+  size_t lists, theta, count, bucket, armed, bytes;
 };
 static int64_t sieve_stride() {
   static const int64_t s = [] {
@@ -1405,7 +1419,8 @@ static SieveWs sieve_ws(int64_t B, int64_t N) {
   w.theta = round_up((int64_t)(B * ts * q8s::KC * sizeof(Cand)), 256);
   w.count = w.theta + round_up(B * 4, 256);
   w.bucket = w.count + round_up(B * 4, 256);
-  w.bytes = w.bucket + (size_t)B * q8s::SIEVE_CAP * sizeof(Cand);
+  w.armed = w.bucket + (size_t)B * q8s::SIEVE_CAP * sizeof(Cand);   // sieve_arm_kernel's flag
+  w.bytes = w.armed + 256;
   return w;
 }
 
@@ -1553,6 +1568,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   uint32_t* theta = reinterpret_cast<uint32_t*>(wsb + w.theta);
   int* count = reinterpret_cast<int*>(wsb + w.count);
   Cand* bucket = reinterpret_cast<Cand*>(wsb + w.bucket);
+  uint32_t* armed = reinterpret_cast<uint32_t*>(wsb + w.armed);
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
   if (phases & 1) phases |= 12;   // phase 1 = sample + thresholds (4), then the sieve (8)
   if (phases & 12) {
@@ -1602,13 +1618,17 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       if (phases & 4) {
         OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
         hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, s.cand, s.ntg,
-                           theta, count, B, std::max(k, sieve_rank(rows)));
+                           theta, count, B, std::max(k, sieve_rank(rows)), armed);
         OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
       }
       a.theta = theta;
       a.count = count;
       a.bucket = bucket;
       a.cap = q8s::SIEVE_CAP;
+      if (phases & 8) {
+        hipLaunchKernelGGL(q8s::sieve_arm_kernel, dim3(1), dim3(256), 0, st, armed, count, B, (int)q8s::SIEVE_CAP);
+        OFR_LAUNCH_CHECK("f6 sieve_arm_kernel");
+      }
       if (!(phases & 8)) {
         // sample + thresholds only
       } else if (f6_shape() == 384) {

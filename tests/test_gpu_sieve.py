@@ -318,3 +318,29 @@ def test_f6x2_row_sample_certified_results_exact(monkeypatch):
         got = out[1].cpu().numpy()
         assert np.array_equal(np.sort(got[cert], 1), np.sort(want[cert], 1)), mode
     assert kept["rows"].mean() < 0.5 * kept["panels"].mean(), (kept["rows"].mean(), kept["panels"].mean())
+
+
+def test_second_sieve_pass_uncertifies_not_duplicates():
+    """ofr_knn_f6 phases 8 twice on one sample pass (API misuse: the sieve appends to the buckets the
+    sample pass reset): duplicated candidates could certify a top-k that repeats a row, so the second
+    pass marks every bucket overflowed -- no query certified, bound -inf -- and the tier chain still
+    returns the exact top-k (classifier.py:104-119)."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    G, Q = _clustered(800, 10, 96, 64, 17)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    Qd = g.query_rows(Q)
+    qq = g.quantize_queries(Qd, tier="f6")
+    out = g.search_q8_phase(4 | 8 | 2, Qd, qq, 3)
+    torch.cuda.synchronize()
+    first = (out[0].cpu().numpy().copy(), out[1].cpu().numpy().copy())
+    assert int(qq["cert"].sum()) > len(Q) // 2
+    g.search_q8_phase(8, Qd, qq, 3)                     # again, without a sample pass
+    out = g.search_q8_phase(2, Qd, qq, 3, out=out)
+    torch.cuda.synchronize()
+    assert int(qq["cert"].sum()) == 0
+    assert torch.all(torch.isneginf(qq["bound"]))
+    g.search_q8_phase(4 | 8 | 2, Qd, qq, 3, out=out)    # a fresh sample pass re-arms the sieve
+    torch.cuda.synchronize()
+    assert np.array_equal(out[1].cpu().numpy(), first[1]) and np.array_equal(out[0].cpu().numpy(), first[0])
+    assert int(qq["cert"].sum()) > len(Q) // 2
