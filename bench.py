@@ -582,6 +582,7 @@ def main():
 
     if rank == 0:
         value = B * args.steps / elapsed
+        coll = "RCCL" if world > 1 and dist.get_backend() == "nccl" else "gloo"   # the collectives' backend
         tr = committed_traffic({"gallery": nl, "batch": B, "d": d, "D": D, "k": k, "search": args.search})
         result = {
             "metric": "query faces/sec (Fisherfaces proj + 1-NN, 1M gallery) at 1/2/4/8 GPUs",
@@ -594,9 +595,9 @@ def main():
             "config": {"workload": "configs[2]: Fisherfaces projection + 1-NN, 1M-image gallery (100k ids x 10), "
                                    "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1",
                        "gallery": N, "global_batch": B, "d": d, "D": D, "k": k,
-                       "parallelism": (f"gallery-rows/{world}, query prep sharded + RCCL all-gather of rows, RCCL all-gather of "
-                                       f"top-k + bounds (global certificate)" if shard_prep else
-                                       f"gallery-rows/{world} + RCCL all-gather of top-k")
+                       "parallelism": (f"gallery-rows/{world}, query prep sharded + {coll} all-gather of rows, {coll} all-gather "
+                                       f"of top-k + bounds (global certificate)" if shard_prep else
+                                       f"gallery-rows/{world} + {coll} all-gather of top-k")
                        if world > 1 else "1 GPU"},
             "roofline": {"kernel": kname, "bound": "mfma",
                          "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s" if not use_q8 else "TOPS",
