@@ -644,9 +644,8 @@ struct EngineW {
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
         }
-        // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0), G(s+3) into G(s)'s (g0)
-        if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(rg2s, f, g2, k2);
-        if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(rq2s, q0, k2);
+        // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0) -- rows 0-6, each copy
+        // issued right behind an MFMA so that its issue overlaps the MFMA's execution -- G(s+3) into G(s)'s (g0)
         if constexpr (i == 10) gcopy<W, 0>(rg3s, f, g0, k3);   // piece 1: in the middle of rows 10 / 11
         if constexpr (i == NA - 1) {
           // rows 10 and 11 run together (below, i == 10)
@@ -669,8 +668,11 @@ struct EngineW {
         } else {
           mm(a[i % RING], b[0], acc[i][0]);
           a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? i + 2 : 0) * 16>(ac);
+          if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(rg2s, f, g2, k2);
+          mm(a[i % RING], b[1], acc[i][1]);
+          if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(rq2s, q0, k2);
 #pragma unroll
-          for (int c = 1; c < NB; ++c) mm(a[i % RING], b[c], acc[i][c]);
+          for (int c = 2; c < NB; ++c) mm(a[i % RING], b[c], acc[i][c]);
         }
         __builtin_amdgcn_sched_barrier(0);
       };
