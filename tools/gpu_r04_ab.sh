@@ -5,7 +5,7 @@ set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/ab_$1
 mkdir -p $O
-timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $R/tests/test_gpu_sieve.py > $O/tests.txt 2>&1
+timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $R/tests/test_gpu_sieve.py $R/tests/test_gpu_parity.py $R/tests/test_gpu_configs.py -k "sieve or projection or project or duplicate or row_sample or f6x2" > $O/tests.txt 2>&1
 for rep in 1 2; do
   for v in new base; do
     if [ $v = base ]; then export OFR_LIB=$R/tools/var/libocvf_base.so; else unset OFR_LIB; fi
