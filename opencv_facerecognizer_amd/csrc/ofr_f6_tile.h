@@ -669,10 +669,12 @@ struct EngineW {
           mm(a[i % RING], b[0], acc[i][0]);
           a[(i + 2) % RING] = fragA<WR * 192 + (i + 2 < NA ? i + 2 : 0) * 16>(ac);
           if constexpr (i <= 6) gcopy<W, (i <= 6 ? i + 2 : 0)>(rg2s, f, g2, k2);
-          mm(a[i % RING], b[1], acc[i][1]);
-          if constexpr (i >= 1 && i <= 6) qcopy<W, (i >= 1 && i <= 6 ? i - 1 : 0)>(rq2s, q0, k2);
 #pragma unroll
-          for (int c = 2; c < NB; ++c) mm(a[i % RING], b[c], acc[i][c]);
+          for (int c = 1; c < 5; ++c) mm(a[i % RING], b[c], acc[i][c]);
+          // Q(s+2) in rows 4-9, four MFMAs behind the row's G(s+2) piece
+          if constexpr (i >= 4 && i <= 9) qcopy<W, (i >= 4 && i <= 9 ? i - 4 : 0)>(rq2s, q0, k2);
+#pragma unroll
+          for (int c = 5; c < NB; ++c) mm(a[i % RING], b[c], acc[i][c]);
         }
         __builtin_amdgcn_sched_barrier(0);
       };
