@@ -68,13 +68,15 @@ def main():
     import tempfile
     tmp = os.path.join(tempfile.mkdtemp(prefix="bench_proj_"), "y")   # outputs are large: not under gpurun_out
     for eng in a.engines.split(","):
-        env = dict(os.environ, OFR_PROJ_ENGINE=eng)
-        out = f"{tmp}_{eng}"
+        # "lib=<path>": the default engine of another build of the library (same-box A/B)
+        env = dict(os.environ, OFR_LIB=eng[4:]) if eng.startswith("lib=") else dict(os.environ, OFR_PROJ_ENGINE=eng)
+        key = f"{len(res['engines'])}:{eng}"
+        out = f"{tmp}_{len(res['engines'])}"
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--out", out, "--batch", str(a.batch), "--D",
                str(a.D), "--d", str(a.d), "--reps", str(a.reps), "--check-rows", str(a.check_rows)]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
-            res["engines"][eng] = {"error": r.stderr[-2000:]}
+            res["engines"][key] = {"error": r.stderr[-2000:]}
             print(json.dumps(res), flush=True)
             sys.exit(r.returncode)
         rec = json.loads(r.stdout.strip().splitlines()[-1])
@@ -95,7 +97,7 @@ def main():
                                    "image0_features": [int(x) for x in bad[bad[:, 0] == 0][:64, 1]],
                                    "image0_diffs": [float(y64[0, x] - ref[2][0, x]) for x in bad[bad[:, 0] == 0][:12, 1]],
                                    "per_image": [int((bad[:, 0] == i).sum()) for i in range(16)]}
-        res["engines"][eng] = rec
+        res["engines"][key] = rec
         print(eng, rec, file=sys.stderr, flush=True)
     ok = all(v.get("identical_to_" + ref[0], True) for v in res["engines"].values())
     res["all_identical"] = ok
