@@ -162,18 +162,17 @@ __device__ __forceinline__ void mainloop(const Feed& f, int nk, i32x4 (&acc)[NA]
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       }
-      // each copy issued right behind an MFMA, so that its issue overlaps the MFMA's execution
+      if constexpr (i % 4 == 0 && i <= 12) acopy<W, (i % 4 == 0 && i <= 12 ? 2 + i / 4 : 0)>(f, va, g2, k2);
+      if constexpr (i % 4 == 2 && i <= 14) bcopy<W, (i % 4 == 2 && i <= 14 ? i / 4 : 0)>(f, vb, q0, k2);
+      if constexpr (i == NA - 2) acopy<W, 0>(f, va, g0, k3);
       if constexpr (i == NA - 1) {
         // rows 22 and 23 run together (below)
       } else if constexpr (i == NA - 2) {
         a[0] = frag<0>(an);   // s + 1's A[0] into A[21]'s slot
-        mfma<false>(a[1], b[0], acc[22][0]);
-        acopy<W, 0>(f, va, g0, k3);
-        mfma<false>(a[2], b[0], acc[23][0]); b[0] = frag<W * 64 + 0>(bn);
+        mfma<false>(a[1], b[0], acc[22][0]); mfma<false>(a[2], b[0], acc[23][0]); b[0] = frag<W * 64 + 0>(bn);
         mfma<false>(a[1], b[1], acc[22][1]); mfma<false>(a[2], b[1], acc[23][1]); b[1] = frag<W * 64 + 16>(bn);
-        mfma<false>(a[1], b[2], acc[22][2]);
         acopy<W, 1>(f, va, g0, k3);
-        mfma<false>(a[2], b[2], acc[23][2]); b[2] = frag<W * 64 + 32>(bn);
+        mfma<false>(a[1], b[2], acc[22][2]); mfma<false>(a[2], b[2], acc[23][2]); b[2] = frag<W * 64 + 32>(bn);
         mfma<false>(a[1], b[3], acc[22][3]); mfma<false>(a[2], b[3], acc[23][3]); b[3] = frag<W * 64 + 48>(bn);
         a[1] = frag<16>(an);  // s + 1's A[1] into A[22]'s slot
       } else {
@@ -181,8 +180,6 @@ __device__ __forceinline__ void mainloop(const Feed& f, int nk, i32x4 (&acc)[NA]
         if constexpr (i == 0) b[0] = xor80(b[0]);
         mfma<AG>(a[i % RING], b[0], acc[i][0]);
         a[(i + 2) % RING] = frag<(i + 2 < NA ? i + 2 : 0) * 16>(ac);
-        if constexpr (i % 4 == 0 && i <= 12) acopy<W, (i % 4 == 0 && i <= 12 ? 2 + i / 4 : 0)>(f, va, g2, k2);
-        if constexpr (i % 4 == 2 && i <= 14) bcopy<W, (i % 4 == 2 && i <= 14 ? i / 4 : 0)>(f, vb, q0, k2);
         if constexpr (i == 0) b[1] = xor80(b[1]);
         mfma<AG>(a[i % RING], b[1], acc[i][1]);
         if constexpr (i == 0) b[2] = xor80(b[2]);
