@@ -34,7 +34,7 @@ def main():
     dev = _lib.device()
     N, B, d, per = int(os.environ.get("N", 1_000_000)), 4096, 9999, 10
     P, _ = build_projection(10000, d, dev)
-    bank = IdentityBank(N // per, 100, 100, device=dev)
+    bank = IdentityBank(-(-N // per), 100, 100, device=dev)   # row j shows identity j // per
     ld = round_up(d, 32)
     G = torch.zeros((N, ld), dtype=torch.float32, device=dev)
     m = col_mean_u8(bank.images(torch.arange(8192, device=dev) // per, seed=SEED + 1000), 10000)

@@ -48,7 +48,7 @@ def main():
     D, d, B, k, per = 10000, 9999, 4096, 1, 10
     N = args.gallery
     P, _ = build_projection(D, d, dev)
-    bank = IdentityBank(N // per, 100, 100, device=dev)
+    bank = IdentityBank(-(-N // per), 100, 100, device=dev)   # row j shows identity j // per
     ld = max(32, round_up(d, 32))
     for noise in [float(x) for x in args.noise.split(",")]:
         g = build_gallery(P, bank, per, 0, N, N, d, ld, dev, noise=noise)

@@ -41,7 +41,7 @@ def main():
     ff._eigenvectors = np.asmatrix(W)
     ff._eigenvalues = np.ones(d, np.float32)
     ff._num_components = d
-    bank = IdentityBank(N // per_id, side, side, device=dev)
+    bank = IdentityBank(-(-N // per_id), side, side, device=dev)   # row j shows identity j // per_id
     P = Projection(W=W, device=dev)
     F = torch.empty((N, d), dtype=torch.float64, device=dev)
     for c0 in range(0, N, 8192):

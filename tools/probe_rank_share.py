@@ -46,7 +46,7 @@ def main():
     side, d, per_id, B, k, G = 100, 9999, 10, a.batch, 1, a.gpus
     N = a.gallery // G
     P, _ = build_projection(side * side, d, dev)
-    bank = IdentityBank(a.gallery // per_id, side, side, device=dev)
+    bank = IdentityBank(-(-a.gallery // per_id), side, side, device=dev)   # row j shows identity j // per_id
     ld = round_up(d, 32)
     g = build_gallery(P, bank, per_id, 0, N, a.gallery, d, ld, dev)          # rank 0's rows
     g._tier_gallery("f6")
