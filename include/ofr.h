@@ -223,12 +223,13 @@ int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int6
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, const void* St,
                        int64_t Ns, const float* sscale, const float* saux, void* workspace, size_t workspace_bytes);
 /* The row step of the sample (64) and its builder: gallery rows j * 64 for j in [j0, j1) (X = row 0
- * of the fp32 gallery, ldx its leading dimension) are quantized into sample row j of tiles / scale /
- * stats (as ofr_f6_quantize_rows_at) and saux[j] = aux[j * 64].  A gallery of N rows has j1 =
- * ceil(N / 64); an append of rows [N0, N1) extends it with j0 = ceil(N0 / 64), j1 = ceil(N1 / 64). */
+ * of the N-row fp32 gallery, ldx its leading dimension; j1 <= ceil(N / 64)) are quantized into sample
+ * row j of tiles / scale / stats (as ofr_f6_quantize_rows_at) and saux[j] = aux[j * 64].  A gallery of
+ * N rows has j1 = ceil(N / 64); an append of rows [N0, N1) extends it with j0 = ceil(N0 / 64),
+ * j1 = ceil(N1 / 64) (N = N1).                                                                    */
 int64_t ofr_f6_sample_step(void);
-int ofr_f6_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1, const float* aux,
-                       void* tiles, size_t tiles_bytes, float* scale, double* stats, float* saux);
+int ofr_f6_sample_rows(void* stream, const float* X, int64_t N, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
+                       const float* aux, void* tiles, size_t tiles_bytes, float* scale, double* stats, float* saux);
 /* Phase 2 of ofr_knn_f6 split for a gallery sharded over ranks (new; replaces the
  * per-rank re-rank of classifier.py:104-119's loop at G > 1).  After phase 1 on every shard:
  *   stage 1 selects each query's 16 candidates into the workspace and writes ub[B][k] -- upper
@@ -268,8 +269,8 @@ int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d
  * saux the fp6 tier's sample (ofr_f6_sample_rows), St2 the second slices of the same rows
  * (ofr_f6x2_sample_rows: rows j * 64 for j in [j0, j1) into sample row j of tiles2, with their scales
  * and f6x2 stats).                                                                               */
-int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1, void* tiles2,
-                         size_t tiles_bytes, float* scale, double* stats);
+int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t N, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
+                         void* tiles2, size_t tiles_bytes, float* scale, double* stats);
 int ofr_knn_f6x2_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                          const void* Qt2, const float* qscale, const double* qstats, const float* G, int64_t N,
                          int64_t ldg, int64_t d, const void* Gt, const void* Gt2, const float* gscale,

@@ -432,14 +432,14 @@ class FloatGallery:
         """Extend the f6 tier's row sample over gallery rows [N0, N1) (ofr_f6_sample_rows)."""
         step = _lib.load().ofr_f6_sample_step()
         j0, j1 = -(-N0 // step), -(-N1 // step)
-        call("ofr_f6_sample_rows", stream(), ptr(self._Gbuf), self.ld, self.d, j0, j1, ptr(self._auxbuf), ptr(g["St"]),
-             g["St"].numel(), ptr(g["sscale"]), ptr(g["sstats"]), ptr(g["saux"]))
+        call("ofr_f6_sample_rows", stream(), ptr(self._Gbuf), N1, self.ld, self.d, j0, j1, ptr(self._auxbuf),
+             ptr(g["St"]), g["St"].numel(), ptr(g["sscale"]), ptr(g["sstats"]), ptr(g["saux"]))
 
     def _sample_rows2(self, g, N0, N1):
         """Extend the f6x2 tier's second-slice row sample over gallery rows [N0, N1) (ofr_f6x2_sample_rows)."""
         step = _lib.load().ofr_f6_sample_step()
         j0, j1 = -(-N0 // step), -(-N1 // step)
-        call("ofr_f6x2_sample_rows", stream(), ptr(self._Gbuf), self.ld, self.d, j0, j1, ptr(g["St2"]),
+        call("ofr_f6x2_sample_rows", stream(), ptr(self._Gbuf), N1, self.ld, self.d, j0, j1, ptr(g["St2"]),
              g["St2"].numel(), ptr(g["sscale2"]), ptr(g["sstats2"]))
 
     @staticmethod

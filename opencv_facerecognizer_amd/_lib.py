@@ -69,7 +69,8 @@ SIGNATURES = {
                                    c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                    c_vp, c_sz]),
     "ofr_f6_sample_step": (c_i64, []),
-    "ofr_f6_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp]),
+    "ofr_f6_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp,
+                                   c_vp]),
     "ofr_knn_f6_merge_pruned": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp, c_sz]),
@@ -77,7 +78,7 @@ SIGNATURES = {
     "ofr_f6x2_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp]),
     "ofr_knn_f6x2": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz]),
-    "ofr_f6x2_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp]),
+    "ofr_f6x2_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp]),
     "ofr_knn_f6x2_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                      c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      c_vp, c_i64, c_vp, c_vp, c_vp, c_sz]),

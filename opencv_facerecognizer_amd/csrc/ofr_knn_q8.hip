@@ -1310,9 +1310,10 @@ extern "C" int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, i
 
 extern "C" int64_t ofr_f6_sample_step(void) { return q8s::SAMPLE_STEP; }
 
-extern "C" int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
-                                    void* tiles2, size_t tiles_bytes, float* scale, double* stats) {
-  OFR_CHECK_ARG(j0 >= 0 && j1 >= j0 && d >= 1 && ldx >= d, "ofr_f6x2_sample_rows: bad sizes");
+extern "C" int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t N, int64_t ldx, int64_t d, int64_t j0,
+                                    int64_t j1, void* tiles2, size_t tiles_bytes, float* scale, double* stats) {
+  OFR_CHECK_ARG(j0 >= 0 && j1 >= j0 && d >= 1 && ldx >= d && N >= 0, "ofr_f6x2_sample_rows: bad sizes");
+  OFR_CHECK_ARG(j1 <= cdiv(N, q8s::SAMPLE_STEP), "ofr_f6x2_sample_rows: j1 past the gallery's sample (ceil(N / 64))");
   if (j1 == j0) return OFR_OK;
   OFR_CHECK_ARG(X, "ofr_f6x2_sample_rows: null pointer");
   OFR_CHECK_ARG(ldx < INT64_MAX / q8s::SAMPLE_STEP, "ofr_f6x2_sample_rows: leading dimension too large");
@@ -1320,10 +1321,11 @@ extern "C" int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t ldx, i
                                    nullptr, tiles2, tiles_bytes, scale, stats);
 }
 
-extern "C" int ofr_f6_sample_rows(void* stream, const float* X, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
-                                  const float* aux, void* tiles, size_t tiles_bytes, float* scale, double* stats,
-                                  float* saux) {
-  OFR_CHECK_ARG(j0 >= 0 && j1 >= j0 && d >= 1 && ldx >= d, "ofr_f6_sample_rows: bad sizes");
+extern "C" int ofr_f6_sample_rows(void* stream, const float* X, int64_t N, int64_t ldx, int64_t d, int64_t j0,
+                                  int64_t j1, const float* aux, void* tiles, size_t tiles_bytes, float* scale,
+                                  double* stats, float* saux) {
+  OFR_CHECK_ARG(j0 >= 0 && j1 >= j0 && d >= 1 && ldx >= d && N >= 0, "ofr_f6_sample_rows: bad sizes");
+  OFR_CHECK_ARG(j1 <= cdiv(N, q8s::SAMPLE_STEP), "ofr_f6_sample_rows: j1 past the gallery's sample (ceil(N / 64))");
   if (j1 == j0) return OFR_OK;
   OFR_CHECK_ARG(X && aux && saux, "ofr_f6_sample_rows: null pointer");
   OFR_CHECK_ARG(ldx < INT64_MAX / q8s::SAMPLE_STEP, "ofr_f6_sample_rows: leading dimension too large");

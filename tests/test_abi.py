@@ -32,3 +32,10 @@ def test_error_paths_without_device():
     rc = lib.ofr_knn_f32(None, 0, None, 1, 32, None, 1, 32, 3, None, 99, 0, None, None, None, 0)
     assert rc == -2 and b"k must be" in lib.ofr_last_error()
     assert lib.ofr_knn_workspace_bytes(4096, 1000000, 1) >= 4096 * (1000000 // 256) * 8 * 8
+    # the row sample of the fp6 sieve (round 4): at most ceil(N / 64) rows, no reads past the gallery
+    assert lib.ofr_f6_sample_step() == 64
+    rc = lib.ofr_f6_sample_rows(None, None, 1000, 32, 32, 0, 17, None, None, 0, None, None, None)
+    assert rc == -1 and b"past the gallery" in lib.ofr_last_error()
+    rc = lib.ofr_f6x2_sample_rows(None, None, 1000, 32, 32, 0, 17, None, 0, None, None)
+    assert rc == -1 and b"past the gallery" in lib.ofr_last_error()
+    assert lib.ofr_f6_sample_rows(None, None, 1000, 32, 32, 16, 16, None, None, 0, None, None, None) == 0   # empty
