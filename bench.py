@@ -12,9 +12,12 @@ certificate (phase 2) + the fallback tiers of the uncertified queries
 fp32-MFMA pass (ofr_knn_tiles_f32) instead.  The steps are pipelined over three
 query buffers (StepPipeline): the tile pass owns the main stream, the next
 batch's preparation and this batch's merge follow it on a side stream.
-Inputs are resident in HBM before the timed region.  W is random (no trained
-checkpoint exists at this scale), gallery/queries are synthetic (see
-opencv_facerecognizer_amd/synthetic.py).
+Inputs are resident in HBM before the timed region.  W is the Fisherfaces W the
+reference's trainer produces (thetrainer.py:120-124, Fisherfaces() defaults) from
+configs[1]'s synthetic training set (10k identities x 10 faces), trained on the
+device in the untimed setup (SURVEY §8d: "1M images projected with config-2 W");
+--w random keeps the round-1..4 random N(0, 1/D) W.  Gallery/queries are synthetic
+(see opencv_facerecognizer_amd/synthetic.py).
 
 Multi-GPU (torch.distributed.run, one process per GPU): the 1M gallery is
 sharded by rows over the ranks; each rank projects and quantizes B/G of the
@@ -41,8 +44,9 @@ sys.path.insert(0, ROOT)
 from opencv_facerecognizer_amd import _lib  # noqa: E402
 from opencv_facerecognizer_amd._device import FloatGallery, Workspace, round_up  # noqa: E402
 from opencv_facerecognizer_amd.parallel import (certify_sharded, exchange_topk, gather_rows, gather_rows_async,  # noqa: E402
-                                                merge_sharded, merge_topk, shard_range)
-from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_gallery, build_projection  # noqa: E402
+                                                merge_sharded, merge_topk, shard_range, share_block_scales)
+from opencv_facerecognizer_amd.synthetic import (SEED, IdentityBank, build_gallery, build_projection,  # noqa: E402
+                                                 build_trained_projection)
 
 PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
 PEAK_I8_MFMA = 5.0e15       # int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, matrix cores)
@@ -72,6 +76,9 @@ def parse():
                     help="pixel-noise levels of the crowded-neighbour stress runs (same shape, 1 GPU); '' to skip")
     ap.add_argument("--stress-steps", type=int, default=3)
     ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (100k-row gallery), 1 GPU")
+    ap.add_argument("--w", choices=["trained", "random"], default="trained",
+                    help="trained: Fisherfaces W trained on configs[1]'s 100k faces (SURVEY §8d); random: N(0, 1/D)")
+    ap.add_argument("--train-ids", type=int, default=10_000, help="identities of the W training set (x --per-id faces)")
     ap.add_argument("--search", choices=["f6", "q8", "fp32"], default="f6",
                     help="f6: certified fp6 coarse pass (uncertified queries go down the int8 tiers, then fp32); "
                          "q8: start at the certified int8 tier; fp32: fp32-MFMA pass")
@@ -259,6 +266,23 @@ def certificate_margin(gallery, Qd, qq, nsample=64):
     return {"median": float(np.median(r)), "min": float(r.min()), "sample": int(len(r))}
 
 
+def feature_profile(gallery, rows=8192):
+    """How the centred gallery features spread over the 32-feature blocks (the fp6 tier quantizes a
+    row with ONE scale, so a row whose energy sits in a few blocks loses the rest to the step size),
+    and the fp6 tier's residual ||x - x~|| / ||x~|| per row (the e / a of the certificate)."""
+    n = min(rows, gallery.N)
+    G = gallery.G[:n, :gallery.d].double()
+    nb = -(-gallery.d // 32)
+    Gp = torch.nn.functional.pad(G, (0, nb * 32 - gallery.d))
+    rms = Gp.pow(2).reshape(n, nb, 32).mean(dim=(0, 2)).sqrt().cpu().numpy()
+    st = gallery._tier_gallery("f6")["stats"][:n]
+    rel = (st[:, 1] / st[:, 0]).cpu().numpy()
+    return {"block_rms_first8": [round(float(x), 2) for x in rms[:8]],
+            "block_rms_quantiles_rest": [round(float(x), 2) for x in np.quantile(rms[8:], [0, 0.5, 1])] if nb > 8 else [],
+            "row_max_over_rms": float(torch.median(G.abs().amax(1) / G.pow(2).mean(1).sqrt()).item()),
+            "f6_residual_rel_median": float(np.median(rel)), "f6_residual_rel_max": float(rel.max()), "rows": n}
+
+
 def stress_run(P, bank, args, noise, device, N=None):
     """Crowded neighbours: the headline shape (1M gallery, B = 4096, d = 9999) with the pixel noise
     raised so that identities crowd together and the fp6 certificate fails; the uncertified queries
@@ -385,8 +409,16 @@ def main():
 
     # ---- setup (untimed): W, gallery shard, queries -------------------------------------
     t0 = time.perf_counter()
-    P, Wt = build_projection(D, d, device)
     bank = IdentityBank(n_ids, H, W, device=device)
+    w_info = {"kind": "random N(0, 1/D)"}
+    if args.w == "trained":
+        P, Wt, w_info = build_trained_projection(bank, args.per_id, args.train_ids * args.per_id, D, device)
+        w_info["kind"] = "Fisherfaces() trained on configs[1]'s faces"
+        if P.d != d:
+            raise SystemExit(f"trained W has d={P.d}, --dim {d}: pass --dim {P.d}")
+        log(rank, f"trained W: {w_info}")
+    else:
+        P, Wt = build_projection(D, d, device)
     ld = max(32, round_up(d, 32))
     gallery = build_gallery(P, bank, args.per_id, n0, nl, N, d, ld, device)
     gq = torch.Generator(device=device)
@@ -402,6 +434,8 @@ def main():
     use_q8 = args.search in ("f6", "q8")
     tier0 = "f6" if args.search == "f6" else 1
     if use_q8:
+        if world > 1:
+            share_block_scales(gallery)     # every rank quantizes alike: the fp6 query panels are all-gathered
         for t in FloatGallery.tier_path(tier0)[:-1]:
             gallery._tier_gallery(t)                              # quantized gallery tiers (once, untimed)
     fallbacks = []
@@ -593,7 +627,9 @@ def main():
                       "q8": "i8 (int8 MFMA coarse scores, certified; fp64 exact re-rank)",
                       "fp32": "f32 (fp32 MFMA scores, fp64 exact re-rank)"}[args.search], "data": "synthetic",
             "config": {"workload": "configs[2]: Fisherfaces projection + 1-NN, 1M-image gallery (100k ids x 10), "
-                                   "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1",
+                                   "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1, W = "
+                                   + ("Fisherfaces() trained on configs[1]'s 100k faces (10k ids x 10)"
+                                      if args.w == "trained" else "random N(0, 1/D)"),
                        "gallery": N, "global_batch": B, "d": d, "D": D, "k": k,
                        "parallelism": (f"gallery-rows/{world}, query prep sharded + {coll} all-gather of rows, {coll} all-gather "
                                        f"of top-k + bounds (global certificate)" if shard_prep else
@@ -627,6 +663,8 @@ def main():
             "sieve_kept_rows_per_query": kept,
             "top1_identity_acc": acc,
             "certificate_margin_fp6": margin,
+            "projection_w": w_info,
+            "feature_profile": feature_profile(gallery) if args.search == "f6" else None,
             "small_batch": small,
         }
         if world == 1 and not args.no_cpu:

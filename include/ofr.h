@@ -172,7 +172,19 @@ int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, 
  * 128-feature stages, 24 KiB per (panel, stage) (layout: csrc/ofr_f6_tile.h);
  * ofr_f6_tiles_bytes(R, d) bytes, rows past R in the last panel zeroed.
  * stats[3] = (||x~||, ||x - x~||, 0); maxima as ofr_q8_quantize_rows.
- * ofr_knn_f6: v_mfma_scale_f32_32x32x64_f8f6f4 (fp6 x fp6, unit block scales)
+ * Column-block scales (round 5; every f6 / f6x2 entry point's trailing bscale,
+ * null = unit): one E8M0 byte per 32 features (4 * ceil(d / 128) bytes, 4-byte
+ * aligned), shared by a gallery and every query batch searched against it:
+ * feature k is quantized as x_k / 2^e with e = bscale[k / 32] - 127, the row
+ * scale s = max_k |x_k| / 2^e_k / 7.5, x~_k = s 2^e_k v_k, and the MFMA applies
+ * 2^e_k to both operands.  ofr_f6_block_sumsq accumulates per-block sums of
+ * squares over rows (sums [ceil(d / 32)] fp64, +=, zero them first; shards
+ * all-reduce them); ofr_f6_block_scales turns them into bytes with
+ * e_b = rint(log2(rms_b / max rms)) in [-63, 0] (127 past d).  A trained
+ * Fisherfaces W puts most of the feature variance into its leading columns; one
+ * row scale alone then leaves the rest a few fp6 steps (residual 0.11 of the
+ * row norm against 0.03).
+ * ofr_knn_f6: v_mfma_scale_f32_32x32x64_f8f6f4 (fp6 x fp6, column-block scales)
  * sums v_q.v_g with fp32 accumulation, whose error (<= (2 nst + 64) 2^-23
  * a_q A) is added to the certificate bound; otherwise the ofr_knn_q8 contract
  * (exact fp64 re-rank of the best 16 coarse rows, cert[q], bound[q]).
@@ -197,19 +209,22 @@ size_t ofr_f6_tiles_bytes(int64_t R, int64_t d);
  * the destination row), zeroing the rest of the last panel; then recompute the
  * gallery maxima over all rows with ofr_q8_maxima.                           */
 int ofr_f6_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int64_t row0,
-                            void* tiles, size_t tiles_bytes, float* scale, double* stats);
+                            void* tiles, size_t tiles_bytes, float* scale, double* stats, const uint8_t* bscale);
 int ofr_q8_maxima(void* stream, const double* stats, const float* aux, int64_t R, double* maxima);
+int ofr_f6_block_sumsq(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, double* sums);
+int ofr_f6_block_scales(void* stream, const double* sums, int64_t d, uint8_t* bscale);
 size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N);
 size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N);
 int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
-                         size_t tiles_bytes, float* scale, double* stats, const float* aux, double* maxima);
+                         size_t tiles_bytes, float* scale, double* stats, const float* aux, double* maxima,
+                         const uint8_t* bscale);
 /* The fp6 sieve kernel ofr_knn_f6 launches for B > 32, as the profiler names it (profiling labels). */
 const char* ofr_f6_sieve_kernel(void);
 int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
-               void* workspace, size_t workspace_bytes);
+               void* workspace, size_t workspace_bytes, const uint8_t* bscale);
 /* ofr_knn_f6 with a ROW sample for the sieve thresholds (B > 32; new, same contract otherwise).
  * St/sscale/saux: fp6 tiles (ofr_f6_tiles_bytes(Ns, d) bytes), row scales and aux terms of Ns <=
  * ceil(N / 64) gallery rows, written by ofr_f6_sample_rows (rows 0, 64, 128, ...).  The threshold
@@ -221,7 +236,8 @@ int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int6
                        const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, const void* St,
-                       int64_t Ns, const float* sscale, const float* saux, void* workspace, size_t workspace_bytes);
+                       int64_t Ns, const float* sscale, const float* saux, void* workspace, size_t workspace_bytes,
+                       const uint8_t* bscale);
 /* The row step of the sample (64) and its builder: gallery rows j * 64 for j in [j0, j1) (X = row 0
  * of the N-row fp32 gallery, ldx its leading dimension; j1 <= ceil(N / 64)) are quantized into sample
  * row j of tiles / scale / stats (as ofr_f6_quantize_rows_at) and saux[j] = aux[j * 64].  A gallery of
@@ -229,7 +245,8 @@ int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int6
  * j1 = ceil(N1 / 64) (N = N1).                                                                    */
 int64_t ofr_f6_sample_step(void);
 int ofr_f6_sample_rows(void* stream, const float* X, int64_t N, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
-                       const float* aux, void* tiles, size_t tiles_bytes, float* scale, double* stats, float* saux);
+                       const float* aux, void* tiles, size_t tiles_bytes, float* scale, double* stats, float* saux,
+                       const uint8_t* bscale);
 /* Phase 2 of ofr_knn_f6 split for a gallery sharded over ranks (new; replaces the
  * per-rank re-rank of classifier.py:104-119's loop at G > 1).  After phase 1 on every shard:
  *   stage 1 selects each query's 16 candidates into the workspace and writes ub[B][k] -- upper
@@ -262,26 +279,28 @@ int ofr_knn_f6_merge_pruned(void* stream, int stage, const float* Q, int64_t B, 
  * 3 nst MFMAs.  Same contract and workspace (ofr_knn_f6_workspace_bytes).        */
 int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles1,
                            void* tiles2, size_t tiles_bytes, float* scale, double* stats, const float* aux,
-                           double* maxima);
+                           double* maxima, const uint8_t* bscale);
 int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int64_t row0,
-                              void* tiles1, void* tiles2, size_t tiles_bytes, float* scale, double* stats);
+                              void* tiles1, void* tiles2, size_t tiles_bytes, float* scale, double* stats,
+                              const uint8_t* bscale);
 /* ofr_knn_f6x2 with the sieve thresholds from the row sample (as ofr_knn_f6_sampled): St / sscale /
  * saux the fp6 tier's sample (ofr_f6_sample_rows), St2 the second slices of the same rows
  * (ofr_f6x2_sample_rows: rows j * 64 for j in [j0, j1) into sample row j of tiles2, with their scales
  * and f6x2 stats).                                                                               */
 int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t N, int64_t ldx, int64_t d, int64_t j0, int64_t j1,
-                         void* tiles2, size_t tiles_bytes, float* scale, double* stats);
+                         void* tiles2, size_t tiles_bytes, float* scale, double* stats, const uint8_t* bscale);
 int ofr_knn_f6x2_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                          const void* Qt2, const float* qscale, const double* qstats, const float* G, int64_t N,
                          int64_t ldg, int64_t d, const void* Gt, const void* Gt2, const float* gscale,
                          const float* aux, const double* gmax, int k, int64_t index_base, double* out_d,
                          int64_t* out_i, int* cert, double* bound, const void* St, const void* St2, int64_t Ns,
-                         const float* sscale, const float* saux, void* workspace, size_t workspace_bytes);
+                         const float* sscale, const float* saux, void* workspace, size_t workspace_bytes,
+                         const uint8_t* bscale);
 int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt, const void* Qt2,
                  const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                  const void* Gt, const void* Gt2, const float* gscale, const float* aux, const double* gmax, int k,
                  int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
-                 size_t workspace_bytes);
+                 size_t workspace_bytes, const uint8_t* bscale);
 
 /* Merge P sorted (distance, index) lists per query into the best k:
  * in_d/in_i [B][P*kin] (list p at columns [p*kin, (p+1)*kin)), ascending by
@@ -479,6 +498,9 @@ typedef struct ofr_knn_shard {
   const float* sscale;
   const float* saux;
   const void* St2;          /* optional: the second slices of the sample (ofr_f6x2_sample_rows) for f6x2 */
+  /* the shard's column-block scales (ofr_f6_block_scales; null: unit), also those of its query tiles
+     Qt -- round 5, appended */
+  const uint8_t* bscale;
 } ofr_knn_shard;
 int ofr_comm_init_all(int ndev, const int* devices, ofr_comm** comm);
 int ofr_comm_destroy(ofr_comm* comm);

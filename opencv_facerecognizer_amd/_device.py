@@ -205,6 +205,7 @@ class FloatGallery:
             call("ofr_row_aux", stream(), self.metric, ptr(self.G), self.N, self.d, self.ld, ptr(self.aux))
         self.ws = Workspace()
         self.q8 = None
+        self.bscale = None                       # fp6 tiers' column-block scales (block_scales)
         self._twin = None
         self.last_fallbacks = 0
         self.tier_failures = {}                  # tier -> recent uncertified fraction (start_tier)
@@ -244,13 +245,14 @@ class FloatGallery:
         if self._twin is not None:                 # Cosine: the unit-row twin grows with it
             self._twin.append(self.unit_rows(self.G[N0:N1])[:, :self.d])
         for tier, g in (self.q8 or {}).items():     # "f6" before "f6x2": insertion order
+            # the fp6 tiers keep the column-block scales they were built with (any scales are exact)
             if tier == "f6":
                 call("ofr_f6_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, ptr(g["Gs"]),
-                     g["Gs"].numel(), ptr(g["scale"]), ptr(g["stats"]))
+                     g["Gs"].numel(), ptr(g["scale"]), ptr(g["stats"]), ptr(self.bscale))
                 self._sample_rows(g, N0, N1)
             elif tier == "f6x2":                       # the first slice is the f6 tier's, extended above
                 call("ofr_f6x2_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, None,
-                     ptr(g["Gs2"]), g["Gs2"].numel(), ptr(g["scale"]), ptr(g["stats"]))
+                     ptr(g["Gs2"]), g["Gs2"].numel(), ptr(g["scale"]), ptr(g["stats"]), ptr(self.bscale))
                 self._sample_rows2(g, N0, N1)
             else:
                 call("ofr_q8_quantize_rows", stream(), tier, ptr(self.G[N0:]), n, self.d, self.ld, ptr(g["Gs"][N0:]),
@@ -375,6 +377,41 @@ class FloatGallery:
             prev = self.tier_failures.get(tier)
             self.tier_failures[tier] = f if prev is None else 0.5 * (prev + f)
 
+    # -- column-block scales of the fp6 tiers (ofr_f6_block_scales) -------------------
+    # One E8M0 byte per 32 features, shared by the gallery's fp6 tiles and every query batch: feature k
+    # is quantized as x_k / 2^e with e = rint(log2(rms of its block / the largest block rms)), so the
+    # row scale no longer lets the few high-variance columns of a trained Fisherfaces W (LDA eigenvalue
+    # order) crush the rest into a handful of fp6 steps.  Any scales are exact for the certificate
+    # (the stats are of the values stored); they only decide how tight it is.  OFR_F6_BLOCK_SCALES=0:
+    # unit scales (the round-1..4 quantization).
+    def block_sums(self):
+        """Per-32-feature-block sums of squares of the gallery rows (fp64 device [ceil(d / 32)]): what a
+        sharded gallery all-reduces before set_block_scales, so every rank quantizes alike."""
+        sums = torch.zeros(-(-self.d // 32), dtype=torch.float64, device=self.G.device)
+        call("ofr_f6_block_sumsq", stream(), ptr(self.G), self.N, self.d, self.ld, ptr(sums))
+        return sums
+
+    def set_block_scales(self, sums):
+        """Column-block scales from block sums of squares (block_sums, possibly all-reduced); before the
+        fp6 tiers are built (they keep the scales they were quantized with)."""
+        if self.q8 and any(t in self.q8 for t in ("f6", "f6x2")):
+            raise RuntimeError("set_block_scales: the fp6 tiers are already built with other scales")
+        if os.environ.get("OFR_F6_BLOCK_SCALES", "1") == "0":
+            self.bscale = None
+            return None
+        nbytes = 4 * -(-self.d // 128)
+        self.bscale = torch.empty(nbytes, dtype=torch.uint8, device=self.G.device)
+        call("ofr_f6_block_scales", stream(), ptr(sums), self.d, ptr(self.bscale))
+        return self.bscale
+
+    def _block_scales(self):
+        """The fp6 tiers' column-block scales, made from this gallery's rows on first use."""
+        if self.bscale is None and not getattr(self, "_bscale_done", False):
+            self._bscale_done = True
+            if self.N > 0:
+                self.set_block_scales(self.block_sums())
+        return self.bscale
+
     @staticmethod
     def _q8_ld(d, slices):
         return round_up(d, 128) if slices == 1 else 2 * round_up(d, 64)
@@ -395,7 +432,7 @@ class FloatGallery:
                 nbytes = lib.ofr_f6_tiles_bytes(cap, self.d)
                 Gs = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
                 call("ofr_f6_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, ptr(Gs), nbytes,
-                     ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
+                     ptr(gs), ptr(st), ptr(self.aux), ptr(gmax), ptr(self._block_scales()))
                 # the sieve's row sample (ofr_knn_f6_sampled): rows 0, 64, 128, ... in their own tiles
                 ns = -(-cap // lib.ofr_f6_sample_step())
                 sbytes = lib.ofr_f6_tiles_bytes(ns, self.d)
@@ -410,7 +447,7 @@ class FloatGallery:
                 nbytes = _lib.load().ofr_f6_tiles_bytes(cap, self.d)
                 Gs2 = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
                 call("ofr_f6x2_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, None, ptr(Gs2),
-                     nbytes, ptr(gs), ptr(st), ptr(self.aux), ptr(gmax))
+                     nbytes, ptr(gs), ptr(st), ptr(self.aux), ptr(gmax), ptr(self._block_scales()))
                 # second slices of the f6 tier's row sample (ofr_knn_f6x2_sampled)
                 s1 = self._tier_gallery("f6")
                 ns = int(s1["sscale"].numel())
@@ -433,14 +470,14 @@ class FloatGallery:
         step = _lib.load().ofr_f6_sample_step()
         j0, j1 = -(-N0 // step), -(-N1 // step)
         call("ofr_f6_sample_rows", stream(), ptr(self._Gbuf), N1, self.ld, self.d, j0, j1, ptr(self._auxbuf),
-             ptr(g["St"]), g["St"].numel(), ptr(g["sscale"]), ptr(g["sstats"]), ptr(g["saux"]))
+             ptr(g["St"]), g["St"].numel(), ptr(g["sscale"]), ptr(g["sstats"]), ptr(g["saux"]), ptr(self.bscale))
 
     def _sample_rows2(self, g, N0, N1):
         """Extend the f6x2 tier's second-slice row sample over gallery rows [N0, N1) (ofr_f6x2_sample_rows)."""
         step = _lib.load().ofr_f6_sample_step()
         j0, j1 = -(-N0 // step), -(-N1 // step)
         call("ofr_f6x2_sample_rows", stream(), ptr(self._Gbuf), N1, self.ld, self.d, j0, j1, ptr(g["St2"]),
-             g["St2"].numel(), ptr(g["sscale2"]), ptr(g["sstats2"]))
+             g["St2"].numel(), ptr(g["sscale2"]), ptr(g["sstats2"]), ptr(self.bscale))
 
     @staticmethod
     def row_sample():
@@ -467,10 +504,10 @@ class FloatGallery:
                        bound=torch.empty(B, dtype=torch.float64, device=dev_), tier=tier, B=B, **extra)
         if tier == "f6":
             call("ofr_f6_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
-                 out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None)
+                 out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None, ptr(self._block_scales()))
         elif tier == "f6x2":
             call("ofr_f6x2_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]), ptr(out["Qs2"]),
-                 out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None)
+                 out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None, ptr(self._block_scales()))
         else:
             call("ofr_q8_quantize_rows", stream(), tier, ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
                  out["Qs"].shape[1], ptr(out["scale"]), ptr(out["stats"]), None, None)
@@ -516,23 +553,24 @@ class FloatGallery:
                  ptr(qq["scale"]), ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]),
                  ptr(g["Gs2"]), ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]),
                  ptr(out[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(s1["St"]), ptr(g["St2"]), ns,
-                 ptr(s1["sscale"]), ptr(s1["saux"]), ptr(ws), ws.numel())
+                 ptr(s1["sscale"]), ptr(s1["saux"]), ptr(ws), ws.numel(), ptr(self.bscale))
         elif tier == "f6x2":
             call("ofr_knn_f6x2", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["Qs2"]),
                  ptr(qq["scale"]), ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]),
                  ptr(g["Gs2"]), ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]),
-                 ptr(out[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(ws), ws.numel())
+                 ptr(out[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(ws), ws.numel(), ptr(self.bscale))
         elif tier == "f6" and self.row_sample():
             ns = -(-self.N // lib.ofr_f6_sample_step())
             call("ofr_knn_f6_sampled", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
                  ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),
                  ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
-                 ptr(qq["bound"]), ptr(g["St"]), ns, ptr(g["sscale"]), ptr(g["saux"]), ptr(ws), ws.numel())
+                 ptr(qq["bound"]), ptr(g["St"]), ns, ptr(g["sscale"]), ptr(g["saux"]), ptr(ws), ws.numel(),
+                 ptr(self.bscale))
         elif tier == "f6":
             call("ofr_knn_f6", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
                  ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),
                  ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
-                 ptr(qq["bound"]), ptr(ws), ws.numel())
+                 ptr(qq["bound"]), ptr(ws), ws.numel(), ptr(self.bscale))
         else:
             call("ofr_knn_q8", stream(), phases, tier, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
                  ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), g["ld"],

@@ -57,31 +57,33 @@ SIGNATURES = {
     "ofr_normalize_rows_f32": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
     "ofr_cosine_pairs": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp]),
     "ofr_f6_tiles_bytes": (c_sz, [c_i64, c_i64]),
-    "ofr_f6_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp]),
+    "ofr_f6_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp, c_vp]),
     "ofr_q8_maxima": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "ofr_knn_f6_workspace_bytes": (c_sz, [c_i64, c_i64]),
     "ofr_f6_sieve_kernel": (ctypes.c_char_p, []),
     "ofr_knn_f6_sieve_counts_offset": (c_sz, [c_i64, c_i64]),
-    "ofr_f6_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp]),
+    "ofr_f6_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ofr_knn_f6": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
-                           c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz]),
+                           c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ofr_knn_f6_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
                                    c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
-                                   c_vp, c_sz]),
+                                   c_vp, c_sz, c_vp]),
     "ofr_f6_sample_step": (c_i64, []),
+    "ofr_f6_block_sumsq": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "ofr_f6_block_scales": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "ofr_f6_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp,
-                                   c_vp]),
+                                   c_vp, c_vp]),
     "ofr_knn_f6_merge_pruned": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp, c_sz]),
-    "ofr_f6x2_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp]),
-    "ofr_f6x2_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp]),
+    "ofr_f6x2_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "ofr_f6x2_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp]),
     "ofr_knn_f6x2": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
-                             c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz]),
-    "ofr_f6x2_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp]),
+                             c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "ofr_f6x2_sample_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp, c_vp]),
     "ofr_knn_f6x2_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                      c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                     c_vp, c_i64, c_vp, c_vp, c_vp, c_sz]),
+                                     c_vp, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "ofr_class_sums_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "ofr_class_between_f64": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "ofr_class_sub_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
@@ -145,7 +147,7 @@ class KnnShard(ctypes.Structure):
                 ("out_d", c_vp), ("out_i", c_vp), ("cert", c_vp),
                 ("Gt2", c_vp), ("gscale2", c_vp), ("gmax2", c_vp), ("G8", c_vp), ("ld8", c_i64), ("gscale8", c_vp),
                 ("gmax8", c_vp), ("tier_counts", c_vp), ("St", c_vp), ("Ns", c_i64), ("sscale", c_vp), ("saux", c_vp),
-                ("St2", c_vp)]
+                ("St2", c_vp), ("bscale", c_vp)]
 
 
 class OfrError(RuntimeError):

@@ -350,10 +350,11 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
     char* ws = (char*)s.workspace;
     int rc = s.St ? ofr_knn_f6_sampled(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
                                        s.gscale, s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
-                                       s.St, s.Ns, s.sscale, s.saux, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N))
+                                       s.St, s.Ns, s.sscale, s.saux, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N),
+                                       s.bscale)
                   : ofr_knn_f6(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt, s.gscale,
                                s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, ws + L[p].knn,
-                               ofr_knn_f6_workspace_bytes(B, s.N));
+                               ofr_knn_f6_workspace_bytes(B, s.N), s.bscale);
     if (rc) return rc;
     rc = ofr_knn_f6_merge_pruned(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
                                  s.gscale, s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
@@ -491,16 +492,16 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
       double* qst = (double*)(ws + L[p].qstats);
       if (stage == F6X2) {
         rc = ofr_f6x2_quantize_rows(s.stream, sq, n, d, s.ldq, ws + L[p].qt1, ws + L[p].qt2, L[p].tiles_bytes, qs, qst,
-                                    nullptr, nullptr);
+                                    nullptr, nullptr, s.bscale);
         if (rc) return rc;
         rc = s.St && s.St2
                  ? ofr_knn_f6x2_sampled(s.stream, 3, sq, n, s.ldq, ws + L[p].qt1, ws + L[p].qt2, qs, qst, s.G, s.N,
                                         s.ldg, d, s.Gt, s.Gt2, s.gscale2, s.aux, s.gmax2, k, s.index_base, ld_, li_,
                                         lc_, lb_, s.St, s.St2, s.Ns, s.sscale, s.saux, ws + L[p].knn,
-                                        ofr_knn_f6_workspace_bytes(n, s.N))
+                                        ofr_knn_f6_workspace_bytes(n, s.N), s.bscale)
                  : ofr_knn_f6x2(s.stream, 3, sq, n, s.ldq, ws + L[p].qt1, ws + L[p].qt2, qs, qst, s.G, s.N, s.ldg, d,
                                 s.Gt, s.Gt2, s.gscale2, s.aux, s.gmax2, k, s.index_base, ld_, li_, lc_, lb_,
-                                ws + L[p].knn, ofr_knn_f6_workspace_bytes(n, s.N));
+                                ws + L[p].knn, ofr_knn_f6_workspace_bytes(n, s.N), s.bscale);
       } else if (stage == Q8X2) {
         // the query slices share the gallery's row layout (ofr_knn_q8 takes one ld for both)
         rc = ofr_q8_quantize_rows(s.stream, 2, sq, n, d, s.ldq, (int8_t*)(ws + L[p].q8), s.ld8, qs, qst, nullptr,

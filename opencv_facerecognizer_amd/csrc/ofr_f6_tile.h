@@ -1,8 +1,14 @@
 // fp6 (e2m3) MFMA tile engine of the certified search's first tier (ofr_knn_q8.hip).
 //
 // C[a][b] = sum_k A[a][k] * B[b][k] over e2m3 rows (values m/8 .. 7.5, exact products),
-// v_mfma_scale_f32_32x32x64_f8f6f4 with both formats fp6 (cbsz = blgp = 2) and unit E8M0
-// scales: the per-row scale is folded into the epilogue like the int8 tiers' scale.  The
+// v_mfma_scale_f32_32x32x64_f8f6f4 with both formats fp6 (cbsz = blgp = 2).  Per-row fp32 scales are
+// folded into the epilogue like the int8 tiers' scale; the E8M0 block scales of the MFMA carry
+// per-COLUMN-block scales (round 5, "bscale"): one byte per 32 features, the same for the gallery
+// and the query rows, so an element decodes to s_row * 2^(bscale[k / 32] - 127) * v and the MFMA
+// applies 2^(2 e_B) to each block's products (both operands take the block's byte).  A trained
+// Fisherfaces W concentrates the feature variance in its leading columns (LDA eigenvalue order):
+// one row scale would leave the other columns a few fp6 steps (residual 0.11 of the row norm against
+// 0.029 on isotropic rows); column-block scales equalise the blocks first.  The
 // fp32 accumulation is the only inexact step: measured <= 3 * 2^-24 * sum|a b| over a
 // 160-MFMA chain (tools/mx_probe.hip); the certificate budgets (nmfma + 64) * 2^-23.
 // On gfx950 this instruction runs at twice the int8 MFMA rate per clock and moves 0.75 B
@@ -76,6 +82,50 @@ constexpr int SCALE_ONE = 0x7f7f7f7f;    // E8M0 2^0 in every byte
 constexpr int SCALE_X2 = 0x7b7b7b7b;     // E8M0 2^-4
 constexpr int X2_SHIFT = 4;              // second slice weight 2^-X2_SHIFT
 
+// Column-block scales of stage ks: 4 E8M0 bytes, blocks 4 ks .. 4 ks + 3 (bs: never null -- the host
+// passes a table of unit scales, q8s::unit_bscale, when the caller gives none).
+//
+// In the tile engines the dword comes in by an explicit scalar load (s_load_dword, inline asm) and is
+// turned into the lane's operand by an asm VALU shift placed right behind one of the engine's own
+// s_waitcnt lgkmcnt(0) (asm volatile statements keep their order).  A plain C++ load of it is not
+// selected as a scalar load (the kernels write global memory, so it is not provably unclobbered): it
+// becomes a vector load whose vmcnt the compiler then waits for among the stage copies, and its use
+// gets hoisted to the top of the next stage (measured: an s_waitcnt vmcnt(13) at every stage top).
+// The untracked scalar load only ever makes the compiler's own lgkmcnt waits stricter (LDS returns in
+// order; an extra outstanding operation can only delay the count).
+__device__ __forceinline__ uint32_t sload_bscale(const uint32_t* bs, int ks) {
+  uint32_t raw;
+  // uniform, but the compiler may hold it in a VGPR: the "s" constraint alone does not move it
+  const uint32_t off = (uint32_t)__builtin_amdgcn_readfirstlane((int)(4u * (uint32_t)ks));
+  asm volatile("s_load_dword %0, %1, %2" : "=s"(raw) : "s"(bs), "s"(off) : "memory");
+  return raw;
+}
+// raw >> lsh (the lane's byte in the low byte), after the caller's lgkmcnt(0): asm, so that it stays
+// behind that wait
+__device__ __forceinline__ int lane_byte(uint32_t raw, uint32_t lsh) {
+  int v;
+  asm volatile("v_lshrrev_b32_e64 %0, %1, %2" : "=v"(v) : "v"(lsh), "s"(raw));
+  return v;
+}
+// The MFMA scale operands of stage kt from the lane's block byte v (the operand reads the low byte
+// only), minus the segment's 2^-4 on a second slice.  The block bytes are >= 0x40
+// (ofr_f6_block_scales), so the subtraction stays inside the low byte.
+template <int NSEG>
+__device__ __forceinline__ void block_scales(int v, int kt, int nst, int& sa, int& sb) {
+  if constexpr (NSEG == 1) {
+    sa = v; sb = v;
+  } else {
+    sa = kt >= 2 * nst ? v - X2_SHIFT : v;
+    sb = (kt >= nst && kt < 2 * nst) ? v - X2_SHIFT : v;
+  }
+}
+// the stage of segment-relative index ks of stage kt (NSEG segments of nst stages)
+template <int NSEG>
+__device__ __forceinline__ int seg_stage(int kt, int nst) {
+  if constexpr (NSEG == 1) return kt;
+  else return kt - (kt >= 2 * nst ? 2 : (kt >= nst ? 1 : 0)) * nst;
+}
+
 template <int NSEG>
 __device__ __forceinline__ void seg_src(int kt, int nst, const char* G, const char* G2, const char* Q, const char* Q2,
                                         const char*& g, const char*& q, int& ks) {
@@ -87,17 +137,6 @@ __device__ __forceinline__ void seg_src(int kt, int nst, const char* G, const ch
     ks = kt - sg * nst;
     g = sg == 2 ? G2 : G;
     q = sg == 1 ? Q2 : Q;
-  }
-}
-
-// E8M0 block scales of stage kt's MFMAs (gallery operand A, query operand B)
-template <int NSEG>
-__device__ __forceinline__ void seg_scales(int kt, int nst, int& sa, int& sb) {
-  if constexpr (NSEG == 1) {
-    sa = SCALE_ONE; sb = SCALE_ONE;
-  } else {
-    sa = kt >= 2 * nst ? SCALE_X2 : SCALE_ONE;
-    sb = (kt >= nst && kt < 2 * nst) ? SCALE_X2 : SCALE_ONE;
   }
 }
 
@@ -205,7 +244,7 @@ struct Engine {
   template <int NSEG = 1>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
                                                   int nst, f32x16 (&acc)[4][CT], const char* G2 = nullptr,
-                                                  const char* Q2 = nullptr) {
+                                                  const char* Q2 = nullptr, const uint32_t* bs = nullptr) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
 #pragma unroll
@@ -223,10 +262,22 @@ struct Engine {
     };
     // branch-free: a stage past the end re-loads the last one onto itself (same bytes)
     const int last = NSEG * nst - 1;
-    int sa = SCALE_ONE, sb = SCALE_ONE;
     static_assert(NST == 3, "hand-off below assumes 3 stages");
 #pragma unroll
     for (int s = 0; s < NST; ++s) issue(s < last ? s : last);
+
+    // block scales: MFMA step j of a stage covers blocks 2 j + h of its four (the lane's half h)
+    const uint32_t lsh0 = 8u * (uint32_t)h, lsh1 = 8u * (uint32_t)(2 + h);
+    int sa[2], sb[2];
+    auto scales = [&](uint32_t raw, int kt, int (&xa)[2], int (&xb)[2]) {   // behind an lgkmcnt(0)
+      block_scales<NSEG>(lane_byte(raw, lsh0), kt, nst, xa[0], xb[0]);
+      block_scales<NSEG>(lane_byte(raw, lsh1), kt, nst, xa[1], xb[1]);
+    };
+    {
+      const uint32_t raw0 = sload_bscale(bs, seg_stage<NSEG>(0, nst));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      scales(raw0, 0, sa, sb);
+    }
 
     i32x8 ga[2][4], qb[2][CT];
     auto frags = [&](const char* st, int j) {
@@ -241,19 +292,24 @@ struct Engine {
 #pragma unroll
         for (int c = 0; c < CT; ++c)
           acc[i][c] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ga[j][i], qb[j][c], acc[i][c], 2, 2, 0,
-                                                                      sa, 0, sb);
+                                                                      sa[j], 0, sb[j]);
     };
 
     wait_vm<2 * IPW>();   // stage 0 landed; 1 and 2 may be in flight
     barrier();
     frags(smem, 0);
     for (int kt = 0; kt < last; ++kt) {
-      seg_scales<NSEG>(kt, nst, sa, sb);
+      // the next stage's block scales: a scalar load here, read after the barrier below (whose
+      // lgkmcnt(0) it joins), so the wait for it never drains fresh fragment reads
+      const uint32_t raw = sload_bscale(bs, seg_stage<NSEG>(kt + 1, nst));
       frags(smem + (kt % NST) * STAGE, 1);
       mfmas(0);
       interleave();
       wait_vm<IPW>();     // stage kt+1 landed; kt+2 may be in flight
       barrier();
+      int na[2], nb[2];
+      scales(raw, kt + 1, na, nb);
+      __builtin_amdgcn_sched_barrier(0);
       {
         const int nx = kt + NST;
         issue(nx < last ? nx : last);
@@ -262,8 +318,8 @@ struct Engine {
       mfmas(1);
       interleave();
       __builtin_amdgcn_sched_group_barrier(0x020, IPW, 0);
+      sa[0] = na[0]; sa[1] = na[1]; sb[0] = nb[0]; sb[1] = nb[1];
     }
-    seg_scales<NSEG>(last, nst, sa, sb);
     frags(smem + (last % NST) * STAGE, 1);
     mfmas(0);
     interleave();
@@ -319,9 +375,10 @@ struct Engine16 {
   template <int NSEG = 1>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
                                                   int nst, f32x4 (&acc)[NA][NB], const char* G2 = nullptr,
-                                                  const char* Q2 = nullptr) {
+                                                  const char* Q2 = nullptr, const uint32_t* bs = nullptr) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr = wave / WQ, wc = wave % WQ, r16 = lane & 15;
+    const uint32_t lsh = 8u * (uint32_t)(lane >> 4);   // the lane's 32-feature block of a stage
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll
@@ -341,7 +398,12 @@ struct Engine16 {
       Engine<8>::dma_buf4(g, gp, q, qp, nst, ks, smem + (s % NST) * STAGE);
     }
     i32x6 a[NA], b[NB];
-    int sa = SCALE_ONE, sb = SCALE_ONE;
+    int sa, sb;
+    {
+      const uint32_t raw0 = sload_bscale(bs, seg_stage<NSEG>(0, nst));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      block_scales<NSEG>(lane_byte(raw0, lsh), 0, nst, sa, sb);
+    }
     auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) { c = mfma(x, y, c, sa, sb); };
     auto readA = [&](const char* st, int i) { a[i] = frag16(st, wr * 128 + i * 16 + r16); };
     auto readB = [&](const char* st, int c) { b[c] = frag16(st + PANEL, wc * QW + c * 16 + r16); };
@@ -352,7 +414,7 @@ struct Engine16 {
 #pragma unroll
     for (int c = 0; c < NB; ++c) readB(smem, c);
     for (int kt = 0; kt < last; ++kt) {
-      seg_scales<NSEG>(kt, nst, sa, sb);
+      const uint32_t raw = sload_bscale(bs, seg_stage<NSEG>(kt + 1, nst));   // the next stage's block scales
       __builtin_amdgcn_sched_barrier(0);
       wait_vm<2 * IPW>();   // stage kt+1 landed (kt+2 may be in flight)
       __builtin_amdgcn_s_barrier();
@@ -364,12 +426,14 @@ struct Engine16 {
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       __builtin_amdgcn_sched_barrier(0);
-      // lgkmcnt(2): the refill is exactly two LDS instructions (frag16: ds_read_b128 + ds_read_b64, the
-      // part1 address opaque so they cannot be fused), and LDS returns in order, so at most those two
-      // may still be in flight and every read of the previous stage (all from the buffer re-filled
-      // below) is done.  Scalar loads sharing the counter can only make the wait stricter.
-      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      // Every read of the previous stage (all from the buffer re-filled below) must be done: with only
+      // the refill's two LDS reads in flight lgkmcnt(2) would do (round 2), but the next stage's block
+      // scales (a scalar load, out of order) share the counter, so this engine waits for all of them
+      // (the non-default sieve engine, OFR_F6_SHAPE=16, and its two-slice pass).
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      int na, nb;
+      block_scales<NSEG>(lane_byte(raw, lsh), kt + 1, nst, na, nb);
       __builtin_amdgcn_sched_barrier(0);
       {
         const int nx = kt + NST;
@@ -399,8 +463,9 @@ struct Engine16 {
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      sa = na;
+      sb = nb;
     }
-    seg_scales<NSEG>(last, nst, sa, sb);
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll
@@ -453,12 +518,14 @@ struct EngineW {
     __amdgpu_buffer_rsrc_t rg, rq;
     __amdgpu_buffer_rsrc_t rg2, rq2;   // the second-slice tiles (NSEG = 3, the two-slice tier f6x2)
     uint32_t gsrc[GPW];
+    const uint32_t* bs;                // column-block scales, one dword per stage (null: unit)
   };
 
   template <int W, int NSEG = 1>
   static __device__ __forceinline__ void feed_init(Feed& f, const char* G, int64_t N, const char* Q, int64_t qp,
                                                    int64_t nst, int64_t gt, const char* G2 = nullptr,
-                                                   const char* Q2 = nullptr) {
+                                                   const char* Q2 = nullptr, const uint32_t* bs = nullptr) {
+    f.bs = bs;
     const int64_t h0 = 3 * gt, p0 = h0 >> 1;
     const int64_t pb = nst * (int64_t)PANEL;                 // bytes per 256-row panel
     const int64_t rem = panels(N) * pb - p0 * pb;
@@ -557,12 +624,18 @@ struct EngineW {
 
   // NSEG: segments of nst stages (seg_src): 1 = the fp6 tier; 3 = the two-slice tier f6x2, whose
   // stages of segment 1 / 2 read the query / gallery second slices (f.rq2 / f.rg2) with block scale
-  // 2^-4 on that operand (seg_scales)
+  // 2^-4 on that operand (block_scales)
   template <int W, int NSEG = 1>
   static __device__ __forceinline__ void mainloop(const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
     constexpr int WR = W >> 1, WC = W & 1;
-    int sc = SCALE_ONE;
-    asm volatile("" : "+v"(sc));
+    // block scales of the current stage (sa: gallery operand, sb: query; NSEG = 1 uses sa for both)
+    const uint32_t lsh = 8u * ((threadIdx.x & 63) >> 4);   // the lane's 32-feature block of a stage
+    int sa, sb;
+    {
+      const uint32_t raw0 = sload_bscale(f.bs, seg_stage<NSEG>(0, nst));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      block_scales<NSEG>(lane_byte(raw0, lsh), 0, nst, sa, sb);
+    }
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll
@@ -620,18 +693,19 @@ struct EngineW {
       const Bases ac = abase(g0), an = abase(g1), bn = bbase(q1);
       const uint32_t k2 = kso(s + 2), k3 = kso(s + 3);
       const __amdgpu_buffer_rsrc_t rg2s = rgs(s + 2), rq2s = rqs(s + 2), rg3s = rgs(s + 3);
-      int sa = SCALE_ONE, sb = SCALE_ONE;
-      if constexpr (NSEG == 3) {
-        seg_scales<NSEG>(s, nst, sa, sb);
-        asm volatile("" : "+v"(sa), "+v"(sb));
-      }
+      // the next stage's block scales: a scalar load in row 2 (behind barrier A), turned into the
+      // lanes' operands right behind barrier B, whose lgkmcnt(0) the wait for it joins (no fresh
+      // fragment read is in flight there); taken over at the end of the stage
+      uint32_t raw = 0;
+      int na = 0, nb = 0;
       auto row = [&](auto ii) {
         constexpr int i = decltype(ii)::value;
         constexpr bool AG = i < NAA;
         auto mm = [&](const i32x6& x, const i32x6& y, f32x4& c) {
-          if constexpr (NSEG == 1) mfma<AG>(x, y, c, sc);
+          if constexpr (NSEG == 1) mfma<AG>(x, y, c, sa);
           else mfma2<AG>(x, y, c, sa, sb);
         };
+        if constexpr (i == 2) raw = sload_bscale(f.bs, seg_stage<NSEG>(s < last ? s + 1 : last, nst));
         if constexpr (i == 1) {              // barrier A: Q(s) consumed by every wave
           // Q(s)'s reads (row 11 of s - 1) are older than row 0's gallery read, the only one allowed in flight
           asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
@@ -642,6 +716,7 @@ struct EngineW {
           wait_vm<GPW + QPW>();
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
+          block_scales<NSEG>(lane_byte(raw, lsh), s < last ? s + 1 : last, nst, na, nb);
           __builtin_amdgcn_sched_barrier(0);
         }
         // G(s+2) into G(s-1)'s slot (= g2's ring position), Q(s+2) into Q(s)'s (q0) -- rows 0-6, each copy
@@ -694,6 +769,8 @@ struct EngineW {
       g0 = g1; g1 = g2; g2 = gt_;
       const uint32_t qt_ = q0;
       q0 = q1; q1 = qt_;
+      sa = na;
+      sb = nb;
       if (s == last) wait_drain();
       __builtin_amdgcn_sched_barrier(0);
     }

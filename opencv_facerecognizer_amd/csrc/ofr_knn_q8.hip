@@ -68,6 +68,9 @@ struct TileArgs {
   const int8_t* G2;
   const int8_t* Q2;
   int serp;   // wide sieve pass: odd tile groups walk the query tiles backwards (tile_kernel_f6w)
+  // fp6 tiers: column-block scales, one dword of 4 E8M0 bytes per 128-feature stage (null: unit;
+  // ofr_f6_block_scales), the same for the gallery and the query tiles
+  const uint32_t* bs;
 };
 
 // ---- keys of the tile epilogue (ofr_keys.h: order-preserving u32 keys, med3 key lists) ----
@@ -252,7 +255,7 @@ __global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
   f6t::f32x16 acc[4][CT];
   E::template mainloop<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
                              p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
-                             reinterpret_cast<const char*>(p.Q2));
+                             reinterpret_cast<const char*>(p.Q2), p.bs);
   auto cval = [&](int rt, auto ctc, int r) {
     constexpr int ct = decltype(ctc)::value;
     return acc[rt][ct][r];
@@ -328,7 +331,7 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
   f6t::f32x4 acc[8][4];
   E::mainloop<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG,
-                    acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2));
+                    acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2), p.bs);
   // sieve operands after the main loop (the 16x16 engine needs every register in it)
   float ga = __builtin_inff(), gs = 0.f, sq2[4], th[4];
   if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
@@ -359,7 +362,7 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
   E::Feed f;
   E::feed_init<W, NSEG>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ,
                         p.nk / NSEG, g0 / E::TGW, reinterpret_cast<const char*>(p.G2),
-                        reinterpret_cast<const char*>(p.Q2));
+                        reinterpret_cast<const char*>(p.Q2), p.bs);
   E::mainloop<W, NSEG>(f, p.nk / NSEG, acc);
   float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
   uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
@@ -507,8 +510,12 @@ __global__ void __launch_bounds__(512) stream_kernel_f6(TileArgs p) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (k0 + u < nsteps)
-        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[u], b[u], acc, 2, 2, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+      if (k0 + u < nsteps) {
+        // 64-feature step k = 2 stage + j: the lane's block is 2 j + h of the stage's four
+        const int k = k0 + u;
+        const int sc = (int)(p.bs[k >> 1] >> (8u * (uint32_t)(2 * (k & 1) + h)));
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[u], b[u], acc, 2, 2, 0, sc, 0, sc);
+      }
   }
   __syncthreads();
   const int nvalid = p.N - g0 < TG ? (int)(p.N - g0) : TG;
@@ -993,17 +1000,25 @@ __device__ __forceinline__ uint32_t e2m3_code(double r, double& q) {
 // bytes and scale.  Stats of f6x2: a = s (|v1| + 2^-4 |v2|) >= |x~| (it also bounds the sum of
 // |products| the fp32 accumulation error is proportional to), e = |x - x~|, t = s 2^-4 |v2| (the
 // dropped 2^-8 x2.y2 term is at most t_q t_g).
+//
+// Column-block scales (bscale, null: unit; ofr_f6_block_scales): feature k of every row is quantized
+// as x / 2^e with e = bscale[k / 32] - 127, so the row scale s = max_k |x_k| / 2^e_k / 7.5 and
+// x~_k = s 2^e_k v_k (the MFMA applies 2^e_k to both operands of block k / 32).  The stats are of x~
+// in the original coordinates: a = ||x~||, e = ||x - x~|| (f6x2: a = s (||v1||' + 2^-4 ||v2||') with
+// ||v||' = (sum_k 2^2e_k v_k^2)^1/2 -- it bounds ||x~|| and the sum of |products| alike, t likewise).
 template <bool X2>
 __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_t ldx, int64_t d, int64_t nst,
                                                           int64_t row0, char* tiles, float* scale, double* stats,
-                                                          char* tiles2) {
+                                                          char* tiles2, const uint8_t* bscale) {
   __shared__ float redf[4];
   __shared__ double red[4][3];
   const int64_t row = row0 + blockIdx.x;   // destination row (X row blockIdx.x)
   const float* x = X + (int64_t)blockIdx.x * ldx;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // 2^-e_B, exact (e_B in [-63, 0]: a normal power of two)
+  auto binv = [&](int64_t g) { return bscale ? __builtin_ldexpf(1.0f, 127 - (int)bscale[g]) : 1.0f; };
   float mx = 0.f;
-  for (int64_t i = threadIdx.x; i < d; i += blockDim.x) mx = fmaxf(mx, fabsf(x[i]));
+  for (int64_t i = threadIdx.x; i < d; i += blockDim.x) mx = fmaxf(mx, fabsf(x[i]) * binv(i >> 5));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
   if (lane == 0) redf[wave] = mx;
@@ -1024,6 +1039,9 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
   const int rl = (int)(row & 255);
   for (int64_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
     uint32_t w[6] = {0, 0, 0, 0, 0, 0}, w2[6] = {0, 0, 0, 0, 0, 0};
+    // this 32-feature group is column block g: x / (s 2^e) and s 2^e v, both exact power-of-two rescalings
+    const double bi = (double)binv(g), bs = 1.0 / bi;
+    const double inv_b = inv_sd * bi, sd_b = sd * bs;
     float xg[32];
     if (vec4 && g * 32 + 32 <= d) {
 #pragma unroll
@@ -1041,15 +1059,15 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
       if (k < d) {
         const double xv = (double)xg[e];
         double qv;
-        const uint32_t c = e2m3_code(xv * inv_sd, qv);
-        double xt = sd * qv;   // exact: 24-bit s times a 4-bit significand
+        const uint32_t c = e2m3_code(xv * inv_b, qv);
+        double xt = sd_b * qv;   // exact: 24-bit s times a 4-bit significand and a power of two
         const int bit = 6 * e;
         if constexpr (X2) {
           double qv2;
-          const uint32_t c2 = e2m3_code((xv - xt) * inv_sd * 16.0, qv2);
-          sa += qv * qv;
-          s2 += qv2 * qv2;
-          xt += sd * qv2 * 0.0625;   // exact (a 28-bit significand at most)
+          const uint32_t c2 = e2m3_code((xv - xt) * inv_b * 16.0, qv2);
+          sa += bs * bs * qv * qv;
+          s2 += bs * bs * qv2 * qv2;
+          xt += sd_b * qv2 * 0.0625;   // exact (a 28-bit significand at most)
           w2[bit >> 5] |= c2 << (bit & 31);
           if ((bit & 31) > 26) w2[(bit >> 5) + 1] |= c2 >> (32 - (bit & 31));
         } else {
@@ -1143,10 +1161,78 @@ __global__ void __launch_bounds__(256) maxima_kernel(const double* stats, const 
     for (int c = 0; c < 4; ++c) gmax[c] = fmax(fmax(red[0][c], red[1][c]), fmax(red[2][c], red[3][c]));
 }
 
+// Column-block statistics of the fp6 tiers (ofr_f6_block_sumsq): sums[b] += sum over the rows of
+// x_k^2 for the 32 features k of block b (fp64 atomics, one per block and workgroup).
+__global__ void __launch_bounds__(256) block_sumsq_kernel(const float* X, int64_t R, int64_t d, int64_t ldx,
+                                                          int64_t rows_per_wg, double* sums) {
+  const int64_t nb = (d + 31) / 32;
+  const int64_t r0 = blockIdx.y * rows_per_wg, r1 = r0 + rows_per_wg < R ? r0 + rows_per_wg : R;
+  for (int64_t b = blockIdx.x * 8 + (threadIdx.x >> 5); b < nb && b < (int64_t)(blockIdx.x + 1) * 8; b += 8) {
+    const int64_t k = b * 32 + (threadIdx.x & 31);
+    double acc = 0.0;
+    if (k < d)
+      for (int64_t r = r0; r < r1; ++r) {
+        const double v = (double)X[r * ldx + k];
+        acc += v * v;
+      }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 32);
+    if ((threadIdx.x & 31) == 0) atomicAdd(sums + b, acc);
+  }
+}
+
+// sums[nb] -> E8M0 bytes [4 nst]: e_b = rint(log2(rms_b / rms_max)) clamped to [-63, 0] (block 0 of the
+// largest mean square gets 2^0), 127 (2^0) for empty blocks and the padding blocks past d.
+__global__ void __launch_bounds__(256) block_scales_kernel(const double* sums, int64_t nb, int64_t npad,
+                                                           uint8_t* bscale) {
+  __shared__ double red[4];
+  double m = 0.0;
+  for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) m = fmax(m, sums[b]);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  for (int64_t b = threadIdx.x; b < npad; b += blockDim.x) {
+    int e = 0;
+    if (b < nb && sums[b] > 0.0 && m > 0.0) {
+      const double l = 0.5 * log2(sums[b] / m);
+      e = (int)rint(l);
+      e = e < -63 ? -63 : (e > 0 ? 0 : e);
+    }
+    bscale[b] = (uint8_t)(127 + e);
+  }
+}
+
+// Unit column-block scales (E8M0 2^0 in every byte) for callers that pass none: the engines always
+// load a stage's dword (one code path), from this table when bscale is null.
+constexpr int UNIT_BS_STAGES = 4096;   // d <= 524,288 without a caller table
+struct UnitScales {
+  uint32_t v[UNIT_BS_STAGES];
+  constexpr UnitScales() : v() {
+    for (int i = 0; i < UNIT_BS_STAGES; ++i) v[i] = 0x7f7f7f7fu;
+  }
+};
+__device__ UnitScales unit_bs_table = UnitScales();
+
 }  // namespace q8s
 }  // namespace ofr
 
 using namespace ofr;
+
+// the unit table's address on the current device (a __device__ variable exists once per device)
+static const uint32_t* unit_bscale() {
+  static const uint32_t* addr[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!addr[dev]) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(q8s::unit_bs_table)) != hipSuccess) return nullptr;
+    addr[dev] = (const uint32_t*)a;
+  }
+  return addr[dev];
+}
 
 static int64_t q8_min_ld(int slices, int64_t d) { return slices == 1 ? round_up(d, 128) : 2 * round_up(d, 64); }
 
@@ -1238,18 +1324,23 @@ extern "C" size_t ofr_f6_tiles_bytes(int64_t R, int64_t d) {
   return R <= 0 || d <= 0 ? 0 : (size_t)f6t::tiles_bytes(R, d);
 }
 
+// bscale (null: unit) must be 4-byte aligned and hold 4 * ceil(d / 128) bytes (ofr_f6_block_scales)
+static bool bscale_ok(const uint8_t* bscale) { return ((uintptr_t)bscale & 3) == 0; }
+
 extern "C" int ofr_f6_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx,
-                                       int64_t row0, void* tiles, size_t tiles_bytes, float* scale, double* stats) {
+                                       int64_t row0, void* tiles, size_t tiles_bytes, float* scale, double* stats,
+                                       const uint8_t* bscale) {
   OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d && row0 >= 0, "ofr_f6_quantize_rows_at: bad sizes");
   if (R == 0) return OFR_OK;
   OFR_CHECK_ARG(X && tiles && scale && stats, "ofr_f6_quantize_rows_at: null pointer");
   OFR_CHECK_ARG(row0 + R < 0x7fffffffLL, "ofr_f6_quantize_rows_at: too many rows");
   OFR_CHECK_ARG(tiles_bytes >= ofr_f6_tiles_bytes(row0 + R, d), "ofr_f6_quantize_rows_at: tile buffer too small");
   OFR_CHECK_ARG((uintptr_t)tiles % 16 == 0, "ofr_f6_quantize_rows_at: tiles must be 16-byte aligned");
+  OFR_CHECK_ARG(bscale_ok(bscale), "ofr_f6_quantize_rows_at: bscale must be 4-byte aligned");
   hipStream_t st = (hipStream_t)stream;
   const int64_t nst = f6t::stages(d);
   hipLaunchKernelGGL(q8s::quantize_f6_kernel<false>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
-                     (char*)tiles, scale, stats, nullptr);
+                     (char*)tiles, scale, stats, nullptr, bscale);
   OFR_LAUNCH_CHECK("f6 quantize_kernel");
   const int64_t end = row0 + R;
   if (end % 256) {
@@ -1261,7 +1352,7 @@ extern "C" int ofr_f6_quantize_rows_at(void* stream, const float* X, int64_t R, 
 
 extern "C" int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx,
                                          int64_t row0, void* tiles1, void* tiles2, size_t tiles_bytes, float* scale,
-                                         double* stats) {
+                                         double* stats, const uint8_t* bscale) {
   OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d && row0 >= 0, "ofr_f6x2_quantize_rows_at: bad sizes");
   if (R == 0) return OFR_OK;
   OFR_CHECK_ARG(X && tiles2 && scale && stats, "ofr_f6x2_quantize_rows_at: null pointer");
@@ -1269,10 +1360,11 @@ extern "C" int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R
   OFR_CHECK_ARG(tiles_bytes >= ofr_f6_tiles_bytes(row0 + R, d), "ofr_f6x2_quantize_rows_at: tile buffer too small");
   OFR_CHECK_ARG(((uintptr_t)tiles1 | (uintptr_t)tiles2) % 16 == 0,
                 "ofr_f6x2_quantize_rows_at: tiles must be 16-byte aligned");
+  OFR_CHECK_ARG(bscale_ok(bscale), "ofr_f6x2_quantize_rows_at: bscale must be 4-byte aligned");
   hipStream_t st = (hipStream_t)stream;
   const int64_t nst = f6t::stages(d);
   hipLaunchKernelGGL(q8s::quantize_f6_kernel<true>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
-                     (char*)tiles1, scale, stats, (char*)tiles2);
+                     (char*)tiles1, scale, stats, (char*)tiles2, bscale);
   OFR_LAUNCH_CHECK("f6x2 quantize_kernel");
   const int64_t end = row0 + R;
   if (end % 256) {
@@ -1294,43 +1386,66 @@ extern "C" int ofr_q8_maxima(void* stream, const double* stats, const float* aux
 
 extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
                                     size_t tiles_bytes, float* scale, double* stats, const float* aux,
-                                    double* maxima) {
-  const int rc = ofr_f6_quantize_rows_at(stream, X, R, d, ldx, 0, tiles, tiles_bytes, scale, stats);
+                                    double* maxima, const uint8_t* bscale) {
+  const int rc = ofr_f6_quantize_rows_at(stream, X, R, d, ldx, 0, tiles, tiles_bytes, scale, stats, bscale);
   if (rc || R == 0 || !maxima) return rc;
   return ofr_q8_maxima(stream, stats, aux, R, maxima);
 }
 
 extern "C" int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles1,
                                       void* tiles2, size_t tiles_bytes, float* scale, double* stats, const float* aux,
-                                      double* maxima) {
-  const int rc = ofr_f6x2_quantize_rows_at(stream, X, R, d, ldx, 0, tiles1, tiles2, tiles_bytes, scale, stats);
+                                      double* maxima, const uint8_t* bscale) {
+  const int rc = ofr_f6x2_quantize_rows_at(stream, X, R, d, ldx, 0, tiles1, tiles2, tiles_bytes, scale, stats,
+                                           bscale);
   if (rc || R == 0 || !maxima) return rc;
   return ofr_q8_maxima(stream, stats, aux, R, maxima);
 }
 
 extern "C" int64_t ofr_f6_sample_step(void) { return q8s::SAMPLE_STEP; }
 
+extern "C" int ofr_f6_block_sumsq(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, double* sums) {
+  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d, "ofr_f6_block_sumsq: bad sizes");
+  if (R == 0) return OFR_OK;
+  OFR_CHECK_ARG(X && sums, "ofr_f6_block_sumsq: null pointer");
+  const int64_t nb = cdiv(d, 32), rows = 4096;
+  OFR_CHECK_ARG(cdiv(R, rows) < 65536, "ofr_f6_block_sumsq: too many rows for one call");
+  hipLaunchKernelGGL(q8s::block_sumsq_kernel, dim3((unsigned)cdiv(nb, 8), (unsigned)cdiv(R, rows)), dim3(256), 0,
+                     (hipStream_t)stream, X, R, d, ldx, rows, sums);
+  OFR_LAUNCH_CHECK("f6 block_sumsq_kernel");
+  return OFR_OK;
+}
+
+extern "C" int ofr_f6_block_scales(void* stream, const double* sums, int64_t d, uint8_t* bscale) {
+  OFR_CHECK_ARG(d >= 1 && sums && bscale, "ofr_f6_block_scales: bad arguments");
+  OFR_CHECK_ARG(bscale_ok(bscale), "ofr_f6_block_scales: bscale must be 4-byte aligned");
+  hipLaunchKernelGGL(q8s::block_scales_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, sums, cdiv(d, 32),
+                     4 * f6t::stages(d), bscale);
+  OFR_LAUNCH_CHECK("f6 block_scales_kernel");
+  return OFR_OK;
+}
+
 extern "C" int ofr_f6x2_sample_rows(void* stream, const float* X, int64_t N, int64_t ldx, int64_t d, int64_t j0,
-                                    int64_t j1, void* tiles2, size_t tiles_bytes, float* scale, double* stats) {
+                                    int64_t j1, void* tiles2, size_t tiles_bytes, float* scale, double* stats,
+                                    const uint8_t* bscale) {
   OFR_CHECK_ARG(j0 >= 0 && j1 >= j0 && d >= 1 && ldx >= d && N >= 0, "ofr_f6x2_sample_rows: bad sizes");
   OFR_CHECK_ARG(j1 <= cdiv(N, q8s::SAMPLE_STEP), "ofr_f6x2_sample_rows: j1 past the gallery's sample (ceil(N / 64))");
   if (j1 == j0) return OFR_OK;
   OFR_CHECK_ARG(X, "ofr_f6x2_sample_rows: null pointer");
   OFR_CHECK_ARG(ldx < INT64_MAX / q8s::SAMPLE_STEP, "ofr_f6x2_sample_rows: leading dimension too large");
   return ofr_f6x2_quantize_rows_at(stream, X + j0 * q8s::SAMPLE_STEP * ldx, j1 - j0, d, ldx * q8s::SAMPLE_STEP, j0,
-                                   nullptr, tiles2, tiles_bytes, scale, stats);
+                                   nullptr, tiles2, tiles_bytes, scale, stats, bscale);
 }
 
 extern "C" int ofr_f6_sample_rows(void* stream, const float* X, int64_t N, int64_t ldx, int64_t d, int64_t j0,
                                   int64_t j1, const float* aux, void* tiles, size_t tiles_bytes, float* scale,
-                                  double* stats, float* saux) {
+                                  double* stats, float* saux, const uint8_t* bscale) {
   OFR_CHECK_ARG(j0 >= 0 && j1 >= j0 && d >= 1 && ldx >= d && N >= 0, "ofr_f6_sample_rows: bad sizes");
   OFR_CHECK_ARG(j1 <= cdiv(N, q8s::SAMPLE_STEP), "ofr_f6_sample_rows: j1 past the gallery's sample (ceil(N / 64))");
   if (j1 == j0) return OFR_OK;
   OFR_CHECK_ARG(X && aux && saux, "ofr_f6_sample_rows: null pointer");
   OFR_CHECK_ARG(ldx < INT64_MAX / q8s::SAMPLE_STEP, "ofr_f6_sample_rows: leading dimension too large");
   const int rc = ofr_f6_quantize_rows_at(stream, X + j0 * q8s::SAMPLE_STEP * ldx, j1 - j0, d,
-                                         ldx * q8s::SAMPLE_STEP, j0, tiles, tiles_bytes, scale, stats);
+                                         ldx * q8s::SAMPLE_STEP, j0, tiles, tiles_bytes, scale, stats, bscale);
   if (rc) return rc;
   hipLaunchKernelGGL(q8s::sample_aux_kernel, dim3((unsigned)cdiv(j1 - j0, 256)), dim3(256), 0, (hipStream_t)stream,
                      aux, j0, j1, q8s::SAMPLE_STEP, saux);
@@ -1460,17 +1575,18 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
                        size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2 = nullptr,
-                       const void* Gt2 = nullptr, const F6Sample* smp = nullptr);
+                       const void* Gt2 = nullptr, const F6Sample* smp = nullptr, const uint8_t* bscale = nullptr);
 
 extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                           const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
                           int64_t d, const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                           int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
-                          void* workspace, size_t workspace_bytes) {
+                          void* workspace, size_t workspace_bytes, const uint8_t* bscale) {
   OFR_CHECK_ARG(phases >= 1 && phases <= 15,
                 "ofr_knn_f6: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
-                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr);
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, nullptr, nullptr, nullptr,
+                     bscale);
 }
 
 extern "C" int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
@@ -1478,7 +1594,8 @@ extern "C" int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int6
                                   int64_t d, const void* Gt, const float* gscale, const float* aux,
                                   const double* gmax, int k, int64_t index_base, double* out_d, int64_t* out_i,
                                   int* cert, double* bound, const void* St, int64_t Ns, const float* sscale,
-                                  const float* saux, void* workspace, size_t workspace_bytes) {
+                                  const float* saux, void* workspace, size_t workspace_bytes,
+                                  const uint8_t* bscale) {
   OFR_CHECK_ARG(phases >= 1 && phases <= 15,
                 "ofr_knn_f6_sampled: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
   OFR_CHECK_ARG(St && sscale && saux, "ofr_knn_f6_sampled: null sample pointer");
@@ -1486,7 +1603,7 @@ extern "C" int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int6
   OFR_CHECK_ARG((uintptr_t)St % 16 == 0, "ofr_knn_f6_sampled: sample tiles must be 16-byte aligned");
   const F6Sample smp{St, Ns, sscale, saux, nullptr};
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
-                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, nullptr, nullptr, &smp);
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, nullptr, nullptr, &smp, bscale);
 }
 
 extern "C" int ofr_knn_f6x2_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
@@ -1495,7 +1612,8 @@ extern "C" int ofr_knn_f6x2_sampled(void* stream, int phases, const float* Q, in
                                     const float* gscale, const float* aux, const double* gmax, int k,
                                     int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
                                     const void* St, const void* St2, int64_t Ns, const float* sscale,
-                                    const float* saux, void* workspace, size_t workspace_bytes) {
+                                    const float* saux, void* workspace, size_t workspace_bytes,
+                                    const uint8_t* bscale) {
   OFR_CHECK_ARG(phases >= 1 && phases <= 15,
                 "ofr_knn_f6x2_sampled: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
   OFR_CHECK_ARG(Qt2 && Gt2, "ofr_knn_f6x2_sampled: null second-slice tiles");
@@ -1506,20 +1624,21 @@ extern "C" int ofr_knn_f6x2_sampled(void* stream, int phases, const float* Q, in
   OFR_CHECK_ARG(((uintptr_t)St | (uintptr_t)St2) % 16 == 0, "ofr_knn_f6x2_sampled: sample tiles must be 16-byte aligned");
   const F6Sample smp{St, Ns, sscale, saux, St2};
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
-                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, Qt2, Gt2, &smp);
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, Qt2, Gt2, &smp, bscale);
 }
 
 extern "C" int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                             const void* Qt2, const float* qscale, const double* qstats, const float* G, int64_t N,
                             int64_t ldg, int64_t d, const void* Gt, const void* Gt2, const float* gscale,
                             const float* aux, const double* gmax, int k, int64_t index_base, double* out_d,
-                            int64_t* out_i, int* cert, double* bound, void* workspace, size_t workspace_bytes) {
+                            int64_t* out_i, int* cert, double* bound, void* workspace, size_t workspace_bytes,
+                            const uint8_t* bscale) {
   OFR_CHECK_ARG(phases >= 1 && phases <= 15,
                 "ofr_knn_f6x2: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
   OFR_CHECK_ARG(Qt2 && Gt2, "ofr_knn_f6x2: null second-slice tiles");
   if (B >= 1 && B <= 32) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6x2: needs more than 32 queries (the sieve pass)");
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
-                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, Qt2, Gt2);
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, Qt2, Gt2, nullptr, bscale);
 }
 
 extern "C" int ofr_knn_f6_merge_pruned(void* stream, int stage, const float* Q, int64_t B, int64_t ldq,
@@ -1539,7 +1658,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
                        size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2, const void* Gt2,
-                       const F6Sample* smp) {
+                       const F6Sample* smp, const uint8_t* bscale) {
   const bool two = Gt2 != nullptr;   // the two-slice tier f6x2: three segments of stages (f6t::seg_src)
   OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_f6: bad sizes (empty galleries use ofr_knn_f32)");
   if (k < 1 || k > q8s::KC) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6: k must be in [1, 16]");
@@ -1550,6 +1669,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   OFR_CHECK_ARG(((uintptr_t)Qt | (uintptr_t)Gt | (uintptr_t)Qt2 | (uintptr_t)Gt2 | (uintptr_t)workspace) % 16 == 0,
                 "ofr_knn_f6: tiles and workspace must be 16-byte aligned");
   OFR_CHECK_ARG(!two || B > 32, "ofr_knn_f6x2: needs more than 32 queries");
+  OFR_CHECK_ARG(bscale_ok(bscale), "ofr_knn_f6: bscale must be 4-byte aligned");
   // the sieve's per-query count reaches at most cap + 1 + N (saturating overflow + one per row)
   OFR_CHECK_ARG(N < 0x7fffffffLL - 2 * q8s::SIEVE_CAP, "ofr_knn_f6: N too large for one shard");
   OFR_CHECK_ARG(workspace_bytes >= ofr_knn_f6_workspace_bytes(B, N), "ofr_knn_f6: workspace too small");
@@ -1560,6 +1680,13 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   a.Q = (const int8_t*)Qt; a.B = B; a.qscale = qscale;
   a.nk = (int)f6t::stages(d) * (two ? 3 : 1);
   a.G2 = (const int8_t*)Gt2; a.Q2 = (const int8_t*)Qt2;
+  a.bs = reinterpret_cast<const uint32_t*>(bscale);
+  if (!a.bs) {
+    if (f6t::stages(d) > q8s::UNIT_BS_STAGES)
+      return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6: d > 524288 needs a column-block scale table (bscale)");
+    a.bs = unit_bscale();
+    if (!a.bs) return fail(OFR_E_DEVICE, "ofr_knn_f6: unit block-scale table not found on the device");
+  }
   a.cand = reinterpret_cast<Cand*>(workspace);
   a.ntq = f6t::panels(B);
   a.ntg = f6t::panels(N);

@@ -423,6 +423,52 @@ class LDA(_DeviceProjMixin, AbstractFeature):
         return "LDA (num_components=%d)" % (self._num_components)
 
 
+def fisherfaces_device(Xd, D, y, num_components=0):
+    """The device pipeline of ``Fisherfaces.compute`` (feature.py:211-229) on resident uint8 faces
+    Xd [n][>= D] with labels y (0..c-1): PCA(n - c) then LDA(num_components), W = P . L.  Returns
+    (LDA eigenvalues fp64 host [m], W device fp64 [D][m], m, regime); nothing of the faces or of W
+    leaves the device.  Regimes by what PCA keeps (training.py): pixel / gram / cov."""
+    from .. import training
+    y = np.asarray(y)
+    lay = training.Layout(y, Xd.device)
+    n, c = lay.n, lay.c
+    k = n - c                                              # PCA(n - c), feature.py:219 / :88-89
+    if k <= 0 or k > n - 1:
+        k = n - 1
+    k = min(k, D, n)                                       # columns of the economy SVD
+    m = num_components                                     # LDA(num_components), feature.py:155-158
+    if m <= 0 or m > c - 1:
+        m = c - 1
+    if k >= D:
+        # PCA keeps every pixel dimension (a rotation): LDA in pixel space, W = V directly
+        regime = "pixel"
+        Sw, Sb = training.finite("pixel_scatter", *training.pixel_scatter(training.pixel_pieces(Xd, D, lay),
+                                                                          lay.counts, n))
+        evals, Wd = lda_eigen(Sw, Sb, m, device_out=True)
+        del Sw, Sb
+    elif n <= D:
+        # n x n Gram of the centred faces: U_k = XC^T V_k / sigma_k, features V_k sigma_k
+        regime = "gram"
+        evals, Wd = training.fisher_gram(Xd, D, lay, y, k, m)
+    else:
+        # D x D covariance: P = leading k eigenvectors, features XC P, W = P L
+        regime = "cov"
+        pieces = training.pixel_pieces(Xd, D, lay)
+        lam, Pd = training.finite("eigh_desc", *training.eigh_desc(
+            training.finite("covariance", training.covariance(pieces, n)), k))
+        del pieces
+        Pd = Pd.contiguous()
+        mu = training.mean_image(Xd, D, lay)
+        shift = _device.gemm_f64(mu.reshape(1, -1).contiguous(), Pd).reshape(-1)
+        Fd = _device.Projection(Wt_device=Pd.t().contiguous(), D=D).project(Xd, shift64=shift, f64=True)
+        Sw, Sb = training.finite("feature_scatter", *training.feature_scatter(Fd, y))
+        del Fd
+        evals, L = lda_eigen(Sw, Sb, m)
+        L32 = np.asarray(L, dtype=np.float32).astype(np.float64)          # feature.py:176
+        Wd = _device.gemm_f64(Pd, _device.f64_dev(L32))                      # feature.py:229
+    return evals, Wd, m, regime
+
+
 class Fisherfaces(_DeviceProjMixin, AbstractFeature):
     """feature.py:206-260."""
 
@@ -438,43 +484,7 @@ class Fisherfaces(_DeviceProjMixin, AbstractFeature):
         Xd, D, kind = _device_rows(X)
         if kind != "u8":
             return self._compute_chain(X, y)
-        from .. import training
-        lay = training.Layout(y, Xd.device)
-        n, c = lay.n, lay.c
-        k = n - c                                              # PCA(n - c), feature.py:219 / :88-89
-        if k <= 0 or k > n - 1:
-            k = n - 1
-        k = min(k, D, n)                                       # columns of the economy SVD
-        m = self._num_components                               # LDA(num_components), feature.py:155-158
-        if m <= 0 or m > c - 1:
-            m = c - 1
-        if k >= D:
-            # PCA keeps every pixel dimension (a rotation): LDA in pixel space, W = V directly
-            self._regime = "pixel"
-            Sw, Sb = training.finite("pixel_scatter", *training.pixel_scatter(training.pixel_pieces(Xd, D, lay),
-                                                                              lay.counts, n))
-            evals, Wd = lda_eigen(Sw, Sb, m, device_out=True)
-            del Sw, Sb
-        elif n <= D:
-            # n x n Gram of the centred faces: U_k = XC^T V_k / sigma_k, features V_k sigma_k
-            self._regime = "gram"
-            evals, Wd = training.fisher_gram(Xd, D, lay, y, k, m)
-        else:
-            # D x D covariance: P = leading k eigenvectors, features XC P, W = P L
-            self._regime = "cov"
-            pieces = training.pixel_pieces(Xd, D, lay)
-            lam, Pd = training.finite("eigh_desc", *training.eigh_desc(
-                training.finite("covariance", training.covariance(pieces, n)), k))
-            del pieces
-            Pd = Pd.contiguous()
-            mu = training.mean_image(Xd, D, lay)
-            shift = _device.gemm_f64(mu.reshape(1, -1).contiguous(), Pd).reshape(-1)
-            Fd = _device.Projection(Wt_device=Pd.t().contiguous(), D=D).project(Xd, shift64=shift, f64=True)
-            Sw, Sb = training.finite("feature_scatter", *training.feature_scatter(Fd, y))
-            del Fd
-            evals, L = lda_eigen(Sw, Sb, m)
-            L32 = np.asarray(L, dtype=np.float32).astype(np.float64)          # feature.py:176
-            Wd = _device.gemm_f64(Pd, _device.f64_dev(L32))                      # feature.py:229
+        evals, Wd, m, self._regime = fisherfaces_device(Xd, D, y, self._num_components)
         self._eigenvalues = np.array(evals, dtype=np.float32, copy=True)      # :226-227 (LDA's, float32)
         self._num_components = m
         self._eigenvectors = np.asmatrix(Wd.cpu().numpy())

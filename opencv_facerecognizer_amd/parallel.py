@@ -247,6 +247,16 @@ def allreduce_sum(tensors, group=None):
     return tensors
 
 
+def share_block_scales(gallery, group=None):
+    """Column-block scales of a sharded gallery's fp6 tiers from the block sums of squares of ALL its
+    rows (one all-reduce of ceil(d / 32) fp64 values): every rank then quantizes its shard and its
+    share of a query batch alike, as the all-gathered fp6 query panels require (bench.py's sharded
+    preparation).  Before the fp6 tiers are built."""
+    sums = gallery.block_sums()
+    allreduce_sum([sums], group)
+    return gallery.set_block_scales(sums)
+
+
 def gather_ragged_rows(x, group=None):
     """All-gather row blocks of different lengths (dim 0), rank-major: pads every block to the longest
     one for the collective and trims it again."""
@@ -440,6 +450,7 @@ class DeviceComm:
                 s.G, s.N, s.ldg, s.Gt = g.G.data_ptr(), g.N, g.ld, t["Gs"].data_ptr()
                 s.gscale, s.aux, s.gmax = t["scale"].data_ptr(), g.aux.data_ptr(), t["gmax"].data_ptr()
                 s.index_base = int(getattr(g, "index_base", 0))
+                s.bscale = g.bscale.data_ptr() if g.bscale is not None else None   # the shard's (and qq's)
                 s.workspace, s.workspace_bytes = ws.data_ptr(), nbytes
                 s.out_d, s.out_i, s.cert = out_d.data_ptr(), out_i.data_ptr(), cert.data_ptr()
                 if g.row_sample():                        # the sieve thresholds from the shard's row sample

@@ -26,13 +26,16 @@ class IdentityBank:
     """Caches coarse grids of all identities on the device for fast batch generation."""
 
     def __init__(self, n_ids, H, W, seed=SEED, device="cuda"):
-        self.H, self.W, self.device = H, W, device
+        self.H, self.W, self.device, self.n_ids = H, W, device, int(n_ids)
         g = _gen(seed, device)
         self.grids = torch.randn((n_ids, 1, 13, 13), generator=g, device=device, dtype=torch.float32)
 
     def images(self, ids, seed, noise=12.0):
         """ids: int64 device tensor -> uint8 [len(ids)][H*W] images (pixel noise N(0, noise^2); the
-        bench's stress runs raise it to crowd the identities together)."""
+        bench's stress runs raise it to crowd the identities together).  Ids outside 0 .. n_ids - 1
+        raise ValueError on the host (an out-of-range gather of the grids would fault the device)."""
+        if len(ids) and (int(ids.min()) < 0 or int(ids.max()) >= self.n_ids):
+            raise ValueError(f"identity ids must lie in 0..{self.n_ids - 1} (got {int(ids.min())}..{int(ids.max())})")
         g = _gen(seed, self.device)
         up = F.interpolate(self.grids[ids], size=(self.H, self.W), mode="bilinear", align_corners=False)[:, 0]
         noise = torch.randn(up.shape, generator=g, device=self.device) * float(noise)
@@ -49,6 +52,53 @@ def build_projection(D, d, device):
     g.manual_seed(SEED + 5)
     Wt = torch.randn((d, D), generator=g, device=device) / np.sqrt(D)
     return Projection(Wt_device=Wt, D=D, device=device), Wt
+
+
+def build_trained_projection(bank, per_id, n_train, D, device, num_components=0, group=None):
+    """The Fisherfaces W the reference's trainer would produce (thetrainer.py:120-124: Fisherfaces()
+    defaults) from the synthetic training set of configs[1]: the n_train faces of gallery_chunks' rows
+    0 .. n_train - 1 of an n_train-image gallery (identity j // per_id, labels 0..c-1), trained on the
+    device (feature.fisherfaces_device: pixel regime at 100k x 10,000).  With torch.distributed
+    initialised, rank 0 trains and W is broadcast (every rank must project with the same bits).
+    Returns (Projection, W^T device fp64 [d][D], info dict)."""
+    import time
+    import torch.distributed as dist
+    from ._device import Projection
+    from .facerec.feature import fisherfaces_device
+    n_ids = -(-n_train // per_id)
+    _check_ids(bank, n_ids)
+    sharded = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    t0 = time.perf_counter()
+    info = {}
+    if not sharded or dist.get_rank(group) == 0:
+        X = torch.empty((n_train, D), dtype=torch.uint8, device=device)
+        for c0 in range(0, n_train, GALLERY_CHUNK):
+            rows = torch.arange(c0, min(c0 + GALLERY_CHUNK, n_train), device=device)
+            X[c0:c0 + len(rows)] = bank.images(rows // per_id, seed=SEED + 1000 + c0 // GALLERY_CHUNK)
+        y = np.arange(n_train) // per_id
+        evals, Wd, m, regime = fisherfaces_device(X, D, y, num_components)
+        del X
+        Wt = Wd.t().contiguous()
+        del Wd
+        info = {"regime": regime, "n_train": n_train, "identities": n_ids, "d": m,
+                "eigenvalues_head": [float(v) for v in np.asarray(evals)[:4]]}
+    if sharded:
+        shape = torch.zeros(2, dtype=torch.int64, device=device)
+        if dist.get_rank(group) == 0:
+            shape[0], shape[1] = Wt.shape[0], Wt.shape[1]
+        dist.broadcast(shape, 0, group=group)
+        if dist.get_rank(group) != 0:
+            Wt = torch.empty((int(shape[0]), int(shape[1])), dtype=torch.float64, device=device)
+        dist.broadcast(Wt, 0, group=group)
+    torch.cuda.synchronize(device)
+    info["train_s"] = time.perf_counter() - t0
+    return Projection(Wt_device=Wt, D=D, device=device), Wt, info
+
+
+def _check_ids(bank, n_ids):
+    """Identity indices past the bank would index its device grids out of bounds: refuse on the host."""
+    if n_ids > bank.n_ids:
+        raise ValueError(f"{n_ids} identities requested from a bank of {bank.n_ids}")
 
 
 GALLERY_CHUNK = 8192
@@ -85,6 +135,9 @@ def build_gallery(P, bank, per_id, n0, nl, N, d, ld, device, noise=12.0):
     index_base n0), centred on gallery_centre (fp64, the same on every rank)."""
     from . import _lib
     from ._device import FloatGallery
+    _check_ids(bank, -(-N // per_id))
+    if not (0 <= n0 and nl >= 0 and n0 + nl <= N):
+        raise ValueError(f"gallery rows [{n0}, {n0 + nl}) outside the {N}-image gallery")
     centre = gallery_centre(P, bank, per_id, N, device, noise)
     G = torch.zeros((nl, ld), dtype=torch.float32, device=device)
     for c0, Y in gallery_chunks(P, bank, per_id, n0, n0 + nl, N, centre, noise):

@@ -2,7 +2,10 @@
 
 * configs[1]: 100x100 faces, 10k identities x 10 = 100k gallery, d = 9999, B = 4096 through
   PredictableModel.predict_batch (projection + certified search chain); 64 sampled queries
-  against the float64 oracle, every query's identity and the per-tier certificate counts.
+  against the float64 oracle, every query's identity and the per-tier certificate counts -- with a
+  random W and (round 5) with the Fisherfaces W trained on the gallery's own faces (the reference
+  trainer's model, thetrainer.py:120-124: its LDA columns put most of the feature variance into the
+  leading blocks, which the fp6 tier's column-block scales absorb).
 * configs[2]: the 1M-gallery sharding path -- parallel.certify_sharded on 2 gloo ranks sharing
   one device (the OFR_ONE_DEVICE rehearsal), with the REAL FloatGallery on data where only
   rank 1's fp6 sieve bucket overflows: the query must go down the chain, never be certified
@@ -59,16 +62,23 @@ def _fisher_model(W):
 
 
 @pytest.mark.timeout(600)
-def test_config1_100k_gallery_d9999_batch4096(monkeypatch):
-    from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank
+@pytest.mark.parametrize("w", ["random", "trained"])
+def test_config1_100k_gallery_d9999_batch4096(monkeypatch, w):
+    from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_trained_projection
     monkeypatch.setenv("OFR_SEARCH", "auto")
     dev = torch.device("cuda", 0)
     ids, per, side, d, B = 10_000, 10, 100, 9999, 4096
     N, D = ids * per, side * side
-    r = np.random.default_rng(SEED + 31)
-    W = r.normal(0, 1 / np.sqrt(D), (D, d))
-    model = _fisher_model(W)
     bank = IdentityBank(ids, side, side, device=dev)
+    if w == "trained":
+        _, Wt, info = build_trained_projection(bank, per, N, D, dev)
+        assert info["regime"] == "pixel" and Wt.shape == (d, D), info
+        W = Wt.t().cpu().numpy()
+        del Wt
+    else:
+        r = np.random.default_rng(SEED + 31)
+        W = r.normal(0, 1 / np.sqrt(D), (D, d))
+    model = _fisher_model(W)
     feats = np.empty((N, d))
     for c0 in range(0, N, 8192):
         rows = torch.arange(c0, min(N, c0 + 8192), device=dev)
@@ -83,8 +93,12 @@ def test_config1_100k_gallery_d9999_batch4096(monkeypatch):
     g = model.classifier._gallery()
     counts = list(g.last_fallbacks)
     acc = float(np.mean(idx[:, 0] // per == ids_q.cpu().numpy()))
+    print(f"configs[1] W={w}: uncertified after each tier {counts}, top-1 identity accuracy {acc}")
     assert acc >= 0.99, acc
     assert counts[0] <= B // 100, counts          # identity-bank data: the fp6 tier certifies almost all
+    if w == "trained":
+        bs = g._block_scales()
+        assert bs is not None and int(bs.min()) < 127   # the trained W's variance profile is absorbed
     s = np.random.default_rng(5).choice(B, 64, replace=False)
     Qf = model.feature.project_device(Xq[torch.from_numpy(s).to(dev)], f64=True).cpu().numpy()
     ri, rd, r2 = _exact_top1(Qf, feats)
@@ -195,7 +209,8 @@ def _c2_worker(rank, ws, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
         from opencv_facerecognizer_amd._device import round_up
-        from opencv_facerecognizer_amd.parallel import certify_sharded, gather_rows, merge_sharded, shard_range
+        from opencv_facerecognizer_amd.parallel import (certify_sharded, gather_rows, merge_sharded, shard_range,
+                                                        share_block_scales)
         from opencv_facerecognizer_amd.synthetic import build_gallery
         dev = torch.device("cuda", 0)
         N, d, B, k = C2["N"], C2["d"], C2["B"], C2["k"]
@@ -203,6 +218,7 @@ def _c2_worker(rank, ws, port, out):
         n0, n1 = shard_range(N, rank, ws)
         g = build_gallery(P, bank, C2["per"], n0, n1 - n0, N, d, max(32, round_up(d, 32)), dev)
         print(f"config2 rank {rank}: shard of {g.N} rows built", flush=True)
+        share_block_scales(g)            # the fp6 query panels are all-gathered: one set of block scales
         b0, b1 = shard_range(B, rank, ws)
         Qd_loc = P.project(Xq[b0:b1], shift64=g.shift64)
         qq = g.gather_queries(g.quantize_queries(Qd_loc, tier="f6"))

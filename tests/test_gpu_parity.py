@@ -195,10 +195,25 @@ def _decode_f6_tiles(tiles, R, d):
     return val[:R]
 
 
+def _block_scales_host(d, seed, spread):
+    """Random column-block scales (E8M0 bytes, 4 per 128-feature stage; exponents 0 .. -spread, 127 past d)
+    -> (device uint8 tensor or None, per-feature 2^e fp64 [d])."""
+    if spread is None:
+        return None, np.ones(d)
+    nb, npad = -(-d // 32), 4 * -(-d // 128)
+    e = -_rng(seed).integers(0, spread + 1, nb)
+    e[0] = 0
+    b = np.full(npad, 127, np.uint8)
+    b[:nb] = 127 + e
+    return torch.from_numpy(b).cuda(), np.repeat(2.0 ** e, 32)[:d]
+
+
+@pytest.mark.parametrize("spread", [None, 8])
 @pytest.mark.parametrize("R,d", [(1, 3), (300, 99), (513, 260), (256, 128), (40, 1000)])
-def test_f6_quantize_rows_vs_host(R, d):
-    """ofr_f6_quantize_rows: every value is the nearest e2m3 value of x/s (ties either way), s = max|x|/7.5
-    rounded up, padding is zero, and the stats are ||x~|| and ||x - x~|| of x~ = s v."""
+def test_f6_quantize_rows_vs_host(R, d, spread):
+    """ofr_f6_quantize_rows: every value is the nearest e2m3 value of x / (s 2^e) (ties either way), e the
+    feature's column-block exponent (spread None: unit scales), s = max|x / 2^e| / 7.5 rounded up, padding is
+    zero, and the stats are ||x~|| and ||x - x~|| of x~ = s 2^e v."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._lib import call, ptr, stream
     r = _rng(R * 7 + d)
@@ -207,6 +222,7 @@ def test_f6_quantize_rows_vs_host(R, d):
     if R > 2:
         X[2] = 0                                                          # all-zero row
         X[1, 0] = 1e6                                                     # one huge feature
+    bs, f = _block_scales_host(d, R + d, spread)
     ldx = d + 5
     Xd = torch.zeros((R, ldx), dtype=torch.float32, device="cuda")
     Xd[:, :d] = torch.from_numpy(X).cuda()
@@ -214,23 +230,24 @@ def test_f6_quantize_rows_vs_host(R, d):
     T = torch.full((nbytes,), 0xAB, dtype=torch.uint8, device="cuda")
     sc = torch.empty(R, dtype=torch.float32, device="cuda")
     st = torch.empty((R, 3), dtype=torch.float64, device="cuda")
-    call("ofr_f6_quantize_rows", stream(), ptr(Xd), R, d, ldx, ptr(T), nbytes, ptr(sc), ptr(st), None, None)
+    call("ofr_f6_quantize_rows", stream(), ptr(Xd), R, d, ldx, ptr(T), nbytes, ptr(sc), ptr(st), None, None, ptr(bs))
     torch.cuda.synchronize()
     Vall = _decode_f6_tiles(T.cpu().numpy(), -(-R // 256) * 256, d)
     assert np.all(Vall[R:] == 0)                                          # tail rows of the last panel
     V = Vall[:R]
     s = sc.cpu().numpy().astype(np.float64)
     assert np.all(V[:, d:] == 0)
-    mx = np.abs(X).max(1).astype(np.float64)
+    Xn = X.astype(np.float64) / f                                         # exact power-of-two rescaling
+    mx = np.abs(Xn).max(1)
     assert np.all(np.where(mx > 0, mx / s, 0) <= 7.5)
     assert np.all(np.where(mx > 0, s <= np.nextafter(np.float32(mx / 7.5), np.float32(np.inf)) * (1 + 1e-6), s == 1))
     grid = _e2m3_values()
-    r_ = np.abs(X / s[:, None])
+    r_ = np.abs(Xn / s[:, None])
     err = np.abs(np.abs(V[:, :d]) - r_)
     best = np.abs(r_[..., None] - grid).min(-1)
     assert np.all(err <= best + 1e-12)                                    # nearest representable value
     assert np.all((np.sign(V[:, :d]) == np.sign(X)) | (V[:, :d] == 0))
-    Xt = s[:, None] * V[:, :d]
+    Xt = s[:, None] * f * V[:, :d]
     a = np.linalg.norm(Xt, axis=1)
     e = np.linalg.norm(X.astype(np.float64) - Xt, axis=1)
     got = st.cpu().numpy()
@@ -240,11 +257,12 @@ def test_f6_quantize_rows_vs_host(R, d):
     assert np.all(got[:, 2] == 0)
 
 
+@pytest.mark.parametrize("spread", [None, 8])
 @pytest.mark.parametrize("R,d", [(1, 3), (300, 99), (513, 260), (40, 1000)])
-def test_f6x2_quantize_rows_vs_host(R, d):
+def test_f6x2_quantize_rows_vs_host(R, d, spread):
     """ofr_f6x2_quantize_rows: the first slice is byte-identical to ofr_f6_quantize_rows (same scale), the
-    second holds the nearest e2m3 value of 2^4 (x/s - v1), and the stats are (s(|v1| + |v2|/16),
-    |x - x~|, s |v2|/16) of x~ = s (v1 + v2/16)."""
+    second holds the nearest e2m3 value of 2^4 (x / 2^e / s - v1), and the stats are (s(|v1|' + |v2|'/16),
+    |x - x~|, s |v2|'/16) of x~ = s 2^e (v1 + v2/16), |v|' = |2^e v| (e: column-block exponents)."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._lib import call, ptr, stream
     r = _rng(R * 5 + d)
@@ -252,6 +270,7 @@ def test_f6x2_quantize_rows_vs_host(R, d):
     if R > 2:
         X[2] = 0
         X[1, 0] = 1e6
+    bs, f = _block_scales_host(d, R * 3 + d, spread)
     ldx = d + 3
     Xd = torch.zeros((R, ldx), dtype=torch.float32, device="cuda")
     Xd[:, :d] = torch.from_numpy(X).cuda()
@@ -262,8 +281,8 @@ def test_f6x2_quantize_rows_vs_host(R, d):
     sc, sc0 = (torch.empty(R, dtype=torch.float32, device="cuda") for _ in range(2))
     st, st0 = (torch.empty((R, 3), dtype=torch.float64, device="cuda") for _ in range(2))
     call("ofr_f6x2_quantize_rows", stream(), ptr(Xd), R, d, ldx, ptr(T1), ptr(T2), nbytes, ptr(sc), ptr(st), None,
-         None)
-    call("ofr_f6_quantize_rows", stream(), ptr(Xd), R, d, ldx, ptr(T0), nbytes, ptr(sc0), ptr(st0), None, None)
+         None, ptr(bs))
+    call("ofr_f6_quantize_rows", stream(), ptr(Xd), R, d, ldx, ptr(T0), nbytes, ptr(sc0), ptr(st0), None, None, ptr(bs))
     torch.cuda.synchronize()
     assert torch.equal(T1, T0) and torch.equal(sc, sc0)
     P = -(-R // 256) * 256
@@ -272,17 +291,17 @@ def test_f6x2_quantize_rows_vs_host(R, d):
     assert np.all(V2[R:] == 0) and np.all(V2[:R, d:] == 0)
     V1, V2 = V1[:R, :d], V2[:R, :d]
     s = sc.cpu().numpy().astype(np.float64)[:, None]
-    u = 16.0 * (X.astype(np.float64) - s * V1) / s
+    u = 16.0 * (X.astype(np.float64) / f - s * V1) / s
     assert np.all(np.abs(u) <= 4.0 + 1e-9)
     grid = _e2m3_values()
     best = np.abs(np.abs(u)[..., None] - grid).min(-1)
     assert np.all(np.abs(np.abs(V2) - np.abs(u)) <= best + 1e-9)             # nearest (ties either way)
     assert np.all((np.sign(V2) == np.sign(u)) | (V2 == 0) | (np.abs(u) < 1e-9))
-    Xt = s * (V1 + V2 / 16.0)
+    Xt = s * f * (V1 + V2 / 16.0)
     got = st.cpu().numpy()
-    a = s[:, 0] * (np.linalg.norm(V1, axis=1) + np.linalg.norm(V2, axis=1) / 16.0)
+    a = s[:, 0] * (np.linalg.norm(f * V1, axis=1) + np.linalg.norm(f * V2, axis=1) / 16.0)
     e = np.linalg.norm(X.astype(np.float64) - Xt, axis=1)
-    t = s[:, 0] * np.linalg.norm(V2, axis=1) / 16.0
+    t = s[:, 0] * np.linalg.norm(f * V2, axis=1) / 16.0
     for j, ref in enumerate((a, e, t)):
         np.testing.assert_allclose(got[:, j], ref, rtol=1e-11, atol=0)
         assert np.all(got[:, j] >= ref)
@@ -291,6 +310,33 @@ def test_f6x2_quantize_rows_vs_host(R, d):
     e1 = st0.cpu().numpy()[:, 1]
     ok = e1 > 0
     assert np.median(got[ok, 1] / e1[ok]) < 0.1
+
+
+def test_f6_block_scales_from_sums():
+    """ofr_f6_block_sumsq + ofr_f6_block_scales: sums of squares per 32-feature block (accumulated over
+    calls), bytes 127 + rint(log2(rms_b / max rms)) clamped to [-63, 0], 127 for empty and padding blocks."""
+    from opencv_facerecognizer_amd._lib import call, ptr, stream
+    d, R = 300, 777
+    r = _rng(31)
+    sig = np.repeat(2.0 ** -r.uniform(0, 12, -(-d // 32)), 32)[:d]
+    sig[64:96] = 0                                                     # an empty block
+    X = (r.normal(0, 1, (R, d)) * sig).astype(np.float32)
+    ldx = 320
+    Xd = torch.zeros((R, ldx), dtype=torch.float32, device="cuda")
+    Xd[:, :d] = torch.from_numpy(X).cuda()
+    sums = torch.zeros(-(-d // 32), dtype=torch.float64, device="cuda")
+    call("ofr_f6_block_sumsq", stream(), ptr(Xd[:500]), 500, d, ldx, ptr(sums))
+    call("ofr_f6_block_sumsq", stream(), ptr(Xd[500:]), R - 500, d, ldx, ptr(sums))
+    bs = torch.full((4 * -(-d // 128),), 0, dtype=torch.uint8, device="cuda")
+    call("ofr_f6_block_scales", stream(), ptr(sums), d, ptr(bs))
+    torch.cuda.synchronize()
+    X64 = X.astype(np.float64)
+    ref = np.array([(X64[:, b * 32:(b + 1) * 32] ** 2).sum() for b in range(-(-d // 32))])
+    np.testing.assert_allclose(sums.cpu().numpy(), ref, rtol=1e-12)
+    e = np.where(ref > 0, np.clip(np.rint(0.5 * np.log2(np.where(ref > 0, ref, 1) / ref.max())), -63, 0), 0)
+    want = np.full(bs.numel(), 127)
+    want[:len(e)] = 127 + e
+    assert np.array_equal(bs.cpu().numpy(), want)
 
 
 @pytest.mark.parametrize("k", [1, 4])

@@ -11,9 +11,11 @@ Reference: classifier.py:104-119 (the exact k nearest of the whole gallery).
   8-wave engine (OFR_F6_SHAPE=16): every query keeps EXACTLY the 30,000 copies, all with one key.
 * Headline shape (configs[2]: N = 1M, d = 9,999, B = 4,096): for 64 sampled queries the exact
   coarse score of every row is computed from the device's own fp6 codes (decoded from the tiled
-  layout; products of e2m3 values and their sums are exact in fp64), and the bucket must hold every
-  row whose exact score is below theta by more than the fp32 accumulation bound, and nothing above
-  theta by more than it.
+  layout; products of e2m3 values, times the column-block scales 2^2e, and their sums are exact in
+  fp64), and the bucket must hold every row whose exact score is below theta by more than the fp32
+  accumulation bound, and nothing above theta by more than it.  Round 5: with the random W of rounds
+  1-4 (column-block scales all 2^0) and with the Fisherfaces W trained on configs[1]'s faces (the
+  headline's W: blocks 2^0 .. 2^-5, so the MFMA's per-lane scale operands are exercised).
 """
 import numpy as np
 import pytest
@@ -110,13 +112,19 @@ def _decode_panels(tiles, p0, p1, nst, d, table):
 
 
 @pytest.mark.timeout(900)
-def test_sieve_complete_vs_exact_scores_headline_shape():
+@pytest.mark.parametrize("w", ["random", "trained"])
+def test_sieve_complete_vs_exact_scores_headline_shape(w):
     from opencv_facerecognizer_amd._device import round_up
-    from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_gallery, build_projection
+    from opencv_facerecognizer_amd.synthetic import (SEED, IdentityBank, build_gallery, build_projection,
+                                                     build_trained_projection)
     dev = torch.device("cuda", 0)
     N, per, side, d, B = 1_000_000, 10, 100, 9999, 4096
-    P, _ = build_projection(side * side, d, dev)
     bank = IdentityBank(N // per, side, side, device=dev)
+    if w == "trained":
+        P, _, info = build_trained_projection(bank, per, 100_000, side * side, dev)
+        assert P.d == d, info
+    else:
+        P, _ = build_projection(side * side, d, dev)
     g = build_gallery(P, bank, per, 0, N, N, d, max(32, round_up(d, 32)), dev)
     gq = torch.Generator(device=dev)
     gq.manual_seed(SEED + 7)
@@ -133,11 +141,17 @@ def test_sieve_complete_vs_exact_scores_headline_shape():
     assert np.all((cnt >= 16) & (cnt <= g.SIEVE_CAP)), cnt
     nst = -(-d // 128)
     table = _e2m3_table(dev)
+    # column-block scales: feature k decodes to s 2^e v, e = bscale[k / 32] - 127 (gallery and queries)
+    bs = g._block_scales()
+    f = (torch.ones(d, dtype=torch.float64, device=dev) if bs is None else
+         torch.pow(2.0, bs.double() - 127.0).repeat_interleave(32)[:d])
+    if w == "trained":
+        assert bs is not None and int(bs[:-(-d // 32)].min()) < 127, "a trained W must give non-unit block scales"
     # the sampled queries' codes: their panels of the query tiles
     Vq = torch.empty((64, d), dtype=torch.float64, device=dev)
     for j, b in enumerate(s):
         pnl = b // 256
-        Vq[j] = _decode_panels(qq["Qs"], pnl, pnl + 1, nst, d, table)[b % 256]
+        Vq[j] = _decode_panels(qq["Qs"], pnl, pnl + 1, nst, d, table)[b % 256] * f
     sq = qq["scale"].index_select(0, sd).double()
     # sanity: the decoded codes times the row scale are the quantized query rows (residual ~3 %)
     res = (Qd.index_select(0, sd)[:, :d].double() - sq[:, None] * Vq).norm(dim=1) / Qd.index_select(0, sd)[:, :d].double().norm(dim=1)
@@ -155,7 +169,7 @@ def test_sieve_complete_vs_exact_scores_headline_shape():
         p1 = min(npan, p0 + PCH)
         Vg = _decode_panels(gt["Gs"], p0, p1, nst, d, table)
         r0, r1 = p0 * 256, min(N, p1 * 256)
-        Vg = Vg[:r1 - r0]
+        Vg = Vg[:r1 - r0] * f
         dot = Vq @ Vg.t()                             # exact: multiples of 2^-6, |sum| < 2^53 ulp range
         sab = Vqa @ Vg.abs().t()
         t = 2.0 * sq[:, None] * gscale[None, r0:r1]

@@ -7,6 +7,10 @@
 //    Checked against an exact host product on random codes and scales.
 // 2. accumulation numerics: a chain of 160 MFMAs (K = 10240) against the exact sum, error
 //    relative to sum |a b|, on random data and on a cancelling sum.
+// 2b. the same for v_mfma_scale_f32_16x16x128_f8f6f4 (the sieve engines' MFMA): lane l = (q = l >> 4,
+//    r = l & 15) holds A[row r][k = 32q + j] / B[k = 32q + j][col r] and the E8M0 scale of that block;
+//    C/D register g of lane l = row 4 (l >> 4) + g, col l & 15.  Per-(row, block) scales 2^-7..2^7 and
+//    column-block scales (one byte per 32 features, the same for all rows: the fp6 tier's layout).
 // 3. rate: back-to-back scaled fp6 MFMAs on register operands, 1 and 2 waves per SIMD, all
 //    CUs, next to v_mfma_i32_32x32x32_i8.
 #include <hip/hip_runtime.h>
@@ -38,6 +42,16 @@ __global__ void chain(const i32x8* a, const i32x8* b, const int* sa, const int* 
     acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[m * 64 + l], b[m * 64 + l], acc, 2, 2, 0, sa[m * 64 + l], 0,
                                                          sb[m * 64 + l]);
   for (int r = 0; r < 16; ++r) out[l * 16 + r] = acc[r];
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__global__ void chain16(const i32x8* a, const i32x8* b, const int* sa, const int* sb, int nmf, float* out) {
+  const int l = threadIdx.x;
+  f32x4 acc = {};
+  for (int m = 0; m < nmf; ++m)
+    acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[m * 64 + l], b[m * 64 + l], acc, 2, 2, 0, sa[m * 64 + l], 0,
+                                                          sb[m * 64 + l]);
+  for (int r = 0; r < 4; ++r) out[l * 4 + r] = acc[r];
 }
 
 __global__ void __launch_bounds__(512, 1) rate_fp6(const int* seed, int iters, float* out, long long* stamps) {
@@ -169,6 +183,77 @@ static double run_chain(const Frag& A, const Frag& B, int nmf, double* maxrel, d
   return bad;
 }
 
+// 16x16x128: codes [nmf][16 rows][128 k], scales [nmf][16 rows][4 blocks]
+static double run_chain16(const Frag& A, const Frag& B, int nmf, double* maxabs_over_sum) {
+  std::vector<int> ad((size_t)nmf * 64 * 8, 0), as((size_t)nmf * 64), bd((size_t)nmf * 64 * 8, 0), bs((size_t)nmf * 64);
+  auto pk = [&](const Frag& f, std::vector<int>& dw, std::vector<int>& sc) {
+    for (int m = 0; m < nmf; ++m)
+      for (int l = 0; l < 64; ++l) {
+        const int q = l >> 4, r = l & 15;
+        uint32_t* w = (uint32_t*)&dw[((size_t)m * 64 + l) * 8];
+        for (int j = 0; j < 32; ++j) {
+          const uint32_t c = (uint32_t)f.code[((size_t)m * 16 + r) * 128 + 32 * q + j] & 63u;
+          const int bit = 6 * j;
+          w[bit >> 5] |= c << (bit & 31);
+          if ((bit & 31) > 26) w[(bit >> 5) + 1] |= c >> (32 - (bit & 31));
+        }
+        sc[(size_t)m * 64 + l] = f.scale[((size_t)m * 16 + r) * 4 + q];
+      }
+  };
+  pk(A, ad, as);
+  pk(B, bd, bs);
+  int *da, *dsa, *db, *dsb;
+  float* dout;
+  CK(hipMalloc(&da, ad.size() * 4)); CK(hipMalloc(&db, bd.size() * 4));
+  CK(hipMalloc(&dsa, as.size() * 4)); CK(hipMalloc(&dsb, bs.size() * 4));
+  CK(hipMalloc(&dout, 64 * 4 * 4));
+  CK(hipMemcpy(da, ad.data(), ad.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(db, bd.data(), bd.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dsa, as.data(), as.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dsb, bs.data(), bs.size() * 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(chain16, dim3(1), dim3(64), 0, 0, (const i32x8*)da, (const i32x8*)db, dsa, dsb, nmf, dout);
+  CK(hipDeviceSynchronize());
+  std::vector<float> out(64 * 4);
+  CK(hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost));
+  double worst_abs = 0;
+  int bad = 0;
+  for (int l = 0; l < 64; ++l)
+    for (int g = 0; g < 4; ++g) {
+      const int col = l & 15, row = 4 * (l >> 4) + g;
+      double ex = 0, sabs = 0;
+      for (int m = 0; m < nmf; ++m)
+        for (int k = 0; k < 128; ++k) {
+          const double av = e2m3(A.code[((size_t)m * 16 + row) * 128 + k]) *
+                            std::ldexp(1.0, A.scale[((size_t)m * 16 + row) * 4 + k / 32] - 127);
+          const double bv = e2m3(B.code[((size_t)m * 16 + col) * 128 + k]) *
+                            std::ldexp(1.0, B.scale[((size_t)m * 16 + col) * 4 + k / 32] - 127);
+          ex += av * bv;
+          sabs += std::fabs(av * bv);
+        }
+      const double err = std::fabs((double)out[l * 4 + g] - ex);
+      if (err > 1e-3 * sabs + 1e-30) ++bad;
+      if (sabs > 0) worst_abs = std::fmax(worst_abs, err / sabs);
+    }
+  *maxabs_over_sum = worst_abs;
+  CK(hipFree(da)); CK(hipFree(db)); CK(hipFree(dsa)); CK(hipFree(dsb)); CK(hipFree(dout));
+  return bad;
+}
+
+static Frag rand_frag16(int nmf, uint32_t& s, int smin, int smax, bool colblock) {
+  Frag f;
+  f.code.resize((size_t)nmf * 16 * 128);
+  f.scale.resize((size_t)nmf * 16 * 4);
+  auto rnd = [&]() { s ^= s << 13; s ^= s >> 17; s ^= s << 5; return s; };
+  for (auto& c : f.code) c = rnd() & 63;
+  for (int m = 0; m < nmf; ++m)
+    for (int b = 0; b < 4; ++b) {
+      const int cb = smin + (int)(rnd() % (uint32_t)(smax - smin + 1));
+      for (int r = 0; r < 16; ++r)
+        f.scale[((size_t)m * 16 + r) * 4 + b] = colblock ? cb : smin + (int)(rnd() % (uint32_t)(smax - smin + 1));
+    }
+  return f;
+}
+
 static Frag rand_frag(int nmf, uint32_t& s, int smin, int smax, bool cancel_sign) {
   Frag f;
   f.code.resize((size_t)nmf * 32 * 64);
@@ -216,6 +301,28 @@ int main(int argc, char** argv) {
     printf("chain 160 cancelling: %d mismatches, max err / sum|ab| = %.3e (%.2f x 2^-24)\n", (int)bad, abs_sum,
            abs_sum * 16777216.0);
   }
+  // 2b. the 16x16x128 form
+  {
+    Frag A = rand_frag16(1, s, 124, 130, false), B = rand_frag16(1, s, 124, 130, false);
+    const double bad = run_chain16(A, B, 1, &abs_sum);
+    printf("16x16x128 layout (1 mfma, per-lane scales): %s, %d mismatches, max err / sum|ab| = %.3e\n",
+           bad == 0 ? "OK" : "FAIL", (int)bad, abs_sum);
+  }
+  for (int trial = 0; trial < 3; ++trial) {
+    Frag A = rand_frag16(80, s, 107, 127, true), B = A;
+    Frag Bq = rand_frag16(80, s, 107, 127, true);
+    for (size_t i = 0; i < B.scale.size(); ++i) B.code = Bq.code;   // same column-block scales, other codes
+    const double bad = run_chain16(A, B, 80, &abs_sum);
+    printf("16x16x128 chain 80, column-block scales 2^-20..2^0: %d mismatches, max err / sum|ab| = %.3e (%.2f x 2^-24)\n",
+           (int)bad, abs_sum, abs_sum * 16777216.0);
+  }
+  for (int trial = 0; trial < 3; ++trial) {
+    Frag A = rand_frag16(80, s, 120, 134, false), B = rand_frag16(80, s, 120, 134, false);
+    const double bad = run_chain16(A, B, 80, &abs_sum);
+    printf("16x16x128 chain 80, per-lane scales 2^-7..2^7: %d mismatches, max err / sum|ab| = %.3e (%.2f x 2^-24)\n",
+           (int)bad, abs_sum, abs_sum * 16777216.0);
+  }
+  if (argc > 1) return 0;   // numerics only
   // 3. rate
   int dev = 0, ncu = 0;
   CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
