@@ -134,17 +134,25 @@ def cpu_baseline(Wt, gallery, Xq, N_total, seconds):
 
 def committed_traffic(cfg):
     """HBM-side bytes per launch of the search pass from the committed rocprofv3 PMC passes
-    (profiles/*_pmc_summary.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 guide), if measured at this config."""
+    (profiles/*_pmc_summary.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 guide), if measured at this
+    config: among the summaries of this exact config (W kind included; summaries without one were
+    measured on the random W) the one with the latest measured_utc (written by tools/pmc_summary.py;
+    summaries without it count as older than any with it).  (bytes, file) or None."""
     import glob
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+    cands = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")):
         try:
             s = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if s.get("config") == cfg:
-            best = (s["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
-    return best
+        c = dict(s.get("config") or {})
+        c.setdefault("w", "random")
+        if c == cfg and s.get("traffic_bytes_per_launch") is not None:
+            cands.append((s.get("measured_utc", ""), os.path.basename(f), s["traffic_bytes_per_launch"]))
+    if not cands:
+        return None
+    _, name, tr = max(cands)
+    return tr, os.path.join("profiles", name)
 
 
 class StepPipeline:
@@ -353,30 +361,39 @@ def stress_run(P, bank, args, noise, device, N=None):
     return res
 
 
-def launch_ranks(n):
+def launch_ranks(n, cmd=None, poll_s=0.2):
     """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK, LOCAL_RANK,
     WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT) and wait for them.  Runs before anything
-    touches the GPU; the children are new processes (no exec of this one).  Returns the exit status:
-    the first non-zero child status, else 0.  Rank 0 prints the JSON line."""
+    touches the GPU; the children are new processes (no exec of this one).  Every child is polled: the
+    first non-zero exit, from whichever rank, terminates the others (they would wait in a collective
+    forever) and is returned; 0 once all exited cleanly.  Rank 0 prints the JSON line.  cmd: the child
+    command line (tests), default this script with the same arguments."""
     import socket
     import subprocess
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen(cmd, env=env))
     status = 0
-    for p in procs:
-        rc = p.wait()
-        if rc and not status:
-            status = rc
-            for q in procs:            # one rank failed: the others would wait in a collective forever
-                if q.poll() is None:
-                    q.terminate()
-    return status
+    while True:
+        live = 0
+        for p in procs:
+            rc = p.poll()
+            if rc is None:
+                live += 1
+            elif rc and not status:
+                status = rc
+                for q in procs:
+                    if q.poll() is None:
+                        q.terminate()
+        if not live:
+            return status
+        time.sleep(poll_s)
 
 
 def main():
@@ -409,7 +426,8 @@ def main():
 
     # ---- setup (untimed): W, gallery shard, queries -------------------------------------
     t0 = time.perf_counter()
-    bank = IdentityBank(n_ids, H, W, device=device)
+    # the trained W's training set (configs[1]: identities 0 .. train_ids - 1) may reach past a small gallery's
+    bank = IdentityBank(max(n_ids, args.train_ids if args.w == "trained" else 0), H, W, device=device)
     w_info = {"kind": "random N(0, 1/D)"}
     if args.w == "trained":
         P, Wt, w_info = build_trained_projection(bank, args.per_id, args.train_ids * args.per_id, D, device)
@@ -617,7 +635,8 @@ def main():
     if rank == 0:
         value = B * args.steps / elapsed
         coll = "RCCL" if world > 1 and dist.get_backend() == "nccl" else "gloo"   # the collectives' backend
-        tr = committed_traffic({"gallery": nl, "batch": B, "d": d, "D": D, "k": k, "search": args.search})
+        tr = committed_traffic({"gallery": nl, "batch": B, "d": d, "D": D, "k": k, "search": args.search,
+                                "w": args.w})
         result = {
             "metric": "query faces/sec (Fisherfaces proj + 1-NN, 1M gallery) at 1/2/4/8 GPUs",
             "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

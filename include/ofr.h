@@ -196,7 +196,7 @@ int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, 
  * ofr_knn_f6_workspace_bytes(B, N) bytes, 16-byte aligned, kept between the
  * phase-1 and phase-2 calls; after phase 1 the int32 kept-row counts [B] sit
  * at byte ofr_knn_f6_sieve_counts_offset(B, N) of it (SIZE_MAX: no sieve,
- * B <= 32).  Env OFR_SIEVE_STRIDE (default 64) sets the sample stride.
+ * B <= 32).  The panel sample takes every 64th 256-row panel.
  * Phase 1 in two calls (a pipelined caller overlaps other work with the second
  * only): phases 4 = the sample pass + thresholds (B <= 32: the whole stream
  * pass), 8 = the sieve pass (after a phases-4 call on the same workspace;

@@ -238,7 +238,7 @@ struct Engine {
   //      kt's buffer after the first MFMA
   // so every fragment read has a block of MFMAs to land behind and each barrier falls while
   // the matrix pipe still drains the previous block (2 % faster than a hand-off at the stage
-  // boundary, which exposes the step-0 reads after every barrier: tools/f6_probe.hip).
+  // boundary, which exposes the step-0 reads after every barrier: the round-1 engine probe).
   // Fragments double-buffered by j; 3 LDS stages (kt+1 read next, kt+2 and kt+3 in flight).
   // NSEG: segments of nst stages each (seg_src); G2 / Q2 only for NSEG = 3
   template <int NSEG = 1>

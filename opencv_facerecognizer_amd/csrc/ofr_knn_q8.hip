@@ -176,7 +176,7 @@ __device__ __forceinline__ void tile_epilogue(char* smem, const TileArgs& p, int
 // (truncated key > theta) or was kept and lost to the 16th, so tau = min(theta, 16th kept)
 // bounds every excluded row exactly as before.  theta only steers the volume: a bucket that
 // overflows its cap makes the query uncertified (bound -inf), never wrong.
-constexpr int64_t SIEVE_STRIDE = 64;   // sample: gallery tiles 0, 64, 128, ... (OFR_SIEVE_STRIDE overrides)
+constexpr int64_t SIEVE_STRIDE = 64;   // panel sample (ofr_knn_f6): gallery tiles 0, 64, 128, ...
 constexpr int64_t SIEVE_CAP = 32768;   // kept rows per query (256 KiB; ~16 * SIEVE_STRIDE expected, heavy tail)
 constexpr int SIEVE_HCAP = 8192;       // LDS hit slots per tile (64 KiB)
 constexpr int SIEVE_RANK = 16;         // theta = this-th best key of the sample (ofr_knn_f6's sieve_rank)
@@ -460,7 +460,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
 // one 8-wave workgroup per CU.
 // Epilogue: the 32 x 32 scores of each wave -> per-query best 16 (keys, as tile_epilogue),
 // merged over the 8 waves through LDS -> the panel's best 16 rows per query.
-constexpr int SU = 8;   // loads in flight per wave (tools/f6_probe.hip: 8 + non-temporal = 74 % of HBM peak, 4 = 68 %)
+constexpr int SU = 8;   // loads in flight per wave (round-1 probe: 8 + non-temporal = 74 % of HBM peak, 4 = 68 %)
 
 template <bool NT = false>
 __device__ __forceinline__ f6t::i32x8 stream_frag(const char* stage, int j, int h, int row) {
@@ -710,14 +710,7 @@ __global__ void __launch_bounds__(256) sieve_arm_kernel(uint32_t* armed, int* co
 // (distance.py:60) of the survivors in coarse order, one wave per candidate (float4 loads, lane
 // partial sums, shuffle reduction), until the coarse bound proves the rest cannot reach the
 // k-th; (3) sort by (distance, index) and the certificate.
-// OFR_MERGE_PROBE_V: compile-time probe bits for tools/build_merge_probe.sh only (the library
-// build never defines it): 1 = bucket head instead of its best 16, 2 = no |q|^2 pass, 4 = no
-// exact re-rank -- each gives wrong results, to time the kernel's parts.
-#ifndef OFR_MERGE_PROBE_V
-#define OFR_MERGE_PROBE_V 0
-#endif
 __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
-  constexpr int V = OFR_MERGE_PROBE_V;
   __shared__ Cand lists[256 * KC];
   __shared__ double exact[KC];
   __shared__ double red[4];
@@ -738,12 +731,7 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     if (p.count) {
       const int64_t c = p.count[q];
       overflow = c > p.cap || c < 0;   // rows were dropped (and a tile-level overflow writes none): no candidates
-      if constexpr ((V & 1) != 0) {
-        if (threadIdx.x < KC) lists[threadIdx.x] = p.cand[(size_t)q * p.cap + threadIdx.x];
-        __syncthreads();
-      } else {
-        block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
-      }
+      block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
     } else {
       block_best(p.cand + (size_t)q * p.T * KC, p.T * KC, lists);
     }
@@ -751,7 +739,7 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     // bound by the memory latency, not the bytes
     constexpr int RU = 8;
     qq = 0;
-    for (int64_t j0 = threadIdx.x; (V & 2) == 0 && j0 < p.d; j0 += (int64_t)RU * blockDim.x) {
+    for (int64_t j0 = threadIdx.x; j0 < p.d; j0 += (int64_t)RU * blockDim.x) {
       float x[RU];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
@@ -810,7 +798,7 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     const int c = 4 * r + wave;
     const Cand cc = lists[c];
     double a = 0;
-    if (cc.i != CAND_EMPTY && (V & 4) == 0) {
+    if (cc.i != CAND_EMPTY) {
       const float* gr = p.G + (int64_t)cc.i * p.ldg;
       int64_t j0 = 0;
       if (vec) {
@@ -1468,48 +1456,35 @@ extern "C" const char* ofr_f6_sieve_kernel(void) {
 
 // Engine of the sieve pass: 384 = v_mfma_scale_f32_16x16x128 on 384 x 256 tiles, one wave per SIMD
 // (f6t::EngineW, default since round 3: 22.2 -> 20.1 ms); 16 = the same MFMA on 256 x 256 tiles, 8
-// waves (f6t::Engine16, OFR_F6_SHAPE=16; also the two-slice tier's engine).  Read at every call (the
-// workspace does not depend on it), so a test can run both sieve engines in one process.
+// waves (f6t::Engine16, OFR_F6_SHAPE=16: the comparison engine of tests/test_gpu_sieve.py).  Read at
+// every call (the workspace does not depend on it), so a test can run both sieve engines in one
+// process; any other value is an error (-1), not a silent default.
 static int f6_shape() {
   const char* e = getenv("OFR_F6_SHAPE");
-  return e && atoi(e) == 16 ? 16 : 384;
+  if (!e || !*e) return 384;
+  const int v = atoi(e);
+  return v == 16 || v == 384 ? v : -1;
 }
 
 // gallery tiles per tile group of the wide sieve pass (i8t::tile_coords): 2, so the ~32 workgroups
 // resident on one XCD cover 2 gallery x 16 query tiles (every query panel of a 4096 batch) -- same-box
 // A/B (profiles/r03_f6w_group_ab.log): 20.57-20.76 ms per pass at 2, 20.70 at 4, 21.2-21.4 at 3,
-// 21.6-21.7 at 8, 23.1-23.2 at 16.  OFR_F6W_GROUP overrides (probe)
-static int f6w_group() {
-  static const int g = [] {
-    const char* e = getenv("OFR_F6W_GROUP");
-    const int v = e ? atoi(e) : 0;
-    return v >= 1 && v <= 64 ? v : 2;
-  }();
-  return g;
-}
+// 21.6-21.7 at 8, 23.1-23.2 at 16.
+constexpr int F6W_GROUP = 2;
 
 // serpentine query order across the wide sieve pass's tile groups: the query panels a group ends on
 // are the ones the next group starts on, while their stages are still in the XCD's L2 -- same-box
 // A/B (profiles/r04_f6w_order_ab.txt): 60.0 -> 51.9 GB of L2<->fabric traffic per launch (FETCH_SIZE
-// x 2), 21.56 -> 21.45 ms.  OFR_F6W_SERP=0 restores the plain order (probe).
-static int f6w_serp() {
-  const char* e = getenv("OFR_F6W_SERP");
-  return e && atoi(e) == 0 ? 0 : 1;
-}
+// x 2), 21.56 -> 21.45 ms.
+constexpr int F6W_SERP = 1;
 
 // f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
 // thresholds, counts and buckets (each 256-byte aligned)
 struct SieveWs {
   size_t lists, theta, count, bucket, armed, bytes;
 };
-static int64_t sieve_stride() {
-  static const int64_t s = [] {
-    const char* e = getenv("OFR_SIEVE_STRIDE");
-    const long v = e ? atol(e) : 0;
-    return v >= 1 && v <= 4096 ? (int64_t)v : q8s::SIEVE_STRIDE;
-  }();
-  return s;
-}
+// the panel sample's stride (ofr_knn_f6: every 64th 256-row panel)
+static int64_t sieve_stride() { return q8s::SIEVE_STRIDE; }
 
 // Rank of the sample's key that becomes the sieve threshold theta (at least k).  theta only steers
 // the volume: the certificate's tau = min(theta, 16th kept key) bounds every row left out whatever
@@ -1518,12 +1493,8 @@ static int64_t sieve_stride() {
 // sieve hits and a shorter bucket for the merge), but a panel sample of a gallery stored identity by
 // identity holds whole clusters of one face (profiles/r04_sieve_stride_rank_ab.txt: ranks 4 and 8
 // leave queries uncertified).  A row sample (ofr_knn_f6_sampled) holds at most a row or two of any
-// cluster, and its 4th best key keeps ~4 x 64 rows.  OFR_SIEVE_RANK overrides both (read at every call).
-static int sieve_rank(bool rows) {
-  const char* e = getenv("OFR_SIEVE_RANK");
-  const int v = e ? atoi(e) : 0;
-  return v >= 1 && v <= q8s::KC ? v : rows ? q8s::SIEVE_RANK_ROWS : q8s::SIEVE_RANK;
-}
+// cluster, and its 4th best key keeps ~4 x 64 rows.
+static int sieve_rank(bool rows) { return rows ? q8s::SIEVE_RANK_ROWS : q8s::SIEVE_RANK; }
 
 // sample rows of an N-row gallery (ofr_knn_f6_sampled: at most this many)
 static int64_t sample_rows(int64_t N) { return cdiv(N > 0 ? N : 1, q8s::SAMPLE_STEP); }
@@ -1699,6 +1670,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   Cand* bucket = reinterpret_cast<Cand*>(wsb + w.bucket);
   uint32_t* armed = reinterpret_cast<uint32_t*>(wsb + w.armed);
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
+  OFR_CHECK_ARG(f6_shape() > 0, "ofr_knn_f6: OFR_F6_SHAPE must be 384 (default) or 16");
   if (phases & 1) phases |= 12;   // phase 1 = sample + thresholds (4), then the sieve (8)
   if (phases & 12) {
     if (!sieve) {   // HBM regime: one 32-query block, gallery streamed straight to VGPRs
@@ -1763,8 +1735,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       } else if (f6_shape() == 384) {
         q8s::TileArgs wa = a;   // 384-row gallery tiles over the same 256-row panel layout
         wa.ntg = cdiv(N, f6t::EngineW::TGW);
-        wa.gg = wa.ntg < f6w_group() ? wa.ntg : f6w_group();
-        wa.serp = f6w_serp();
+        wa.gg = wa.ntg < F6W_GROUP ? wa.ntg : F6W_GROUP;
+        wa.serp = F6W_SERP;
         OFR_CHECK_ARG(wa.ntq * wa.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
         if (two)
           hipLaunchKernelGGL(q8s::tile_kernel_f6w<3>, dim3((unsigned)(wa.ntq * wa.ntg)), dim3(f6t::EngineW::NT),

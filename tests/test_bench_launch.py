@@ -23,6 +23,21 @@ def test_gpus_flag_must_match_launcher_world_size():
     assert "--gpus 2 but WORLD_SIZE=1" in p.stderr
 
 
+def test_launch_ranks_stops_on_any_rank_failure():
+    """a crash of rank 1 while rank 0 is still running (e.g. blocked in a collective) must end
+    the launch at once with rank 1's status, not wait for rank 0."""
+    import time
+    sys.path.insert(0, ROOT)
+    import bench
+    child = [sys.executable, "-c",
+             "import os, sys, time\nif os.environ['RANK'] == '1': sys.exit(3)\ntime.sleep(120)"]
+    t0 = time.monotonic()
+    assert bench.launch_ranks(2, cmd=child, poll_s=0.05) == 3
+    assert time.monotonic() - t0 < 30
+    ok = [sys.executable, "-c", "import sys; sys.exit(0)"]
+    assert bench.launch_ranks(3, cmd=ok, poll_s=0.05) == 0
+
+
 @pytest.mark.gpu
 def test_bench_gpus_2_spawns_two_ranks():
     env = dict(os.environ, OFR_DIST_BACKEND="gloo", OFR_ONE_DEVICE="1")

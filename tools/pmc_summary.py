@@ -12,6 +12,7 @@ config matches its own run.
 """
 import collections
 import csv
+import datetime
 import json
 import os
 import shutil
@@ -54,7 +55,10 @@ def main():
     out = {
         "config": {"gallery": cfg["gallery"], "batch": cfg["global_batch"], "d": cfg["d"], "D": cfg["D"],
                    "k": cfg["k"],
-                   "search": "f6" if "fp6" in bench["dtype"] else ("q8" if "i8" in bench["dtype"] else "fp32")},
+                   "search": "f6" if "fp6" in bench["dtype"] else ("q8" if "i8" in bench["dtype"] else "fp32"),
+                   "w": "trained" if "trained" in cfg.get("workload", "") else "random"},
+        # bench.committed_traffic takes the newest summary of its config (file names do not order rounds)
+        "measured_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
         "kernel": " + ".join(knames), "launches": min(v["launches"] for v in per.values()), "rocprof_avg_ns": avg_ns,
         "bench_launch_ms": bench["roofline"].get("launch_ms"),
         "counters_per_launch": dict(c),
