@@ -79,6 +79,14 @@ def parse():
     ap.add_argument("--w", choices=["trained", "random"], default="trained",
                     help="trained: Fisherfaces W trained on configs[1]'s 100k faces (SURVEY §8d); random: N(0, 1/D)")
     ap.add_argument("--train-ids", type=int, default=10_000, help="identities of the W training set (x --per-id faces)")
+    ap.add_argument("--config4", type=int, default=1,
+                    help="1 GPU: train the headline's W through the reference API (PredictableModel(Fisherfaces(), "
+                         "NearestNeighbor()).compute on configs[1]'s faces) and report it as configs[4]; 0: the "
+                         "device-only training pipeline (untimed)")
+    ap.add_argument("--api", type=int, default=1,
+                    help="1 GPU, with --config4: configs[1] through PredictableModel.predict_batch on host faces")
+    ap.add_argument("--config3", type=int, default=1,
+                    help="1 GPU: configs[3] (LBPH: ExtendedLBP + SpatialHistogram + ChiSquare 1-NN) through the API")
     ap.add_argument("--search", choices=["f6", "q8", "fp32"], default="f6",
                     help="f6: certified fp6 coarse pass (uncertified queries go down the int8 tiers, then fp32); "
                          "q8: start at the certified int8 tier; fp32: fp32-MFMA pass")
@@ -90,13 +98,13 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(Wt, gallery, Xq, N_total, seconds):
+def cpu_baseline(P, gallery, Xq, N_total, seconds):
     """Reference-faithful oracle (classifier.py:104-108 loop, 1 Python thread) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import facerec_oracle as O  # the checker; timed here as the CPU baseline
     n_s = min(4000, gallery.N)
     G_s = gallery.G[:n_s, : gallery.d].double().cpu().numpy() + gallery.shift64.cpu().numpy()
-    W = Wt.double().cpu().numpy().T.copy()                   # D x d, float64 like the reference
+    W = P.weights_f64().cpu().numpy()                         # D x d, float64 like the reference
     X = Xq.cpu().numpy()
     t_proj, t_item, nq = 0.0, 0.0, 0
     deadline = time.perf_counter() + seconds
@@ -274,6 +282,166 @@ def certificate_margin(gallery, Qd, qq, nsample=64):
     return {"median": float(np.median(r)), "min": float(r.min()), "sample": int(len(r))}
 
 
+def train_config4(bank, per_id, n_train, H, W, device):
+    """configs[4] through the reference API, timed: PredictableModel(Fisherfaces(), NearestNeighbor(
+    EuclideanDistance(), k=1)).compute(list of n_train uint8 HxW faces, labels) -- thetrainer.py:113-124
+    + :176 (TheTrainer.get_model / train), model.py:49-51, feature.py:211-235.  The faces are configs[1]'s
+    training set (identities 0 .. n_train / per_id - 1, synthetic.gallery_chunks' seeds).  Returns the
+    model (its W is the headline's, its classifier the configs[1] gallery of the training features)
+    and the record: wall time, the device eigensolve split out (rocSOLVER dsygvd / dsyevd)."""
+    from ocvfacerec.facerec.classifier import NearestNeighbor
+    from ocvfacerec.facerec.distance import EuclideanDistance
+    from ocvfacerec.facerec.feature import Fisherfaces
+    from ocvfacerec.facerec.model import PredictableModel
+    from opencv_facerecognizer_amd import _device as dv
+    from opencv_facerecognizer_amd.synthetic import GALLERY_CHUNK
+    D = H * W
+    X = torch.empty((n_train, D), dtype=torch.uint8, device=device)
+    for c0 in range(0, n_train, GALLERY_CHUNK):
+        rows = torch.arange(c0, min(c0 + GALLERY_CHUNK, n_train), device=device)
+        X[c0:c0 + len(rows)] = bank.images(rows // per_id, seed=SEED + 1000 + c0 // GALLERY_CHUNK)
+    X_list = list(X.reshape(n_train, H, W).cpu().numpy())     # the reference's input: a list of 2-D images
+    del X
+    y = np.arange(n_train) // per_id
+    eig = {"sygv_dsygvd": 0.0, "eigh_dsyevd": 0.0}
+    saved = dv.sygv_desc_f64, dv.eigh_desc_f64
+
+    def timed(name, fn):
+        def w(*a, **kw):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            r = fn(*a, **kw)
+            torch.cuda.synchronize()
+            eig[name] += time.perf_counter() - t
+            return r
+        return w
+    dv.sygv_desc_f64, dv.eigh_desc_f64 = timed("sygv_dsygvd", saved[0]), timed("eigh_dsyevd", saved[1])
+    try:
+        model = PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=1))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        model.compute(X_list, y)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    finally:
+        dv.sygv_desc_f64, dv.eigh_desc_f64 = saved
+    ff = model.feature
+    rec = {"workload": f"configs[4]: PredictableModel(Fisherfaces(), NearestNeighbor(EuclideanDistance(), k=1))"
+                       f".compute on {n_train} faces of {n_train // per_id} identities, {H}x{W} (D={D})",
+           "wall_s": wall, "device_eigensolve_s": eig, "rest_s": wall - sum(eig.values()),
+           "regime": getattr(ff, "_regime", "?"), "d": int(ff._num_components),
+           "eigenvalues_head": [float(v) for v in np.asarray(ff._eigenvalues)[:4]],
+           "note": "wall includes the host list -> device upload and the host (d, 1) feature matrices the API "
+                   "returns; the W it trains is the headline's"}
+    del X_list
+    return model, rec
+
+
+def api_predict(model, bank, n_ids, B, H, W, device, reps=3):
+    """configs[1] through the reference API: PredictableModel.predict_batch (model.py:53-55 for a batch)
+    on a host list of B uint8 HxW faces against the model's own 100k-row gallery.  Wall clock per call
+    (stack + upload, projection, the certified search, the host results), and its parts."""
+    from ocvfacerec.facerec.classifier import results
+    gq = torch.Generator(device=device)
+    gq.manual_seed(SEED + 37)
+    ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
+    Xq = list(bank.images(ids_q, seed=SEED + 98).reshape(B, H, W).cpu().numpy())
+    model.predict_batch(Xq)                              # warm: the gallery's tiers, workspaces
+    torch.cuda.synchronize()
+    walls, parts = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        preds = model.predict_batch(Xq)
+        walls.append(time.perf_counter() - t0)
+    for _ in range(reps):                                # the same call in its three parts
+        t0 = time.perf_counter()
+        Xd = torch.from_numpy(np.stack([np.asarray(x).reshape(-1) for x in Xq])).to(device)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        d_, i_ = model._search_device(Xd)
+        dh, ih = d_.cpu().numpy(), i_.cpu().numpy()
+        t2 = time.perf_counter()
+        results(dh, ih, model.classifier.y)
+        t3 = time.perf_counter()
+        parts.append((t1 - t0, t2 - t1, t3 - t2))
+    ms = 1e3 * float(np.median(walls))
+    labels = np.array([p[0] for p in preds])
+    g = model.classifier._gallery()
+    pm = 1e3 * np.median(np.array(parts), axis=0)
+    return {"workload": f"configs[1] through PredictableModel.predict_batch: a host list of {B} uint8 {H}x{W} faces "
+                        f"against the trained model's {g.N}-row gallery",
+            "queries_per_s": B / (ms * 1e-3), "ms_per_call": ms,
+            "parts_ms": {"stack_and_upload": float(pm[0]), "projection_and_search": float(pm[1]),
+                         "results_host": float(pm[2])},
+            "uncertified_after_each_tier": list(g.last_fallbacks),
+            "top1_identity_acc": float(np.mean(labels == ids_q.cpu().numpy()))}
+
+
+def config3_run(device, N=65536, B=4096, per_id=8, reps=3):
+    """configs[3] through the reference API (tools/bench_lbph_model.py): PredictableModel(SpatialHistogram(
+    ExtendedLBP(1, 8), (8, 8)), NearestNeighbor(ChiSquareDistance(), k=1)).compute on N 128x128 faces, then
+    predict_batch of B query faces (feature.py:266-305, lbp.py:80-130, distance.py:112-116).  The chi2 pass's
+    roofline: 16 fp16 MFMA flops per (pair, bin) of the low-rank form against 2.5 PF dense."""
+    from ocvfacerec.facerec.classifier import NearestNeighbor
+    from ocvfacerec.facerec.distance import ChiSquareDistance
+    from ocvfacerec.facerec.feature import SpatialHistogram
+    from ocvfacerec.facerec.lbp import ExtendedLBP
+    from ocvfacerec.facerec.model import PredictableModel
+    H = 128
+    n_ids = (N + per_id - 1) // per_id
+    bank = IdentityBank(n_ids, H, H, device=device)
+    Xg = bank.images(torch.arange(N, device=device) // per_id, seed=SEED + 11).reshape(N, H, H).cpu().numpy()
+    gq = torch.Generator(device=device)
+    gq.manual_seed(SEED + 12)
+    ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
+    Xq = bank.images(ids_q, seed=SEED + 13).reshape(B, H, H).cpu().numpy()
+    model = PredictableModel(SpatialHistogram(ExtendedLBP(1, 8), (8, 8)), NearestNeighbor(ChiSquareDistance(), k=1))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    model.compute(list(Xg), np.arange(N) // per_id)
+    torch.cuda.synchronize()
+    t_compute = time.perf_counter() - t0
+    del Xg
+    model.predict_batch(Xq)
+    torch.cuda.synchronize()
+    walls = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        preds = model.predict_batch(Xq)
+        walls.append(time.perf_counter() - t0)
+    sh, clf = model.feature, model.classifier
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    Qd = torch.from_numpy(Xq).to(device)
+    ms_h, ms_s = [], []
+    for _ in range(reps):
+        e[0].record()
+        C, cell, cb = sh.counts_batch(Qd)
+        e[1].record()
+        clf.search_counts(C, cell, cb, 1)
+        e[2].record()
+        torch.cuda.synchronize()
+        ms_h.append(e[0].elapsed_time(e[1]))
+        ms_s.append(e[1].elapsed_time(e[2]))
+    g = clf._gallery()
+    ms = 1e3 * float(np.median(walls))
+    flops = 16.0 * B * N * 16384
+    ms_s_med = float(np.median(ms_s))
+    labels = np.array([p[0] for p in preds])
+    out = {"workload": f"configs[3]: PredictableModel(SpatialHistogram(ExtendedLBP(1, 8), (8, 8)), NearestNeighbor("
+                       f"ChiSquareDistance(), k=1)): compute on {N} faces {H}x{H}, predict_batch of {B}",
+           "queries_per_s": B / (ms * 1e-3), "ms_per_call": ms, "compute_s": t_compute,
+           "device_ms": {"query_histograms": float(np.median(ms_h)), "chi2_search": ms_s_med},
+           "chi2_roofline": {"kernel": "c2m::chi2_mfma_kernel + merge (ofr_chi2_knn, whole search)", "bound": "mfma",
+                             "achieved": flops / (ms_s_med * 1e-3) / 1e12, "peak": 2500.0, "unit": "TFLOP/s",
+                             "frac": flops / (ms_s_med * 1e-3) / 2.5e15,
+                             "algorithmic_flops": flops},
+           "chi2_uncertified_after_each_pass": list(g.last_fallbacks),
+           "top1_identity_acc": float(np.mean(labels == ids_q.cpu().numpy()))}
+    del model, clf, sh, g
+    torch.cuda.empty_cache()
+    return out
+
+
 def feature_profile(gallery, rows=8192):
     """How the centred gallery features spread over the 32-feature blocks (the fp6 tier quantizes a
     row with ONE scale, so a row whose energy sits in a few blocks loses the rest to the step size),
@@ -429,14 +597,30 @@ def main():
     # the trained W's training set (configs[1]: identities 0 .. train_ids - 1) may reach past a small gallery's
     bank = IdentityBank(max(n_ids, args.train_ids if args.w == "trained" else 0), H, W, device=device)
     w_info = {"kind": "random N(0, 1/D)"}
-    if args.w == "trained":
+    c4 = api = None
+    if args.w == "trained" and world == 1 and args.config4:
+        # configs[4]: the reference API trains the W (timed); then configs[1] through the API on its model
+        model1, c4 = train_config4(bank, args.per_id, args.train_ids * args.per_id, H, W, device)
+        log(rank, f"configs[4]: {c4['wall_s']:.2f} s ({c4['device_eigensolve_s']})")
+        P = model1.feature._proj()
+        Wt = None
+        w_info = {"kind": "Fisherfaces() trained on configs[1]'s faces through PredictableModel.compute",
+                  "regime": c4["regime"], "n_train": args.train_ids * args.per_id, "identities": args.train_ids,
+                  "d": c4["d"], "eigenvalues_head": c4["eigenvalues_head"], "train_s": c4["wall_s"]}
+        if args.api:
+            api = api_predict(model1, bank, args.train_ids, B, H, W, device)
+            log(rank, f"api: {api['queries_per_s']:.0f} q/s {api['parts_ms']}")
+        model1.classifier.__dict__.pop("_dev", None)             # the 100k gallery; P (the W) stays
+        del model1
+        torch.cuda.empty_cache()
+    elif args.w == "trained":
         P, Wt, w_info = build_trained_projection(bank, args.per_id, args.train_ids * args.per_id, D, device)
         w_info["kind"] = "Fisherfaces() trained on configs[1]'s faces"
-        if P.d != d:
-            raise SystemExit(f"trained W has d={P.d}, --dim {d}: pass --dim {P.d}")
-        log(rank, f"trained W: {w_info}")
     else:
         P, Wt = build_projection(D, d, device)
+    if P.d != d:
+        raise SystemExit(f"W has d={P.d}, --dim {d}: pass --dim {P.d}")
+    log(rank, f"W: {w_info}")
     ld = max(32, round_up(d, 32))
     gallery = build_gallery(P, bank, args.per_id, n0, nl, N, d, ld, device)
     gq = torch.Generator(device=device)
@@ -683,11 +867,13 @@ def main():
             "top1_identity_acc": acc,
             "certificate_margin_fp6": margin,
             "projection_w": w_info,
+            "config4": c4,
+            "api": api,
             "feature_profile": feature_profile(gallery) if args.search == "f6" else None,
             "small_batch": small,
         }
         if world == 1 and not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(Wt, gallery, Xq, N, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(P, gallery, Xq, N, args.cpu_seconds)
             result["speedup_vs_cpu"] = value / result["cpu_baseline"]["value"]
         if world == 1 and args.search == "f6" and (args.stress.strip() or args.config1):
             gallery.q8, gallery.G, gallery._Gbuf = None, None, None      # free the headline gallery first
@@ -703,6 +889,13 @@ def main():
             for r in result["stress"]:
                 log(rank, f"stress noise {r['pixel_noise']}: {r['queries_per_s']:.0f} q/s, uncertified "
                           f"{r['uncertified_after_each_tier']}, margin {r['certificate_margin_fp6']}")
+        if world == 1 and args.config3:
+            del gallery
+            torch.cuda.empty_cache()
+            result["config3"] = config3_run(device)
+            log(rank, f"configs[3]: {result['config3']['queries_per_s']:.0f} q/s")
+        if result.get("config1") and api:
+            api["vs_engine_config1"] = api["queries_per_s"] / result["config1"]["queries_per_s"]
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

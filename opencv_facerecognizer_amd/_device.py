@@ -120,6 +120,16 @@ class Projection:
         call("ofr_qproj_prepare", stream(), dt, ptr(Wt), self.d, self.D, Wt.shape[1], ptr(self.Aq), self.ldk,
              ptr(self.scale), ptr(self.K))
         self.ldy = max(32, round_up(self.d, 32))
+        self._Wt_src = Wt_device             # the caller's W^T (device), or None: weights_f64 rebuilds W from it
+
+    def weights_f64(self):
+        """W (D x d) as fp64 on the device: the training's fp64 W (_W64, set by Fisherfaces._prime_proj), else
+        the W^T this projection was made from."""
+        if getattr(self, "_W64", None) is not None:
+            return self._W64
+        if self._Wt_src is not None:
+            return self._Wt_src[:, :self.D].double().t()
+        return f64_dev(np.asarray(self.W_host, np.float64))
 
     def project(self, Xd, shift64=None, out=None, f64=False):
         """Xd: uint8 [B][ldx] device rows.  fp32 [B][ldy] (zero pad) or fp64 [B][d]."""
