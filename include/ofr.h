@@ -302,6 +302,19 @@ int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ld
                  int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
                  size_t workspace_bytes, const uint8_t* bscale);
 
+/* Any k (round 5; replaces NearestNeighbor.predict classifier.py:104-119 for the k the tiers
+ * above do not serve -- they keep 16 candidates per tile): the reference's distance of every
+ * (query, row) pair in fp64 (Euclidean distance.py:57-60, Cosine :74-77 with NaN for a zero row,
+ * ChiSquare :112-116), then per query the k smallest by (distance, row), NaN last.  Q [B][ldq] of
+ * qdtype, G [N][ldg] of gdtype (OFR_DT_*; integer rows are counts, value = count / denom as the
+ * reference's float64 histograms; denom 1 for float rows).  out_d / out_i [B][k]; entries past
+ * min(k, N) are (+inf, -1).  min(k, N) <= 4096 (else OFR_E_UNSUPPORTED).  Workspace
+ * ofr_knn_deep_workspace_bytes(B, N) bytes (a block of the distance matrix, <= 2 GiB).          */
+size_t ofr_knn_deep_workspace_bytes(int64_t B, int64_t N);
+int ofr_knn_deep(void* stream, int metric, const void* Q, int64_t B, int64_t ldq, int qdtype, const void* G,
+                 int64_t N, int64_t ldg, int gdtype, int64_t d, double denom, int k, int64_t index_base,
+                 double* out_d, int64_t* out_i, void* workspace, size_t workspace_bytes);
+
 /* Merge P sorted (distance, index) lists per query into the best k:
  * in_d/in_i [B][P*kin] (list p at columns [p*kin, (p+1)*kin)), ascending by
  * (distance, index); out [B][k].  Used after the RCCL all-gather of per-rank

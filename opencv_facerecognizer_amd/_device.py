@@ -753,6 +753,8 @@ class FloatGallery:
         return self._search_f32(Qd, k, index_base)
 
     def _search_f32(self, Qd, k, index_base=0):
+        if k > _lib.MAX_K:
+            return search_deep(self.metric, Qd, _lib.DT_F32, self.G, _lib.DT_F32, self.d, 1.0, k, index_base)
         B = Qd.shape[0]
         out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
         out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)
@@ -878,8 +880,12 @@ class Chi2Gallery:
         """Certified ChiSquare top-k: the fp32 VALU pass with its error bound; the queries it cannot
         certify are re-run with fp64 per-term arithmetic (ofr_chi2_knn_exact).  self.last_fallbacks
         = (uncertified after the fp32 pass, uncertified after the exact pass: near-ties at fp32 key
-        resolution, 2^-23 relative)."""
+        resolution, 2^-23 relative).  k > 16: the exact any-k pass (search_deep)."""
         B = Qd.shape[0]
+        if k > _lib.MAX_K:
+            self.last_fallbacks = (0,)
+            return search_deep(_lib.METRIC_CHISQUARE, Qd, self.dtype, self.G, self.dtype, self.nbins, self.denom, k,
+                               index_base)
         out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
         out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)
         cert = torch.empty(B, dtype=torch.int32, device=Qd.device)
@@ -911,6 +917,20 @@ class Chi2Gallery:
         if self.dtype != _lib.DT_F32:
             return self.counts_rows(arr)
         return f32_rows(np.asarray(arr, np.float64), ld=self.G.shape[1])
+
+
+def search_deep(metric, Q, qdtype, G, gdtype, d, denom, k, index_base=0):
+    """Any k (> 16 in practice): the reference's distance of every (query, row) pair in fp64 and the k
+    smallest per query by (distance, row), NaN last (ofr_knn_deep; classifier.py:104-119, distance.py).
+    Q [B][>= d], G [N][>= d] device rows of the given OFR dtypes (counts: value = count / denom).
+    Returns (fp64 [B][k], int64 [B][k]); entries past N are (+inf, -1)."""
+    B, N = int(Q.shape[0]), int(G.shape[0]) if G is not None else 0
+    out_d = torch.empty((B, k), dtype=torch.float64, device=Q.device)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=Q.device)
+    ws = Workspace().get(_lib.load().ofr_knn_deep_workspace_bytes(B, N), Q.device) if N else None
+    call("ofr_knn_deep", stream(), metric, ptr(Q), B, Q.shape[1], qdtype, ptr(G), N, G.shape[1] if N else d, gdtype,
+         d, float(denom), int(k), index_base, ptr(out_d), ptr(out_i), ptr(ws), 0 if ws is None else ws.numel())
+    return out_d, out_i
 
 
 def topk_pack(d, i, bound=None):
