@@ -223,6 +223,7 @@ def test_f6_quantize_rows_vs_host(R, d, spread):
         X[2] = 0                                                          # all-zero row
         X[1, 0] = 1e6                                                     # one huge feature
     bs, f = _block_scales_host(d, R + d, spread)
+    X = (X * f).astype(np.float32)          # columns spread like the scales (a trained W's feature profile)
     ldx = d + 5
     Xd = torch.zeros((R, ldx), dtype=torch.float32, device="cuda")
     Xd[:, :d] = torch.from_numpy(X).cuda()
@@ -271,6 +272,7 @@ def test_f6x2_quantize_rows_vs_host(R, d, spread):
         X[2] = 0
         X[1, 0] = 1e6
     bs, f = _block_scales_host(d, R * 3 + d, spread)
+    X = (X * f).astype(np.float32)          # columns spread like the scales (a trained W's feature profile)
     ldx = d + 3
     Xd = torch.zeros((R, ldx), dtype=torch.float32, device="cuda")
     Xd[:, :d] = torch.from_numpy(X).cuda()
