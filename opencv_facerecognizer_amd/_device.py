@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 import numpy as np
 import torch
@@ -69,6 +70,62 @@ def u8_rows(a, device=None):
     out = torch.zeros((n, ldx), dtype=torch.uint8, device=device)
     out[:, :D] = t
     return out
+
+
+class _PinnedStage:
+    """Page-locked staging for host face batches (predict_batch / compute on a host list of images): the
+    items are stacked chunk by chunk into one of two 8 MiB pinned halves while the other half's copy to
+    the device runs, so neither a fresh pageable stack (page faults on 41 MB at B = 4,096) nor a
+    synchronous pageable copy sits on the call's path, and the pinned memory stays 16 MiB whatever
+    the batch.  One stage per process; a lock serialises its users; per half an event keeps the host
+    from overwriting bytes a copy (of this call or an earlier one) still reads."""
+
+    HALF = 8 << 20
+
+    def __init__(self):
+        self.buf = None
+        self.ev = [None, None]
+        self.lock = threading.Lock()
+
+    def upload(self, items, D, device):
+        n = len(items)
+        ldx = round_up(max(D, 1), 16)
+        out = torch.empty((n, ldx), dtype=torch.uint8, device=device)
+        if ldx != D:
+            out[:, D:] = 0
+        rows = max(1, self.HALF // max(D, 1))
+        shape = np.asarray(items[0]).shape
+        with self.lock:
+            if self.buf is None or self.buf.numel() < 2 * rows * D:
+                self.buf = torch.empty(2 * max(rows * D, self.HALF), dtype=torch.uint8, pin_memory=True)
+                self.ev = [None, None]
+            half = self.buf.numel() // 2
+            host = self.buf.numpy()
+            for j, c0 in enumerate(range(0, n, rows)):
+                c1, h = min(n, c0 + rows), j & 1
+                if self.ev[h] is not None:
+                    self.ev[h].synchronize()
+                np.stack(items[c0:c1], out=host[h * half:h * half + (c1 - c0) * D].reshape((c1 - c0,) + shape))
+                out[c0:c1, :D].copy_(self.buf[h * half:h * half + (c1 - c0) * D].view(c1 - c0, D), non_blocking=True)
+                self.ev[h] = torch.cuda.Event()
+                self.ev[h].record()
+        return out
+
+
+_STAGE = _PinnedStage()
+
+
+def upload_u8_items(items, device=None):
+    """A host list of equally-shaped uint8 images -> device rows [n][round_up(D, 16)] through the pinned
+    staging buffer; None when the items are not such a list (the caller stacks them itself)."""
+    if not len(items) or isinstance(items, np.ndarray):
+        return None
+    first = np.asarray(items[0])
+    if first.dtype != np.uint8 or type(items[0]) is not np.ndarray:
+        return None
+    if any(type(x) is not np.ndarray or x.dtype != np.uint8 or x.shape != first.shape for x in items):
+        return None
+    return _STAGE.upload(items, int(first.size), device or dev())
 
 
 def u8_images(a, device=None):

@@ -354,16 +354,25 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
 // stages (p.G2 / p.Q2 the second slices).  The epilogue is sieve_epilogue16's for the 192 x 128
 // wave tile: element r of acc[i][c] of lane l is gallery row WR*192 + 16 i + 4 (l / 16) + r, query
 // WC*128 + 16 c + l % 16.
+// The wave's main loop (its copy-piece offsets compile-time: one body per wave index W) ...
 template <int W, int NSEG>
-__device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t g0, int64_t q0) {
+__device__ __forceinline__ void f6w_main(const TileArgs& p, int64_t g0, int64_t q0,
+                                         f6t::f32x4 (&acc)[f6t::EngineW::NA][f6t::EngineW::NB]) {
   using E = f6t::EngineW;
-  f6t::f32x4 acc[E::NA][E::NB];
-  constexpr int WR = W >> 1;
   E::Feed f;
   E::feed_init<W, NSEG>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ,
                         p.nk / NSEG, g0 / E::TGW, reinterpret_cast<const char*>(p.G2),
                         reinterpret_cast<const char*>(p.Q2), p.bs);
   E::mainloop<W, NSEG>(f, p.nk / NSEG, acc);
+}
+
+// ... and the sieve epilogue, ONE copy for the four waves (the wave's row / column offsets at run time):
+// four specialised copies of its ~4,000 instructions (the 384 unrolled hit sites) overflowed the
+// instruction cache every tile.
+__device__ __forceinline__ void f6w_epilogue(char* smem, const TileArgs& p, int64_t g0, int64_t q0, int wave,
+                                             f6t::f32x4 (&acc)[f6t::EngineW::NA][f6t::EngineW::NB]) {
+  using E = f6t::EngineW;
+  const int WR = wave >> 1;
   float* gtab = reinterpret_cast<float*>(smem);                                   // [384][2]
   uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + E::TGW * 8);
   uint2* hits = reinterpret_cast<uint2*>(smem + E::TGW * 8 + 16);                 // [HCAPW]
@@ -377,7 +386,7 @@ __device__ __forceinline__ void f6w_body(char* smem, const TileArgs& p, int64_t 
     gtab[2 * r + 1] = ok ? p.gscale[g0 + r] : 0.f;
   }
   if (threadIdx.x == 0) *nhit = 0;
-  const int lane = threadIdx.x & 63, wc = W & 1, g4 = (lane >> 4) * 4, r16 = lane & 15;
+  const int lane = threadIdx.x & 63, wc = wave & 1, g4 = (lane >> 4) * 4, r16 = lane & 15;
   float sq2[E::NB], th[E::NB];
 #pragma unroll
   for (int c = 0; c < E::NB; ++c) {
@@ -444,11 +453,26 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   // serpentine: the last query panels of a group are the first of the next, while still in L2
   if (p.serp && ((t / (p.gg * p.ntq)) & 1)) qt = p.ntq - 1 - qt;
   const int64_t g0 = gt * E::TGW, q0 = qt * f6t::TQ;
-  switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
-    case 0: f6w_body<0, NSEG>(smem, p, g0, q0); break;
-    case 1: f6w_body<1, NSEG>(smem, p, g0, q0); break;
-    case 2: f6w_body<2, NSEG>(smem, p, g0, q0); break;
-    default: f6w_body<3, NSEG>(smem, p, g0, q0); break;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  f6t::f32x4 acc[E::NA][E::NB];
+  if constexpr (NSEG == 1) {
+    switch (wave) {   // the wave's role, compile time in the main loop
+      case 0: f6w_main<0, NSEG>(p, g0, q0, acc); break;
+      case 1: f6w_main<1, NSEG>(p, g0, q0, acc); break;
+      case 2: f6w_main<2, NSEG>(p, g0, q0, acc); break;
+      default: f6w_main<3, NSEG>(p, g0, q0, acc); break;
+    }
+    f6w_epilogue(smem, p, g0, q0, wave, acc);
+  } else {
+    // the two-slice pass keeps one epilogue per wave: compiled shared, its extra segment registers
+    // spill and the epilogue read one accumulator (row block 7, query block 7) wrongly
+    // (tools/diag_f6x2_engines.py, profiles/r05_diag_f6x2.txt)
+    switch (wave) {
+      case 0: f6w_main<0, NSEG>(p, g0, q0, acc); f6w_epilogue(smem, p, g0, q0, 0, acc); break;
+      case 1: f6w_main<1, NSEG>(p, g0, q0, acc); f6w_epilogue(smem, p, g0, q0, 1, acc); break;
+      case 2: f6w_main<2, NSEG>(p, g0, q0, acc); f6w_epilogue(smem, p, g0, q0, 2, acc); break;
+      default: f6w_main<3, NSEG>(p, g0, q0, acc); f6w_epilogue(smem, p, g0, q0, 3, acc); break;
+    }
   }
 }
 

@@ -82,6 +82,10 @@ def _stack_rows(X):
 
 def _device_rows(X):
     """Items -> (device rows, D, kind): uint8 images use the u8 layout, everything else fp64."""
+    if isinstance(X, (list, tuple)):
+        Xd = _device.upload_u8_items(X)             # a host list of uint8 faces: pinned, overlapped upload
+        if Xd is not None:
+            return Xd, int(np.asarray(X[0]).size), "u8"
     A = _stack_rows(X)
     if A.dtype == np.uint8:
         return _device.u8_rows(A), A.shape[1], "u8"
@@ -140,6 +144,10 @@ class _DeviceProjMixin:
             if X.dtype != torch.uint8:
                 raise TypeError("device face batches must be uint8")
             return P.project(_device.u8_rows(X), shift64=sh, f64=f64)
+        if isinstance(X, (list, tuple)):
+            Xd = _device.upload_u8_items(X)         # a host list of uint8 faces: pinned, overlapped upload
+            if Xd is not None:
+                return P.project(Xd, shift64=sh, f64=f64)
         A = X if isinstance(X, np.ndarray) and X.ndim == 2 and not isinstance(X, np.matrix) else _stack_rows(X)
         if A.dtype == np.uint8:
             return P.project(_device.u8_rows(A), shift64=sh, f64=f64)

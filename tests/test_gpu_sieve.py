@@ -268,14 +268,16 @@ def test_row_sample_extended_by_append():
     assert torch.equal(i_, i2) and torch.allclose(d_, d2, rtol=1e-9)
 
 
-def test_f6x2_wide_engine_matches_8wave_engine(monkeypatch):
-    """The two-slice tier's sieve pass on the wide engine (tile_kernel_f6w<3>, default) keeps exactly the
-    rows, with exactly the keys, of the 8-wave engine (tile_kernel_f6s<3>, OFR_F6_SHAPE=16): both sum
-    the same 16x16x128 MFMAs stage by stage in the same order.  Crowded data (the tier's use), d = 320
-    (3 stages per segment, a partial last stage), a partial last gallery tile and query panel."""
+@pytest.mark.parametrize("tier", ["f6", "f6x2"])
+def test_wide_engine_matches_8wave_engine(monkeypatch, tier):
+    """Both fp6 tiers: the wide engine's sieve pass (tile_kernel_f6w, default; round 5: the fp6 tier's
+    epilogue is one copy shared by its four waves) keeps exactly the rows, with exactly the keys, of the
+    8-wave engine (OFR_F6_SHAPE=16): they sum the same 16x16x128 MFMAs stage by stage in the same order.
+    Clustered data (the fp6 tier: well separated; f6x2: crowded), d = 320 (a partial last stage), a
+    partial last gallery tile and query panel, so every wave and query block of the tile is checked."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
-    G, Q = _clustered(2003, 9, 320, 300, 31)
+    G, Q = _clustered(2003, 9, 320, 300, 31 if tier == "f6x2" else 32)
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     Qd = g.query_rows(Q)
     state, res = {}, {}
@@ -284,7 +286,7 @@ def test_f6x2_wide_engine_matches_8wave_engine(monkeypatch):
             monkeypatch.setenv("OFR_F6_SHAPE", "16")
         else:
             monkeypatch.delenv("OFR_F6_SHAPE", raising=False)
-        qq = g.quantize_queries(Qd, tier="f6x2")
+        qq = g.quantize_queries(Qd, tier=tier)
         out = g.search_q8_phase(4 | 8 | 2, Qd, qq, 4)
         torch.cuda.synchronize()
         theta, count, keys, rows = g.sieve_state(len(Q))
