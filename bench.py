@@ -646,7 +646,8 @@ def main():
     # all-gathered (fp6 panels need whole 256-row blocks per rank)
     b0, b1 = shard_range(B, rank, world)
     shard_prep = world > 1 and B % world == 0 and (tier0 != "f6" or (B // world) % 256 == 0)
-    starts = []              # the first tier of every batch (one device)
+    starts = []              # the first tier of every batch (FloatGallery.start_tier; sharded too: every rank
+                             # keeps the same global failure statistics, certify_sharded)
     # the step pipeline (StepPipeline): three query buffers, each with its own result lists
     bufs = [dict(Qd=Qd if j == 0 else torch.zeros_like(Qd), qq=None, pending=None, qq_loc=None,
                  out=out if j == 0 else tuple(torch.empty_like(t) for t in out),
@@ -659,7 +660,9 @@ def main():
         if shard_prep:
             P.project(Xq[b0:b1], shift64=gallery.shift64, out=b["Qd_loc"])   # this rank's faces
             if use_q8:
-                b["qq_loc"] = gallery.quantize_queries(b["Qd_loc"], b["qq_loc"], tier=tier0)
+                tier = gallery.start_tier(B) if tier0 == "f6" else tier0
+                starts.append(str(tier))
+                b["qq_loc"] = gallery.quantize_queries(b["Qd_loc"], b["qq_loc"], tier=tier)
                 b["qq"] = gallery.gather_queries(b["qq_loc"])
                 # the fp32 rows are read from phase 2 on: their all-gather overlaps the tile pass
                 b["pending"] = gather_rows_async(b["Qd_loc"])
@@ -668,8 +671,8 @@ def main():
                 b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
         else:
             P.project(Xq, shift64=gallery.shift64, out=b["Qd"])          # fp32(W^T x - c), exact int8 MFMA
-            if use_q8:       # one device: the adaptive start tier (FloatGallery.start_tier; f6 here)
-                tier = gallery.start_tier(B) if tier0 == "f6" and world == 1 else tier0
+            if use_q8:       # the adaptive start tier (FloatGallery.start_tier; f6 here)
+                tier = gallery.start_tier(B) if tier0 == "f6" else tier0
                 starts.append(str(tier))
                 b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier)
 

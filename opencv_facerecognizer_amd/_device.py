@@ -585,14 +585,15 @@ class FloatGallery:
         the ranks, rank-major).  The fp6 tiles concatenate only whole 256-row panels: every rank's
         block must be a multiple of 256 rows (int8 tiers: any equal split)."""
         from .parallel import gather_rows
-        if qq["tier"] == "f6" and qq["B"] % 256:
+        if qq["tier"] in ("f6", "f6x2") and qq["B"] % 256:
             raise ValueError("fp6 query tiles gather whole 256-row panels: rows per rank must be a multiple of 256")
         # scales (fp32, exact in fp64) and stats travel as one [rows][4] fp64 block: two collectives, not three
         side = gather_rows(torch.cat([qq["scale"].to(torch.float64).reshape(-1, 1), qq["stats"]], 1).contiguous(), group)
         B = side.shape[0]
+        extra = {"Qs2": gather_rows(qq["Qs2"], group)} if qq["tier"] == "f6x2" else {}
         return dict(Qs=gather_rows(qq["Qs"], group), scale=side[:, 0].to(torch.float32).contiguous(),
                     stats=side[:, 1:].contiguous(), cert=torch.empty(B, dtype=torch.int32, device=side.device),
-                    bound=torch.empty(B, dtype=torch.float64, device=side.device), tier=qq["tier"], B=B)
+                    bound=torch.empty(B, dtype=torch.float64, device=side.device), tier=qq["tier"], B=B, **extra)
 
     def search_q8_phase(self, phases, Qd, qq, k, index_base=0, out=None, workspace=None):
         """phases 1 = quantized tiles, 2 = merge + exact re-rank + certificate (cert in qq["cert"]), 3 = both.

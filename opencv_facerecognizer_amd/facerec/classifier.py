@@ -318,7 +318,9 @@ class NearestNeighbor(AbstractClassifier):
         B = int(Qd.shape[0])
         n0 = getattr(g, "index_base", 0)
         if isinstance(g, FloatGallery) and g.metric == _lib.METRIC_EUCLIDEAN and g.use_q8(B, k):
-            qq = g.quantize_queries(Qd, tier=g.first_tier())
+            # adaptive start tier: every rank holds the same global failure statistics (certify_sharded)
+            g.last_start_tier = g.start_tier(B)
+            qq = g.quantize_queries(Qd, tier=g.last_start_tier)
             out = g.search_q8_phase(1, Qd, qq, k, n0)
             merge_sharded(g, Qd, qq, k, n0, out, group)
             (md, mi), counts = certify_sharded(g, Qd, qq, k, out, n0, group)

@@ -202,6 +202,9 @@ def certify_sharded(gallery, Qd, qq, k, out, index_base, group=None):
     rows = open_rows(cert)
     counts = [int(rows.numel())]
     tier = qq["tier"]
+    # the adaptive start tier's statistics (FloatGallery.start_tier): the counts are global -- the same on
+    # every rank -- so every rank's gallery takes the same start-tier decisions and the collectives match
+    gallery.note_failures(tier, int(qq["B"]), counts[0])
     while rows.numel():
         tier = gallery.next_tier(tier, int(rows.numel()))
         sub = Qd.index_select(0, rows).contiguous()
@@ -218,6 +221,7 @@ def certify_sharded(gallery, Qd, qq, k, out, index_base, group=None):
             break
         still = open_rows(c2)
         counts.append(int(still.numel()))
+        gallery.note_failures(tier, int(rows.numel()), counts[-1])
         rows = rows.index_select(0, still)
     return (md, mi), counts
 

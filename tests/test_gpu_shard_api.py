@@ -213,3 +213,82 @@ def test_pruned_merge_equals_plain_merge(sharded):
         assert skipped >= 100, skipped      # of 300 queries, about half belong to the other shard
     Q, G, _ = _identity_blocks()
     _check_search("EuclideanDistance", Q, G, sharded[0]["pruned"][3], sharded[0]["pruned"][4], K)
+
+
+# ---------------------------------------------------------------------------
+# the adaptive start tier on a sharded gallery (VERDICT r4 "do this" #6)
+# ---------------------------------------------------------------------------
+def _crowded():
+    """tests/test_gpu_pipeline.py's clusters (>= 90 % of the fp6 tier's queries uncertified)."""
+    r = np.random.default_rng(3)
+    d, K_, per, B = 128, 200, 40, 300
+    mu = r.normal(0, 1, (K_, d))
+    G = (mu[np.arange(K_ * per) % K_] + r.normal(0, 0.5, (K_ * per, d))).astype(np.float32).astype(np.float64)
+    Q = (mu[r.integers(0, K_, B)] + r.normal(0, 0.5, (B, d))).astype(np.float32).astype(np.float64)
+    return Q, G, np.arange(K_ * per) % K_
+
+
+def _adaptive_worker(rank, ws, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from ocvfacerec.facerec.classifier import NearestNeighbor
+        from ocvfacerec.facerec.distance import EuclideanDistance
+        from opencv_facerecognizer_amd._device import FloatGallery
+        Q, G, y = _crowded()
+        res = {}
+        for mode in ("0", "1"):
+            os.environ["OFR_ADAPTIVE_TIER"] = mode
+            clf = NearestNeighbor(EuclideanDistance(), k=2)
+            clf.compute(list(G), y)
+            clf.shard()
+            starts, outs = [], []
+            for _ in range(FloatGallery.REPROBE + 1):
+                d, i = clf.search(Q)
+                g = clf._gallery()
+                starts.append(g.last_start_tier)
+                outs.append((d, i, tuple(g.last_fallbacks)))
+            res[mode] = (starts, outs)
+        out.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_sharded_adaptive_start_tier_matches_fixed_chain():
+    """2 gloo ranks on one device, crowded clusters: with the adaptive start tier both ranks switch to
+    the two-slice tier after the first batch and re-probe fp6 every REPROBE-th batch -- identically,
+    since the failure counts they learn from are the global certificate's -- and every batch's global
+    top-k equals the fixed-start chain's bit for bit (classifier.py:104-119)."""
+    import torch.multiprocessing as mp
+    from opencv_facerecognizer_amd._device import FloatGallery
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_adaptive_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, r = q.get(timeout=500)
+        res[rank] = r
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        fixed_starts, fixed = res[rank]["0"]
+        starts, outs = res[rank]["1"]
+        assert all(s == "f6" for s in fixed_starts), fixed_starts
+        assert fixed[0][2][0] >= 0.9 * 300, fixed[0][2]                # the fp6 tier fails (crowded)
+        assert starts[0] == "f6" and starts[1] == "f6x2", starts
+        assert starts[FloatGallery.REPROBE - 1] == "f6" and starts.count("f6") == 2, starts
+        for (d, i, _), (dw, iw, _) in zip(outs, fixed):
+            assert np.array_equal(i, iw) and np.array_equal(d, dw)
+    assert res[0]["1"][0] == res[1]["1"][0]                           # both ranks switch identically
+    for (d0, i0, c0), (d1, i1, c1) in zip(res[0]["1"][1], res[1]["1"][1]):
+        assert np.array_equal(i0, i1) and np.array_equal(d0, d1) and c0 == c1
+    oracle_i = np.argsort(O.pairwise("EuclideanDistance", *_crowded()[:2]), axis=1, kind="stable")[:, :2]
+    got = res[0]["1"][1][0][1]
+    assert (np.sort(got, 1) == np.sort(oracle_i, 1)).mean() > 0.99   # exact top-2 (up to oracle near-ties)

@@ -156,6 +156,10 @@ class _MockShardGallery:
     def __init__(self, G, n0, overflow=()):
         self.G, self.n0 = G, n0
         self.overflow = np.asarray(overflow, dtype=np.int64)   # first-tier queries whose sieve bucket overflows
+        self.noted = []                                        # the adaptive start tier's statistics
+
+    def note_failures(self, tier, B, failed):
+        self.noted.append((str(tier), int(B), int(failed)))
 
     def next_tier(self, tier, nrows):
         return self.TIER_CHAIN[self.TIER_CHAIN.index(tier) + 1]
@@ -165,7 +169,7 @@ class _MockShardGallery:
         return d, i + self.n0
 
     def quantize_queries(self, sub, tier):
-        return {"tier": tier, "Q": sub.numpy()}
+        return {"tier": tier, "Q": sub.numpy(), "B": len(sub)}
 
     def search_q8_phase(self, phases, sub, q2, k, index_base):
         d, i = self._local(q2["Q"], k)
@@ -198,8 +202,7 @@ def _cert_worker(rank, ws, port, k, out, overflow=False):
         qq = g.quantize_queries(Qt, "f6")
         d, i = g.search_q8_phase(3, Qt, qq, k, n0)
         (md, mi), counts = par.certify_sharded(g, Qt, qq, k, (d, i), n0)
-        if rank == 0:
-            out.put((md.numpy(), mi.numpy(), counts))
+        out.put((rank, md.numpy(), mi.numpy(), counts, g.noted))
     finally:
         dist.destroy_process_group()
 
@@ -274,14 +277,26 @@ def test_sharded_global_certificate_and_collective_fallback(k):
     procs = [ctx.Process(target=_cert_worker, args=(r, 2, port, k, q)) for r in range(2)]
     for p in procs:
         p.start()
-    md, mi, counts = q.get(timeout=120)
+    res = _collect(q, 2)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    md, mi, counts, noted = res[0]
     Q, G = _data()
     ref_d, ref_i = O.nn_search_vectorized("EuclideanDistance", Q, G, k)
     assert np.array_equal(mi, ref_i) and np.allclose(md, ref_d, rtol=0, atol=0)
     assert counts[0] > 0 and len(counts) >= 2            # the loose first-tier bound forced fallbacks
+    # the adaptive start tier's statistics: the global counts, the same on both ranks (round 5)
+    assert noted == res[1][3] and noted[0] == ("f6", len(Q), counts[0])
+    assert [n[2] for n in noted] == counts
+
+
+def _collect(q, n):
+    res = {}
+    for _ in range(n):
+        item = q.get(timeout=120)
+        res[item[0]] = item[1:]
+    return res
 
 
 @pytest.mark.parametrize("k", [1, 3])
@@ -295,7 +310,7 @@ def test_sharded_overflowed_rank_is_never_certified(k):
     procs = [ctx.Process(target=_cert_worker, args=(r, 2, port, k, q, True)) for r in range(2)]
     for p in procs:
         p.start()
-    md, mi, counts = q.get(timeout=120)
+    md, mi, counts, _ = _collect(q, 2)[0]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
