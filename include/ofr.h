@@ -238,6 +238,20 @@ int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int6
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, const void* St,
                        int64_t Ns, const float* sscale, const float* saux, void* workspace, size_t workspace_bytes,
                        const uint8_t* bscale);
+/* Prefix tier f6p: ofr_knn_f6_sampled whose sample and sieve passes score only the
+ * first pstages 128-feature stages of the same tiles (1 <= pstages <= ceil(d / 128)).  aux / saux are
+ * the PREFIX terms |g_m|^2 of the rows and of the row sample (ofr_row_aux over the first
+ * min(d, 128 pstages) features, saux[j] = aux[64 j]); gmax is the f6 tier's.  A row's squared distance
+ * is at least that of its first features, so the certificate and the bound (-> the merge's exact fp64
+ * re-rank of the full rows) hold as for ofr_knn_f6; on features whose discriminating variance sits in
+ * the leading columns (Fisherfaces / Eigenfaces output, eigenvalues descending) it certifies at a
+ * fraction of the coarse work.  Replaces the same search as ofr_knn_f6 (classifier.py:94-129).     */
+int ofr_knn_f6p_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                        const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
+                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
+                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, const void* St,
+                        int64_t Ns, const float* sscale, const float* saux, void* workspace, size_t workspace_bytes,
+                        const uint8_t* bscale, int pstages);
 /* The row step of the sample (64) and its builder: gallery rows j * 64 for j in [j0, j1) (X = row 0
  * of the N-row fp32 gallery, ldx its leading dimension; j1 <= ceil(N / 64)) are quantized into sample
  * row j of tiles / scale / stats (as ofr_f6_quantize_rows_at) and saux[j] = aux[j * 64].  A gallery of

@@ -317,6 +317,10 @@ class FloatGallery:
                 call("ofr_f6_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, ptr(g["Gs"]),
                      g["Gs"].numel(), ptr(g["scale"]), ptr(g["stats"]), ptr(self.bscale))
                 self._sample_rows(g, N0, N1)
+            elif tier == "f6p":                        # tiles shared with f6 (extended above): the prefix terms
+                call("ofr_row_aux", stream(), _lib.METRIC_EUCLIDEAN, ptr(self._Gbuf[N0:]), n, g["pdim"], self.ld,
+                     ptr(g["paux"][N0:]))
+                g["spaux"] = self._prefix_sample_aux(g["paux"], N1)
             elif tier == "f6x2":                       # the first slice is the f6 tier's, extended above
                 call("ofr_f6x2_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, None,
                      ptr(g["Gs2"]), g["Gs2"].numel(), ptr(g["scale"]), ptr(g["stats"]), ptr(self.bscale))
@@ -336,8 +340,13 @@ class FloatGallery:
     # quantized tiers only answer where the certificate proves the result exact.
     # OFR_SEARCH picks the first tier: auto (= f6), q8 (tier 1), q8x2 (tier 2) or fp32.  NEXT: the
     # stage after each tier (f6x2 is finer than int8 x1, so its failures go on to int8 x2).
-    TIER_CHAIN = ("f6", "f6x2", 1, 2, "fp32")
-    NEXT = {"f6": "f6x2", "f6x2": 2, 1: 2, 2: "fp32"}
+    # Tier "f6p" (prefix tier, before f6 when the gallery has one -- prefix_stages): the f6 tiles and
+    # queries, scored on their first pstages 128-feature stages only.  Every squared distance is at least
+    # its prefix part, so a query certifies as in f6 (merge_kernel's prefix bound); one that does not
+    # runs the full f6 pass next.
+    TIER_CHAIN = ("f6p", "f6", "f6x2", 1, 2, "fp32")
+    NEXT = {"f6p": "f6", "f6": "f6x2", "f6x2": 2, 1: 2, 2: "fp32"}
+    F6_TIERS = ("f6p", "f6", "f6x2")
 
     @classmethod
     def tier_path(cls, first):
@@ -427,6 +436,8 @@ class FloatGallery:
     def start_tier(self, B):
         """First tier for a batch of B queries (see above); counts the batch."""
         first = self.first_tier()
+        if first == "f6" and self.prefix_stages():
+            first = "f6p"
         if B < self.ADAPT_MIN_BATCH or os.environ.get("OFR_ADAPTIVE_TIER", "1") != "1":
             return first
         self._starts += 1
@@ -460,9 +471,11 @@ class FloatGallery:
 
     def set_block_scales(self, sums):
         """Column-block scales from block sums of squares (block_sums, possibly all-reduced); before the
-        fp6 tiers are built (they keep the scales they were quantized with)."""
-        if self.q8 and any(t in self.q8 for t in ("f6", "f6x2")):
+        fp6 tiers are built (they keep the scales they were quantized with).  The same sums choose the
+        prefix tier's length (prefix_stages), so the ranks of a sharded gallery agree on it too."""
+        if self.q8 and any(t in self.q8 for t in self.F6_TIERS):
             raise RuntimeError("set_block_scales: the fp6 tiers are already built with other scales")
+        self._pst = self.choose_prefix(sums.cpu().numpy(), self.d, self.N)
         if os.environ.get("OFR_F6_BLOCK_SCALES", "1") == "0":
             self.bscale = None
             return None
@@ -479,6 +492,59 @@ class FloatGallery:
                 self.set_block_scales(self.block_sums())
         return self.bscale
 
+    # -- prefix tier f6p (ofr_knn_f6p_sampled) ------------------------------------------
+    # Fisherfaces / Eigenfaces features come in eigenvalue order: the discriminating variance sits in
+    # the leading columns (the trained W of the headline: 6 blocks of rms 54-272 against 11 for the other
+    # 307).  A block is "leading" when its mean square is >= PREFIX_RATIO x the median block's; the
+    # prefix covers the stages up to the last leading block, when that is at most 1/PREFIX_MAX_FRAC of
+    # the stages and holds >= PREFIX_MIN_SHARE of the total variance.  Isotropic features (a random W)
+    # have no prefix, and a gallery whose prefix certifies badly is skipped by start_tier like any tier.
+    # OFR_F6_PREFIX: auto (default), 0 (off) or a stage count (tests / A-B).
+    PREFIX_RATIO = 8.0
+    PREFIX_MAX_FRAC = 4
+    PREFIX_MIN_SHARE = 0.5
+
+    @classmethod
+    def choose_prefix(cls, sums, d, N):
+        """Prefix stages (0: no prefix tier) from the per-32-feature block sums of squares of the rows."""
+        env = os.environ.get("OFR_F6_PREFIX", "auto")
+        nst = -(-d // 128)
+        if env != "auto":
+            v = int(env)
+            return min(max(v, 0), nst)
+        if N < 1 or nst < cls.PREFIX_MAX_FRAC or os.environ.get("OFR_SIEVE_SAMPLE", "rows") == "panels":
+            return 0
+        width = np.minimum(32, d - 32 * np.arange(len(sums)))
+        ms = np.asarray(sums, np.float64) / (N * width)
+        med = float(np.median(ms))
+        lead = np.nonzero(ms >= cls.PREFIX_RATIO * med)[0] if med > 0 else np.zeros(0, np.int64)
+        if not len(lead):
+            return 0
+        pst = -(-32 * (int(lead[-1]) + 1) // 128)
+        nb = 4 * pst                                     # the 32-feature blocks of pst stages
+        share = float(ms[:nb].dot(width[:nb]) / ms.dot(width))
+        if pst * cls.PREFIX_MAX_FRAC > nst or share < cls.PREFIX_MIN_SHARE:
+            return 0
+        return pst
+
+    def prefix_stages(self):
+        """Stages of the prefix tier for this gallery (0: none); Euclidean galleries, decided with the
+        block scales (set_block_scales)."""
+        if getattr(self, "_pst", None) is not None:
+            return self._pst
+        if self.metric != _lib.METRIC_EUCLIDEAN or self.N == 0:
+            return 0
+        if getattr(self, "_pst", None) is None:
+            if self.bscale is None and not getattr(self, "_bscale_done", False):
+                self._block_scales()
+            if getattr(self, "_pst", None) is None:     # block scales were off or set elsewhere
+                self._pst = self.choose_prefix(self.block_sums().cpu().numpy(), self.d, self.N)
+        return self._pst
+
+    def _prefix_sample_aux(self, paux, N):
+        """Prefix terms of the row sample (rows 0, 64, 128, ...): saux[j] = paux[64 j]."""
+        return paux[:N:_lib.load().ofr_f6_sample_step()].contiguous()
+
     @staticmethod
     def _q8_ld(d, slices):
         return round_up(d, 128) if slices == 1 else 2 * round_up(d, 64)
@@ -494,6 +560,16 @@ class FloatGallery:
             st = torch.empty((cap, 3), dtype=torch.float64, device=dev_)
             gmax = torch.empty(4, dtype=torch.float64, device=dev_)
             extra = {}
+            if tier == "f6p":                     # the f6 tier's tiles, sample and maxima + the prefix terms
+                g6 = self._tier_gallery("f6")
+                pdim = min(self.d, 128 * self.prefix_stages())
+                if pdim < 1:
+                    raise RuntimeError("f6p: this gallery has no prefix tier (prefix_stages() == 0)")
+                paux = torch.empty(cap, dtype=torch.float32, device=dev_)
+                call("ofr_row_aux", stream(), _lib.METRIC_EUCLIDEAN, ptr(self.G), self.N, pdim, self.ld, ptr(paux))
+                self.q8[tier] = dict(g6, paux=paux, pdim=pdim, pst=self.prefix_stages(),
+                                     spaux=self._prefix_sample_aux(paux, self.N))
+                return self.q8[tier]
             if tier == "f6":
                 lib = _lib.load()
                 nbytes = lib.ofr_f6_tiles_bytes(cap, self.d)
@@ -558,7 +634,7 @@ class FloatGallery:
         dev_ = Qd.device
         if out is None or out["B"] != B or out["tier"] != tier:
             extra = {}
-            if tier in ("f6", "f6x2"):
+            if tier in self.F6_TIERS:
                 nb = max(1, _lib.load().ofr_f6_tiles_bytes(B, self.d))
                 Qs = torch.empty(nb, dtype=torch.uint8, device=dev_)
                 if tier == "f6x2":
@@ -569,7 +645,7 @@ class FloatGallery:
                        stats=torch.empty((B, 3), dtype=torch.float64, device=dev_),
                        cert=torch.empty(B, dtype=torch.int32, device=dev_),
                        bound=torch.empty(B, dtype=torch.float64, device=dev_), tier=tier, B=B, **extra)
-        if tier == "f6":
+        if tier in ("f6", "f6p"):                  # the prefix tier scores the first stages of the same tiles
             call("ofr_f6_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
                  out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None, ptr(self._block_scales()))
         elif tier == "f6x2":
@@ -585,7 +661,7 @@ class FloatGallery:
         the ranks, rank-major).  The fp6 tiles concatenate only whole 256-row panels: every rank's
         block must be a multiple of 256 rows (int8 tiers: any equal split)."""
         from .parallel import gather_rows
-        if qq["tier"] in ("f6", "f6x2") and qq["B"] % 256:
+        if qq["tier"] in self.F6_TIERS and qq["B"] % 256:
             raise ValueError("fp6 query tiles gather whole 256-row panels: rows per rank must be a multiple of 256")
         # scales (fp32, exact in fp64) and stats travel as one [rows][4] fp64 block: two collectives, not three
         side = gather_rows(torch.cat([qq["scale"].to(torch.float64).reshape(-1, 1), qq["stats"]], 1).contiguous(), group)
@@ -601,7 +677,7 @@ class FloatGallery:
         int8 tiers run all of phase 1 under bit 4 and nothing under bit 8.
         workspace: a Workspace of the caller's instead of the gallery's."""
         tier = qq["tier"]
-        if tier not in ("f6", "f6x2") and phases & 12:
+        if tier not in self.F6_TIERS and phases & 12:
             phases = (phases & 3) | (1 if phases & 4 else 0)
             if phases == 0:
                 return out
@@ -611,10 +687,17 @@ class FloatGallery:
             out = (torch.empty((B, k), dtype=torch.float64, device=Qd.device),
                    torch.empty((B, k), dtype=torch.int64, device=Qd.device))
         lib = _lib.load()
-        nbytes = (lib.ofr_knn_f6_workspace_bytes(B, self.N) if tier in ("f6", "f6x2")
+        nbytes = (lib.ofr_knn_f6_workspace_bytes(B, self.N) if tier in self.F6_TIERS
                   else lib.ofr_knn_q8_workspace_bytes(B, self.N))
         ws = (workspace or self.ws).get(nbytes, Qd.device)
-        if tier == "f6x2" and self.row_sample():
+        if tier == "f6p":
+            ns = -(-self.N // lib.ofr_f6_sample_step())
+            call("ofr_knn_f6p_sampled", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
+                 ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),
+                 ptr(g["paux"]), ptr(g["gmax"]), k, index_base, ptr(out[0]), ptr(out[1]), ptr(qq["cert"]),
+                 ptr(qq["bound"]), ptr(g["St"]), ns, ptr(g["sscale"]), ptr(g["spaux"]), ptr(ws), ws.numel(),
+                 ptr(self.bscale), g["pst"])
+        elif tier == "f6x2" and self.row_sample():
             s1 = self._tier_gallery("f6")
             ns = -(-self.N // lib.ofr_f6_sample_step())
             call("ofr_knn_f6x2_sampled", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["Qs2"]),
@@ -741,7 +824,7 @@ class FloatGallery:
         gm = self._tier_gallery(tier)["gmax"]
         A, E, T, aux = gm[0], gm[1], gm[2], gm[3]
         a, e, t = stats[:, 0], stats[:, 1], stats[:, 2]
-        nseg = {"f6": 1, "f6x2": 3}.get(tier, 0)
+        nseg = {"f6p": 1, "f6": 1, "f6x2": 3}.get(tier, 0)
         gamma = (2 * nseg * -(-self.d // 128) + 64) * 2.0 ** -23 if nseg else 0.0
         return 2.0 * (a * E + e * A + e * E + t * T) + 2.0 ** -20 * (aux + 2.0 * a * A) + 2.0 * gamma * a * A
 
@@ -756,7 +839,8 @@ class FloatGallery:
             return
         nxt = self.NEXT[tier]
         after = self.NEXT.get(nxt)
-        if after is None or after == "fp32" or int(rows.numel()) <= SMALL_BATCH:
+        # from the prefix tier: its bound is of the prefix distance, which predicts nothing of f6's
+        if tier == "f6p" or after is None or after == "fp32" or int(rows.numel()) <= SMALL_BATCH:
             self._queue(pending, nxt, rows)
             return
         sub = Qd.index_select(0, rows).contiguous()

@@ -68,6 +68,9 @@ SIGNATURES = {
     "ofr_knn_f6_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
                                    c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                    c_vp, c_sz, c_vp]),
+    "ofr_knn_f6p_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
+                                    c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                    c_vp, c_sz, c_vp, c_int]),
     "ofr_knn_deep_workspace_bytes": (c_sz, [c_i64, c_i64]),
     "ofr_knn_deep": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_i64, c_int, c_i64, c_dbl, c_int,
                              c_i64, c_vp, c_vp, c_vp, c_sz]),

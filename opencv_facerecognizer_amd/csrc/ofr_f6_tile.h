@@ -240,10 +240,11 @@ struct Engine {
   // the matrix pipe still drains the previous block (2 % faster than a hand-off at the stage
   // boundary, which exposes the step-0 reads after every barrier: the round-1 engine probe).
   // Fragments double-buffered by j; 3 LDS stages (kt+1 read next, kt+2 and kt+3 in flight).
-  // NSEG: segments of nst stages each (seg_src); G2 / Q2 only for NSEG = 3
+  // NSEG: segments of nst stages each (seg_src); G2 / Q2 only for NSEG = 3.  nst = the panels' stage
+  // count (layout); nsp = the stages run per segment: nst, or with NSEG = 1 a prefix (the prefix tier)
   template <int NSEG = 1>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
-                                                  int nst, f32x16 (&acc)[4][CT], const char* G2 = nullptr,
+                                                  int nst, int nsp, f32x16 (&acc)[4][CT], const char* G2 = nullptr,
                                                   const char* Q2 = nullptr, const uint32_t* bs = nullptr) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr = wave / WQ, wc = wave % WQ, h = lane >> 5, r32 = lane & 31;
@@ -261,7 +262,7 @@ struct Engine {
       dma(g, gp, q, qp, nst, ks, smem + (kt % NST) * STAGE);
     };
     // branch-free: a stage past the end re-loads the last one onto itself (same bytes)
-    const int last = NSEG * nst - 1;
+    const int last = NSEG * nsp - 1;
     static_assert(NST == 3, "hand-off below assumes 3 stages");
 #pragma unroll
     for (int s = 0; s < NST; ++s) issue(s < last ? s : last);
@@ -374,7 +375,7 @@ struct Engine16 {
   // need no second register set (acc 128 + fragments 72 registers).
   template <int NSEG = 1>
   static __device__ __forceinline__ void mainloop(char* smem, const char* G, int64_t gp, const char* Q, int64_t qp,
-                                                  int nst, f32x4 (&acc)[NA][NB], const char* G2 = nullptr,
+                                                  int nst, int nsp, f32x4 (&acc)[NA][NB], const char* G2 = nullptr,
                                                   const char* Q2 = nullptr, const uint32_t* bs = nullptr) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr = wave / WQ, wc = wave % WQ, r16 = lane & 15;
@@ -383,7 +384,7 @@ struct Engine16 {
     for (int i = 0; i < NA; ++i)
 #pragma unroll
       for (int c = 0; c < NB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int last = NSEG * nst - 1;
+    const int last = NSEG * nsp - 1;   // nsp: stages run per segment (Engine<8>::mainloop)
     auto issue = [&](int kt) {
       const char *g, *q;
       int ks;
@@ -624,7 +625,8 @@ struct EngineW {
 
   // NSEG: segments of nst stages (seg_src): 1 = the fp6 tier; 3 = the two-slice tier f6x2, whose
   // stages of segment 1 / 2 read the query / gallery second slices (f.rq2 / f.rg2) with block scale
-  // 2^-4 on that operand (block_scales)
+  // 2^-4 on that operand (block_scales).  nst: the stages run per segment -- the panels' stage count
+  // (feed_init's), or with NSEG = 1 a prefix of it (the prefix tier)
   template <int W, int NSEG = 1>
   static __device__ __forceinline__ void mainloop(const Feed& f, int nst, f32x4 (&acc)[NA][NB]) {
     constexpr int WR = W >> 1, WC = W & 1;

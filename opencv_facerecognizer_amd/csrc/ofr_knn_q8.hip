@@ -71,6 +71,9 @@ struct TileArgs {
   // fp6 tiers: column-block scales, one dword of 4 E8M0 bytes per 128-feature stage (null: unit;
   // ofr_f6_block_scales), the same for the gallery and the query tiles
   const uint32_t* bs;
+  // stages run per segment: nk / NSEG, or fewer -- the prefix tier f6p scores only the first nkp
+  // stages of the tiles (nk stays their layout)
+  int nkp;
 };
 
 // ---- keys of the tile epilogue (ofr_keys.h: order-preserving u32 keys, med3 key lists) ----
@@ -254,7 +257,7 @@ __global__ void __launch_bounds__(NW * 64, 1) tile_kernel_f6(TileArgs p) {
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
   f6t::f32x16 acc[4][CT];
   E::template mainloop<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt,
-                             p.nk / NSEG, acc, reinterpret_cast<const char*>(p.G2),
+                             p.nk / NSEG, p.nkp, acc, reinterpret_cast<const char*>(p.G2),
                              reinterpret_cast<const char*>(p.Q2), p.bs);
   auto cval = [&](int rt, auto ctc, int r) {
     constexpr int ct = decltype(ctc)::value;
@@ -331,7 +334,7 @@ __global__ void __launch_bounds__(512, 1) tile_kernel_f6s(TileArgs p) {
   const int64_t g0 = gp * TG, q0 = qt * f6t::TQ;
   f6t::f32x4 acc[8][4];
   E::mainloop<NSEG>(smem, reinterpret_cast<const char*>(p.G), gp, reinterpret_cast<const char*>(p.Q), qt, p.nk / NSEG,
-                    acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2), p.bs);
+                    p.nkp, acc, reinterpret_cast<const char*>(p.G2), reinterpret_cast<const char*>(p.Q2), p.bs);
   // sieve operands after the main loop (the 16x16 engine needs every register in it)
   float ga = __builtin_inff(), gs = 0.f, sq2[4], th[4];
   if (threadIdx.x < TG && g0 + threadIdx.x < p.N) {
@@ -363,7 +366,7 @@ __device__ __forceinline__ void f6w_main(const TileArgs& p, int64_t g0, int64_t 
   E::feed_init<W, NSEG>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ,
                         p.nk / NSEG, g0 / E::TGW, reinterpret_cast<const char*>(p.G2),
                         reinterpret_cast<const char*>(p.Q2), p.bs);
-  E::mainloop<W, NSEG>(f, p.nk / NSEG, acc);
+  E::mainloop<W, NSEG>(f, p.nkp, acc);
 }
 
 // ... and the sieve epilogue, ONE copy for the four waves (the wave's row / column offsets at run time):
@@ -520,7 +523,7 @@ __global__ void __launch_bounds__(512) stream_kernel_f6(TileArgs p) {
   }
   const char* gpan = reinterpret_cast<const char*>(p.G) + gt * (int64_t)p.nk * f6t::PANEL;
   const char* qpan = reinterpret_cast<const char*>(p.Q);
-  const int nsteps = 2 * p.nk, grow = wave * 32 + r32;
+  const int nsteps = 2 * p.nkp, grow = wave * 32 + r32;   // nkp <= nk: the prefix tier's first stages
   f6t::f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -609,6 +612,11 @@ struct MergeArgs {
   double* qd;
   double* ub_local;
   const double* ub;
+  // prefix tier f6p: the coarse scores cover features [0, dpre) only (0: all d).  A row's squared
+  // distance is at least that of its first dpre features, S_m + |q_m|^2 with S_m = |g_m|^2 - 2 q_m.g_m
+  // (the prefix scores, within dS of the keys), so the bounds below use |q_m|^2 for |q|^2 and a key
+  // bounds nothing from above (no ub_local).
+  int64_t dpre;
 };
 
 // Best KC (distance, index) of the n candidates at src (16-byte aligned) into lists[0..KC),
@@ -762,17 +770,19 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     // loads batched 8 deep: with few queries (one block each) a loop with one load per iteration is
     // bound by the memory latency, not the bytes
     constexpr int RU = 8;
+    const int64_t dm = p.dpre > 0 && p.dpre < p.d ? p.dpre : p.d;   // the features the keys cover
     qq = 0;
-    for (int64_t j0 = threadIdx.x; j0 < p.d; j0 += (int64_t)RU * blockDim.x) {
+    for (int64_t j0 = threadIdx.x; j0 < dm; j0 += (int64_t)RU * blockDim.x) {
       float x[RU];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int64_t j = j0 + (int64_t)u * blockDim.x;
-        x[u] = j < p.d ? qr[j] : 0.f;
+        x[u] = j < dm ? qr[j] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < RU; ++u) qq += (double)x[u] * (double)x[u];
     }
+    // qq = |q_m|^2 over the keys' features (all d but for the prefix tier), the base of every bound
     qq = block_sum_f64(qq, red);
     // dS(q): |S - S~| <= dS for every row, S = d^2 - |q|^2
     const double qa = p.qstats[q * 3 + 0], qe = p.qstats[q * 3 + 1], qt = p.qstats[q * 3 + 2];
@@ -791,7 +801,7 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
         for (int j = 0; j < kk; ++j) {
           const Cand c = lists[j];
           const double t = (double)c.d;
-          p.ub_local[q * kk + j] = c.i == CAND_EMPTY || overflow
+          p.ub_local[q * kk + j] = c.i == CAND_EMPTY || overflow || p.dpre > 0   // a prefix key: no upper bound
                                        ? __builtin_inf()
                                        : (t + fabs(t) * 0x1p-14 + dS + qq) * (1.0 + 1e-12) + 1e-300;
         }
@@ -1570,7 +1580,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
                        size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2 = nullptr,
-                       const void* Gt2 = nullptr, const F6Sample* smp = nullptr, const uint8_t* bscale = nullptr);
+                       const void* Gt2 = nullptr, const F6Sample* smp = nullptr, const uint8_t* bscale = nullptr,
+                       int pstages = 0);
 
 extern "C" int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                           const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
@@ -1599,6 +1610,31 @@ extern "C" int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int6
   const F6Sample smp{St, Ns, sscale, saux, nullptr};
   return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
                      out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, nullptr, nullptr, &smp, bscale);
+}
+
+// Prefix tier f6p: ofr_knn_f6_sampled with the sample and sieve passes scoring only the
+// first pstages 128-feature stages of the same tiles.  aux / saux are the PREFIX terms |g_m|^2 of the
+// rows and of the row sample (ofr_row_aux over the first min(d, 128 pstages) features); gmax is the f6
+// tier's (its aux maximum bounds the prefix terms).  Every row's squared distance is at least its
+// prefix distance, so the certificate holds as for f6; the B x N coarse work shrinks by pstages / nst.
+extern "C" int ofr_knn_f6p_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                                   const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
+                                   int64_t d, const void* Gt, const float* gscale, const float* aux,
+                                   const double* gmax, int k, int64_t index_base, double* out_d, int64_t* out_i,
+                                   int* cert, double* bound, const void* St, int64_t Ns, const float* sscale,
+                                   const float* saux, void* workspace, size_t workspace_bytes,
+                                   const uint8_t* bscale, int pstages) {
+  OFR_CHECK_ARG(phases >= 1 && phases <= 15,
+                "ofr_knn_f6p_sampled: phases: bits 1 (tiles) = 4 (sample + thresholds) + 8 (sieve), 2 (merge)");
+  OFR_CHECK_ARG(d >= 1 && pstages >= 1 && pstages <= f6t::stages(d),
+                "ofr_knn_f6p_sampled: pstages must be in [1, ceil(d / 128)]");
+  OFR_CHECK_ARG(St && sscale && saux, "ofr_knn_f6p_sampled: null sample pointer");
+  OFR_CHECK_ARG(Ns >= 1 && Ns <= sample_rows(N), "ofr_knn_f6p_sampled: sample rows must be in [1, ceil(N / 64)]");
+  OFR_CHECK_ARG((uintptr_t)St % 16 == 0, "ofr_knn_f6p_sampled: sample tiles must be 16-byte aligned");
+  const F6Sample smp{St, Ns, sscale, saux, nullptr};
+  return knn_f6_impl(stream, phases, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, 0, nullptr, nullptr, nullptr, &smp, bscale,
+                     pstages);
 }
 
 extern "C" int ofr_knn_f6x2_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
@@ -1653,7 +1689,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
                        int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound, void* workspace,
                        size_t workspace_bytes, int merge_mode, double* ub, const void* Qt2, const void* Gt2,
-                       const F6Sample* smp, const uint8_t* bscale) {
+                       const F6Sample* smp, const uint8_t* bscale, int pstages) {
   const bool two = Gt2 != nullptr;   // the two-slice tier f6x2: three segments of stages (f6t::seg_src)
   OFR_CHECK_ARG(B >= 0 && N >= 1 && d >= 1, "ofr_knn_f6: bad sizes (empty galleries use ofr_knn_f32)");
   if (k < 1 || k > q8s::KC) return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6: k must be in [1, 16]");
@@ -1674,6 +1710,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   a.G = (const int8_t*)Gt; a.N = N; a.ld = 0; a.gscale = gscale; a.aux = aux;
   a.Q = (const int8_t*)Qt; a.B = B; a.qscale = qscale;
   a.nk = (int)f6t::stages(d) * (two ? 3 : 1);
+  // prefix tier: the first pstages stages (one slice only); otherwise every stage of each segment
+  a.nkp = pstages > 0 && !two && pstages < f6t::stages(d) ? pstages : (int)f6t::stages(d);
   a.G2 = (const int8_t*)Gt2; a.Q2 = (const int8_t*)Qt2;
   a.bs = reinterpret_cast<const uint32_t*>(bscale);
   if (!a.bs) {
@@ -1784,6 +1822,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
     const double gamma = (double)(2 * a.nk + 64) * 0x1p-23;
     q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, gamma, k, index_base, out_d, out_i, cert, bound};
     m.mode = merge_mode;
+    m.dpre = a.nkp < f6t::stages(d) ? (int64_t)a.nkp * f6t::BK : 0;
     m.sel = reinterpret_cast<Cand*>(wsb + f6_ws_core(B, N));
     m.qd = reinterpret_cast<double*>(wsb + f6_ws_core(B, N) + f6_ws_qd(B));
     if (merge_mode == 1) m.ub_local = ub;

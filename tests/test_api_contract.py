@@ -138,7 +138,7 @@ def test_start_tier_policy_host_logic(monkeypatch):
     monkeypatch.setenv("OFR_SEARCH", "auto")
     monkeypatch.delenv("OFR_ADAPTIVE_TIER", raising=False)
     g = FloatGallery.__new__(FloatGallery)
-    g.tier_failures, g._starts = {}, 0
+    g.tier_failures, g._starts, g._pst = {}, 0, 0          # no prefix tier (isotropic features)
     assert g.start_tier(4096) == "f6"
     g.note_failures("f6", 4096, 4096)
     assert g.start_tier(4096) == "f6x2"
@@ -157,6 +157,57 @@ def test_start_tier_policy_host_logic(monkeypatch):
     assert seen.count("f6") == 2 and seen.count("f6x2") == 2 * FloatGallery.REPROBE - 2
     monkeypatch.setenv("OFR_ADAPTIVE_TIER", "0")
     assert g.start_tier(4096) == "f6"
+
+
+def test_prefix_tier_start_and_skip_host_logic(monkeypatch):
+    """With a prefix (FloatGallery.prefix_stages > 0) the chain starts at f6p, whose failures go on to
+    f6 (no skip prediction: a prefix bound says nothing of f6's); a failing prefix is skipped."""
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    monkeypatch.delenv("OFR_ADAPTIVE_TIER", raising=False)
+    assert FloatGallery.tier_path("f6p") == ("f6p", "f6", "f6x2", 2, "fp32")
+    g = FloatGallery.__new__(FloatGallery)
+    g.tier_failures, g._starts, g._pst = {}, 0, 2
+    assert g.start_tier(4096) == "f6p" and g.start_tier(8) == "f6p"
+    g.note_failures("f6p", 4096, 4000)
+    assert g.start_tier(4096) == "f6"
+    monkeypatch.setenv("OFR_SEARCH", "q8")
+    assert g.start_tier(4096) == 1                        # an explicit int8 start ignores the prefix
+
+
+def _block_sums(ms, N, d):
+    width = np.minimum(32, d - 32 * np.arange(len(ms)))
+    return np.asarray(ms, np.float64) * N * width
+
+
+def test_choose_prefix_host_logic(monkeypatch):
+    """FloatGallery.choose_prefix: stages up to the last block whose mean square is >= PREFIX_RATIO x
+    the median, if they are <= 1/PREFIX_MAX_FRAC of the stages and hold >= PREFIX_MIN_SHARE of the
+    variance; OFR_F6_PREFIX forces a count or 0."""
+    from opencv_facerecognizer_amd._device import FloatGallery as F
+    monkeypatch.delenv("OFR_F6_PREFIX", raising=False)
+    monkeypatch.delenv("OFR_SIEVE_SAMPLE", raising=False)
+    d = 9999
+    nb = -(-d // 32)
+    # the trained W's profile (bench feature_profile): 6 blocks of rms 272 .. 54, the rest ~11.4
+    rms = np.full(nb, 11.4)
+    rms[:6] = [272, 218, 180, 137, 87, 54]
+    assert F.choose_prefix(_block_sums(rms ** 2, 1000, d), d, 1000) == 2       # features 0..191 -> 2 stages
+    assert F.choose_prefix(_block_sums(np.full(nb, 130.0), 1000, d), d, 1000) == 0   # isotropic
+    spread = rms.copy()
+    spread[300] = 500                                      # a leading block late: prefix too long
+    assert F.choose_prefix(_block_sums(spread ** 2, 1000, d), d, 1000) == 0
+    weak = np.full(nb, 11.4)
+    weak[0] = 40                                           # one loud block, but < half of the variance
+    assert F.choose_prefix(_block_sums(weak ** 2, 1000, d), d, 1000) == 0
+    assert F.choose_prefix(_block_sums(rms ** 2, 1000, 400)[:13], 400, 1000) == 0   # 4 stages: too few
+    monkeypatch.setenv("OFR_SIEVE_SAMPLE", "panels")       # the prefix tier has the row sample only
+    assert F.choose_prefix(_block_sums(rms ** 2, 1000, d), d, 1000) == 0
+    monkeypatch.delenv("OFR_SIEVE_SAMPLE")
+    monkeypatch.setenv("OFR_F6_PREFIX", "3")
+    assert F.choose_prefix(_block_sums(np.full(nb, 130.0), 1000, d), d, 1000) == 3
+    monkeypatch.setenv("OFR_F6_PREFIX", "0")
+    assert F.choose_prefix(_block_sums(rms ** 2, 1000, d), d, 1000) == 0
 
 
 def test_results_batch_equals_per_row_reference_vote():
