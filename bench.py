@@ -155,6 +155,7 @@ def committed_traffic(cfg):
             continue
         c = dict(s.get("config") or {})
         c.setdefault("w", "random")
+        c.setdefault("tier", c.get("search"))         # summaries before the prefix tier: the search's tier
         if c == cfg and s.get("traffic_bytes_per_launch") is not None:
             cands.append((s.get("measured_utc", ""), os.path.basename(f), s["traffic_bytes_per_launch"]))
     if not cands:
@@ -802,15 +803,24 @@ def main():
     margin = certificate_margin(gallery, Qd, qq) if args.search == "f6" and world == 1 else None
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
+    # the tier the timed steps started at (FloatGallery.start_tier): f6p (the prefix tier) when the
+    # gallery's features put their variance in the leading columns, f6 otherwise
+    tier_used = max(set(starts[-args.steps:]), key=starts[-args.steps:].count) if starts else None
+    pst = gallery.prefix_stages() if tier_used == "f6p" else 0
     if args.search == "f6":
-        # the dominant kernel is the sieve pass: it alone does all 2 B N d of the algorithmic work (the
-        # sample pass before it re-does 1/64 of it to set the thresholds); its launch is timed by its own
-        # events on the main stream, phase 1 (sample + thresholds + sieve) is reported beside it
+        # the dominant kernel is the sieve pass: it scores every (query, row) pair -- over all d features
+        # (tier f6: 2 B N d) or over the first m = 128 pst of them (tier f6p: 2 B N m; the rest of each
+        # distance is never needed to certify) -- (the sample pass before it re-does 1/64 of it to set the
+        # thresholds); its launch is timed by its own events on the main stream, phase 1 (sample +
+        # thresholds + sieve) is reported beside it
         sieve = _lib.load().ofr_f6_sieve_kernel().decode()                    # the variant the library launches
-        peak, kname = PEAK_F6_MFMA, "ofr_knn_f6 sieve pass (fp6 e2m3): " + sieve
+        dm = min(d, 128 * pst) if pst else d                                 # the features the pass scores
+        flops_tiles = 2.0 * B * nl * dm
+        peak, kname = PEAK_F6_MFMA, ("ofr_knn_f6p_sampled prefix sieve pass (fp6 e2m3, first %d of %d features): "
+                                     % (dm, d) if pst else "ofr_knn_f6 sieve pass (fp6 e2m3): ") + sieve
         achieved = flops_tiles / (ms_sieve * 1e-3)
-        alg_bytes_tiles = 0.75 * (nl * d + B * d)                    # 6 bits per feature, gallery + queries
-        ntg_, ntq_, nst_ = -(-nl // 256), -(-B // 256), -(-d // 128)
+        alg_bytes_tiles = 0.75 * (nl * dm + B * dm)                  # 6 bits per feature, gallery + queries
+        ntg_, ntq_, nst_ = -(-nl // 256), -(-B // 256), -(-dm // 128)
         wide = "f6w" in sieve                                        # 384 x 256 tiles: 60 KiB per stage
         fed = (-(-nl // 384) * 61440.0 if wide else ntg_ * 49152.0) * ntq_ * nst_   # copied into LDS per sieve pass
         executed = flops_tiles
@@ -827,13 +837,15 @@ def main():
         value = B * args.steps / elapsed
         coll = "RCCL" if world > 1 and dist.get_backend() == "nccl" else "gloo"   # the collectives' backend
         tr = committed_traffic({"gallery": nl, "batch": B, "d": d, "D": D, "k": k, "search": args.search,
-                                "w": args.w})
+                                "w": args.w, "tier": tier_used or args.search})
         result = {
             "metric": "query faces/sec (Fisherfaces proj + 1-NN, 1M gallery) at 1/2/4/8 GPUs",
             "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None,
-            "dtype": {"f6": "fp6 e2m3 (fp6 MFMA coarse scores, certified; fp64 exact re-rank)",
+            "dtype": {"f6": "fp6 e2m3 (fp6 MFMA coarse scores, certified; fp64 exact re-rank)" + (
+                      f" -- prefix tier f6p: coarse scores of the first {128 * pst} features, certified by the "
+                      f"projection bound" if pst else ""),
                       "q8": "i8 (int8 MFMA coarse scores, certified; fp64 exact re-rank)",
                       "fp32": "f32 (fp32 MFMA scores, fp64 exact re-rank)"}[args.search], "data": "synthetic",
             "config": {"workload": "configs[2]: Fisherfaces projection + 1-NN, 1M-image gallery (100k ids x 10), "

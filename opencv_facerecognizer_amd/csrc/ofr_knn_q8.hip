@@ -479,6 +479,360 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6w(TileArgs p) {
   }
 }
 
+// ---- prefix tier's sieve pass: persistent, one workgroup per CU ------------------------------------
+// With 1 or 2 stages per tile (the prefix tier f6p) the wide engine's tile spends ~6x its MFMA time
+// on fixed costs -- the first copies' latency, the operand-table and threshold loads, the epilogue and
+// the hit flush -- none of it overlapped (tile_kernel_f6w runs one workgroup per CU: its 384
+// accumulators fill the register file).  tile_kernel_f6p keeps one workgroup per CU resident and
+// walks work items = (384-row gallery tile, group of query panels).  Per panel:
+//   top      the panel's query stages landed (copied during the previous panel's compares); the
+//            previous panel's hits get their bucket slots (global atomics, answered under the MFMAs)
+//   MFMAs    the nsp stages from LDS (the gallery tile resident for the whole item), the first MFMA
+//            from a zero accumulator
+//   then     the previous panel's hits written to the buckets; the next panel's (or item's) copies
+//            issued and its operand tables loaded; the compares: every (row block, query column) in
+//            one branch-free pass (a wave mask per row block), then only the row blocks with a hit
+//            again, row by row, into the LDS hit list of this panel.
+// Same wave tiling, fragments, MFMAs and score arithmetic as f6t::EngineW / f6w_epilogue: the kept rows
+// and keys equal tile_kernel_f6w's (tests/test_gpu_prefix.py).  Phase clocks: tools/prefix_sweep.py
+// --trace on a -DOFR_F6P_TRACE build.
+#ifdef OFR_F6P_TRACE
+// probe builds only: shader-clock stamps of workgroup 0's phases for its first 64 panels, into the
+// sample lists region of the workspace (p.cand: dead once the thresholds are set)
+__device__ int f6p_trace_panel;
+__device__ __forceinline__ void f6p_trace_mark(const TileArgs& p, int k) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && f6p_trace_panel < 64)
+    reinterpret_cast<unsigned long long*>(p.cand)[f6p_trace_panel * 8 + k] = __builtin_amdgcn_s_memtime();
+}
+#define F6P_MARK(k) f6p_trace_mark(p, k)
+#else
+#define F6P_MARK(k)
+#endif
+namespace f6p {
+using E = f6t::EngineW;
+constexpr int NSPMAX = 2;                                   // prefix stages held in LDS
+constexpr int GS = 0;                                       // gallery slots [NSPMAX][E::GSLOT]
+constexpr int QS = NSPMAX * E::GSLOT;                       // query slots [NSPMAX][E::QSLOT]
+constexpr int QTAB = QS + NSPMAX * E::QSLOT;                // [2][256] (2 sq, theta) of the panels
+constexpr int GTAB = QTAB + 2 * 256 * 8;                    // [384] (aux, scale) of the gallery tile
+constexpr int NHIT = GTAB + E::TGW * 8;                     // hits of the panel
+constexpr int HITS = NHIT + 16;                             // [HCAP] (key, query << 9 | row)
+constexpr int HCAP = 4096;                                  // hit slots per (tile, panel)
+constexpr int LDS_BYTES = HITS + HCAP * 8;
+static_assert(LDS_BYTES <= 163840, "prefix pass LDS");
+
+// c = a.b into an AGPR accumulator (first stage: no accumulator read).  AGPR row blocks only: with a
+// VGPR destination ("=v", even early-clobber) the compiler gave the result the registers of a fragment
+// that a previous, still executing MFMA was reading (the last row's query fragments die there); the
+// hazard recognizer does not see into asm, so that MFMA read them overwritten -- one-stage passes lost
+// query column block 5 (tests/test_gpu_prefix.py, round 5).  VGPR row blocks start from accumulators
+// zeroed before the stage's first MFMA (as f6t::EngineW), with the accumulating form.
+__device__ __forceinline__ void mfma0a(const f6t::i32x6& a, const f6t::i32x6& b, f6t::f32x4& c, int sc) {
+  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
+               : "=&a"(c) : "v"(a), "v"(b), "v"(sc));
+}
+
+// wave W's copy pieces of the gallery tile gt (all NSP stages) / of query panel qp
+template <int W, int NSP>
+__device__ __forceinline__ void copy_gallery(const TileArgs& p, int64_t gt) {
+  E::Feed f;
+  E::feed_init<W, 1>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), 0, p.nk, gt);
+#pragma unroll
+  for (int s = 0; s < NSP; ++s) {
+    const uint32_t so = GS + s * E::GSLOT, ko = (uint32_t)s * f6t::PANEL;
+    E::gcopy<W, 0>(f.rg, f, so, ko); E::gcopy<W, 1>(f.rg, f, so, ko); E::gcopy<W, 2>(f.rg, f, so, ko);
+    E::gcopy<W, 3>(f.rg, f, so, ko); E::gcopy<W, 4>(f.rg, f, so, ko); E::gcopy<W, 5>(f.rg, f, so, ko);
+    E::gcopy<W, 6>(f.rg, f, so, ko); E::gcopy<W, 7>(f.rg, f, so, ko); E::gcopy<W, 8>(f.rg, f, so, ko);
+  }
+}
+template <int W, int NSP>
+__device__ __forceinline__ void copy_queries(const TileArgs& p, int64_t qp) {
+  const int64_t pb = (int64_t)p.nk * f6t::PANEL;
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(reinterpret_cast<const char*>(p.Q) + qp * pb), 0, (int)pb, 0x00020000);
+#pragma unroll
+  for (int s = 0; s < NSP; ++s) {
+    const uint32_t so = QS + s * E::QSLOT, ko = (uint32_t)s * f6t::PANEL;
+    E::qcopy<W, 0>(rq, so, ko); E::qcopy<W, 1>(rq, so, ko); E::qcopy<W, 2>(rq, so, ko);
+    E::qcopy<W, 3>(rq, so, ko); E::qcopy<W, 4>(rq, so, ko); E::qcopy<W, 5>(rq, so, ko);
+  }
+}
+template <int NSP>
+__device__ __forceinline__ void copies(int wave, const TileArgs& p, bool gallery, int64_t gt, int64_t qp) {
+  switch (wave) {
+    case 0: if (gallery) copy_gallery<0, NSP>(p, gt); copy_queries<0, NSP>(p, qp); break;
+    case 1: if (gallery) copy_gallery<1, NSP>(p, gt); copy_queries<1, NSP>(p, qp); break;
+    case 2: if (gallery) copy_gallery<2, NSP>(p, gt); copy_queries<2, NSP>(p, qp); break;
+    default: if (gallery) copy_gallery<3, NSP>(p, gt); copy_queries<3, NSP>(p, qp); break;
+  }
+}
+
+// Lane-derived values come from tid, the thread index laundered through an empty asm at every panel:
+// computed from threadIdx.x they are loop invariants, and the compiler hoisted every fragment address
+// and hit payload of the four waves out of the persistent loops -- ~2,000 registers, spilled.
+__device__ __forceinline__ E::Bases lane_bases(uint32_t slot, uint32_t tid, uint32_t qstride, uint32_t p1off) {
+  const uint32_t lane = tid & 63, q = lane >> 4, l = lane & 15, qo = (q & 1) << 4;
+  return E::Bases{slot + q * qstride + l * 16, slot + q * qstride + p1off + (l + qo) * 8,
+                  slot + q * qstride + p1off + (l - qo) * 8};
+}
+// the MFMAs of stage S of one (tile, panel) from the LDS slots into acc (stage 0 starts from zero)
+template <int W, int S>
+__device__ __forceinline__ void stage_mfmas(int scs, uint32_t tid, f6t::f32x4 (&acc)[E::NA][E::NB]) {
+  constexpr int WR = W >> 1, WC = W & 1;
+  const E::Bases ab = lane_bases(GS + S * E::GSLOT, tid, 3072, 2048);    // E::abase
+  const E::Bases bb = lane_bases(QS + S * E::QSLOT, tid, 6144, 4096);    // E::bbase
+  if constexpr (S == 0) {   // the VGPR accumulators zeroed before any MFMA: their registers are theirs alone
+#pragma unroll
+    for (int i = E::NAA; i < E::NA; ++i)
+#pragma unroll
+      for (int c = 0; c < E::NB; ++c) acc[i][c] = f6t::f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  f6t::i32x6 a[E::RING], b[E::NB];
+  b[0] = E::fragB<WC * 128 + 0>(bb); b[1] = E::fragB<WC * 128 + 16>(bb); b[2] = E::fragB<WC * 128 + 32>(bb);
+  b[3] = E::fragB<WC * 128 + 48>(bb); b[4] = E::fragB<WC * 128 + 64>(bb); b[5] = E::fragB<WC * 128 + 80>(bb);
+  b[6] = E::fragB<WC * 128 + 96>(bb); b[7] = E::fragB<WC * 128 + 112>(bb);
+  a[0] = E::fragA<WR * 192 + 0>(ab);
+  a[1] = E::fragA<WR * 192 + 16>(ab);
+  auto row = [&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    constexpr bool AG = i < E::NAA;
+    if constexpr (i + 2 < E::NA) a[(i + 2) % E::RING] = E::fragA<WR * 192 + (i + 2 < E::NA ? i + 2 : 0) * 16>(ab);
+#pragma unroll
+    for (int c = 0; c < E::NB; ++c) {
+      if constexpr (S == 0 && AG) mfma0a(a[i % E::RING], b[c], acc[i][c], scs);
+      else E::mfma<AG>(a[i % E::RING], b[c], acc[i][c], scs);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // rows in order: fragments read two rows ahead, not all at once
+  };
+  row(std::integral_constant<int, 0>{}); row(std::integral_constant<int, 1>{});
+  row(std::integral_constant<int, 2>{}); row(std::integral_constant<int, 3>{});
+  row(std::integral_constant<int, 4>{}); row(std::integral_constant<int, 5>{});
+  row(std::integral_constant<int, 6>{}); row(std::integral_constant<int, 7>{});
+  row(std::integral_constant<int, 8>{}); row(std::integral_constant<int, 9>{});
+  row(std::integral_constant<int, 10>{}); row(std::integral_constant<int, 11>{});
+}
+template <int NSP>
+__device__ __forceinline__ void mfmas(int wave, const int (&sc)[NSPMAX], uint32_t tid,
+                                      f6t::f32x4 (&acc)[E::NA][E::NB]) {
+  auto run = [&](auto wc) {
+    constexpr int W = decltype(wc)::value;
+    stage_mfmas<W, 0>(sc[0], tid, acc);
+    if constexpr (NSP > 1) stage_mfmas<W, 1>(sc[NSP - 1], tid, acc);
+  };
+  switch (wave) {
+    case 0: run(std::integral_constant<int, 0>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 3>{}); break;
+  }
+  E::wait_drain();
+}
+
+// The sieve compares of one (tile, panel): f6w_epilogue's, with the operand tables in LDS and the hits
+// into the LDS list.  (Round 5 tried a branch-free first pass over all row blocks with a second pass for
+// the blocks with a hit: it kept every accumulator live through both, spilled, and was slower.)
+// The VGPR accumulators (row blocks NAA..NA-1) go first: their registers are free for the rest.
+__device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t g0, int wave, uint32_t tid,
+                                         const float* qt, f6t::f32x4 (&acc)[E::NA][E::NB]) {
+  const int WR = wave >> 1;
+  const float* gtab = reinterpret_cast<const float*>(smem + GTAB);
+  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + NHIT);
+  uint2* hits = reinterpret_cast<uint2*>(smem + HITS);
+  const int nvalid = p.N - g0 < E::TGW ? (int)(p.N - g0) : E::TGW;
+  const int lane = tid & 63, wc = wave & 1, g4 = (lane >> 4) * 4, r16 = lane & 15;
+  float sq2[E::NB], th[E::NB];
+#pragma unroll
+  for (int c = 0; c < E::NB; ++c) {
+    const int ql = wc * 128 + c * 16 + r16;
+    sq2[c] = qt[2 * ql + 0];
+    th[c] = qt[2 * ql + 1];
+  }
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int ii = 0; ii < E::NA; ++ii) {
+    const int i = (ii + E::NAA) % E::NA;
+    const int gl0 = WR * 192 + i * 16 + g4;
+    const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
+    const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
+    const f32x2 avp[2] = {f32x2{t0.x, t0.z}, f32x2{t1.x, t1.z}}, svp[2] = {f32x2{t0.y, t0.w}, f32x2{t1.y, t1.w}};
+    float sc[4][E::NB];
+    uint64_t col[E::NB];
+    uint64_t any = 0;
+#pragma unroll
+    for (int c = 0; c < E::NB; ++c) {
+#pragma unroll
+      for (int rp = 0; rp < 2; ++rp) {
+        const f32x2 t = svp[rp] * sq2[c];
+        const f32x2 x = __builtin_elementwise_fma(-t, f32x2{acc[i][c][2 * rp], acc[i][c][2 * rp + 1]}, avp[rp]);
+        sc[2 * rp][c] = x.x;
+        sc[2 * rp + 1][c] = x.y;
+      }
+      const float mn = fminf(fminf(sc[0][c], sc[1][c]), fminf(sc[2][c], sc[3][c]));
+      col[c] = __builtin_amdgcn_ballot_w64(!(mn > th[c]));   // NaN th ("keep every row") passes
+      any |= col[c];
+    }
+    if (any == 0) continue;   // uniform; ~2 kept pairs per panel and wave on gallery data
+#pragma unroll
+    for (int c = 0; c < E::NB; ++c) {
+      if (col[c] == 0) continue;   // uniform
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!(sc[r][c] > th[c]) && gl0 + r < nvalid) {   // padding rows (aux +inf) pass only a NaN th
+          const int ql = wc * 128 + c * 16 + r16;
+          const uint32_t kb = __float_as_uint(key_score(score_key(sc[r][c], 0)));
+          const uint32_t slot = atomicAdd(nhit, 1u);
+          if (slot < (uint32_t)HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
+        }
+    }
+  }
+}
+
+// Flush of the hit list (tile rows from g0, queries from q0) into the per-query buckets, split so that
+// the global atomics' round trip runs under the next panel's MFMAs: begin takes each thread's hit into
+// registers -- the list is free for the next compares -- and reserves its slot (a longer list, rare on
+// large galleries, is flushed here whole; an overflowed one pushes the panel's queries past their cap:
+// uncertified, as sieve_flush), end writes the entries.
+struct Pending {
+  int64_t q;
+  int slot;
+  uint2 hv;
+};
+__device__ __forceinline__ Pending flush_begin(char* smem, const TileArgs& p, int64_t g0, int64_t q0,
+                                               uint32_t tid) {
+  Pending pd{-1, 0, make_uint2(0u, 0u)};
+  const uint32_t nh = *reinterpret_cast<const uint32_t*>(smem + NHIT);
+  const uint2* hits = reinterpret_cast<const uint2*>(smem + HITS);
+  if (nh > (uint32_t)HCAP) {
+    if (tid < (uint32_t)f6t::TQ && q0 + tid < p.B) atomicMax(p.count + q0 + tid, (int)p.cap + 1);
+  } else if (nh > (uint32_t)E::NT) {
+    for (uint32_t e = tid; e < nh; e += E::NT) {
+      const uint2 hv = hits[e];
+      const int64_t q = q0 + (int)(hv.y >> 9);
+      if (q < p.B) {
+        const int slot = atomicAdd(p.count + q, 1);
+        if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(hv.x), (int)(g0 + (hv.y & 511u))};
+      }
+    }
+  } else if (tid < nh) {
+    pd.hv = hits[tid];
+    pd.q = q0 + (int)(pd.hv.y >> 9);
+    if (pd.q < p.B) pd.slot = atomicAdd(p.count + pd.q, 1);
+    else pd.q = -1;
+  }
+  return pd;
+}
+__device__ __forceinline__ void flush_end(const TileArgs& p, int64_t g0, const Pending& pd) {
+  if (pd.q >= 0 && pd.slot < p.cap)
+    p.bucket[pd.q * p.cap + pd.slot] = Cand{__uint_as_float(pd.hv.x), (int)(g0 + (pd.hv.y & 511u))};
+}
+
+// (2 sq, theta) of query q0 + tid (past B: no row kept) and (aux, scale) of tile row r
+__device__ __forceinline__ float2 panel_operands(const TileArgs& p, int64_t q0, uint32_t tid) {
+  const int64_t q = q0 + tid;
+  return q < p.B ? make_float2(2.0f * p.qscale[q], key_float(p.theta[q] | 0xffu)) : make_float2(0.f, -__builtin_inff());
+}
+__device__ __forceinline__ float2 tile_operands(const TileArgs& p, int64_t g0, int r) {
+  return g0 + r < p.N ? make_float2(p.aux[g0 + r], p.gscale[g0 + r]) : make_float2(__builtin_inff(), 0.f);
+}
+}  // namespace f6p
+
+// p.ntg gallery tiles of 384 rows x p.ntq query panels; work item w = (gallery tile w / ngrp, query
+// panels [qg * (w % ngrp), ...) of the group size qg); NSP = p.nkp <= f6p::NSPMAX stages.
+template <int NSP>
+__global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg) {
+  using E = f6t::EngineW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t ngrp = (p.ntq + qg - 1) / qg, items = p.ntg * ngrp;
+  // the stages' block scales (the same for every tile)
+  const uint32_t lsh = 8u * ((threadIdx.x & 63) >> 4);
+  int sc[f6p::NSPMAX];
+  {
+    const uint32_t r0 = f6t::sload_bscale(p.bs, 0), r1 = f6t::sload_bscale(p.bs, NSP > 1 ? 1 : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sc[0] = f6t::lane_byte(r0, lsh);
+    sc[1] = f6t::lane_byte(r1, lsh);
+  }
+  float2* qtab = reinterpret_cast<float2*>(smem + f6p::QTAB);
+  float2* gtab = reinterpret_cast<float2*>(smem + f6p::GTAB);
+  int64_t w = blockIdx.x;
+  if (w >= items) return;
+  // 32-bit index arithmetic (the host bounds items below 2^31)
+  const uint32_t ng32 = (uint32_t)ngrp, qg32 = (uint32_t)qg;
+  auto item_gt = [&](int64_t it) { return (int64_t)((uint32_t)it / ng32); };
+  auto item_q0 = [&](int64_t it) { return (int64_t)(((uint32_t)it % ng32) * qg32); };
+  auto item_q1 = [&](int64_t it) { const int64_t e = item_q0(it) + qg; return e < p.ntq ? e : p.ntq; };
+  // prologue: the first item's gallery stages and first panel, its operand tables, empty hit lists
+  f6p::copies<NSP>(wave, p, true, item_gt(w), item_q0(w));
+  for (int r = threadIdx.x; r < E::TGW; r += E::NT) gtab[r] = f6p::tile_operands(p, item_gt(w) * E::TGW, r);
+  qtab[threadIdx.x] = f6p::panel_operands(p, item_q0(w) * f6t::TQ, threadIdx.x);
+  if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(smem + f6p::NHIT) = 0u;
+  int buf = 0;                        // qtab slot of the current panel
+  int64_t pg0 = 0, pq0 = 0;           // the previous panel's tile row / query base (its hits: the list)
+  bool prev = false;
+  for (;;) {
+    const int64_t gt = item_gt(w), qp1 = item_q1(w);
+    for (int64_t qp = item_q0(w); qp < qp1; ++qp) {
+#ifdef OFR_F6P_TRACE
+      if (blockIdx.x == 0 && threadIdx.x == 0) f6p_trace_panel = (int)(qp - item_q0(w)) + 16 * (int)(w / gridDim.x);
+#endif
+      F6P_MARK(0);
+      f6t::wait_vm<0>();   // this panel's copies (and the previous panel's bucket stores)
+      f6t::barrier();
+      F6P_MARK(1);
+      uint32_t tid = threadIdx.x;      // f6p::lane_bases
+      asm volatile("" : "+v"(tid));
+      const f6p::Pending pd = prev ? f6p::flush_begin(smem, p, pg0, pq0, tid) : f6p::Pending{-1, 0, {0u, 0u}};
+      f6t::f32x4 acc[E::NA][E::NB];   // per panel: stage 0 writes every accumulator
+      f6p::mfmas<NSP>(wave, sc, tid, acc);
+      f6t::barrier();   // every wave's fragment reads of the slots done: refill them
+      F6P_MARK(2);
+      f6p::flush_end(p, pg0, pd);
+      if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(smem + f6p::NHIT) = 0u;   // read in flush_begin above
+      // what comes next: the next panel of this item, or the next item's gallery tile and first panel
+      const bool more = qp + 1 < qp1;
+      const int64_t wn = more ? w : w + gridDim.x;
+      const bool next = more || wn < items;
+      float2 nq = make_float2(0.f, 0.f), ng0 = nq, ng1 = nq;
+      if (next) {
+        // the tables first: vmcnt counts in order, so their wait (after the compares) is not a wait for
+        // the copies issued behind them
+        const int64_t qn = more ? qp + 1 : item_q0(wn);
+        nq = f6p::panel_operands(p, qn * f6t::TQ, tid);          // written after the compares
+        if (!more) {
+          ng0 = f6p::tile_operands(p, item_gt(wn) * E::TGW, (int)tid);
+          if (tid < (uint32_t)(E::TGW - E::NT)) ng1 = f6p::tile_operands(p, item_gt(wn) * E::TGW, (int)tid + E::NT);
+        }
+        f6p::copies<NSP>(wave, p, !more, item_gt(wn), qn);
+      }
+      __syncthreads();   // the hit list's reset visible
+      F6P_MARK(3);
+      f6p::compares(smem, p, gt * E::TGW, wave, tid, reinterpret_cast<const float*>(qtab + buf * 256), acc);
+      F6P_MARK(4);
+      __syncthreads();   // every wave's compares done: the tables may change
+      if (next) {
+        qtab[(buf ^ 1) * 256 + tid] = nq;
+        if (!more) {
+          gtab[tid] = ng0;
+          if (tid < (uint32_t)(E::TGW - E::NT)) gtab[tid + E::NT] = ng1;
+        }
+      }
+      F6P_MARK(5);
+      pg0 = gt * E::TGW;
+      pq0 = qp * f6t::TQ;
+      prev = true;
+      buf ^= 1;
+    }
+    w += gridDim.x;
+    if (w >= items) break;
+  }
+  // the last panel's hits
+  f6t::wait_vm<0>();
+  f6t::barrier();
+  const f6p::Pending pd = f6p::flush_begin(smem, p, pg0, pq0, threadIdx.x);
+  f6p::flush_end(p, pg0, pd);
+}
+
 // ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
 // One workgroup per 256-row gallery panel, wave w owns rows 32w..32w+31 against the (single)
 // 32-row query block, loading its fragments straight to VGPRs from the f6 tiled layout (each
@@ -1256,6 +1610,32 @@ static const uint32_t* unit_bscale() {
   return addr[dev];
 }
 
+// compute units of the current device (the persistent prefix pass runs one workgroup on each)
+static int device_cus() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus[dev] = 0;
+  return cus[dev];
+}
+
+// query panels per work item of tile_kernel_f6p: the largest group (fewest gallery-tile loads) whose
+// last round of items over the CUs wastes little -- the makespan in panels, ceil(items / cus) x qg,
+// plus half a panel per item for its gallery copies and tables, is minimal
+static int64_t f6p_group(int64_t ntg, int64_t ntq, int cus) {
+  int64_t best = ntq, cost = INT64_MAX;
+  for (int64_t div = 1; div <= ntq; div *= 2) {
+    const int64_t qg = (ntq + div - 1) / div, items = ntg * ((ntq + qg - 1) / qg);
+    const int64_t rounds = (items + cus - 1) / cus, c = rounds * (2 * qg + 1);
+    if (c < cost) {
+      cost = c;
+      best = qg;
+    }
+  }
+  return best;
+}
+
 static int64_t q8_min_ld(int slices, int64_t d) { return slices == 1 ? round_up(d, 128) : 2 * round_up(d, 64); }
 
 extern "C" int ofr_q8_quantize_rows(void* stream, int slices, const float* X, int64_t R, int64_t d, int64_t ldx,
@@ -1512,6 +1892,13 @@ constexpr int F6W_GROUP = 2;
 // x 2), 21.56 -> 21.45 ms.
 constexpr int F6W_SERP = 1;
 
+// The prefix tier's sieve pass on tile_kernel_f6p (persistent; default) or, OFR_F6P_PERSIST=0, on
+// tile_kernel_f6w (one workgroup per tile: the A/B reference).  Read at every call.
+static bool f6p_persistent() {
+  const char* e = getenv("OFR_F6P_PERSIST");
+  return !(e && e[0] == '0');
+}
+
 // f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
 // thresholds, counts and buckets (each 256-byte aligned)
 struct SieveWs {
@@ -1752,6 +2139,10 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f6t::EngineW::LDS_BYTES);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 wide tile)");
         }
+        for (const void* f : {(const void*)q8s::tile_kernel_f6p<1>, (const void*)q8s::tile_kernel_f6p<2>}) {
+          hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, q8s::f6p::LDS_BYTES);
+          if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 prefix pass)");
+        }
         attr_done = true;
       }
       // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel, or of the row sample -> thresholds
@@ -1794,6 +2185,22 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       }
       if (!(phases & 8)) {
         // sample + thresholds only
+      } else if (f6_shape() == 384 && a.nkp <= q8s::f6p::NSPMAX && a.nkp < f6t::stages(d) && !two &&
+                 f6p_persistent() && device_cus() > 0) {
+        // the prefix tier's short pass: persistent workgroups, the gallery tile resident (tile_kernel_f6p)
+        q8s::TileArgs wa = a;
+        wa.ntg = cdiv(N, f6t::EngineW::TGW);
+        const int cus = device_cus();
+        const int64_t qg = f6p_group(wa.ntg, wa.ntq, cus);
+        const int64_t items = wa.ntg * cdiv(wa.ntq, qg);
+        OFR_CHECK_ARG(items < 0x7fffffffLL, "ofr_knn_f6: grid too large");
+        const unsigned grid = (unsigned)std::min<int64_t>(items, cus);
+        if (a.nkp == 1)
+          hipLaunchKernelGGL(q8s::tile_kernel_f6p<1>, dim3(grid), dim3(f6t::EngineW::NT), q8s::f6p::LDS_BYTES, st, wa,
+                             qg);
+        else
+          hipLaunchKernelGGL(q8s::tile_kernel_f6p<2>, dim3(grid), dim3(f6t::EngineW::NT), q8s::f6p::LDS_BYTES, st, wa,
+                             qg);
       } else if (f6_shape() == 384) {
         q8s::TileArgs wa = a;   // 384-row gallery tiles over the same 256-row panel layout
         wa.ntg = cdiv(N, f6t::EngineW::TGW);

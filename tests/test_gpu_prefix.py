@@ -178,3 +178,43 @@ def test_prefix_tier_extended_by_append():
     torch.cuda.synchronize()
     assert g.last_start_tier == "f6p"
     assert np.array_equal(np.sort(i_.cpu().numpy(), 1), np.sort(_exact_topk(g, Qd, 4), 1))
+
+
+@pytest.mark.parametrize("pst,B,n_id", [(1, 300, 2003), (2, 700, 1501), (2, 4096, 997)])
+def test_persistent_prefix_pass_matches_per_tile_pass(monkeypatch, pst, B, n_id):
+    """tile_kernel_f6p (persistent, the default for pstages <= 2) keeps exactly the rows, with exactly the
+    keys, of tile_kernel_f6w on the same prefix (OFR_F6P_PERSIST=0): the same MFMAs in the same order and
+    the same compares.  Partial last gallery tile and query panel; B = 4096: 16 query panels per item."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_F6_PREFIX", str(pst))
+    G, Q = _lda_like(n_id, 9, 1280, B, seed=pst * 7 + B)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    assert g.prefix_stages() == pst
+    Qd = g.query_rows(Q)
+    state, res = {}, {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("OFR_F6P_PERSIST", mode)
+        qq = g.quantize_queries(Qd, tier="f6p")
+        out = g.search_q8_phase(4 | 8 | 2, Qd, qq, 3)
+        torch.cuda.synchronize()
+        theta, count, keys, rows = g.sieve_state(B)
+        count = count.cpu().numpy().copy()
+        assert np.all((count >= 3) & (count <= g.SIEVE_CAP)), count
+        pairs = []
+        rows_h, keys_h = rows.cpu().numpy(), keys.cpu().numpy()
+        for b in range(B):
+            r = rows_h[b, :count[b]]
+            kk = keys_h[b, :count[b]]
+            o = np.argsort(r)
+            pairs.append((r[o], kk[o]))
+        state[mode] = (count, pairs)
+        res[mode] = (out[0].cpu().numpy(), out[1].cpu().numpy(), qq["cert"].cpu().numpy().copy())
+    assert np.array_equal(state["1"][0], state["0"][0])
+    for b in range(B):
+        assert np.array_equal(state["1"][1][b][0], state["0"][1][b][0]), b
+        assert np.array_equal(state["1"][1][b][1].view(np.uint32), state["0"][1][b][1].view(np.uint32)), b
+    for j in range(3):
+        assert np.array_equal(res["1"][j], res["0"][j])
+    assert res["1"][2].all()
+    assert np.array_equal(np.sort(res["1"][1], 1), np.sort(_exact_topk(g, Qd, 3), 1))

@@ -52,11 +52,14 @@ def main():
     log = open(os.path.join(P, "kt.log")).read().strip().splitlines()
     bench = json.loads([ln for ln in log if ln.startswith("{")][-1])
     cfg = bench["config"]
+    search = "f6" if "fp6" in bench["dtype"] else ("q8" if "i8" in bench["dtype"] else "fp32")
     out = {
         "config": {"gallery": cfg["gallery"], "batch": cfg["global_batch"], "d": cfg["d"], "D": cfg["D"],
                    "k": cfg["k"],
-                   "search": "f6" if "fp6" in bench["dtype"] else ("q8" if "i8" in bench["dtype"] else "fp32"),
-                   "w": "trained" if "trained" in cfg.get("workload", "") else "random"},
+                   "search": search,
+                   "w": "trained" if "trained" in cfg.get("workload", "") else "random",
+                   # the tier the timed steps started at (f6p: the prefix tier's pass)
+                   "tier": max((bench.get("start_tiers") or {"": 0}).items(), key=lambda t: t[1])[0] or search},
         # bench.committed_traffic takes the newest summary of its config (file names do not order rounds)
         "measured_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
         "kernel": " + ".join(knames), "launches": min(v["launches"] for v in per.values()), "rocprof_avg_ns": avg_ns,
