@@ -813,7 +813,8 @@ def main():
         # distance is never needed to certify) -- (the sample pass before it re-does 1/64 of it to set the
         # thresholds); its launch is timed by its own events on the main stream, phase 1 (sample +
         # thresholds + sieve) is reported beside it
-        sieve = _lib.load().ofr_f6_sieve_kernel().decode()                    # the variant the library launches
+        lib = _lib.load()                                                     # the variant the library launches
+        sieve = (lib.ofr_f6p_sieve_kernel(pst) if pst else lib.ofr_f6_sieve_kernel()).decode()
         dm = min(d, 128 * pst) if pst else d                                 # the features the pass scores
         flops_tiles = 2.0 * B * nl * dm
         peak, kname = PEAK_F6_MFMA, ("ofr_knn_f6p_sampled prefix sieve pass (fp6 e2m3, first %d of %d features): "
@@ -821,8 +822,10 @@ def main():
         achieved = flops_tiles / (ms_sieve * 1e-3)
         alg_bytes_tiles = 0.75 * (nl * dm + B * dm)                  # 6 bits per feature, gallery + queries
         ntg_, ntq_, nst_ = -(-nl // 256), -(-B // 256), -(-dm // 128)
-        wide = "f6w" in sieve                                        # 384 x 256 tiles: 60 KiB per stage
+        wide = "f6w" in sieve or "f6p" in sieve                      # 384 x 256 tiles: 60 KiB per stage
         fed = (-(-nl // 384) * 61440.0 if wide else ntg_ * 49152.0) * ntq_ * nst_   # copied into LDS per sieve pass
+        if "f6p" in sieve:       # the persistent pass copies a gallery tile once per item of query panels
+            fed = -(-nl // 384) * ntq_ * nst_ * 24576.0 + -(-nl // 384) * nst_ * 36864.0 * (ntq_ / 16.0)
         executed = flops_tiles
     elif use_q8:
         peak, kname = PEAK_I8_MFMA, "q8s::tile_kernel<1> (ofr_knn_q8 phase 1, one int8 slice)"

@@ -220,6 +220,9 @@ int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int
                          const uint8_t* bscale);
 /* The fp6 sieve kernel ofr_knn_f6 launches for B > 32, as the profiler names it (profiling labels). */
 const char* ofr_f6_sieve_kernel(void);
+/* the kernel ofr_knn_f6p_sampled's sieve pass launches at pstages (B > 32): the persistent prefix pass
+ * for pstages <= 2 (OFR_F6P_PERSIST=0: the per-tile pass above)                                    */
+const char* ofr_f6p_sieve_kernel(int pstages);
 int ofr_knn_f6(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,

@@ -1868,6 +1868,18 @@ extern "C" const char* ofr_f6_sieve_kernel(void) {
   return names[f6_shape() == 16 ? 0 : 1].c_str();
 }
 
+// name of the kernel the prefix tier's sieve pass (ofr_knn_f6p_sampled, B > 32) launches for pstages
+static bool f6p_persistent();
+extern "C" const char* ofr_f6p_sieve_kernel(int pstages) {
+  static const std::string names[2] = {
+      "q8s::tile_kernel_f6p (persistent prefix pass: one workgroup per CU, 384-row gallery tile resident in LDS, "
+      "16x16x128 fp6 MFMA)",
+      ""};
+  if (pstages >= 1 && pstages <= q8s::f6p::NSPMAX && f6_shape() == 384 && f6p_persistent())
+    return names[0].c_str();
+  return ofr_f6_sieve_kernel();
+}
+
 // Engine of the sieve pass: 384 = v_mfma_scale_f32_16x16x128 on 384 x 256 tiles, one wave per SIMD
 // (f6t::EngineW, default since round 3: 22.2 -> 20.1 ms); 16 = the same MFMA on 256 x 256 tiles, 8
 // waves (f6t::Engine16, OFR_F6_SHAPE=16: the comparison engine of tests/test_gpu_sieve.py).  Read at
@@ -1897,6 +1909,13 @@ constexpr int F6W_SERP = 1;
 static bool f6p_persistent() {
   const char* e = getenv("OFR_F6P_PERSIST");
   return !(e && e[0] == '0');
+}
+// CUs the persistent prefix pass leaves free (OFR_F6P_RESERVE, probe): work queued on other streams --
+// the previous batch's merge -- otherwise waits for the whole pass
+static int f6p_reserve() {
+  const char* e = getenv("OFR_F6P_RESERVE");
+  const int v = e && *e ? atoi(e) : 0;
+  return v < 0 ? 0 : v;
 }
 
 // f6 workspace: B <= 32 the stream kernel's tile lists; otherwise the sieve's sample lists,
@@ -2190,7 +2209,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         // the prefix tier's short pass: persistent workgroups, the gallery tile resident (tile_kernel_f6p)
         q8s::TileArgs wa = a;
         wa.ntg = cdiv(N, f6t::EngineW::TGW);
-        const int cus = device_cus();
+        const int cus = std::max(1, device_cus() - f6p_reserve());
         const int64_t qg = f6p_group(wa.ntg, wa.ntq, cus);
         const int64_t items = wa.ntg * cdiv(wa.ntq, qg);
         OFR_CHECK_ARG(items < 0x7fffffffLL, "ofr_knn_f6: grid too large");
