@@ -513,11 +513,16 @@ using E = f6t::EngineW;
 constexpr int NSPMAX = 2;                                   // prefix stages held in LDS
 constexpr int GS = 0;                                       // gallery slots [NSPMAX][E::GSLOT]
 constexpr int QS = NSPMAX * E::GSLOT;                       // query slots [NSPMAX][E::QSLOT]
-constexpr int QTAB = QS + NSPMAX * E::QSLOT;                // [2][256] (2 sq, theta) of the panels
-constexpr int GTAB = QTAB + 2 * 256 * 8;                    // [384] (aux, scale) of the gallery tile
-constexpr int NHIT = GTAB + E::TGW * 8;                     // hits of the panel
+// operand tables, raw copies of the global arrays (buffer_load ... lds: no registers, no waits until the
+// next panel's top): per panel slot (2) the queries' scale [256] and threshold key [256]; per item slot
+// (2) the tile rows' aux [384] and scale [384]
+constexpr int QSC = QS + NSPMAX * E::QSLOT;                 // [2][256] f32 query scale
+constexpr int QTH = QSC + 2 * 1024;                         // [2][256] u32 theta
+constexpr int GAUX = QTH + 2 * 1024;                        // [2][384] f32 row aux (|g_m|^2)
+constexpr int GSCL = GAUX + 2 * 1536;                       // [2][384] f32 row scale
+constexpr int NHIT = GSCL + 2 * 1536;                       // hits of the panel
 constexpr int HITS = NHIT + 16;                             // [HCAP] (key, query << 9 | row)
-constexpr int HCAP = 4096;                                  // hit slots per (tile, panel)
+constexpr int HCAP = 3836;                                  // hit slots per (tile, panel): the rest of the LDS
 constexpr int LDS_BYTES = HITS + HCAP * 8;
 static_assert(LDS_BYTES <= 163840, "prefix pass LDS");
 
@@ -575,55 +580,75 @@ __device__ __forceinline__ E::Bases lane_bases(uint32_t slot, uint32_t tid, uint
   return E::Bases{slot + q * qstride + l * 16, slot + q * qstride + p1off + (l + qo) * 8,
                   slot + q * qstride + p1off + (l - qo) * 8};
 }
-// the MFMAs of stage S of one (tile, panel) from the LDS slots into acc (stage 0 starts from zero)
-template <int W, int S>
-__device__ __forceinline__ void stage_mfmas(int scs, uint32_t tid, f6t::f32x4 (&acc)[E::NA][E::NB]) {
+// The MFMAs of one (tile, panel): stages [0, NSP) from the LDS slots into acc (stage 0 starts from
+// zero).  As in f6t::EngineW, the next stage's fragments are read in the last rows of the current one
+// (gallery rows 0 and 1 into the ring slots rows 10 and 11 free, each query fragment right after its
+// last MFMA in row 11), so only the panel's first stage waits for its reads.
+template <int W, int NSP>
+__device__ __forceinline__ void panel_mfmas(const int (&sc)[NSPMAX], uint32_t tid, f6t::f32x4 (&acc)[E::NA][E::NB]) {
   constexpr int WR = W >> 1, WC = W & 1;
-  const E::Bases ab = lane_bases(GS + S * E::GSLOT, tid, 3072, 2048);    // E::abase
-  const E::Bases bb = lane_bases(QS + S * E::QSLOT, tid, 6144, 4096);    // E::bbase
-  if constexpr (S == 0) {   // the VGPR accumulators zeroed before any MFMA: their registers are theirs alone
 #pragma unroll
-    for (int i = E::NAA; i < E::NA; ++i)
-#pragma unroll
-      for (int c = 0; c < E::NB; ++c) acc[i][c] = f6t::f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int i = E::NAA; i < E::NA; ++i)   // the VGPR accumulators zeroed before any MFMA: their registers
+#pragma unroll                           // are theirs alone
+    for (int c = 0; c < E::NB; ++c) acc[i][c] = f6t::f32x4{0.f, 0.f, 0.f, 0.f};
   f6t::i32x6 a[E::RING], b[E::NB];
-  b[0] = E::fragB<WC * 128 + 0>(bb); b[1] = E::fragB<WC * 128 + 16>(bb); b[2] = E::fragB<WC * 128 + 32>(bb);
-  b[3] = E::fragB<WC * 128 + 48>(bb); b[4] = E::fragB<WC * 128 + 64>(bb); b[5] = E::fragB<WC * 128 + 80>(bb);
-  b[6] = E::fragB<WC * 128 + 96>(bb); b[7] = E::fragB<WC * 128 + 112>(bb);
-  a[0] = E::fragA<WR * 192 + 0>(ab);
-  a[1] = E::fragA<WR * 192 + 16>(ab);
-  auto row = [&](auto ii) {
-    constexpr int i = decltype(ii)::value;
-    constexpr bool AG = i < E::NAA;
-    if constexpr (i + 2 < E::NA) a[(i + 2) % E::RING] = E::fragA<WR * 192 + (i + 2 < E::NA ? i + 2 : 0) * 16>(ab);
+  {
+    const E::Bases ab = lane_bases(GS, tid, 3072, 2048), bb = lane_bases(QS, tid, 6144, 4096);   // E::abase / bbase
+    b[0] = E::fragB<WC * 128 + 0>(bb); b[1] = E::fragB<WC * 128 + 16>(bb); b[2] = E::fragB<WC * 128 + 32>(bb);
+    b[3] = E::fragB<WC * 128 + 48>(bb); b[4] = E::fragB<WC * 128 + 64>(bb); b[5] = E::fragB<WC * 128 + 80>(bb);
+    b[6] = E::fragB<WC * 128 + 96>(bb); b[7] = E::fragB<WC * 128 + 112>(bb);
+    a[0] = E::fragA<WR * 192 + 0>(ab);
+    a[1] = E::fragA<WR * 192 + 16>(ab);
+  }
+  auto stage = [&](auto sv) {
+    constexpr int S = decltype(sv)::value;
+    constexpr bool NEXT = S + 1 < NSP;
+    const int scs = sc[S];
+    const E::Bases ab = lane_bases(GS + S * E::GSLOT, tid, 3072, 2048);
+    const E::Bases an = lane_bases(GS + (NEXT ? S + 1 : S) * E::GSLOT, tid, 3072, 2048);
+    const E::Bases bn = lane_bases(QS + (NEXT ? S + 1 : S) * E::QSLOT, tid, 6144, 4096);
+    auto row = [&](auto ii) {
+      constexpr int i = decltype(ii)::value;
+      constexpr bool AG = i < E::NAA;
+      if constexpr (i + 2 < E::NA) a[(i + 2) % E::RING] = E::fragA<WR * 192 + (i + 2 < E::NA ? i + 2 : 0) * 16>(ab);
+      else if constexpr (NEXT) a[(i + 2) % E::RING] = E::fragA<WR * 192 + (i + 2 - E::NA) * 16>(an);
+      auto mm = [&](int c) {
+        if constexpr (S == 0 && AG) mfma0a(a[i % E::RING], b[c], acc[i][c], scs);
+        else E::mfma<AG>(a[i % E::RING], b[c], acc[i][c], scs);
+      };
+      if constexpr (i == E::NA - 1 && NEXT) {
+        mm(0); b[0] = E::fragB<WC * 128 + 0>(bn);
+        mm(1); b[1] = E::fragB<WC * 128 + 16>(bn);
+        mm(2); b[2] = E::fragB<WC * 128 + 32>(bn);
+        mm(3); b[3] = E::fragB<WC * 128 + 48>(bn);
+        mm(4); b[4] = E::fragB<WC * 128 + 64>(bn);
+        mm(5); b[5] = E::fragB<WC * 128 + 80>(bn);
+        mm(6); b[6] = E::fragB<WC * 128 + 96>(bn);
+        mm(7); b[7] = E::fragB<WC * 128 + 112>(bn);
+      } else {
 #pragma unroll
-    for (int c = 0; c < E::NB; ++c) {
-      if constexpr (S == 0 && AG) mfma0a(a[i % E::RING], b[c], acc[i][c], scs);
-      else E::mfma<AG>(a[i % E::RING], b[c], acc[i][c], scs);
-    }
-    __builtin_amdgcn_sched_barrier(0);   // rows in order: fragments read two rows ahead, not all at once
+        for (int c = 0; c < E::NB; ++c) mm(c);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // rows in order: fragments read two rows ahead, not all at once
+    };
+    row(std::integral_constant<int, 0>{}); row(std::integral_constant<int, 1>{});
+    row(std::integral_constant<int, 2>{}); row(std::integral_constant<int, 3>{});
+    row(std::integral_constant<int, 4>{}); row(std::integral_constant<int, 5>{});
+    row(std::integral_constant<int, 6>{}); row(std::integral_constant<int, 7>{});
+    row(std::integral_constant<int, 8>{}); row(std::integral_constant<int, 9>{});
+    row(std::integral_constant<int, 10>{}); row(std::integral_constant<int, 11>{});
   };
-  row(std::integral_constant<int, 0>{}); row(std::integral_constant<int, 1>{});
-  row(std::integral_constant<int, 2>{}); row(std::integral_constant<int, 3>{});
-  row(std::integral_constant<int, 4>{}); row(std::integral_constant<int, 5>{});
-  row(std::integral_constant<int, 6>{}); row(std::integral_constant<int, 7>{});
-  row(std::integral_constant<int, 8>{}); row(std::integral_constant<int, 9>{});
-  row(std::integral_constant<int, 10>{}); row(std::integral_constant<int, 11>{});
+  stage(std::integral_constant<int, 0>{});
+  if constexpr (NSP > 1) stage(std::integral_constant<int, 1>{});
 }
 template <int NSP>
 __device__ __forceinline__ void mfmas(int wave, const int (&sc)[NSPMAX], uint32_t tid,
                                       f6t::f32x4 (&acc)[E::NA][E::NB]) {
-  auto run = [&](auto wc) {
-    constexpr int W = decltype(wc)::value;
-    stage_mfmas<W, 0>(sc[0], tid, acc);
-    if constexpr (NSP > 1) stage_mfmas<W, 1>(sc[NSP - 1], tid, acc);
-  };
   switch (wave) {
-    case 0: run(std::integral_constant<int, 0>{}); break;
-    case 1: run(std::integral_constant<int, 1>{}); break;
-    case 2: run(std::integral_constant<int, 2>{}); break;
-    default: run(std::integral_constant<int, 3>{}); break;
+    case 0: panel_mfmas<0, NSP>(sc, tid, acc); break;
+    case 1: panel_mfmas<1, NSP>(sc, tid, acc); break;
+    case 2: panel_mfmas<2, NSP>(sc, tid, acc); break;
+    default: panel_mfmas<3, NSP>(sc, tid, acc); break;
   }
   E::wait_drain();
 }
@@ -632,29 +657,33 @@ __device__ __forceinline__ void mfmas(int wave, const int (&sc)[NSPMAX], uint32_
 // into the LDS list.  (Round 5 tried a branch-free first pass over all row blocks with a second pass for
 // the blocks with a hit: it kept every accumulator live through both, spilled, and was slower.)
 // The VGPR accumulators (row blocks NAA..NA-1) go first: their registers are free for the rest.
-__device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t g0, int wave, uint32_t tid,
-                                         const float* qt, f6t::f32x4 (&acc)[E::NA][E::NB]) {
+__device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t g0, int64_t q0, int wave,
+                                         uint32_t tid, int qb, int gb, f6t::f32x4 (&acc)[E::NA][E::NB]) {
   const int WR = wave >> 1;
-  const float* gtab = reinterpret_cast<const float*>(smem + GTAB);
+  const float* qsc = reinterpret_cast<const float*>(smem + QSC) + qb * 256;
+  const uint32_t* qth = reinterpret_cast<const uint32_t*>(smem + QTH) + qb * 256;
+  const float* gaux = reinterpret_cast<const float*>(smem + GAUX) + gb * E::TGW;
+  const float* gscl = reinterpret_cast<const float*>(smem + GSCL) + gb * E::TGW;
   uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + NHIT);
   uint2* hits = reinterpret_cast<uint2*>(smem + HITS);
   const int nvalid = p.N - g0 < E::TGW ? (int)(p.N - g0) : E::TGW;
   const int lane = tid & 63, wc = wave & 1, g4 = (lane >> 4) * 4, r16 = lane & 15;
-  float sq2[E::NB], th[E::NB];
+  float sq2[E::NB], th[E::NB];   // (2 s_q, theta as a float): fix_query_tables made them at the panel's top
 #pragma unroll
   for (int c = 0; c < E::NB; ++c) {
     const int ql = wc * 128 + c * 16 + r16;
-    sq2[c] = qt[2 * ql + 0];
-    th[c] = qt[2 * ql + 1];
+    sq2[c] = qsc[ql];
+    th[c] = __uint_as_float(qth[ql]);
   }
   typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int ii = 0; ii < E::NA; ++ii) {
     const int i = (ii + E::NAA) % E::NA;
     const int gl0 = WR * 192 + i * 16 + g4;
-    const float4 t0 = reinterpret_cast<const float4*>(gtab)[gl0 / 2];
-    const float4 t1 = reinterpret_cast<const float4*>(gtab)[gl0 / 2 + 1];
-    const f32x2 avp[2] = {f32x2{t0.x, t0.z}, f32x2{t1.x, t1.z}}, svp[2] = {f32x2{t0.y, t0.w}, f32x2{t1.y, t1.w}};
+    // rows past N read zeros (aux 0, scale 0: a score of 0), which the hit test below excludes
+    const float4 ta = *reinterpret_cast<const float4*>(gaux + gl0);
+    const float4 ts = *reinterpret_cast<const float4*>(gscl + gl0);
+    const f32x2 avp[2] = {f32x2{ta.x, ta.y}, f32x2{ta.z, ta.w}}, svp[2] = {f32x2{ts.x, ts.y}, f32x2{ts.z, ts.w}};
     float sc[4][E::NB];
     uint64_t col[E::NB];
     uint64_t any = 0;
@@ -681,7 +710,12 @@ __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t 
           const int ql = wc * 128 + c * 16 + r16;
           const uint32_t kb = __float_as_uint(key_score(score_key(sc[r][c], 0)));
           const uint32_t slot = atomicAdd(nhit, 1u);
-          if (slot < (uint32_t)HCAP) hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
+          if (slot < (uint32_t)HCAP) {
+            hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
+          } else {   // the list is full (small galleries: ~3 % of the pairs kept): straight to the bucket
+            const int bs = atomicAdd(p.count + q0 + ql, 1);
+            if (bs < p.cap) p.bucket[(q0 + ql) * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + gl0 + r)};
+          }
         }
     }
   }
@@ -690,21 +724,19 @@ __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t 
 // Flush of the hit list (tile rows from g0, queries from q0) into the per-query buckets, split so that
 // the global atomics' round trip runs under the next panel's MFMAs: begin takes each thread's hit into
 // registers -- the list is free for the next compares -- and reserves its slot (a longer list, rare on
-// large galleries, is flushed here whole; an overflowed one pushes the panel's queries past their cap:
-// uncertified, as sieve_flush), end writes the entries.
+// large galleries, is flushed here whole; hits past the list's capacity went to the buckets directly),
+// end writes the entries.
 struct Pending {
   int64_t q;
-  int slot;
+  int slot;   // the atomic's answer: read only in flush_end (no wait for it before)
   uint2 hv;
 };
 __device__ __forceinline__ Pending flush_begin(char* smem, const TileArgs& p, int64_t g0, int64_t q0,
                                                uint32_t tid) {
   Pending pd{-1, 0, make_uint2(0u, 0u)};
-  const uint32_t nh = *reinterpret_cast<const uint32_t*>(smem + NHIT);
-  const uint2* hits = reinterpret_cast<const uint2*>(smem + HITS);
-  if (nh > (uint32_t)HCAP) {
-    if (tid < (uint32_t)f6t::TQ && q0 + tid < p.B) atomicMax(p.count + q0 + tid, (int)p.cap + 1);
-  } else if (nh > (uint32_t)E::NT) {
+  const uint32_t nh = min(*reinterpret_cast<const uint32_t*>(smem + NHIT), (uint32_t)HCAP);   // the rest went
+  const uint2* hits = reinterpret_cast<const uint2*>(smem + HITS);                           // to the buckets
+  if (nh > (uint32_t)E::NT) {
     for (uint32_t e = tid; e < nh; e += E::NT) {
       const uint2 hv = hits[e];
       const int64_t q = q0 + (int)(hv.y >> 9);
@@ -722,17 +754,45 @@ __device__ __forceinline__ Pending flush_begin(char* smem, const TileArgs& p, in
   return pd;
 }
 __device__ __forceinline__ void flush_end(const TileArgs& p, int64_t g0, const Pending& pd) {
-  if (pd.q >= 0 && pd.slot < p.cap)
-    p.bucket[pd.q * p.cap + pd.slot] = Cand{__uint_as_float(pd.hv.x), (int)(g0 + (pd.hv.y & 511u))};
+  int slot = pd.slot;
+  // first use of the atomic's answer: the compiler otherwise sign-extended it right behind the atomic,
+  // waiting for the round trip there
+  asm volatile("" : "+v"(slot));
+  if (pd.q >= 0 && slot < p.cap)
+    p.bucket[pd.q * p.cap + slot] = Cand{__uint_as_float(pd.hv.x), (int)(g0 + (pd.hv.y & 511u))};
 }
 
-// (2 sq, theta) of query q0 + tid (past B: no row kept) and (aux, scale) of tile row r
-__device__ __forceinline__ float2 panel_operands(const TileArgs& p, int64_t q0, uint32_t tid) {
-  const int64_t q = q0 + tid;
-  return q < p.B ? make_float2(2.0f * p.qscale[q], key_float(p.theta[q] | 0xffu)) : make_float2(0.f, -__builtin_inff());
+// raw operand tables by LDS-DMA (4 B per lane, one 256-B piece per wave-instruction): query scales and
+// thetas of the 256 queries from q0 into panel slot qb; aux and scales of the 384 rows from g0 into item
+// slot gb (reads past the arrays' ends return zeros)
+__device__ __forceinline__ void table_piece(const void* base, int64_t n_left, uint32_t lds, int piece, uint32_t lane) {
+  const int bytes = n_left <= 0 ? 0 : (n_left >= (1 << 20) ? (1 << 22) : (int)(n_left * 4));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+  // the piece offset in voffset: the range check covers voffset + offset, not soffset
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (OFR_LDS void*)(uintptr_t)(lds + piece * 256), 4, piece * 256 + lane * 4,
+                                           0, 0, 0);
 }
-__device__ __forceinline__ float2 tile_operands(const TileArgs& p, int64_t g0, int r) {
-  return g0 + r < p.N ? make_float2(p.aux[g0 + r], p.gscale[g0 + r]) : make_float2(__builtin_inff(), 0.f);
+__device__ __forceinline__ void load_query_tables(const TileArgs& p, int wave, uint32_t lane, int64_t q0, int qb) {
+  table_piece(p.qscale + q0, p.B - q0, QSC + qb * 1024, wave, lane);
+  table_piece(p.theta + q0, p.B - q0, QTH + qb * 1024, wave, lane);
+}
+// the raw query tables of slot qb -> (2 s_q, key_float(theta | 0xff)), in place; past B: no row kept (the
+// copies read zeros there)
+__device__ __forceinline__ void fix_query_tables(char* smem, const TileArgs& p, int64_t q0, int qb, uint32_t tid) {
+  float* qsc = reinterpret_cast<float*>(smem + QSC) + qb * 256;
+  uint32_t* qth = reinterpret_cast<uint32_t*>(smem + QTH) + qb * 256;
+  const float s2 = 2.0f * qsc[tid];
+  const uint32_t t = qth[tid];
+  qsc[tid] = s2;
+  qth[tid] = __float_as_uint(q0 + tid < p.B ? key_float(t | 0xffu) : -__builtin_inff());
+}
+__device__ __forceinline__ void load_tile_tables(const TileArgs& p, int wave, uint32_t lane, int64_t g0, int gb) {
+  table_piece(p.aux + g0, p.N - g0, GAUX + gb * 1536, wave, lane);
+  table_piece(p.gscale + g0, p.N - g0, GSCL + gb * 1536, wave, lane);
+  if (wave < 2) {   // pieces 4 and 5 of the 384 rows
+    table_piece(p.aux + g0, p.N - g0, GAUX + gb * 1536, wave + 4, lane);
+    table_piece(p.gscale + g0, p.N - g0, GSCL + gb * 1536, wave + 4, lane);
+  }
 }
 }  // namespace f6p
 
@@ -753,8 +813,6 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
     sc[0] = f6t::lane_byte(r0, lsh);
     sc[1] = f6t::lane_byte(r1, lsh);
   }
-  float2* qtab = reinterpret_cast<float2*>(smem + f6p::QTAB);
-  float2* gtab = reinterpret_cast<float2*>(smem + f6p::GTAB);
   int64_t w = blockIdx.x;
   if (w >= items) return;
   // 32-bit index arithmetic (the host bounds items below 2^31)
@@ -763,11 +821,11 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
   auto item_q0 = [&](int64_t it) { return (int64_t)(((uint32_t)it % ng32) * qg32); };
   auto item_q1 = [&](int64_t it) { const int64_t e = item_q0(it) + qg; return e < p.ntq ? e : p.ntq; };
   // prologue: the first item's gallery stages and first panel, its operand tables, empty hit lists
+  f6p::load_tile_tables(p, wave, threadIdx.x & 63, item_gt(w) * E::TGW, 0);
+  f6p::load_query_tables(p, wave, threadIdx.x & 63, item_q0(w) * f6t::TQ, 0);
   f6p::copies<NSP>(wave, p, true, item_gt(w), item_q0(w));
-  for (int r = threadIdx.x; r < E::TGW; r += E::NT) gtab[r] = f6p::tile_operands(p, item_gt(w) * E::TGW, r);
-  qtab[threadIdx.x] = f6p::panel_operands(p, item_q0(w) * f6t::TQ, threadIdx.x);
   if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(smem + f6p::NHIT) = 0u;
-  int buf = 0;                        // qtab slot of the current panel
+  int buf = 0, gb = 0;                // table slots of the current panel / item
   int64_t pg0 = 0, pq0 = 0;           // the previous panel's tile row / query base (its hits: the list)
   bool prev = false;
   for (;;) {
@@ -782,9 +840,12 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
       F6P_MARK(1);
       uint32_t tid = threadIdx.x;      // f6p::lane_bases
       asm volatile("" : "+v"(tid));
+      f6p::fix_query_tables(smem, p, qp * f6t::TQ, buf, tid);   // read after the MFMAs' barrier
       const f6p::Pending pd = prev ? f6p::flush_begin(smem, p, pg0, pq0, tid) : f6p::Pending{-1, 0, {0u, 0u}};
+      F6P_MARK(6);
       f6t::f32x4 acc[E::NA][E::NB];   // per panel: stage 0 writes every accumulator
       f6p::mfmas<NSP>(wave, sc, tid, acc);
+      F6P_MARK(7);
       f6t::barrier();   // every wave's fragment reads of the slots done: refill them
       F6P_MARK(2);
       f6p::flush_end(p, pg0, pd);
@@ -793,35 +854,23 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
       const bool more = qp + 1 < qp1;
       const int64_t wn = more ? w : w + gridDim.x;
       const bool next = more || wn < items;
-      float2 nq = make_float2(0.f, 0.f), ng0 = nq, ng1 = nq;
-      if (next) {
-        // the tables first: vmcnt counts in order, so their wait (after the compares) is not a wait for
-        // the copies issued behind them
+      if (next) {   // the next panel's (and item's) tables and stages, landed by the next panel's top
         const int64_t qn = more ? qp + 1 : item_q0(wn);
-        nq = f6p::panel_operands(p, qn * f6t::TQ, tid);          // written after the compares
-        if (!more) {
-          ng0 = f6p::tile_operands(p, item_gt(wn) * E::TGW, (int)tid);
-          if (tid < (uint32_t)(E::TGW - E::NT)) ng1 = f6p::tile_operands(p, item_gt(wn) * E::TGW, (int)tid + E::NT);
-        }
+        f6p::load_query_tables(p, wave, tid & 63, qn * f6t::TQ, buf ^ 1);
+        if (!more) f6p::load_tile_tables(p, wave, tid & 63, item_gt(wn) * E::TGW, gb ^ 1);
         f6p::copies<NSP>(wave, p, !more, item_gt(wn), qn);
       }
       __syncthreads();   // the hit list's reset visible
       F6P_MARK(3);
-      f6p::compares(smem, p, gt * E::TGW, wave, tid, reinterpret_cast<const float*>(qtab + buf * 256), acc);
+      f6p::compares(smem, p, gt * E::TGW, qp * f6t::TQ, wave, tid, buf, gb, acc);
       F6P_MARK(4);
-      __syncthreads();   // every wave's compares done: the tables may change
-      if (next) {
-        qtab[(buf ^ 1) * 256 + tid] = nq;
-        if (!more) {
-          gtab[tid] = ng0;
-          if (tid < (uint32_t)(E::TGW - E::NT)) gtab[tid + E::NT] = ng1;
-        }
-      }
+      __syncthreads();   // every wave's compares done: the tables may change (next panel's top)
       F6P_MARK(5);
       pg0 = gt * E::TGW;
       pq0 = qp * f6t::TQ;
       prev = true;
       buf ^= 1;
+      if (!more) gb ^= 1;
     }
     w += gridDim.x;
     if (w >= items) break;
@@ -1936,6 +1985,17 @@ static int64_t sieve_stride() { return q8s::SIEVE_STRIDE; }
 // cluster, and its 4th best key keeps ~4 x 64 rows.
 static int sieve_rank(bool rows) { return rows ? q8s::SIEVE_RANK_ROWS : q8s::SIEVE_RANK; }
 
+// The prefix tier's rank: its keys separate the own identity from the rest by a wide gap, and a row
+// sample holds at most one row of an identity, so the sample's 2nd best key is another identity's and
+// keeps ~2 x 64 rows per query (hits and bucket halved against rank 4: +4 % queries/s, same-box A/B
+// profiles/r05_rank_ab.txt; certificates unchanged).  OFR_F6P_RANK: probe override.
+constexpr int SIEVE_RANK_PREFIX = 2;
+static int f6p_rank() {
+  const char* e = getenv("OFR_F6P_RANK");
+  const int v = e && *e ? atoi(e) : SIEVE_RANK_PREFIX;
+  return v < 1 ? 1 : (v > q8s::KC ? q8s::KC : v);
+}
+
 // sample rows of an N-row gallery (ofr_knn_f6_sampled: at most this many)
 static int64_t sample_rows(int64_t N) { return cdiv(N > 0 ? N : 1, q8s::SAMPLE_STEP); }
 
@@ -2190,8 +2250,9 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                            f6t::LDS, st, s);
       if (phases & 4) {
         OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
+        const bool prefix = a.nkp < f6t::stages(d);
         hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, s.cand, s.ntg,
-                           theta, count, B, std::max(k, sieve_rank(rows)), armed);
+                           theta, count, B, std::max(k, prefix && rows ? f6p_rank() : sieve_rank(rows)), armed);
         OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
       }
       a.theta = theta;

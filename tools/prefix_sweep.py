@@ -60,12 +60,13 @@ def main():
         print(f"pst {pst} sieve_ms {np.median(ms):.3f} kept_mean {kept:.1f}", flush=True)
         if a.trace:
             t = g.ws.buf[:64 * 8 * 8].view(torch.int64).view(64, 8).cpu().numpy()
-            names = ["wait_copies", "mfma+barrier", "copy_issue+tables", "compares", "flush", "->next"]
+            names = ["wait_copies", "flush_begin", "mfmas", "barrier", "copy_issue+tables", "compares", "sync"]
             rows = [r for r in t if r[0] > 0 and r[5] > r[0]]
-            dd = np.array([[r[1] - r[0], r[2] - r[1], r[3] - r[2], r[4] - r[3], r[5] - r[4]] for r in rows], np.float64)
+            dd = np.array([[r[1] - r[0], r[6] - r[1], r[7] - r[6], r[2] - r[7], r[3] - r[2], r[4] - r[3], r[5] - r[4]]
+                           for r in rows], np.float64)
             gaps = np.array([rows[j + 1][0] - rows[j][5] for j in range(len(rows) - 1)], np.float64)
             print("  trace panels", len(rows), "median cycles:",
-                  {n: float(np.median(dd[:, j])) for j, n in enumerate(names[:5])},
+                  {n: float(np.median(dd[:, j])) for j, n in enumerate(names)},
                   "gap", float(np.median(gaps)) if len(gaps) else None, flush=True)
 
 
