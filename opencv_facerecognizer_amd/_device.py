@@ -700,11 +700,13 @@ class FloatGallery:
         elif tier == "f6x2" and self.row_sample():
             s1 = self._tier_gallery("f6")
             ns = -(-self.N // lib.ofr_f6_sample_step())
+            # the sample's row scales: the f6x2 builder's own (sscale2), equal to the f6 tier's by construction
+            # (quantize_f6_kernel<true> makes the same per-row scale; test_row_sample_extended_by_append pins it)
             call("ofr_knn_f6x2_sampled", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["Qs2"]),
                  ptr(qq["scale"]), ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]),
                  ptr(g["Gs2"]), ptr(g["scale"]), ptr(self.aux), ptr(g["gmax"]), k, index_base, ptr(out[0]),
                  ptr(out[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(s1["St"]), ptr(g["St2"]), ns,
-                 ptr(s1["sscale"]), ptr(s1["saux"]), ptr(ws), ws.numel(), ptr(self.bscale))
+                 ptr(g["sscale2"]), ptr(s1["saux"]), ptr(ws), ws.numel(), ptr(self.bscale))
         elif tier == "f6x2":
             call("ofr_knn_f6x2", stream(), phases, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["Qs2"]),
                  ptr(qq["scale"]), ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]),

@@ -1085,6 +1085,13 @@ __global__ void __launch_bounds__(256) premerge_kernel(const Cand* cand, int64_t
   if ((int)threadIdx.x < KC) out[(q * PM + blockIdx.x) * KC + threadIdx.x] = lists[threadIdx.x];
 }
 
+// the sieve's arm token for a B-query batch: a magic word and B (a stale or uninitialised workspace
+// word, or one armed for another batch size, does not match)
+__device__ __forceinline__ uint32_t arm_token(int64_t B) {
+  const uint32_t t = 0x5EE7A11Du ^ (uint32_t)(B * 2654435761u);
+  return t ? t : 1u;   // never 0: the disarmed value
+}
+
 // Sieve thresholds from the sample pass's tile lists: theta[q] = the rank-th best key (KEY_NONE
 // when the sample holds fewer than rank rows; rank <= KC); resets the bucket counts.  One wave per query (four
 // per block): each lane keeps the best 16 keys of its strided share (KeyList, one v_med3 per slot),
@@ -1092,7 +1099,8 @@ __global__ void __launch_bounds__(256) premerge_kernel(const Cand* cand, int64_t
 // (score, index): only the 16th score is used, and score_key is monotone).
 __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists, int64_t T, uint32_t* theta,
                                                               int* count, int64_t B, int rank, uint32_t* armed) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *armed = 1u;   // the buckets are reset: one sieve pass may follow
+  // the buckets are reset: one sieve pass may follow (sieve_arm_kernel checks this exact value)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *armed = arm_token(B);
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (q >= B) return;
@@ -1132,11 +1140,13 @@ __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists,
 // every kept row again, and duplicated candidates could certify a top-k that repeats one row: it is
 // made to overflow every bucket instead (uncertified, bound -inf).  One workgroup; disarms.
 __global__ void __launch_bounds__(256) sieve_arm_kernel(uint32_t* armed, int* count, int64_t B, int cap) {
+  // (a workspace never armed for this B holds anything: only the threshold kernel's token for B arms it;
+  // uninitialised memory equals it with probability 2^-32)
   __shared__ uint32_t a;
   if (threadIdx.x == 0) a = __atomic_load_n(armed, __ATOMIC_RELAXED);
   __syncthreads();
   if (threadIdx.x == 0) *armed = 0u;
-  if (a != 1u)
+  if (a != arm_token(B))
     for (int64_t q = threadIdx.x; q < B; q += blockDim.x) count[q] = cap + 1;
 }
 

@@ -57,7 +57,17 @@ def main():
             if rep >= 2:
                 ms.append(e0.elapsed_time(e1))
         kept = g.sieve_counts(B).double().mean().item()
-        print(f"pst {pst} sieve_ms {np.median(ms):.3f} kept_mean {kept:.1f}", flush=True)
+        mm = []
+        for rep in range(5):                           # the merge (exact re-rank + certificate) alone
+            g.search_q8_phase(4 | 8, Qd, qq, 1)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.search_q8_phase(2, Qd, qq, 1)
+            e1.record()
+            torch.cuda.synchronize()
+            mm.append(e0.elapsed_time(e1))
+        print(f"pst {pst} sieve_ms {np.median(ms):.3f} kept_mean {kept:.1f} merge_ms {np.median(mm):.3f} "
+              f"certified {int(qq['cert'].sum())}/{B}", flush=True)
         if a.trace:
             t = g.ws.buf[:64 * 8 * 8].view(torch.int64).view(64, 8).cpu().numpy()
             names = ["wait_copies", "flush_begin", "mfmas", "barrier", "copy_issue+tables", "compares", "sync"]
