@@ -756,7 +756,8 @@ def main():
         Qs = torch.zeros((bs, ld), dtype=torch.float32, device=device)
         P.project(Xq[:bs], shift64=gallery.shift64, out=Qs)
         f6_small = args.search == "f6" and gallery.use_q8(bs, k)
-        qs = gallery.quantize_queries(Qs, tier="f6") if f6_small else None
+        stier = gallery.start_tier(bs) if f6_small else None      # f6p when the gallery has a prefix
+        qs = gallery.quantize_queries(Qs, tier=stier) if f6_small else None
 
         def small_pass():
             if f6_small:
@@ -779,7 +780,7 @@ def main():
         for _ in range(reps):                 # the whole small-batch step: project, search, merge, certificate
             P.project(Xq[:bs], shift64=gallery.shift64, out=Qs)
             if f6_small:
-                qs = gallery.quantize_queries(Qs, qs, tier="f6")
+                qs = gallery.quantize_queries(Qs, qs, tier=stier)
                 o = gallery.search_q8_phase(3, Qs, qs, k, index_base=n0)
                 gallery.fallback(Qs, qs, k, o, index_base=n0)
             else:
@@ -788,12 +789,14 @@ def main():
         torch.cuda.synchronize()
         ms_step = (time.perf_counter() - t1) * 1e3 / reps
         if f6_small:
-            kern = "q8s::stream_kernel_f6 (ofr_knn_f6 phase 1, B<=32)"
-            bytes_t = 0.75 * (nl * d + bs * d)                       # fp6 tiles streamed once per batch
+            dm_s = min(d, 128 * gallery.prefix_stages()) if stier == "f6p" else d   # features the pass streams
+            kern = ("q8s::stream_kernel_f6 (ofr_knn_f6" + ("p_sampled, first %d features" % dm_s if stier == "f6p" else "")
+                    + " phase 1, B<=32)")
+            bytes_t = 0.75 * (nl * dm_s + bs * dm_s)                 # fp6 tiles streamed once per batch
         else:
             kern = "knn_tile_kernel<Cfg<32,4,1,4>> (ofr_knn_tiles_f32, B<=32)"
             bytes_t = nl * d * 4 + bs * d * 4                        # fp32 rows streamed once per batch
-        small.append({"batch": bs, "queries_per_s": bs / (ms_step * 1e-3), "ms_per_batch": ms_step,
+        small.append({"batch": bs, "queries_per_s": bs / (ms_step * 1e-3), "ms_per_batch": ms_step, "tier": stier,
                       "uncertified": (list(gallery.last_fallbacks) if f6_small else None),
                       "roofline": {"kernel": kern, "bound": "hbm", "achieved": bytes_t / (ms_t * 1e-3) / 1e9,
                                    "peak": PEAK_HBM / 1e9, "unit": "GB/s",
