@@ -269,7 +269,10 @@ class StepPipeline:
 def certificate_margin(gallery, Qd, qq, nsample=64):
     """(d_16^2 - d_1^2) / dS of the fp6 tier for a sample of queries: the certificate needs about 2
     (the 16th coarse candidate must clear the k-th exact distance by the bound on both sides).
-    d from the exact fp32 path, dS = the bound merge_kernel uses."""
+    d from the exact fp32 path, dS = the bound merge_kernel uses.  The fp6 tier's own
+    query stats (a batch that started at another tier is quantized for fp6 here)."""
+    if qq.get("tier") != "f6":
+        qq = gallery.quantize_queries(Qd, tier="f6")
     s = torch.arange(0, Qd.shape[0], max(1, Qd.shape[0] // nsample), device=Qd.device)[:nsample]
     dd, _ = gallery._search_f32(Qd.index_select(0, s).contiguous(), 16)
     dd = dd.cpu().numpy()

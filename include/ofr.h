@@ -249,6 +249,11 @@ int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int6
  * re-rank of the full rows) hold as for ofr_knn_f6; on features whose discriminating variance sits in
  * the leading columns (Fisherfaces / Eigenfaces output, eigenvalues descending) it certifies at a
  * fraction of the coarse work.  Replaces the same search as ofr_knn_f6 (classifier.py:94-129).     */
+/* its query rows: only the first pstages stages of each row's f6 tiles written, from the first
+ * min(d, 128 pstages) features, with their own row scale and (prefix) stats                       */
+int ofr_f6_quantize_rows_prefix(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int pstages,
+                                void* tiles, size_t tiles_bytes, float* scale, double* stats,
+                                const uint8_t* bscale);
 int ofr_knn_f6p_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                         const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                         const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,

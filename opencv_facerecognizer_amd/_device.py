@@ -645,7 +645,10 @@ class FloatGallery:
                        stats=torch.empty((B, 3), dtype=torch.float64, device=dev_),
                        cert=torch.empty(B, dtype=torch.int32, device=dev_),
                        bound=torch.empty(B, dtype=torch.float64, device=dev_), tier=tier, B=B, **extra)
-        if tier in ("f6", "f6p"):                  # the prefix tier scores the first stages of the same tiles
+        if tier == "f6p":                          # the prefix stages only (ofr_f6_quantize_rows_prefix)
+            call("ofr_f6_quantize_rows_prefix", stream(), ptr(Qd), B, self.d, Qd.shape[1], self.prefix_stages(),
+                 ptr(out["Qs"]), out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), ptr(self._block_scales()))
+        elif tier == "f6":
             call("ofr_f6_quantize_rows", stream(), ptr(Qd), B, self.d, Qd.shape[1], ptr(out["Qs"]),
                  out["Qs"].numel(), ptr(out["scale"]), ptr(out["stats"]), None, None, ptr(self._block_scales()))
         elif tier == "f6x2":

@@ -1444,7 +1444,7 @@ __device__ __forceinline__ uint32_t e2m3_code(double r, double& q) {
 template <bool X2>
 __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_t ldx, int64_t d, int64_t nst,
                                                           int64_t row0, char* tiles, float* scale, double* stats,
-                                                          char* tiles2, const uint8_t* bscale) {
+                                                          char* tiles2, const uint8_t* bscale, int64_t nsw) {
   __shared__ float redf[4];
   __shared__ double red[4][3];
   const int64_t row = row0 + blockIdx.x;   // destination row (X row blockIdx.x)
@@ -1469,7 +1469,7 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
                                     // stats below are of the values actually stored)
   const bool vec4 = ((ldx & 3) == 0) && (((uintptr_t)X & 15) == 0);
   double sa = 0, se = 0, s2 = 0;
-  const int64_t ngroups = nst * 4;
+  const int64_t ngroups = nsw * 4;   // the stages written: all nst, or a prefix (ofr_f6_quantize_rows_prefix)
   const int64_t poff = (row >> 8) * nst * (int64_t)f6t::PANEL;
   const int rl = (int)(row & 255);
   for (int64_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
@@ -1801,7 +1801,7 @@ extern "C" int ofr_f6_quantize_rows_at(void* stream, const float* X, int64_t R, 
   hipStream_t st = (hipStream_t)stream;
   const int64_t nst = f6t::stages(d);
   hipLaunchKernelGGL(q8s::quantize_f6_kernel<false>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
-                     (char*)tiles, scale, stats, nullptr, bscale);
+                     (char*)tiles, scale, stats, nullptr, bscale, nst);
   OFR_LAUNCH_CHECK("f6 quantize_kernel");
   const int64_t end = row0 + R;
   if (end % 256) {
@@ -1825,7 +1825,7 @@ extern "C" int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R
   hipStream_t st = (hipStream_t)stream;
   const int64_t nst = f6t::stages(d);
   hipLaunchKernelGGL(q8s::quantize_f6_kernel<true>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
-                     (char*)tiles1, scale, stats, (char*)tiles2, bscale);
+                     (char*)tiles1, scale, stats, (char*)tiles2, bscale, nst);
   OFR_LAUNCH_CHECK("f6x2 quantize_kernel");
   const int64_t end = row0 + R;
   if (end % 256) {
@@ -1834,6 +1834,32 @@ extern "C" int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R
       hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)t, end, nst);
       OFR_LAUNCH_CHECK("f6x2 zero_tail");
     }
+  }
+  return OFR_OK;
+}
+
+// The prefix tier's query rows: only the first pstages stages of each row's tiles are written (the
+// prefix pass reads no others), from the first min(d, 128 pstages) features -- their own row scale and
+// stats (a, e of the prefix: the prefix scores' error bound needs no more; the full tier re-quantizes).
+extern "C" int ofr_f6_quantize_rows_prefix(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx,
+                                           int pstages, void* tiles, size_t tiles_bytes, float* scale,
+                                           double* stats, const uint8_t* bscale) {
+  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d, "ofr_f6_quantize_rows_prefix: bad sizes");
+  OFR_CHECK_ARG(pstages >= 1 && pstages <= f6t::stages(d), "ofr_f6_quantize_rows_prefix: pstages in [1, ceil(d / 128)]");
+  if (R == 0) return OFR_OK;
+  OFR_CHECK_ARG(X && tiles && scale && stats, "ofr_f6_quantize_rows_prefix: null pointer");
+  OFR_CHECK_ARG(R < 0x7fffffffLL, "ofr_f6_quantize_rows_prefix: too many rows");
+  OFR_CHECK_ARG(tiles_bytes >= ofr_f6_tiles_bytes(R, d), "ofr_f6_quantize_rows_prefix: tile buffer too small");
+  OFR_CHECK_ARG((uintptr_t)tiles % 16 == 0, "ofr_f6_quantize_rows_prefix: tiles must be 16-byte aligned");
+  OFR_CHECK_ARG(bscale_ok(bscale), "ofr_f6_quantize_rows_prefix: bscale must be 4-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nst = f6t::stages(d), dm = std::min<int64_t>(d, (int64_t)pstages * f6t::BK);
+  hipLaunchKernelGGL(q8s::quantize_f6_kernel<false>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, dm, nst, (int64_t)0,
+                     (char*)tiles, scale, stats, nullptr, bscale, (int64_t)pstages);
+  OFR_LAUNCH_CHECK("f6 quantize_kernel (prefix)");
+  if (R % 256) {
+    hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)tiles, R, nst);
+    OFR_LAUNCH_CHECK("f6 zero_tail");
   }
   return OFR_OK;
 }
