@@ -887,6 +887,16 @@ def main():
             "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else "") + ("+all_gather" if shard_prep else ""):
                            ms_proj, "knn_tiles": ms_tiles,
                            "knn_merge_rerank" + ("+certificate" if use_q8 else ""): ms_merge},
+            # the preparation beside the dominant kernel (round 5: the two take about the same time): the
+            # exact projection W^T x of the batch's faces on the int8 MFMA, four W slices --
+            # 2 D d int8 ops per face and slice, timed with the quantization by the preparation's events
+            "roofline_preparation": {
+                "kernel": "q8::project_q8w_kernel (ofr_project_u8_exact, 4 int8 slices of W) + quantization",
+                "bound": "mfma", "unit": "TOPS", "peak": PEAK_I8_MFMA / 1e12,
+                "algorithmic_ops_per_step": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d,
+                "achieved": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d / (ms_proj * 1e-3) / 1e12,
+                "frac": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d / (ms_proj * 1e-3) / PEAK_I8_MFMA,
+                "ms": ms_proj},
             "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
             "start_tiers": ({t: starts[-args.steps:].count(t) for t in sorted(set(starts[-args.steps:]))}
                             if starts else None),
