@@ -1683,6 +1683,10 @@ static int device_cus() {
 // last round of items over the CUs wastes little -- the makespan in panels, ceil(items / cus) x qg,
 // plus half a panel per item for its gallery copies and tables, is minimal
 static int64_t f6p_group(int64_t ntg, int64_t ntq, int cus) {
+  if (const char* e = getenv("OFR_F6P_GROUP")) {   // probe override
+    const int64_t v = atoll(e);
+    if (v >= 1) return v < ntq ? v : ntq;
+  }
   int64_t best = ntq, cost = INT64_MAX;
   for (int64_t div = 1; div <= ntq; div *= 2) {
     const int64_t qg = (ntq + div - 1) / div, items = ntg * ((ntq + qg - 1) / qg);
