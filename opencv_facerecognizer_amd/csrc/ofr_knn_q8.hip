@@ -1070,6 +1070,49 @@ __device__ __forceinline__ void block_best(const Cand* src, int64_t n, Cand* lis
   }
 }
 
+// Best KC of a short candidate list (a sieve bucket) into lists[0..KC) (4 KC entries of LDS): per-thread
+// lists, a shuffle merge inside each wave, then the four wave lists by thread 0.  The same KC best
+// (distance, index) pairs as block_best (a unique set), in ascending order.
+__device__ __forceinline__ void block_best_small(const Cand* src, int64_t n, Cand* lists) {
+  TopList<KC> L;
+  L.init();
+  for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+    const Cand c = src[e];
+    if (better_f(c.d, c.i, L.d[KC - 1], L.i[KC - 1])) L.insert(c.d, c.i);
+  }
+  for (int off = 1; off < 64; off <<= 1) {
+    float od[KC];
+    int oi[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      od[j] = __shfl_xor(L.d[j], off);
+      oi[j] = __shfl_xor(L.i[j], off);
+    }
+    L.merge(od, oi);
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0 && wave > 0) {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) lists[wave * KC + j] = Cand{L.d[j], L.i[j]};
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      float od[KC];
+      int oi[KC];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        od[j] = lists[w * KC + j].d;
+        oi[j] = lists[w * KC + j].i;
+      }
+      L.merge(od, oi);
+    }
+#pragma unroll
+    for (int j = 0; j < KC; ++j) lists[j] = Cand{L.d[j], L.i[j]};
+  }
+  __syncthreads();
+}
+
 // Small batches: the streaming pass leaves T * KC candidates per query (62.5k at N = 1M), and one
 // merge block per query inserting them into per-thread sorted lists is divergent and serial
 // (240 us per query).  PM blocks per query first reduce contiguous chunks to their best KC.
@@ -1155,8 +1198,11 @@ __global__ void __launch_bounds__(256) sieve_arm_kernel(uint32_t* armed, int* co
 // (distance.py:60) of the survivors in coarse order, one wave per candidate (float4 loads, lane
 // partial sums, shuffle reduction), until the coarse bound proves the rest cannot reach the
 // k-th; (3) sort by (distance, index) and the certificate.
+// SMALL: the sieve's buckets (~120-260 rows per query): block_best_small and 4 KC list entries of LDS
+// instead of block_best's 256 KC (32 KiB), so 4x as many merge blocks fit a CU.
+template <bool SMALL>
 __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
-  __shared__ Cand lists[256 * KC];
+  __shared__ Cand lists[(SMALL ? 4 : 256) * KC];
   __shared__ double exact[KC];
   __shared__ double red[4];
   __shared__ int stop_flag;
@@ -1176,8 +1222,9 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     if (p.count) {
       const int64_t c = p.count[q];
       overflow = c > p.cap || c < 0;   // rows were dropped (and a tile-level overflow writes none): no candidates
-      block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
-    } else {
+      if constexpr (SMALL) block_best_small(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
+      else block_best(p.cand + (size_t)q * p.cap, overflow ? 0 : c, lists);
+    } else if constexpr (!SMALL) {
       block_best(p.cand + (size_t)q * p.T * KC, p.T * KC, lists);
     }
     // loads batched 8 deep: with few queries (one block each) a loop with one load per iteration is
@@ -1777,7 +1824,7 @@ extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, 
   if (phases & 2) {
     OFR_CHECK_ARG(out_d && out_i && cert, "ofr_knn_q8: null output");
     q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, 0.0, k, index_base, out_d, out_i, cert, bound};
-    hipLaunchKernelGGL(q8s::merge_kernel, dim3((unsigned)B), dim3(256), 0, st, m);
+    hipLaunchKernelGGL(q8s::merge_kernel<false>, dim3((unsigned)B), dim3(256), 0, st, m);
     OFR_LAUNCH_CHECK("q8 merge_kernel");
   }
   return OFR_OK;
@@ -2368,7 +2415,10 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       m.cand = pm;
       m.T = q8s::PM;
     }
-    hipLaunchKernelGGL(q8s::merge_kernel, dim3((unsigned)B), dim3(256), 0, st, m);
+    if (sieve)
+      hipLaunchKernelGGL(q8s::merge_kernel<true>, dim3((unsigned)B), dim3(256), 0, st, m);
+    else
+      hipLaunchKernelGGL(q8s::merge_kernel<false>, dim3((unsigned)B), dim3(256), 0, st, m);
     OFR_LAUNCH_CHECK("f6 merge_kernel");
   }
   return OFR_OK;
