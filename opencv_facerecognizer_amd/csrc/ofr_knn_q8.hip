@@ -516,7 +516,7 @@ constexpr int QS = NSPMAX * E::GSLOT;                       // query slots [NSPM
 // operand tables, raw copies of the global arrays (buffer_load ... lds: no registers, no waits until the
 // next panel's top): per panel slot (2) the queries' scale [256] and threshold key [256]; per item slot
 // (2) the tile rows' aux [384] and scale [384]
-constexpr int QSC = QS + NSPMAX * E::QSLOT;                 // [2][256] f32 query scale
+constexpr int QSC = QS + NSPMAX * E::QSLOT;                 // [2][256] f32 query scale (a power of two)
 constexpr int QTH = QSC + 2 * 1024;                         // [2][256] u32 theta
 constexpr int GAUX = QTH + 2 * 1024;                        // [2][384] f32 row aux (|g_m|^2)
 constexpr int GSCL = GAUX + 2 * 1536;                       // [2][384] f32 row scale
@@ -532,9 +532,9 @@ static_assert(LDS_BYTES <= 163840, "prefix pass LDS");
 // hazard recognizer does not see into asm, so that MFMA read them overwritten -- one-stage passes lost
 // query column block 5 (tests/test_gpu_prefix.py, round 5).  VGPR row blocks start from accumulators
 // zeroed before the stage's first MFMA (as f6t::EngineW), with the accumulating form.
-__device__ __forceinline__ void mfma0a(const f6t::i32x6& a, const f6t::i32x6& b, f6t::f32x4& c, int sc) {
-  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
-               : "=&a"(c) : "v"(a), "v"(b), "v"(sc));
+__device__ __forceinline__ void mfma0a(const f6t::i32x6& a, const f6t::i32x6& b, f6t::f32x4& c, int sa, int sb) {
+  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, 0, %3, %4 op_sel_hi:[0,0,0] cbsz:2 blgp:2"
+               : "=&a"(c) : "v"(a), "v"(b), "v"(sa), "v"(sb));
 }
 
 // wave W's copy pieces of the gallery tile gt (all NSP stages) / of query panel qp
@@ -584,9 +584,21 @@ __device__ __forceinline__ E::Bases lane_bases(uint32_t slot, uint32_t tid, uint
 // zero).  As in f6t::EngineW, the next stage's fragments are read in the last rows of the current one
 // (gallery rows 0 and 1 into the ring slots rows 10 and 11 free, each query fragment right after its
 // last MFMA in row 11), so only the panel's first stage waits for its reads.
+//
+// Query scales: the prefix queries' row scales are powers of two 2^e_q (ofr_f6_quantize_rows_prefix), and
+// e_q joins the query operand's E8M0 block scale (per lane: the lane's column), so acc = s_q (q~ . g~)
+// exactly -- a power-of-two rescaling commutes with every rounding of the MFMA -- and the compares need
+// no per-query product (the same scores, bit for bit, as the unfolded f6w pass: tests/test_gpu_prefix.py).
 template <int W, int NSP>
-__device__ __forceinline__ void panel_mfmas(const int (&sc)[NSPMAX], uint32_t tid, f6t::f32x4 (&acc)[E::NA][E::NB]) {
+__device__ __forceinline__ void panel_mfmas(const int (&sc)[NSPMAX], const uint32_t* qex, uint32_t tid,
+                                            f6t::f32x4 (&acc)[E::NA][E::NB]) {
   constexpr int WR = W >> 1, WC = W & 1;
+  int eq[E::NB];   // the lane's query exponent per column block; past B the table reads 0: e_q = 0
+#pragma unroll
+  for (int c = 0; c < E::NB; ++c) {
+    const uint32_t sb = qex[WC * 128 + c * 16 + (tid & 15)];
+    eq[c] = sb != 0u ? (int)((sb >> 23) & 0xffu) - 127 : 0;
+  }
 #pragma unroll
   for (int i = E::NAA; i < E::NA; ++i)   // the VGPR accumulators zeroed before any MFMA: their registers
 #pragma unroll                           // are theirs alone
@@ -604,6 +616,9 @@ __device__ __forceinline__ void panel_mfmas(const int (&sc)[NSPMAX], uint32_t ti
     constexpr int S = decltype(sv)::value;
     constexpr bool NEXT = S + 1 < NSP;
     const int scs = sc[S];
+    int sbq[E::NB];   // query operand scales: the block's byte + e_q (bytes in [0, 191]: no carry out)
+#pragma unroll
+    for (int c = 0; c < E::NB; ++c) sbq[c] = scs + eq[c];
     const E::Bases ab = lane_bases(GS + S * E::GSLOT, tid, 3072, 2048);
     const E::Bases an = lane_bases(GS + (NEXT ? S + 1 : S) * E::GSLOT, tid, 3072, 2048);
     const E::Bases bn = lane_bases(QS + (NEXT ? S + 1 : S) * E::QSLOT, tid, 6144, 4096);
@@ -613,8 +628,8 @@ __device__ __forceinline__ void panel_mfmas(const int (&sc)[NSPMAX], uint32_t ti
       if constexpr (i + 2 < E::NA) a[(i + 2) % E::RING] = E::fragA<WR * 192 + (i + 2 < E::NA ? i + 2 : 0) * 16>(ab);
       else if constexpr (NEXT) a[(i + 2) % E::RING] = E::fragA<WR * 192 + (i + 2 - E::NA) * 16>(an);
       auto mm = [&](int c) {
-        if constexpr (S == 0 && AG) mfma0a(a[i % E::RING], b[c], acc[i][c], scs);
-        else E::mfma<AG>(a[i % E::RING], b[c], acc[i][c], scs);
+        if constexpr (S == 0 && AG) mfma0a(a[i % E::RING], b[c], acc[i][c], scs, sbq[c]);
+        else E::mfma2<AG>(a[i % E::RING], b[c], acc[i][c], scs, sbq[c]);
       };
       if constexpr (i == E::NA - 1 && NEXT) {
         mm(0); b[0] = E::fragB<WC * 128 + 0>(bn);
@@ -642,13 +657,14 @@ __device__ __forceinline__ void panel_mfmas(const int (&sc)[NSPMAX], uint32_t ti
   if constexpr (NSP > 1) stage(std::integral_constant<int, 1>{});
 }
 template <int NSP>
-__device__ __forceinline__ void mfmas(int wave, const int (&sc)[NSPMAX], uint32_t tid,
+__device__ __forceinline__ void mfmas(int wave, const int (&sc)[NSPMAX], const char* smem, int qb, uint32_t tid,
                                       f6t::f32x4 (&acc)[E::NA][E::NB]) {
+  const uint32_t* qex = reinterpret_cast<const uint32_t*>(smem + QSC) + qb * 256;
   switch (wave) {
-    case 0: panel_mfmas<0, NSP>(sc, tid, acc); break;
-    case 1: panel_mfmas<1, NSP>(sc, tid, acc); break;
-    case 2: panel_mfmas<2, NSP>(sc, tid, acc); break;
-    default: panel_mfmas<3, NSP>(sc, tid, acc); break;
+    case 0: panel_mfmas<0, NSP>(sc, qex, tid, acc); break;
+    case 1: panel_mfmas<1, NSP>(sc, qex, tid, acc); break;
+    case 2: panel_mfmas<2, NSP>(sc, qex, tid, acc); break;
+    default: panel_mfmas<3, NSP>(sc, qex, tid, acc); break;
   }
   E::wait_drain();
 }
@@ -660,7 +676,6 @@ __device__ __forceinline__ void mfmas(int wave, const int (&sc)[NSPMAX], uint32_
 __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t g0, int64_t q0, int wave,
                                          uint32_t tid, int qb, int gb, f6t::f32x4 (&acc)[E::NA][E::NB]) {
   const int WR = wave >> 1;
-  const float* qsc = reinterpret_cast<const float*>(smem + QSC) + qb * 256;
   const uint32_t* qth = reinterpret_cast<const uint32_t*>(smem + QTH) + qb * 256;
   const float* gaux = reinterpret_cast<const float*>(smem + GAUX) + gb * E::TGW;
   const float* gscl = reinterpret_cast<const float*>(smem + GSCL) + gb * E::TGW;
@@ -668,13 +683,9 @@ __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t 
   uint2* hits = reinterpret_cast<uint2*>(smem + HITS);
   const int nvalid = p.N - g0 < E::TGW ? (int)(p.N - g0) : E::TGW;
   const int lane = tid & 63, wc = wave & 1, g4 = (lane >> 4) * 4, r16 = lane & 15;
-  float sq2[E::NB], th[E::NB];   // (2 s_q, theta as a float): fix_query_tables made them at the panel's top
+  float th[E::NB];   // theta as a float: fix_query_tables made it at the panel's top
 #pragma unroll
-  for (int c = 0; c < E::NB; ++c) {
-    const int ql = wc * 128 + c * 16 + r16;
-    sq2[c] = qsc[ql];
-    th[c] = __uint_as_float(qth[ql]);
-  }
+  for (int c = 0; c < E::NB; ++c) th[c] = __uint_as_float(qth[wc * 128 + c * 16 + r16]);
   typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int ii = 0; ii < E::NA; ++ii) {
@@ -683,7 +694,9 @@ __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t 
     // rows past N read zeros (aux 0, scale 0: a score of 0), which the hit test below excludes
     const float4 ta = *reinterpret_cast<const float4*>(gaux + gl0);
     const float4 ts = *reinterpret_cast<const float4*>(gscl + gl0);
-    const f32x2 avp[2] = {f32x2{ta.x, ta.y}, f32x2{ta.z, ta.w}}, svp[2] = {f32x2{ts.x, ts.y}, f32x2{ts.z, ts.w}};
+    // 2 s_g: the query scale is in acc already (panel_mfmas); sc = fma(-2 s_g, acc, a) in packed pairs
+    const f32x2 avp[2] = {f32x2{ta.x, ta.y}, f32x2{ta.z, ta.w}};
+    const f32x2 tp[2] = {f32x2{ts.x, ts.y} + f32x2{ts.x, ts.y}, f32x2{ts.z, ts.w} + f32x2{ts.z, ts.w}};
     float sc[4][E::NB];
     uint64_t col[E::NB];
     uint64_t any = 0;
@@ -691,8 +704,7 @@ __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t 
     for (int c = 0; c < E::NB; ++c) {
 #pragma unroll
       for (int rp = 0; rp < 2; ++rp) {
-        const f32x2 t = svp[rp] * sq2[c];
-        const f32x2 x = __builtin_elementwise_fma(-t, f32x2{acc[i][c][2 * rp], acc[i][c][2 * rp + 1]}, avp[rp]);
+        const f32x2 x = __builtin_elementwise_fma(-tp[rp], f32x2{acc[i][c][2 * rp], acc[i][c][2 * rp + 1]}, avp[rp]);
         sc[2 * rp][c] = x.x;
         sc[2 * rp + 1][c] = x.y;
       }
@@ -776,14 +788,11 @@ __device__ __forceinline__ void load_query_tables(const TileArgs& p, int wave, u
   table_piece(p.qscale + q0, p.B - q0, QSC + qb * 1024, wave, lane);
   table_piece(p.theta + q0, p.B - q0, QTH + qb * 1024, wave, lane);
 }
-// the raw query tables of slot qb -> (2 s_q, key_float(theta | 0xff)), in place; past B: no row kept (the
-// copies read zeros there)
+// the raw theta table of slot qb -> key_float(theta | 0xff), in place; past B: no row kept (the copies
+// read zeros there).  The scales stay raw (panel_mfmas reads them before the next barrier).
 __device__ __forceinline__ void fix_query_tables(char* smem, const TileArgs& p, int64_t q0, int qb, uint32_t tid) {
-  float* qsc = reinterpret_cast<float*>(smem + QSC) + qb * 256;
   uint32_t* qth = reinterpret_cast<uint32_t*>(smem + QTH) + qb * 256;
-  const float s2 = 2.0f * qsc[tid];
   const uint32_t t = qth[tid];
-  qsc[tid] = s2;
   qth[tid] = __float_as_uint(q0 + tid < p.B ? key_float(t | 0xffu) : -__builtin_inff());
 }
 __device__ __forceinline__ void load_tile_tables(const TileArgs& p, int wave, uint32_t lane, int64_t g0, int gb) {
@@ -844,7 +853,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
       const f6p::Pending pd = prev ? f6p::flush_begin(smem, p, pg0, pq0, tid) : f6p::Pending{-1, 0, {0u, 0u}};
       F6P_MARK(6);
       f6t::f32x4 acc[E::NA][E::NB];   // per panel: stage 0 writes every accumulator
-      f6p::mfmas<NSP>(wave, sc, tid, acc);
+      f6p::mfmas<NSP>(wave, sc, smem, buf, tid, acc);
       F6P_MARK(7);
       f6t::barrier();   // every wave's fragment reads of the slots done: refill them
       F6P_MARK(2);
@@ -1491,7 +1500,8 @@ __device__ __forceinline__ uint32_t e2m3_code(double r, double& q) {
 template <bool X2>
 __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_t ldx, int64_t d, int64_t nst,
                                                           int64_t row0, char* tiles, float* scale, double* stats,
-                                                          char* tiles2, const uint8_t* bscale, int64_t nsw) {
+                                                          char* tiles2, const uint8_t* bscale, int64_t nsw,
+                                                          int pow2) {
   __shared__ float redf[4];
   __shared__ double red[4][3];
   const int64_t row = row0 + blockIdx.x;   // destination row (X row blockIdx.x)
@@ -1507,7 +1517,15 @@ __global__ void __launch_bounds__(256) quantize_f6_kernel(const float* X, int64_
   __syncthreads();
   mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
   float s = 1.0f;
-  if (mx > 0.f) {
+  if (pow2) {   // s = 2^e, the least with mx / s <= 7.5, e in [-64, 64] (the prefix pass folds e into the MFMA)
+    int e = 0;
+    if (mx > 0.f) {
+      const double m = __builtin_frexp((double)mx / 7.5, &e);   // mx / 7.5 = m 2^e, m in [0.5, 1)
+      if (m == 0.5) --e;
+      e = e < -64 ? -64 : (e > 64 ? 64 : e);
+    }
+    s = __builtin_ldexpf(1.0f, e);
+  } else if (mx > 0.f) {
     s = (float)((double)mx / 7.5);
     while ((double)mx / (double)s > 7.5) s = __uint_as_float(__float_as_uint(s) + 1u);
   }
@@ -1852,7 +1870,7 @@ extern "C" int ofr_f6_quantize_rows_at(void* stream, const float* X, int64_t R, 
   hipStream_t st = (hipStream_t)stream;
   const int64_t nst = f6t::stages(d);
   hipLaunchKernelGGL(q8s::quantize_f6_kernel<false>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
-                     (char*)tiles, scale, stats, nullptr, bscale, nst);
+                     (char*)tiles, scale, stats, nullptr, bscale, nst, 0);
   OFR_LAUNCH_CHECK("f6 quantize_kernel");
   const int64_t end = row0 + R;
   if (end % 256) {
@@ -1876,7 +1894,7 @@ extern "C" int ofr_f6x2_quantize_rows_at(void* stream, const float* X, int64_t R
   hipStream_t st = (hipStream_t)stream;
   const int64_t nst = f6t::stages(d);
   hipLaunchKernelGGL(q8s::quantize_f6_kernel<true>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, d, nst, row0,
-                     (char*)tiles1, scale, stats, (char*)tiles2, bscale, nst);
+                     (char*)tiles1, scale, stats, (char*)tiles2, bscale, nst, 0);
   OFR_LAUNCH_CHECK("f6x2 quantize_kernel");
   const int64_t end = row0 + R;
   if (end % 256) {
@@ -1906,7 +1924,7 @@ extern "C" int ofr_f6_quantize_rows_prefix(void* stream, const float* X, int64_t
   hipStream_t st = (hipStream_t)stream;
   const int64_t nst = f6t::stages(d), dm = std::min<int64_t>(d, (int64_t)pstages * f6t::BK);
   hipLaunchKernelGGL(q8s::quantize_f6_kernel<false>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, dm, nst, (int64_t)0,
-                     (char*)tiles, scale, stats, nullptr, bscale, (int64_t)pstages);
+                     (char*)tiles, scale, stats, nullptr, bscale, (int64_t)pstages, 1);
   OFR_LAUNCH_CHECK("f6 quantize_kernel (prefix)");
   if (R % 256) {
     hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)tiles, R, nst);
