@@ -520,9 +520,10 @@ constexpr int QSC = QS + NSPMAX * E::QSLOT;                 // [2][256] f32 quer
 constexpr int QTH = QSC + 2 * 1024;                         // [2][256] u32 theta
 constexpr int GAUX = QTH + 2 * 1024;                        // [2][384] f32 row aux (|g_m|^2)
 constexpr int GSCL = GAUX + 2 * 1536;                       // [2][384] f32 row scale
-constexpr int NHIT = GSCL + 2 * 1536;                       // hits of the panel
-constexpr int HITS = NHIT + 16;                             // [HCAP] (key, query << 9 | row)
-constexpr int HCAP = 3836;                                  // hit slots per (tile, panel): the rest of the LDS
+constexpr int NHIT = GSCL + 2 * 1536;                       // [4] hits of the panel per wave
+constexpr int HITS = NHIT + 16;                             // [4][HCAPW] (key, query << 9 | row)
+constexpr int HCAPW = 959;                                  // hit slots per wave and (tile, panel)
+constexpr int HCAP = 4 * HCAPW;                             // the rest of the LDS
 constexpr int LDS_BYTES = HITS + HCAP * 8;
 static_assert(LDS_BYTES <= 163840, "prefix pass LDS");
 
@@ -670,7 +671,8 @@ __device__ __forceinline__ void mfmas(int wave, const int (&sc)[NSPMAX], const c
 }
 
 // The sieve compares of one (tile, panel): f6w_epilogue's, with the operand tables in LDS and the hits
-// into the LDS list.  (Round 5 tried a branch-free first pass over all row blocks with a second pass for
+// into the wave's own LDS list.  (Rolling the hit path into one copy per column block or per row block,
+// 21k -> 12k / 6.8k instructions, measured no faster: profiles/r05_rolled_hits_ab.txt.  Round 5 tried a branch-free first pass over all row blocks with a second pass for
 // the blocks with a hit: it kept every accumulator live through both, spilled, and was slower.)
 // The VGPR accumulators (row blocks NAA..NA-1) go first: their registers are free for the rest.
 __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t g0, int64_t q0, int wave,
@@ -679,8 +681,8 @@ __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t 
   const uint32_t* qth = reinterpret_cast<const uint32_t*>(smem + QTH) + qb * 256;
   const float* gaux = reinterpret_cast<const float*>(smem + GAUX) + gb * E::TGW;
   const float* gscl = reinterpret_cast<const float*>(smem + GSCL) + gb * E::TGW;
-  uint32_t* nhit = reinterpret_cast<uint32_t*>(smem + NHIT);
-  uint2* hits = reinterpret_cast<uint2*>(smem + HITS);
+  uint2* hits = reinterpret_cast<uint2*>(smem + HITS) + wave * HCAPW;   // the wave's own list: no atomics,
+  uint32_t cnt = 0;                                                      // its fill count uniform (SGPR)
   const int nvalid = p.N - g0 < E::TGW ? (int)(p.N - g0) : E::TGW;
   const int lane = tid & 63, wc = wave & 1, g4 = (lane >> 4) * 4, r16 = lane & 15;
   float th[E::NB];   // theta as a float: fix_query_tables made it at the panel's top
@@ -717,23 +719,29 @@ __device__ __forceinline__ void compares(char* smem, const TileArgs& p, int64_t 
     for (int c = 0; c < E::NB; ++c) {
       if (col[c] == 0) continue;   // uniform
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (!(sc[r][c] > th[c]) && gl0 + r < nvalid) {   // padding rows (aux +inf) pass only a NaN th
+      for (int r = 0; r < 4; ++r) {
+        const bool h = !(sc[r][c] > th[c]) && gl0 + r < nvalid;   // padding rows (aux +inf): only a NaN th
+        const uint64_t m = __builtin_amdgcn_ballot_w64(h);
+        if (m == 0) continue;   // uniform
+        if (h) {
           const int ql = wc * 128 + c * 16 + r16;
           const uint32_t kb = __float_as_uint(key_score(score_key(sc[r][c], 0)));
-          const uint32_t slot = atomicAdd(nhit, 1u);
-          if (slot < (uint32_t)HCAP) {
+          const uint32_t slot = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (slot < (uint32_t)HCAPW) {
             hits[slot] = make_uint2(kb, ((uint32_t)ql << 9) | (uint32_t)(gl0 + r));
           } else {   // the list is full (small galleries: ~3 % of the pairs kept): straight to the bucket
             const int bs = atomicAdd(p.count + q0 + ql, 1);
             if (bs < p.cap) p.bucket[(q0 + ql) * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + gl0 + r)};
           }
         }
+        cnt += (uint32_t)__builtin_popcountll(m);
+      }
     }
   }
+  if (lane == 0) reinterpret_cast<uint32_t*>(smem + NHIT)[wave] = cnt < (uint32_t)HCAPW ? cnt : (uint32_t)HCAPW;
 }
 
-// Flush of the hit list (tile rows from g0, queries from q0) into the per-query buckets, split so that
+// Flush of the hit lists (tile rows from g0, queries from q0) into the per-query buckets, split so that
 // the global atomics' round trip runs under the next panel's MFMAs: begin takes each thread's hit into
 // registers -- the list is free for the next compares -- and reserves its slot (a longer list, rare on
 // large galleries, is flushed here whole; hits past the list's capacity went to the buckets directly),
@@ -746,11 +754,18 @@ struct Pending {
 __device__ __forceinline__ Pending flush_begin(char* smem, const TileArgs& p, int64_t g0, int64_t q0,
                                                uint32_t tid) {
   Pending pd{-1, 0, make_uint2(0u, 0u)};
-  const uint32_t nh = min(*reinterpret_cast<const uint32_t*>(smem + NHIT), (uint32_t)HCAP);   // the rest went
-  const uint2* hits = reinterpret_cast<const uint2*>(smem + HITS);                           // to the buckets
+  const uint32_t* nw = reinterpret_cast<const uint32_t*>(smem + NHIT);   // the four waves' lists (the rest
+  const uint32_t n0 = nw[0], n1 = nw[1], n2 = nw[2], n3 = nw[3];          // went to the buckets)
+  const uint32_t nh = n0 + n1 + n2 + n3;
+  const uint2* hits = reinterpret_cast<const uint2*>(smem + HITS);
+  auto entry = [&](uint32_t e) {   // entry e of the concatenated lists
+    uint32_t w = 0;
+    if (e >= n0) { e -= n0; w = 1; if (e >= n1) { e -= n1; w = 2; if (e >= n2) { e -= n2; w = 3; } } }
+    return hits[w * HCAPW + e];
+  };
   if (nh > (uint32_t)E::NT) {
     for (uint32_t e = tid; e < nh; e += E::NT) {
-      const uint2 hv = hits[e];
+      const uint2 hv = entry(e);
       const int64_t q = q0 + (int)(hv.y >> 9);
       if (q < p.B) {
         const int slot = atomicAdd(p.count + q, 1);
@@ -758,7 +773,7 @@ __device__ __forceinline__ Pending flush_begin(char* smem, const TileArgs& p, in
       }
     }
   } else if (tid < nh) {
-    pd.hv = hits[tid];
+    pd.hv = entry(tid);
     pd.q = q0 + (int)(pd.hv.y >> 9);
     if (pd.q < p.B) pd.slot = atomicAdd(p.count + pd.q, 1);
     else pd.q = -1;
@@ -833,7 +848,6 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
   f6p::load_tile_tables(p, wave, threadIdx.x & 63, item_gt(w) * E::TGW, 0);
   f6p::load_query_tables(p, wave, threadIdx.x & 63, item_q0(w) * f6t::TQ, 0);
   f6p::copies<NSP>(wave, p, true, item_gt(w), item_q0(w));
-  if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(smem + f6p::NHIT) = 0u;
   int buf = 0, gb = 0;                // table slots of the current panel / item
   int64_t pg0 = 0, pq0 = 0;           // the previous panel's tile row / query base (its hits: the list)
   bool prev = false;
@@ -858,7 +872,6 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
       f6t::barrier();   // every wave's fragment reads of the slots done: refill them
       F6P_MARK(2);
       f6p::flush_end(p, pg0, pd);
-      if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(smem + f6p::NHIT) = 0u;   // read in flush_begin above
       // what comes next: the next panel of this item, or the next item's gallery tile and first panel
       const bool more = qp + 1 < qp1;
       const int64_t wn = more ? w : w + gridDim.x;
@@ -869,7 +882,7 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
         if (!more) f6p::load_tile_tables(p, wave, tid & 63, item_gt(wn) * E::TGW, gb ^ 1);
         f6p::copies<NSP>(wave, p, !more, item_gt(wn), qn);
       }
-      __syncthreads();   // the hit list's reset visible
+      __syncthreads();   // flush_begin's reads of the hit lists done before the compares refill them
       F6P_MARK(3);
       f6p::compares(smem, p, gt * E::TGW, qp * f6t::TQ, wave, tid, buf, gb, acc);
       F6P_MARK(4);

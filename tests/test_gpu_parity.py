@@ -658,7 +658,8 @@ def test_lbp_hist_counts_batch_vs_oracle():
         assert np.array_equal(c[i], ref), i
 
 
-@pytest.mark.parametrize("shape,grid", [((70, 70), (7, 7)), ((61, 93), (5, 4)), ((130, 128), (8, 8))])
+@pytest.mark.parametrize("shape,grid", [((70, 70), (7, 7)), ((61, 93), (5, 4)), ((130, 128), (8, 8)),
+                                        ((130, 128), (2, 2))])
 def test_lbp_hist_r1p8_ragged_vs_oracle(shape, grid):
     """The register-window ExtendedLBP(1, 8) histogram kernel on sizes whose cells leave code rows /
     columns uncovered and whose pixel counts are not multiples of 16 (unaligned image staging)."""
@@ -673,6 +674,25 @@ def test_lbp_hist_r1p8_ragged_vs_oracle(shape, grid):
     c = counts_numpy(counts, cb).astype(np.int64)
     for i in range(24):
         ref, _ = O.spatial_histogram_counts(O.elbp(imgs[i]), 8, grid)
+        assert np.array_equal(c[i], ref), i
+
+
+def test_lbp_hist_r1p8_smooth_faces_vs_oracle():
+    """Smooth images with little noise: the fast r1p8 kernel's fp32 decisions meet many near-ties
+    (flat and mirror-symmetric neighbourhoods, which take the wave through the fp64 sequence) and
+    its integer tie thresholds of points 4 and 6 (b == C) on every centre value."""
+    from ocvfacerec.facerec.feature import SpatialHistogram
+    from opencv_facerecognizer_amd._device import counts_numpy
+    r = _rng(13)
+    protos = r.integers(0, 256, (6, 16, 16)).astype(np.float64)
+    up = np.kron(protos, np.ones((8, 8)))
+    imgs = np.clip(up[np.arange(36) % 6] + r.normal(0, 1.5, (36, 128, 128)), 0, 255).astype(np.uint8)
+    imgs[30:] = np.arange(128, dtype=np.uint8)[None, :, None] * 2      # ramps: every centre value ties
+    sh = SpatialHistogram()
+    counts, cell, cb = sh.counts_device(imgs)
+    c = counts_numpy(counts, cb).astype(np.int64)
+    for i in range(36):
+        ref, _ = O.spatial_histogram_counts(O.elbp(imgs[i]), 8, (8, 8))
         assert np.array_equal(c[i], ref), i
 
 
