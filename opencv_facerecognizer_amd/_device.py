@@ -497,12 +497,16 @@ class FloatGallery:
     # the leading columns (the trained W of the headline: 6 blocks of rms 54-272 against 11 for the other
     # 307).  A block is "leading" when its mean square is >= PREFIX_RATIO x the median block's; the
     # prefix covers the stages up to the last leading block, when that is at most 1/PREFIX_MAX_FRAC of
-    # the stages and holds >= PREFIX_MIN_SHARE of the total variance.  Isotropic features (a random W)
-    # have no prefix, and a gallery whose prefix certifies badly is skipped by start_tier like any tier.
-    # OFR_F6_PREFIX: auto (default), 0 (off) or a stage count (tests / A-B).
+    # the stages and holds >= PREFIX_MIN_SHARE of the total variance; then the shortest prefix that still
+    # holds PREFIX_SHORTEN of that share (the pass's cost grows with its stages, the bound's strength with
+    # the share: on the headline's W one stage holds 0.74 against two stages' 0.83 and keeps as many
+    # candidates, every query certified, 1.22M -> 1.28M queries/s, profiles/r05_prefix_len_ab.txt).
+    # Isotropic features (a random W) have no prefix, and a gallery whose prefix certifies badly is
+    # skipped by start_tier like any tier.  OFR_F6_PREFIX: auto (default), 0 (off) or a stage count.
     PREFIX_RATIO = 8.0
     PREFIX_MAX_FRAC = 4
     PREFIX_MIN_SHARE = 0.5
+    PREFIX_SHORTEN = 0.85
 
     @classmethod
     def choose_prefix(cls, sums, d, N):
@@ -525,6 +529,9 @@ class FloatGallery:
         share = float(ms[:nb].dot(width[:nb]) / ms.dot(width))
         if pst * cls.PREFIX_MAX_FRAC > nst or share < cls.PREFIX_MIN_SHARE:
             return 0
+        for p in range(1, pst):
+            if float(ms[:4 * p].dot(width[:4 * p]) / ms.dot(width)) >= cls.PREFIX_SHORTEN * share:
+                return p
         return pst
 
     def prefix_stages(self):

@@ -183,7 +183,7 @@ def _block_sums(ms, N, d):
 def test_choose_prefix_host_logic(monkeypatch):
     """FloatGallery.choose_prefix: stages up to the last block whose mean square is >= PREFIX_RATIO x
     the median, if they are <= 1/PREFIX_MAX_FRAC of the stages and hold >= PREFIX_MIN_SHARE of the
-    variance; OFR_F6_PREFIX forces a count or 0."""
+    variance, shortened while PREFIX_SHORTEN of that share stays; OFR_F6_PREFIX forces a count or 0."""
     from opencv_facerecognizer_amd._device import FloatGallery as F
     monkeypatch.delenv("OFR_F6_PREFIX", raising=False)
     monkeypatch.delenv("OFR_SIEVE_SAMPLE", raising=False)
@@ -192,7 +192,11 @@ def test_choose_prefix_host_logic(monkeypatch):
     # the trained W's profile (bench feature_profile): 6 blocks of rms 272 .. 54, the rest ~11.4
     rms = np.full(nb, 11.4)
     rms[:6] = [272, 218, 180, 137, 87, 54]
-    assert F.choose_prefix(_block_sums(rms ** 2, 1000, d), d, 1000) == 2       # features 0..191 -> 2 stages
+    # features 0..191 lead (2 stages), but the first stage holds 0.94 of their share -> 1 stage
+    assert F.choose_prefix(_block_sums(rms ** 2, 1000, d), d, 1000) == 1
+    late = rms.copy()
+    late[4:8] = [200, 190, 180, 170]                       # the second stage as loud as the first: 2 stages
+    assert F.choose_prefix(_block_sums(late ** 2, 1000, d), d, 1000) == 2
     assert F.choose_prefix(_block_sums(np.full(nb, 130.0), 1000, d), d, 1000) == 0   # isotropic
     spread = rms.copy()
     spread[300] = 500                                      # a leading block late: prefix too long
