@@ -1,5 +1,7 @@
 #!/bin/bash
 # PMC counters of the LBP histogram kernels, the fp64 r1p8 kernel (OFR_LBP_EXACT64=1) beside the fast one
+# (round 5: the fast kernel and its OFR_LBP_EXACT64 switch were measured and not shipped -- DESIGN.md §8;
+# on the shipped library both passes time the same r1p8 kernel)
 # (run on the GPU box from the repo root; one --pmc pass per group, no trace domains)
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/pmc_lbp
