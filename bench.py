@@ -897,6 +897,13 @@ def main():
                 "achieved": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d / (ms_proj * 1e-3) / 1e12,
                 "frac": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d / (ms_proj * 1e-3) / PEAK_I8_MFMA,
                 "ms": ms_proj},
+            # which of the two is longer per step: since the one-stage prefix pass, the preparation's
+            # projection (roofline_preparation); `roofline` stays the search pass's (the path's own kernel)
+            "dominant_by_time": {"kernel": ("q8::project_q8w_kernel (roofline_preparation)"
+                                            if ms_proj > (ms_sieve if args.search == "f6" else ms_tiles)
+                                            else "the search pass (roofline)"),
+                                 "preparation_ms": ms_proj,
+                                 "search_pass_ms": ms_sieve if args.search == "f6" else ms_tiles},
             "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
             "start_tiers": ({t: starts[-args.steps:].count(t) for t in sorted(set(starts[-args.steps:]))}
                             if starts else None),
