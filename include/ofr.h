@@ -330,7 +330,9 @@ int ofr_knn_f6x2(void* stream, int phases, const float* Q, int64_t B, int64_t ld
  * ChiSquare :112-116), then per query the k smallest by (distance, row), NaN last.  Q [B][ldq] of
  * qdtype, G [N][ldg] of gdtype (OFR_DT_*; integer rows are counts, value = count / denom as the
  * reference's float64 histograms; denom 1 for float rows).  out_d / out_i [B][k]; entries past
- * min(k, N) are (+inf, -1).  min(k, N) <= 4096 (else OFR_E_UNSUPPORTED).  Workspace
+ * min(k, N) are (+inf, -1).  Any k: min(k, N) <= 4096 by a radix select in LDS, above it by a
+ * stable segmented radix sort (buffers of up to ~1.5 GiB allocated per call).  Each distance is the
+ * reference formula in fp64 summed in feature order: within ~1 ulp of numpy's pairwise sum.  Workspace
  * ofr_knn_deep_workspace_bytes(B, N) bytes (a block of the distance matrix, <= 2 GiB).          */
 size_t ofr_knn_deep_workspace_bytes(int64_t B, int64_t N);
 int ofr_knn_deep(void* stream, int metric, const void* Q, int64_t B, int64_t ldq, int qdtype, const void* G,

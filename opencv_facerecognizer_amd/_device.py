@@ -511,11 +511,12 @@ class FloatGallery:
     @classmethod
     def choose_prefix(cls, sums, d, N):
         """Prefix stages (0: no prefix tier) from the per-32-feature block sums of squares of the rows."""
-        env = os.environ.get("OFR_F6_PREFIX", "auto")
+        env = os.environ.get("OFR_F6_PREFIX", "auto").strip()
         nst = -(-d // 128)
         if env != "auto":
-            v = int(env)
-            return min(max(v, 0), nst)
+            if not env.isdigit():
+                raise ValueError(f"OFR_F6_PREFIX must be 'auto' or a stage count (0: off), not {env!r}")
+            return min(int(env), nst)
         if N < 1 or nst < cls.PREFIX_MAX_FRAC or os.environ.get("OFR_SIEVE_SAMPLE", "rows") == "panels":
             return 0
         width = np.minimum(32, d - 32 * np.arange(len(sums)))
@@ -908,7 +909,8 @@ class FloatGallery:
 
     def _search_f32(self, Qd, k, index_base=0):
         if k > _lib.MAX_K:
-            return search_deep(self.metric, Qd, _lib.DT_F32, self.G, _lib.DT_F32, self.d, 1.0, k, index_base)
+            return search_deep(self.metric, Qd, _lib.DT_F32, self.G, _lib.DT_F32, self.d, 1.0, k, index_base,
+                               workspace=self.ws)
         B = Qd.shape[0]
         out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
         out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)
@@ -1039,7 +1041,7 @@ class Chi2Gallery:
         if k > _lib.MAX_K:
             self.last_fallbacks = (0,)
             return search_deep(_lib.METRIC_CHISQUARE, Qd, self.dtype, self.G, self.dtype, self.nbins, self.denom, k,
-                               index_base)
+                               index_base, workspace=self.ws)
         out_d = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
         out_i = torch.empty((B, k), dtype=torch.int64, device=Qd.device)
         cert = torch.empty(B, dtype=torch.int32, device=Qd.device)
@@ -1073,15 +1075,17 @@ class Chi2Gallery:
         return f32_rows(np.asarray(arr, np.float64), ld=self.G.shape[1])
 
 
-def search_deep(metric, Q, qdtype, G, gdtype, d, denom, k, index_base=0):
+def search_deep(metric, Q, qdtype, G, gdtype, d, denom, k, index_base=0, workspace=None):
     """Any k (> 16 in practice): the reference's distance of every (query, row) pair in fp64 and the k
     smallest per query by (distance, row), NaN last (ofr_knn_deep; classifier.py:104-119, distance.py).
     Q [B][>= d], G [N][>= d] device rows of the given OFR dtypes (counts: value = count / denom).
+    workspace: a Workspace to reuse (the gallery's own; its distance block can reach 2 GiB).
     Returns (fp64 [B][k], int64 [B][k]); entries past N are (+inf, -1)."""
     B, N = int(Q.shape[0]), int(G.shape[0]) if G is not None else 0
     out_d = torch.empty((B, k), dtype=torch.float64, device=Q.device)
     out_i = torch.empty((B, k), dtype=torch.int64, device=Q.device)
-    ws = Workspace().get(_lib.load().ofr_knn_deep_workspace_bytes(B, N), Q.device) if N else None
+    ws = ((workspace or Workspace()).get(_lib.load().ofr_knn_deep_workspace_bytes(B, N), Q.device)
+          if N else None)
     call("ofr_knn_deep", stream(), metric, ptr(Q), B, Q.shape[1], qdtype, ptr(G), N, G.shape[1] if N else d, gdtype,
          d, float(denom), int(k), index_base, ptr(out_d), ptr(out_i), ptr(ws), 0 if ws is None else ws.numel())
     return out_d, out_i

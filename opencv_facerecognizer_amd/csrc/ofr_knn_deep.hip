@@ -13,10 +13,17 @@
 //   deep_select_kernel per query the k smallest (distance, row) pairs: an 8-pass radix select of
 //                      the k-th order key (order-preserving u64 of the distance, NaN last as
 //                      argsort puts it), an ordered gather (keys below it, then the lowest rows of
-//                      its ties) and a bitonic sort of the <= 4096 survivors in LDS.
+//                      its ties) and a bitonic sort of the <= 4096 survivors in LDS;
+//   min(k, N) > 4096   (round 6) a stable segmented radix sort of every query's (key, row) pairs
+//                      (rocPRIM), its first k taken: the same order, ties by row.
 // Rows past N come back as (+inf, -1), the convention of every search entry point.
 // Roofline: fp64 VALU (2 flops per pair and feature for Euclidean / Cosine, ~12 for ChiSquare's
-// division) -- a rare path (k > 16), exact by construction, no certificate needed.
+// division) -- a rare path (k > 16), no certificate needed.  Each distance is the reference formula
+// in fp64, its terms summed in feature order with fma: within ~1 ulp of numpy's pairwise float64 sum
+// (distance.py:60, :115-116), so rows whose reference distances are within an ulp may order
+// differently from np.argsort (tests/test_gpu_deep_k.py compares up to such near-ties).
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
 #include "ofr_common.h"
 
 namespace ofr {
@@ -246,6 +253,28 @@ __global__ void __launch_bounds__(256) deep_select_kernel(const double* D, int64
   }
 }
 
+// min(k, N) > MAXK: the order keys and rows of a block of queries (in place over the distances)
+__global__ void deep_keys_kernel(double* D, int32_t* rows, int64_t n, int64_t N) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = dkey(D[i]);
+    reinterpret_cast<uint64_t*>(D)[i] = key;
+    rows[i] = (int32_t)(i % N);
+  }
+}
+__global__ void deep_take_kernel(const uint64_t* keys, const int32_t* rows, int64_t N, int64_t nb, int k, int keff,
+                                 int64_t index_base, double* out_d, int64_t* out_i) {
+  const int64_t q = blockIdx.y;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < k; e += gridDim.x * blockDim.x) {
+    const bool ok = e < keff;
+    out_d[q * k + e] = ok ? kdist(keys[q * N + e]) : __builtin_inf();
+    out_i[q * k + e] = ok ? index_base + rows[q * N + e] : -1;
+  }
+}
+__global__ void deep_offsets_kernel(int* off, int64_t nb, int64_t N) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= nb) off[i] = (int)(i * N);
+}
+
 }  // namespace deep
 }  // namespace ofr
 
@@ -273,14 +302,35 @@ extern "C" int ofr_knn_deep(void* stream, int metric, const void* Q, int64_t B, 
   OFR_CHECK_ARG(qdtype >= OFR_DT_U8 && qdtype <= OFR_DT_F64 && gdtype >= OFR_DT_U8 && gdtype <= OFR_DT_F64,
                 "ofr_knn_deep: bad dtype");
   OFR_CHECK_ARG(denom > 0.0, "ofr_knn_deep: denom must be positive");
-  if (std::min<int64_t>(k, N) > deep::MAXK)
-    return fail(OFR_E_UNSUPPORTED, "ofr_knn_deep: k > 4096 on a gallery of more than 4096 rows");
   if (B == 0) return OFR_OK;
   OFR_CHECK_ARG(Q && out_d && out_i && (N == 0 || (G && workspace)), "ofr_knn_deep: null pointer");
   OFR_CHECK_ARG(N < 0x7fffffffLL, "ofr_knn_deep: N too large");
   OFR_CHECK_ARG(N == 0 || workspace_bytes >= ofr_knn_deep_workspace_bytes(B, N), "ofr_knn_deep: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  const int64_t bc = deep_block(B, N);
+  const bool sorted = std::min<int64_t>(k, N) > deep::MAXK;
+  // the sort path's blocks: a quarter of the distance block (the keys, rows and their sorted copies
+  // take 3x its bytes more, allocated per call: this path is rare)
+  const int64_t bc = sorted ? std::max<int64_t>(1, std::min(deep_block(B, N) / 4, ((int64_t)1 << 30) / std::max<int64_t>(N, 1)))
+                            : deep_block(B, N);
+  char* sbuf = nullptr;
+  if (sorted) {
+    size_t tmp = 0;
+    const int64_t n = bc * N;
+    hipError_t e = rocprim::segmented_radix_sort_pairs(nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                       (const int32_t*)nullptr, (int32_t*)nullptr, (unsigned int)n,
+                                                       (unsigned int)bc, (const int*)nullptr, (const int*)nullptr, 0, 64,
+                                                       st);
+    if (e != hipSuccess) return hip_status(e, "ofr_knn_deep: segmented sort size");
+    e = hipMallocAsync((void**)&sbuf, (size_t)n * 16 + (size_t)(bc + 1) * 4 + tmp + 256, st);
+    if (e != hipSuccess) return hip_status(e, "ofr_knn_deep: sort buffers");
+  }
+  struct Free {
+    char* p;
+    hipStream_t s;
+    ~Free() {
+      if (p) (void)hipFreeAsync(p, s);
+    }
+  } free_sbuf{sbuf, st};
   for (int64_t b0 = 0; b0 < B; b0 += bc) {
     const int64_t nb = std::min(bc, B - b0);
     const int esz = qdtype == OFR_DT_U8 ? 1 : qdtype == OFR_DT_U16 ? 2 : qdtype == OFR_DT_F64 ? 8 : 4;
@@ -297,9 +347,36 @@ extern "C" int ofr_knn_deep(void* stream, int metric, const void* Q, int64_t B, 
         hipLaunchKernelGGL(deep::deep_dist_kernel<OFR_METRIC_CHISQUARE>, grid, dim3(256), 0, st, a);
       OFR_LAUNCH_CHECK("deep_dist_kernel");
     }
-    hipLaunchKernelGGL(deep::deep_select_kernel, dim3((unsigned)nb), dim3(256), 0, st, (const double*)workspace, N, nb,
-                       k, index_base, out_d + b0 * k, out_i + b0 * k);
-    OFR_LAUNCH_CHECK("deep_select_kernel");
+    if (sorted) {
+      const int64_t n = nb * N;
+      uint64_t* kout = reinterpret_cast<uint64_t*>(sbuf);
+      int32_t* rin = reinterpret_cast<int32_t*>(sbuf + (size_t)bc * N * 8);
+      int32_t* rout = rin + bc * N;
+      int* off = reinterpret_cast<int*>(rout + bc * N);
+      void* tmp = reinterpret_cast<char*>(off) + round_up((bc + 1) * 4, 256);
+      size_t tmpb = 0;
+      hipError_t e = rocprim::segmented_radix_sort_pairs(nullptr, tmpb, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                         (const int32_t*)nullptr, (int32_t*)nullptr, (unsigned int)n,
+                                                         (unsigned int)nb, off, off + 1, 0, 64, st);
+      if (e != hipSuccess) return hip_status(e, "ofr_knn_deep: segmented sort size");
+      hipLaunchKernelGGL(deep::deep_keys_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 65536)), dim3(256), 0,
+                         st, (double*)workspace, rin, n, N);
+      OFR_LAUNCH_CHECK("deep_keys_kernel");
+      hipLaunchKernelGGL(deep::deep_offsets_kernel, dim3((unsigned)cdiv(nb + 1, 256)), dim3(256), 0, st, off, nb, N);
+      OFR_LAUNCH_CHECK("deep_offsets_kernel");
+      // stable: equal keys keep their row order (rows ascending in), the ties of np.argsort's order here
+      e = rocprim::segmented_radix_sort_pairs(tmp, tmpb, (const uint64_t*)workspace, kout, rin, rout, (unsigned int)n,
+                                              (unsigned int)nb, off, off + 1, 0, 64, st);
+      if (e != hipSuccess) return hip_status(e, "ofr_knn_deep: segmented sort");
+      const int keff = (int)std::min<int64_t>(k, N);
+      hipLaunchKernelGGL(deep::deep_take_kernel, dim3((unsigned)cdiv(k, 256), (unsigned)nb), dim3(256), 0, st, kout,
+                         rout, N, nb, k, keff, index_base, out_d + b0 * k, out_i + b0 * k);
+      OFR_LAUNCH_CHECK("deep_take_kernel");
+    } else {
+      hipLaunchKernelGGL(deep::deep_select_kernel, dim3((unsigned)nb), dim3(256), 0, st, (const double*)workspace, N,
+                         nb, k, index_base, out_d + b0 * k, out_i + b0 * k);
+      OFR_LAUNCH_CHECK("deep_select_kernel");
+    }
   }
   return OFR_OK;
 }

@@ -39,6 +39,8 @@ namespace ofr {
 namespace q8 {
 
 constexpr int GROUP_F = 4;   // feature tiles per tile group (i8t::tile_coords)
+// the engine's rings, then the epilogue's 32 KiB per wave (project_w_body)
+constexpr int PROJ_LDS = i8w::LDS_BYTES > 4 * 32768 ? i8w::LDS_BYTES : 4 * 32768;
 
 struct Args {
   const uint8_t* X;
@@ -69,14 +71,25 @@ __device__ __forceinline__ void project_w_body(const Args& p, int64_t ft, int64_
   i8w::feed_init(f, p.Aq, p.ldk, p.arows, ft * i8w::TA, p.X, p.ldx, p.B, b0);
   i8w::mainloop<W>(f, p.nk, acc);
   const int lane = threadIdx.x & 63, l16 = lane & 15, g = lane >> 4;
-  // features outer (their scale / K / shift loaded once), the wave's 4 image blocks inner; block 2 (the
-  // VGPR-resident accumulators) first, which frees its 128 registers for the AGPR blocks' conversions
+  // Epilogue through the wave's own 32 KiB of LDS (free after the main loop's last barrier): per
+  // projection block, its 8 x 4 accumulators are stored as they are (ds_write takes AGPR data) and read
+  // back one feature group at a time.  Converted straight from the registers, the compiler moved the
+  // AGPR accumulators into VGPRs at the loop exit and spilled 95 of them to scratch right behind the
+  // last asm MFMAs (whose results the hazard recognizer does not track); now no accumulator is spilled
+  // (tests/test_spill_guard.py).  The "memory" clobber keeps the reads from being forwarded from the
+  // stores.  Same fp64 operations in the same order as before: identical results.
+  OFR_LDS i8w::i32x4* stash = (OFR_LDS i8w::i32x4*)(uintptr_t)(W * 32768);
+  // features outer (their scale / K / shift loaded once), the wave's 4 image blocks inner
 #pragma unroll
-  for (int jj = 0; jj < 3; ++jj)
+  for (int jj = 0; jj < 3; ++jj) {
+    const int jbl = (jj + 2) % 3;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c < i8w::NB; ++c) stash[(r * 4 + c) * 64 + lane] = acc[jbl * 8 + r][c];
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int jbl = (jj + 2) % 3;
-      const int i0 = jbl * 8 + h;
       const int64_t j0 = (ft * 3 + jbl) * 32 + h * 16 + 4 * g;
       double sj[4], kj[4], hj[4];
 #pragma unroll
@@ -91,12 +104,14 @@ __device__ __forceinline__ void project_w_body(const Args& p, int64_t ft, int64_
         const int64_t b = b0 + W * 64 + c * 16 + l16;
         if (b >= p.B) continue;
         double v[4];
+        const i8w::i32x4 s0 = stash[(h * 4 + c) * 64 + lane], s1 = stash[((h + 2) * 4 + c) * 64 + lane];
+        const i8w::i32x4 s2 = stash[((h + 4) * 4 + c) * 64 + lane], s3 = stash[((h + 6) * 4 + c) * 64 + lane];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          double tv = (double)acc[i0][c][e];
-          tv += (double)acc[i0 + 2][c][e] * 0x1p-7;
-          tv += (double)acc[i0 + 4][c][e] * 0x1p-14;
-          tv += (double)acc[i0 + 6][c][e] * 0x1p-21;
+          double tv = (double)s0[e];
+          tv += (double)s1[e] * 0x1p-7;
+          tv += (double)s2[e] * 0x1p-14;
+          tv += (double)s3[e] * 0x1p-21;
           double y = sj[e] * (tv + kj[e]);   // exact: x . Wq[:, j]
           if (p.shift) y -= hj[e];
           v[e] = j0 + e < p.d ? y : 0.0;
@@ -121,6 +136,8 @@ __device__ __forceinline__ void project_w_body(const Args& p, int64_t ft, int64_
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    asm volatile("" ::: "memory");
+  }
 }
 
 __global__ void __launch_bounds__(i8w::NT, 1) project_q8w_kernel(Args p) {
@@ -337,7 +354,7 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   static std::atomic<bool> attr_done{false};
   if (!attr_done.load(std::memory_order_acquire)) {
     hipError_t e = hipFuncSetAttribute((const void*)q8::project_q8w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       i8w::LDS_BYTES);
+                                       q8::PROJ_LDS);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8w)");
     attr_done.store(true, std::memory_order_release);
   }
@@ -377,7 +394,7 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   p.nk = (int)cdiv(D, i8w::BK);
   p.ntb = cdiv(B, i8w::TB);
   OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-  hipLaunchKernelGGL(q8::project_q8w_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), i8w::LDS_BYTES,
+  hipLaunchKernelGGL(q8::project_q8w_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), q8::PROJ_LDS,
                      (hipStream_t)stream, p);
   OFR_LAUNCH_CHECK("project_q8w_kernel");
   return OFR_OK;

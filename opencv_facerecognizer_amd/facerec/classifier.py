@@ -180,6 +180,12 @@ class NearestNeighbor(AbstractClassifier):
             # the same centre on every rank: the mean of all rows, from the host copy every rank holds
             shift = self._stack(self.X).mean(0) if mid == _lib.METRIC_EUCLIDEAN else None
             g = FloatGallery(feats, mid, shift64=shift)
+            if mid == _lib.METRIC_EUCLIDEAN:
+                # the column-block scales and the prefix length from the block sums of ALL rows (one
+                # all-reduce, every rank builds its shard here on its first search): every rank then picks
+                # the same start tier, so their tier chains -- and collectives -- match (certify_sharded)
+                from ..parallel import share_block_scales
+                share_block_scales(g, sh[0])
         g.index_base = n0
         self.__dict__["_dev"] = (key, n, g)
         return g

@@ -99,6 +99,9 @@ def test_config1_100k_gallery_d9999_batch4096(monkeypatch, w):
     if w == "trained":
         bs = g._block_scales()
         assert bs is not None and int(bs.min()) < 127   # the trained W's variance profile is absorbed
+        # the bench's path on the trained W: the prefix tier first (FloatGallery.start_tier), certifying all
+        assert g.prefix_stages() >= 1 and g.last_start_tier == "f6p", (g.prefix_stages(), g.last_start_tier)
+        assert counts[0] == 0, counts
     s = np.random.default_rng(5).choice(B, 64, replace=False)
     Qf = model.feature.project_device(Xq[torch.from_numpy(s).to(dev)], f64=True).cpu().numpy()
     ri, rd, r2 = _exact_top1(Qf, feats)
@@ -234,13 +237,14 @@ def _c2_worker(rank, ws, port, out):
         dist.destroy_process_group()
 
 
-def _c2_exact_top1(sample):
+def _c2_exact_top1(sample, setup=None):
     """float64 top-1 of the sampled queries over the WHOLE 1M gallery (the reference's features,
     feature.py:241-242, exact projection in fp64), streamed in chunks: ||g||^2 - 2 q.g on the host
-    (numpy BLAS) shortlists 32 rows per chunk, distance.py:60 (the oracle) ranks the shortlist."""
+    (numpy BLAS) shortlists 32 rows per chunk, distance.py:60 (the oracle) ranks the shortlist.
+    setup: (P, bank, ids_q, Xq) of the caller (the trained W), else _c2_setup's random W."""
     from opencv_facerecognizer_amd.synthetic import gallery_centre, gallery_chunks
     dev = torch.device("cuda", 0)
-    P, bank, ids_q, Xq = _c2_setup(dev)
+    P, bank, ids_q, Xq = setup if setup is not None else _c2_setup(dev)
     centre = gallery_centre(P, bank, C2["per"], C2["N"], dev)
     Q = P.project(Xq[torch.from_numpy(sample).to(dev)], shift64=centre, f64=True).cpu().numpy()
     best_d = np.full(len(sample), np.inf)
@@ -296,6 +300,54 @@ def test_config2_full_size_two_rank_sharded():
     near = (r2 - rd) <= 1e-4 * rd
     assert np.all((mi0[sample, 0] == ri) | near), (mi0[sample, 0], ri)
     assert np.allclose(md0[sample, 0], rd, rtol=1e-4, atol=0)
+
+
+@pytest.mark.timeout(1200)
+def test_config2_headline_path_trained_w_full_size():
+    """The measured headline path itself (bench.py at N = 1): the Fisherfaces W trained
+    on configs[1]'s 100k faces, the 1M-row gallery (d = 9,999), one 4,096-face batch through the bench's
+    single-GPU step -- exact projection, the adaptive start tier, the prefix tier f6p on the persistent sieve
+    pass, merge + exact re-rank + certificate, the fallback chain.  Asserts that the batch starts at f6p,
+    that the prefix pass kernel is the one launched, that every query certifies there, identity accuracy,
+    and 64 sampled queries against the float64 top-1 over the WHOLE gallery (classifier.py:104-119,
+    distance.py:57-60, feature.py:241-242) with the near-tie rule of _check_search."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import round_up
+    from opencv_facerecognizer_amd.synthetic import SEED, IdentityBank, build_gallery, build_trained_projection
+    dev = torch.device("cuda", 0)
+    N, per, side, d, B = C2["N"], C2["per"], C2["side"], C2["d"], C2["B"]
+    bank = IdentityBank(N // per, side, side, device=dev)
+    P, _, info = build_trained_projection(bank, per, 100_000, side * side, dev)
+    assert P.d == d and info["regime"] == "pixel", info
+    g = build_gallery(P, bank, per, 0, N, N, d, max(32, round_up(d, 32)), dev)
+    print(f"headline: W trained ({info['train_s']:.1f} s), gallery of {g.N} rows built", flush=True)
+    gq = torch.Generator(device=dev)
+    gq.manual_seed(SEED + 7)
+    ids_q = torch.randint(0, N // per, (B,), generator=gq, device=dev)
+    Xq = bank.images(ids_q, seed=SEED + 99)
+    Qd = P.project(Xq, shift64=g.shift64)                 # bench.py prep(): fp32(W^T x - c), exact int8 MFMA
+    pst = g.prefix_stages()
+    tier = g.start_tier(B)
+    assert pst >= 1 and tier == "f6p", (pst, tier)
+    name = _lib.load().ofr_f6p_sieve_kernel(pst)
+    name = name.decode() if isinstance(name, bytes) else str(name)
+    assert "prefix" in name, name                          # the persistent prefix pass, not the f6w fallback
+    qq = g.quantize_queries(Qd, tier=tier)
+    out = g.search_q8_phase(3, Qd, qq, 1)
+    first = g.fallback(Qd, qq, 1, out)
+    kept = g.sieve_counts(B).cpu().numpy()
+    md, mi = out[0].cpu().numpy(), out[1].cpu().numpy()
+    print(f"headline: prefix stages {pst}, uncertified after each tier {g.last_fallbacks}, "
+          f"kept rows per query mean {kept.mean():.0f} max {kept.max()}", flush=True)
+    assert first == 0 and list(g.last_fallbacks) == [0], g.last_fallbacks
+    assert kept.max() <= g.SIEVE_CAP
+    acc = float(np.mean(mi[:, 0] // per == ids_q.cpu().numpy()))
+    assert acc >= 0.99, acc
+    sample = np.random.default_rng(6).choice(B, 64, replace=False)
+    ri, rd, r2, _ = _c2_exact_top1(sample, setup=(P, bank, ids_q, Xq))
+    near = (r2 - rd) <= 1e-4 * rd
+    assert np.all((mi[sample, 0] == ri) | near), (mi[sample, 0], ri)
+    assert np.allclose(md[sample, 0], rd, rtol=1e-4, atol=0)
 
 
 # ---------------------------------------------------------------------------

@@ -138,15 +138,38 @@ def test_nearest_neighbor_predict_any_k_vs_faithful_oracle(metric, k):
     np.testing.assert_allclose(one[1]["distances"], ref[1]["distances"], rtol=1e-4, atol=1e-9)
 
 
-def test_deep_k_limit_reported():
-    """min(k, N) > 4096: OFR_E_UNSUPPORTED with a message, not a wrong answer; k > N is fine."""
+@pytest.mark.parametrize("metric", ["EuclideanDistance", "ChiSquareDistance"])
+def test_deep_k_above_4096_vs_oracle(metric):
+    """min(k, N) > 4096 (round 6: a stable segmented radix sort of every query's (distance, row) keys
+    instead of the LDS select): k = 5,000 < N = 6,000 against the oracle, duplicate rows tied by index,
+    and k > N (every row, then (+inf, -1))."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import search_deep
-    G = torch.zeros((5000, 4), dtype=torch.float32, device="cuda")
-    Q = torch.zeros((2, 4), dtype=torch.float32, device="cuda")
-    with pytest.raises(_lib.OfrError, match="4096"):
-        search_deep(_lib.METRIC_EUCLIDEAN, Q, _lib.DT_F32, G, _lib.DT_F32, 4, 1.0, 4097)
-    d_, i_ = search_deep(_lib.METRIC_EUCLIDEAN, Q, _lib.DT_F32, G[:100], _lib.DT_F32, 4, 1.0, 5000)
+    r = _rng(4097)
+    N, B, d, k = 6000, 3, 12, 5000
+    if metric == "EuclideanDistance":
+        G = r.normal(0, 1, (N, d)).astype(np.float32)
+        Q = r.normal(0, 1, (B, d)).astype(np.float32)
+        mid = _lib.METRIC_EUCLIDEAN
+    else:
+        G = (r.integers(0, 9, (N, d)) / 9.0).astype(np.float32)
+        Q = (r.integers(0, 9, (B, d)) / 9.0).astype(np.float32)
+        mid = _lib.METRIC_CHISQUARE
+    G[100:140] = G[7]                             # 41 tied rows: lowest index first
+    Gd, Qd = torch.from_numpy(G).cuda(), torch.from_numpy(Q).cuda()
+    dd, ii = search_deep(mid, Qd, _lib.DT_F32, Gd, _lib.DT_F32, d, 1.0, k)
     torch.cuda.synchronize()
-    i_ = i_.cpu().numpy()
-    assert np.array_equal(i_[:, :100], np.tile(np.arange(100), (2, 1))) and np.all(i_[:, 100:] == -1)
+    _check(metric, Q.astype(np.float64), G.astype(np.float64), dd.cpu().numpy(), ii.cpu().numpy(), k)
+    ref = O.pairwise(metric, Q.astype(np.float64), G.astype(np.float64))
+    got = ii.cpu().numpy()
+    for b in range(B):
+        ties = np.nonzero(np.isin(got[b], np.r_[7, 100:140]))[0]
+        if len(ties):
+            assert np.array_equal(got[b][ties], np.sort(got[b][ties])), "tied rows out of index order"
+        assert np.all(np.diff(dd.cpu().numpy()[b]) >= 0)
+        assert np.allclose(np.sort(ref[b])[:k], dd.cpu().numpy()[b], rtol=1e-4, atol=1e-9)
+    d2, i2 = search_deep(mid, Qd, _lib.DT_F32, Gd[:4500], _lib.DT_F32, d, 1.0, 5000)   # k > N = 4,500 > 4,096
+    torch.cuda.synchronize()
+    i2 = i2.cpu().numpy()
+    assert np.array_equal(np.sort(i2[:, :4500], axis=1), np.tile(np.arange(4500), (B, 1)))
+    assert np.all(i2[:, 4500:] == -1) and np.all(np.isinf(d2.cpu().numpy()[:, 4500:]))

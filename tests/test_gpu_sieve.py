@@ -91,11 +91,14 @@ def _e2m3_table(device):
     return torch.tensor(np.where(s == 1, -mag, mag), dtype=torch.float64, device=device)
 
 
-def _decode_panels(tiles, p0, p1, nst, d, table):
-    """e2m3 values of panels [p0, p1) -> fp64 [(p1 - p0) * 256][d]."""
+def _decode_panels(tiles, p0, p1, nst, d, table, ns=None):
+    """e2m3 values of panels [p0, p1) -> fp64 [(p1 - p0) * 256][d] (ns: only the first ns stages, the
+    prefix tier's, -> [..][min(d, 128 ns)])."""
     dev = tiles.device
     np_ = p1 - p0
     blk = tiles[p0 * nst * 24576:p1 * nst * 24576].view(np_, nst, 4, 6144)
+    if ns is not None:
+        blk, nst, d = blk[:, :ns], ns, min(d, 128 * ns)
     part0 = blk[..., :4096].reshape(np_, nst, 4, 256, 16)
     part1 = blk[..., 4096:].reshape(np_, nst, 4, 256, 8)
     slot = torch.arange(256, device=dev)
@@ -112,8 +115,11 @@ def _decode_panels(tiles, p0, p1, nst, d, table):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("w", ["random", "trained"])
-def test_sieve_complete_vs_exact_scores_headline_shape(w):
+@pytest.mark.parametrize("w,tier", [("random", "f6"), ("trained", "f6"), ("trained", "f6p")])
+def test_sieve_complete_vs_exact_scores_headline_shape(w, tier):
+    """tier f6p (round 6): the headline's own pass -- the prefix tier on the persistent sieve kernel,
+    scoring the first pstages (choose_prefix) stages of the same tiles with the prefix terms |g_m|^2
+    as the rows' aux and power-of-two query scales."""
     from opencv_facerecognizer_amd._device import round_up
     from opencv_facerecognizer_amd.synthetic import (SEED, IdentityBank, build_gallery, build_projection,
                                                      build_trained_projection)
@@ -130,7 +136,11 @@ def test_sieve_complete_vs_exact_scores_headline_shape(w):
     gq.manual_seed(SEED + 7)
     ids_q = torch.randint(0, N // per, (B,), generator=gq, device=dev)
     Qd = P.project(bank.images(ids_q, seed=SEED + 99), shift64=g.shift64)
-    qq = g.quantize_queries(Qd, tier="f6")
+    ns = None
+    if tier == "f6p":
+        ns = g.prefix_stages()
+        assert ns >= 1 and g.start_tier(B) == "f6p", ns
+    qq = g.quantize_queries(Qd, tier=tier)
     g.search_q8_phase(4 | 8, Qd, qq, 1)
     torch.cuda.synchronize()
     theta, count, keys, rows = g.sieve_state(B)
@@ -140,25 +150,27 @@ def test_sieve_complete_vs_exact_scores_headline_shape(w):
     cnt = count.index_select(0, sd).cpu().numpy()
     assert np.all((cnt >= 16) & (cnt <= g.SIEVE_CAP)), cnt
     nst = -(-d // 128)
+    dm = d if ns is None else min(d, 128 * ns)          # the features the pass scores
     table = _e2m3_table(dev)
     # column-block scales: feature k decodes to s 2^e v, e = bscale[k / 32] - 127 (gallery and queries)
     bs = g._block_scales()
-    f = (torch.ones(d, dtype=torch.float64, device=dev) if bs is None else
-         torch.pow(2.0, bs.double() - 127.0).repeat_interleave(32)[:d])
+    f = (torch.ones(dm, dtype=torch.float64, device=dev) if bs is None else
+         torch.pow(2.0, bs.double() - 127.0).repeat_interleave(32)[:dm])
     if w == "trained":
         assert bs is not None and int(bs[:-(-d // 32)].min()) < 127, "a trained W must give non-unit block scales"
     # the sampled queries' codes: their panels of the query tiles
-    Vq = torch.empty((64, d), dtype=torch.float64, device=dev)
+    Vq = torch.empty((64, dm), dtype=torch.float64, device=dev)
     for j, b in enumerate(s):
         pnl = b // 256
-        Vq[j] = _decode_panels(qq["Qs"], pnl, pnl + 1, nst, d, table)[b % 256] * f
+        Vq[j] = _decode_panels(qq["Qs"], pnl, pnl + 1, nst, d, table, ns)[b % 256] * f
     sq = qq["scale"].index_select(0, sd).double()
     # sanity: the decoded codes times the row scale are the quantized query rows (residual ~3 %)
-    res = (Qd.index_select(0, sd)[:, :d].double() - sq[:, None] * Vq).norm(dim=1) / Qd.index_select(0, sd)[:, :d].double().norm(dim=1)
+    res = (Qd.index_select(0, sd)[:, :dm].double() - sq[:, None] * Vq).norm(dim=1) / Qd.index_select(0, sd)[:, :dm].double().norm(dim=1)
     assert float(res.max()) < 0.06, res
-    gt = g._tier_gallery("f6")
-    gscale, aux = gt["scale"][:N].double(), g.aux[:N].double()
-    gamma = (2 * nst + 64) * 2.0 ** -23
+    gt = g._tier_gallery(tier)
+    gscale = gt["scale"][:N].double()
+    aux = (g.aux if ns is None else gt["paux"])[:N].double()   # f6p: the prefix terms |g_m|^2
+    gamma = (2 * (nst if ns is None else ns) + 64) * 2.0 ** -23
     Vqa = Vq.abs()
     must = [[] for _ in range(64)]
     allowed_hi = [[] for _ in range(64)]
@@ -167,7 +179,7 @@ def test_sieve_complete_vs_exact_scores_headline_shape(w):
     thf_d = torch.from_numpy(thf).to(dev)
     for p0 in range(0, npan, PCH):
         p1 = min(npan, p0 + PCH)
-        Vg = _decode_panels(gt["Gs"], p0, p1, nst, d, table)
+        Vg = _decode_panels(gt["Gs"], p0, p1, nst, d, table, ns)
         r0, r1 = p0 * 256, min(N, p1 * 256)
         Vg = Vg[:r1 - r0] * f
         dot = Vq @ Vg.t()                             # exact: multiples of 2^-6, |sum| < 2^53 ulp range
