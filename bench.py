@@ -140,6 +140,16 @@ def cpu_baseline(P, gallery, Xq, N_total, seconds):
     }
 
 
+def sieve_engine(name):
+    """Short name of the sieve-pass kernel a roofline / PMC record refers to (the committed traffic of one
+    engine is never attributed to another)."""
+    for e in ("prefix_pass_kernel", "tile_kernel_f6p", "tile_kernel_f6w", "tile_kernel_f6s", "tile_kernel<1>",
+              "knn_tile_kernel"):
+        if e in (name or ""):
+            return e
+    return "other"
+
+
 def committed_traffic(cfg):
     """HBM-side bytes per launch of the search pass from the committed rocprofv3 PMC passes
     (profiles/*_pmc_summary.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 guide), if measured at this
@@ -156,6 +166,7 @@ def committed_traffic(cfg):
         c = dict(s.get("config") or {})
         c.setdefault("w", "random")
         c.setdefault("tier", c.get("search"))         # summaries before the prefix tier: the search's tier
+        c.setdefault("engine", sieve_engine(s.get("kernel")))   # summaries before round 6: from their kernel
         if c == cfg and s.get("traffic_bytes_per_launch") is not None:
             cands.append((s.get("measured_utc", ""), os.path.basename(f), s["traffic_bytes_per_launch"]))
     if not cands:
@@ -806,6 +817,30 @@ def main():
                                    "frac": bytes_t / (ms_t * 1e-3) / PEAK_HBM, "launch_ms": ms_t,
                                    "algorithmic_bytes_per_launch": bytes_t}})
 
+    # the merge alone (phase 2 of the last batch again on its workspace: idempotent), and its bytes: the fp32
+    # rows of the candidates it re-ranked exactly (MergeArgs::evals), the query rows, the kept bucket entries
+    merge_roof = None
+    if args.search == "f6" and world == 1:
+        wl = pipe.ws[(args.steps - 1) % StepPipeline.NWS]
+        ms_m = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            gallery.search_q8_phase(2, Qd, qq, k, workspace=wl)
+            e1.record()
+            torch.cuda.synchronize()
+            ms_m.append(e0.elapsed_time(e1))
+        ev_ = gallery.merge_evals(B, wl)
+        kc = gallery.sieve_counts(B, wl)
+        if ev_ is not None:
+            n_ev = float(ev_.double().sum())
+            mb = n_ev * d * 4 + B * d * 4 + (float(kc.double().clamp(0, 32768).sum()) * 8 if kc is not None else 0.0)
+            mm = float(np.median(ms_m))
+            merge_roof = {"kernel": "q8s::merge_kernel<true> (bucket best-16, exact fp64 re-rank of the candidates, "
+                                    "certificate)", "bound": "hbm", "ms_alone": mm,
+                          "exact_reranks_per_query": n_ev / B, "algorithmic_bytes": mb,
+                          "achieved": mb / (mm * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                          "frac": mb / (mm * 1e-3) / PEAK_HBM}
     margin = certificate_margin(gallery, Qd, qq) if args.search == "f6" and world == 1 else None
     flops_tiles = 2.0 * B * nl * d                                    # algorithmic, per launch
     achieved = flops_tiles / (ms_tiles * 1e-3)
@@ -830,7 +865,9 @@ def main():
         ntg_, ntq_, nst_ = -(-nl // 256), -(-B // 256), -(-dm // 128)
         wide = "f6w" in sieve or "f6p" in sieve                      # 384 x 256 tiles: 60 KiB per stage
         fed = (-(-nl // 384) * 61440.0 if wide else ntg_ * 49152.0) * ntq_ * nst_   # copied into LDS per sieve pass
-        if "f6p" in sieve:       # the persistent pass copies a gallery tile once per item of query panels
+        if "prefix_pass_kernel" in sieve:   # per 256-row tile: its 24 KiB image per item, 12 KiB per 128-query step
+            fed = ntg_ * -(-B // 128) * 12288.0 + ntg_ * 24576.0 * max(1.0, -(-B // 128) / 16.0)
+        elif "f6p" in sieve:     # the persistent pass copies a gallery tile once per item of query panels
             fed = -(-nl // 384) * ntq_ * nst_ * 24576.0 + -(-nl // 384) * nst_ * 36864.0 * (ntq_ / 16.0)
         executed = flops_tiles
     elif use_q8:
@@ -846,7 +883,7 @@ def main():
         value = B * args.steps / elapsed
         coll = "RCCL" if world > 1 and dist.get_backend() == "nccl" else "gloo"   # the collectives' backend
         tr = committed_traffic({"gallery": nl, "batch": B, "d": d, "D": D, "k": k, "search": args.search,
-                                "w": args.w, "tier": tier_used or args.search})
+                                "w": args.w, "tier": tier_used or args.search, "engine": sieve_engine(kname)})
         result = {
             "metric": "query faces/sec (Fisherfaces proj + 1-NN, 1M gallery) at 1/2/4/8 GPUs",
             "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -884,6 +921,15 @@ def main():
                                       "bytes_per_launch": fed,
                                       "achieved_TBps": fed / (ms_sieve * 1e-3) / 1e12}}
                             if args.search == "f6" else {})},
+            # the pruned pass against the brute-force work SURVEY §8d prices (2 B N d per step): the rate the step
+            # would imply if every feature of every pair were scored -- the pruning factor made visible (the
+            # prefix tier scores m = 128 pst of the d features; the rest of a distance is never needed)
+            "brute_force_equivalent": {
+                "ops_per_step": 2.0 * B * nl * d, "scored_ops_per_step": flops_tiles if args.search == "f6" else None,
+                "scored_fraction": (flops_tiles / (2.0 * B * nl * d)) if args.search == "f6" else None,
+                "implied_POPS": 2.0 * B * nl * d / (elapsed / args.steps) / 1e15,
+                "note": "not comparable with any peak: the pruned features are bounded, not computed"},
+            "roofline_merge": merge_roof,
             "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else "") + ("+all_gather" if shard_prep else ""):
                            ms_proj, "knn_tiles": ms_tiles,
                            "knn_merge_rerank" + ("+certificate" if use_q8 else ""): ms_merge},

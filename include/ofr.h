@@ -214,6 +214,10 @@ int ofr_q8_maxima(void* stream, const double* stats, const float* aux, int64_t R
 int ofr_f6_block_sumsq(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, double* sums);
 int ofr_f6_block_scales(void* stream, const double* sums, int64_t d, uint8_t* bscale);
 size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N);
+/* byte offset in that workspace of int32 [B]: after a merge (phase 2), the number of candidates each
+ * query re-ranked exactly (its fp32 rows read: that many x d x 4 bytes) -- round 6, for the merge's
+ * HBM roofline                                                                                  */
+size_t ofr_knn_f6_merge_evals_offset(int64_t B, int64_t N);
 size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N);
 int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
                          size_t tiles_bytes, float* scale, double* stats, const float* aux, double* maxima,
@@ -286,6 +290,15 @@ int ofr_knn_f6_merge_pruned(void* stream, int stage, const float* Q, int64_t B, 
                             int64_t d, const void* Gt, const float* gscale, const float* aux, const double* gmax,
                             int k, int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
                             double* ub, void* workspace, size_t workspace_bytes);
+/* The same split for the prefix tier (round 6; after phase 1 of ofr_knn_f6p_sampled, aux = the prefix
+ * terms): a prefix key bounds no distance from above, so stage 1 computes the exact squared distances
+ * of each query's first k candidates (key order) and writes those, ascending, as ub[B][k] -- k real rows
+ * of the shard lie that close.  Stage 2 as above (lower bounds from the prefix keys).              */
+int ofr_knn_f6p_merge_pruned(void* stream, int stage, const float* Q, int64_t B, int64_t ldq, const void* Qt,
+                             const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
+                             int64_t d, const void* Gt, const float* gscale, const float* aux, const double* gmax,
+                             int k, int64_t index_base, double* out_d, int64_t* out_i, int* cert, double* bound,
+                             double* ub, void* workspace, size_t workspace_bytes, int pstages);
 
 /* Two-slice fp6 tier "f6x2" of the certified chain (new: replaces the same loop,
  * classifier.py:104-119, for the queries the fp6 tier could not certify on crowded
@@ -538,6 +551,18 @@ typedef struct ofr_knn_shard {
   /* the shard's column-block scales (ofr_f6_block_scales; null: unit), also those of its query tiles
      Qt -- round 5, appended */
   const uint8_t* bscale;
+  /* optional prefix tier f6p first (ofr_knn_f6p_sampled) -- round 6, appended.  pstages > 0
+     (the same on every shard: choose it from all-reduced block sums) runs it for the whole batch, with
+     its pruned split merge (ofr_knn_f6p_merge_pruned), the exchange and the global certificate; the
+     queries it leaves open then take the fp6 tier (Qt, qscale, qstats are not read for the batch) and
+     the rest of the chain.  Needs the row sample (St). */
+  int pstages;
+  const void* Qtp;          /* the batch's prefix tiles (ofr_f6_quantize_rows_prefix) */
+  const float* qscalep;
+  const double* qstatsp;
+  const float* paux;        /* the shard rows' prefix terms |g_m|^2 (ofr_row_aux over min(d, 128 pstages)) */
+  const float* spaux;       /* the row sample's prefix terms */
+  int64_t* prefix_open;     /* optional out [1] (shard 0): queries the prefix tier left open */
 } ofr_knn_shard;
 int ofr_comm_init_all(int ndev, const int* devices, ofr_comm** comm);
 int ofr_comm_destroy(ofr_comm* comm);

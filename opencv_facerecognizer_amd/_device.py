@@ -745,16 +745,23 @@ class FloatGallery:
     def merge_pruned(self, stage, Qd, qq, k, ub, index_base=0, out=None, workspace=None):
         """The split fp6 merge of a sharded gallery (ofr_knn_f6_merge_pruned, after phase 1 on the same
         workspace -- the gallery's, or the caller's): stage 1 writes ub [B][k] (this shard's upper
-        bounds), stage 2 re-ranks pruned by ub [B] (the global bound) into out / qq["cert"] / qq["bound"]."""
-        g = self._tier_gallery("f6")
+        bounds), stage 2 re-ranks pruned by ub [B] (the global bound) into out / qq["cert"] / qq["bound"].
+        Tier f6p (round 6, ofr_knn_f6p_merge_pruned): stage 1's bounds are the exact squared distances of
+        each query's first k candidates (a prefix key bounds nothing from above)."""
+        tier = qq["tier"]
+        g = self._tier_gallery(tier)
         B = Qd.shape[0]
         lib = _lib.load()
         ws = (workspace or self.ws).get(lib.ofr_knn_f6_workspace_bytes(B, self.N), Qd.device)
         o = out if out is not None else (None, None)
-        call("ofr_knn_f6_merge_pruned", stream(), stage, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]),
-             ptr(qq["stats"]), ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]), ptr(self.aux),
-             ptr(g["gmax"]), k, index_base, ptr(o[0]), ptr(o[1]), ptr(qq["cert"]), ptr(qq["bound"]), ptr(ub), ptr(ws),
-             ws.numel())
+        args = [stream(), stage, ptr(Qd), B, Qd.shape[1], ptr(qq["Qs"]), ptr(qq["scale"]), ptr(qq["stats"]),
+                ptr(self.G), self.N, self.ld, self.d, ptr(g["Gs"]), ptr(g["scale"]),
+                ptr(g["paux"] if tier == "f6p" else self.aux), ptr(g["gmax"]), k, index_base, ptr(o[0]), ptr(o[1]),
+                ptr(qq["cert"]), ptr(qq["bound"]), ptr(ub), ptr(ws), ws.numel()]
+        if tier == "f6p":
+            call("ofr_knn_f6p_merge_pruned", *args, g["pst"])
+        else:
+            call("ofr_knn_f6_merge_pruned", *args)
         return out
 
     def sieve_counts(self, B, workspace=None):
@@ -764,6 +771,15 @@ class FloatGallery:
         off = _lib.load().ofr_knn_f6_sieve_counts_offset(B, self.N)
         w = workspace or self.ws
         if off == ctypes.c_size_t(-1).value or w.buf is None:
+            return None
+        return w.buf[off:off + 4 * B].view(torch.int32)
+
+    def merge_evals(self, B, workspace=None):
+        """Candidates each query of the last fp6-tier merge (phase 2) of a B-query batch on `workspace`
+        re-ranked exactly (int32 device view [B]; its bytes: evals x d x 4 of fp32 rows)."""
+        off = _lib.load().ofr_knn_f6_merge_evals_offset(B, self.N)
+        w = workspace or self.ws
+        if w.buf is None:
             return None
         return w.buf[off:off + 4 * B].view(torch.int32)
 

@@ -60,6 +60,7 @@ SIGNATURES = {
     "ofr_f6_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp, c_vp]),
     "ofr_q8_maxima": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "ofr_knn_f6_workspace_bytes": (c_sz, [c_i64, c_i64]),
+    "ofr_knn_f6_merge_evals_offset": (c_sz, [c_i64, c_i64]),
     "ofr_f6_sieve_kernel": (ctypes.c_char_p, []),
     "ofr_f6p_sieve_kernel": (ctypes.c_char_p, [c_int]),
     "ofr_knn_f6_sieve_counts_offset": (c_sz, [c_i64, c_i64]),
@@ -84,6 +85,9 @@ SIGNATURES = {
     "ofr_knn_f6_merge_pruned": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp, c_sz]),
+    "ofr_knn_f6p_merge_pruned": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp, c_sz, c_int]),
     "ofr_f6x2_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ofr_f6x2_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp]),
     "ofr_knn_f6x2": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64,
@@ -155,7 +159,9 @@ class KnnShard(ctypes.Structure):
                 ("out_d", c_vp), ("out_i", c_vp), ("cert", c_vp),
                 ("Gt2", c_vp), ("gscale2", c_vp), ("gmax2", c_vp), ("G8", c_vp), ("ld8", c_i64), ("gscale8", c_vp),
                 ("gmax8", c_vp), ("tier_counts", c_vp), ("St", c_vp), ("Ns", c_i64), ("sscale", c_vp), ("saux", c_vp),
-                ("St2", c_vp), ("bscale", c_vp)]
+                ("St2", c_vp), ("bscale", c_vp),
+                ("pstages", c_int), ("Qtp", c_vp), ("qscalep", c_vp), ("qstatsp", c_vp), ("paux", c_vp),
+                ("spaux", c_vp), ("prefix_open", c_vp)]
 
 
 class OfrError(RuntimeError):

@@ -295,17 +295,15 @@ __global__ void __launch_bounds__(256) chi2_merge_rerank_kernel(Chi2MergeArgs p)
     if (threadIdx.x == 0) exact[c] = val;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
     double* od = p.out_d + q * p.k;
-    sort_and_write<KC>(lists, exact, p.k, p.index_base, od, p.out_i + q * p.k);
-    if (p.cert) {
+    const double dk = sort_and_write_wave<KC>(lists, exact, p.k, p.index_base, od, p.out_i + q * p.k);
+    if (p.cert && threadIdx.x == 0) {
       // certificate: every row outside the KC candidates has coarse score >= tau (the KC-th
       // candidate; a tile's excluded rows are >= its own KC-th, which is >= tau), so its exact
       // distance is >= tau * scale / (1 + gamma).  The top-k is exact iff the k-th exact distance
       // lies strictly below that (a relative 1e-12 for the fp64 evaluation order).
-      const int kk = p.k < KC ? p.k : KC;
       const Cand last = lists[KC - 1];
-      const double dk = od[kk - 1];
       double bnd = __builtin_inf();
       if (last.i != CAND_EMPTY && p.abs_c1 > 0)
         bnd = ((double)last.d - p.abs_c1 * (tq + (double)*p.tg_max)) * p.scale * (1.0 - 1e-12);

@@ -340,7 +340,18 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
   } restore{cur};
   std::vector<comm::WsLayout> L(P);
   const size_t row_bytes = (size_t)(2 * k + 1) * 8;
-  // 1: the fp6 tile pass and the merge's selection + upper bounds on every shard
+  // the prefix tier first (round 6): the same pstages on every shard, with its tiles and terms
+  const int pst = shards[0].pstages;
+  for (int p = 0; p < P; ++p) {
+    const ofr_knn_shard& s = shards[p];
+    OFR_CHECK_ARG(s.pstages == pst, "ofr_knn_sharded: pstages differs between shards (choose it from all-reduced sums)");
+    OFR_CHECK_ARG(pst == 0 || (s.Qtp && s.qscalep && s.qstatsp && s.paux && s.spaux && s.St),
+                  "ofr_knn_sharded: the prefix tier needs Qtp, qscalep, qstatsp, paux, spaux and the row sample St");
+  }
+  OFR_CHECK_ARG(pst >= 0 && pst <= cdiv(d, 128), "ofr_knn_sharded: pstages must be in [0, ceil(d / 128)]");
+  const bool prefix = pst > 0 && pst < cdiv(d, 128);   // a prefix of every stage is the fp6 tier itself
+  // 1: the first tier's tile pass (fp6, or the prefix tier) and the merge's selection + upper bounds on
+  //    every shard
   for (int p = 0; p < P; ++p) {
     const ofr_knn_shard& s = shards[p];
     hipError_t e = hipSetDevice(c->devices[p]);
@@ -348,13 +359,24 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
     L[p] = comm::layout(B, s.N, s.ldq, k, P);
     OFR_CHECK_ARG(s.workspace && s.workspace_bytes >= L[p].total, "ofr_knn_sharded: workspace too small");
     char* ws = (char*)s.workspace;
-    int rc = s.St ? ofr_knn_f6_sampled(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
-                                       s.gscale, s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
-                                       s.St, s.Ns, s.sscale, s.saux, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N),
-                                       s.bscale)
-                  : ofr_knn_f6(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt, s.gscale,
-                               s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, ws + L[p].knn,
-                               ofr_knn_f6_workspace_bytes(B, s.N), s.bscale);
+    int rc;
+    if (prefix) {
+      rc = ofr_knn_f6p_sampled(s.stream, 1, s.Q, B, s.ldq, s.Qtp, s.qscalep, s.qstatsp, s.G, s.N, s.ldg, d, s.Gt,
+                               s.gscale, s.paux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, s.St, s.Ns,
+                               s.sscale, s.spaux, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N), s.bscale, pst);
+      if (rc) return rc;
+      rc = ofr_knn_f6p_merge_pruned(s.stream, 1, s.Q, B, s.ldq, s.Qtp, s.qscalep, s.qstatsp, s.G, s.N, s.ldg, d, s.Gt,
+                                    s.gscale, s.paux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
+                                    (double*)(ws + L[p].ubl), ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N), pst);
+      if (rc) return rc;
+      continue;
+    }
+    rc = s.St ? ofr_knn_f6_sampled(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
+                                   s.gscale, s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, s.St,
+                                   s.Ns, s.sscale, s.saux, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N), s.bscale)
+              : ofr_knn_f6(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt, s.gscale,
+                           s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, ws + L[p].knn,
+                           ofr_knn_f6_workspace_bytes(B, s.N), s.bscale);
     if (rc) return rc;
     rc = ofr_knn_f6_merge_pruned(s.stream, 1, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
                                  s.gscale, s.aux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
@@ -392,9 +414,12 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
     hipLaunchKernelGGL(comm::kth_bound_kernel, dim3((unsigned)cdiv(B, 128)), dim3(128), 0, (hipStream_t)s.stream,
                        (const double*)(ws + L[p].ubr), P, B, k, ub);
     OFR_LAUNCH_CHECK("kth_bound_kernel");
-    int rc = ofr_knn_f6_merge_pruned(s.stream, 2, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d, s.Gt,
-                                     s.gscale, s.aux, s.gmax, k, s.index_base, ld_, li_, lc_, lb_, ub, ws + L[p].knn,
-                                     ofr_knn_f6_workspace_bytes(B, s.N));
+    int rc = prefix ? ofr_knn_f6p_merge_pruned(s.stream, 2, s.Q, B, s.ldq, s.Qtp, s.qscalep, s.qstatsp, s.G, s.N,
+                                               s.ldg, d, s.Gt, s.gscale, s.paux, s.gmax, k, s.index_base, ld_, li_,
+                                               lc_, lb_, ub, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N), pst)
+                    : ofr_knn_f6_merge_pruned(s.stream, 2, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d,
+                                              s.Gt, s.gscale, s.aux, s.gmax, k, s.index_base, ld_, li_, lc_, lb_, ub,
+                                              ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N));
     if (rc) return rc;
     hipLaunchKernelGGL(comm::pack_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, (hipStream_t)s.stream, ld_, li_,
                        lb_, B, k, (double*)(ws + L[p].send));
@@ -430,9 +455,10 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
   };
   int rc = exchange(B, nullptr, true);
   if (rc) return rc;
-  // 4: the queries the fp6 tier left open go down the chain on every shard: f6x2, int8 x2, exact fp32;
-  //    each stage searches their rows, exchanges the lists (with its bound) and certifies again
-  enum Stage { F6X2 = 1, Q8X2 = 2, F32 = 3 };
+  // 4: the queries the first tier left open go down the chain on every shard: (after the prefix tier:
+  //    fp6,) f6x2, int8 x2, exact fp32; each stage searches their rows, exchanges the lists (with its
+  //    bound) and certifies again
+  enum Stage { F6 = 0, F6X2 = 1, Q8X2 = 2, F32 = 3 };
   bool have_f6x2 = true, have_q8x2 = true;
   for (int p = 0; p < P; ++p) {
     have_f6x2 = have_f6x2 && shards[p].Gt2 && shards[p].gscale2 && shards[p].gmax2;
@@ -464,8 +490,14 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
   };
   rc = open_rows();
   if (rc) return rc;
-  if (counts) counts[0] = n;
-  for (int stage : {(int)F6X2, (int)Q8X2, (int)F32}) {
+  if (prefix) {
+    if (shards[0].prefix_open) shards[0].prefix_open[0] = n;
+  } else if (counts) {
+    counts[0] = n;
+  }
+  for (int stage : {(int)F6, (int)F6X2, (int)Q8X2, (int)F32}) {
+    if (stage == F6 && !prefix) continue;
+    if (stage == F6 && n == 0 && counts) counts[0] = 0;
     if (n == 0) break;
     if (stage == F6X2 && !have_f6x2) continue;
     if (stage == Q8X2 && !have_q8x2) continue;
@@ -490,7 +522,17 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
       int* lc_ = (int*)(ws + L[p].scert);
       float* qs = (float*)(ws + L[p].qscale);
       double* qst = (double*)(ws + L[p].qstats);
-      if (stage == F6X2) {
+      if (stage == F6) {   // the prefix tier's open queries: the fp6 tier on their rows
+        rc = ofr_f6_quantize_rows(s.stream, sq, n, d, s.ldq, ws + L[p].qt1, L[p].tiles_bytes, qs, qst, nullptr,
+                                  nullptr, s.bscale);
+        if (rc) return rc;
+        rc = s.St ? ofr_knn_f6_sampled(s.stream, 3, sq, n, s.ldq, ws + L[p].qt1, qs, qst, s.G, s.N, s.ldg, d, s.Gt,
+                                       s.gscale, s.aux, s.gmax, k, s.index_base, ld_, li_, lc_, lb_, s.St, s.Ns,
+                                       s.sscale, s.saux, ws + L[p].knn, ofr_knn_f6_workspace_bytes(n, s.N), s.bscale)
+                  : ofr_knn_f6(s.stream, 3, sq, n, s.ldq, ws + L[p].qt1, qs, qst, s.G, s.N, s.ldg, d, s.Gt, s.gscale,
+                               s.aux, s.gmax, k, s.index_base, ld_, li_, lc_, lb_, ws + L[p].knn,
+                               ofr_knn_f6_workspace_bytes(n, s.N), s.bscale);
+      } else if (stage == F6X2) {
         rc = ofr_f6x2_quantize_rows(s.stream, sq, n, d, s.ldq, ws + L[p].qt1, ws + L[p].qt2, L[p].tiles_bytes, qs, qst,
                                     nullptr, nullptr, s.bscale);
         if (rc) return rc;

@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(256) knn_merge_rerank_kernel(MergeArgs p) {
     if (threadIdx.x == 0) exact[c] = val;
   }
   __syncthreads();
-  if (threadIdx.x == 0) sort_and_write<KC>(lists, exact, p.k, p.index_base, p.out_d + q * p.k, p.out_i + q * p.k);
+  if (threadIdx.x < 64) sort_and_write_wave<KC>(lists, exact, p.k, p.index_base, p.out_d + q * p.k, p.out_i + q * p.k);
 }
 
 // ---- helpers ----------------------------------------------------------------------

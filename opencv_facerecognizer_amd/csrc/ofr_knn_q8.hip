@@ -904,6 +904,363 @@ __global__ void __launch_bounds__(256, 1) tile_kernel_f6p(TileArgs p, int64_t qg
   f6p::flush_end(p, pg0, pd);
 }
 
+// ---- prefix tier's sieve pass, one stage: two workgroups per CU (round 6) ---------------------------
+// tile_kernel_f6p runs ONE wave per SIMD (its 192 x 128 wave tiles hold 384 accumulators), so the score
+// compares after each panel's MFMAs -- 384 per lane, dependent VALU chains -- run alone: ~8,300 of a
+// panel's ~17,500 cycles, the MFMAs ~1,500 (profiles/r05_f6p_phase_trace.txt).  With one
+// prefix stage an MFMA block is a single instruction and its fragments are read once, so a much smaller
+// wave tile costs little LDS traffic: here each wave owns 64 gallery rows x 128 queries (32 blocks of
+// 16 x 16, 128 accumulator VGPRs, no AGPR reads), a workgroup 256 rows x 128 queries, and TWO workgroups
+// share every CU -- two waves per SIMD, so one wave's compares issue while the other's MFMAs run, and
+// the VALU issues at the two-wave rate.  The MFMAs are compiler builtins (the compiler sees their
+// hazards; no accumulator is pinned by asm: tests/test_spill_guard.py holds this kernel to zero spills).
+// Work item = (256-row gallery tile = one panel of the tiled layout, group of 128-query steps = half
+// panels of the query tiles).  The gallery rows' fragments are read into registers once per item (the
+// tile's 24 KiB image is then free for the next item's copy); per step, behind ONE barrier:
+//   top      own copies landed + barrier; the next step's half panel (12 KiB) and its tables copied
+//            into the other buffer; on an item's 2nd step the next item's gallery tile and tables
+//   flush    the previous step's hits (this wave's LDS list) get their bucket slots: global atomics,
+//            answered under this step's MFMAs
+//   MFMAs    8 query fragments x 4 row blocks
+//   compares per query column the 16 rows' scores fma(-2 s_g, acc, a) (the same arithmetic and query
+//            scale folding as tile_kernel_f6p: bit-identical keys), their min against theta; only a
+//            column with a hit is scored again row by row into the wave's LDS hit list
+//   end      the flushed entries written to the buckets
+namespace pp {
+using E = f6t::EngineW;
+constexpr int NT = 256;
+constexpr int TGR = 256;                       // gallery rows per item (one panel of the tiled layout)
+constexpr int TQH = 128;                       // queries per step (half a query panel)
+constexpr int GT = 0;                          // the gallery tile's stage-0 image (24 KiB, panel layout)
+constexpr int QB = GT + f6t::PANEL;            // [2] half-panel images (E::HPB = 12 KiB each)
+constexpr int QT = QB + 2 * E::HPB;            // [2][128] (theta as a float, the query's scale exponent)
+constexpr int GTB = QT + 2 * 1024;             // [2] {f32 aux [256], f32 scale [256]}
+constexpr int HITS = GTB + 2 * 2048;           // [4][HCAPW] (key bits, ql << 9 | row)
+constexpr int HCAPW = 768;
+constexpr int LDS_BYTES = HITS + 4 * HCAPW * 8;
+static_assert(LDS_BYTES <= 81920, "two workgroups per CU");
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// wave's pieces of the stage-0 image of gallery panel gt (24 pieces of 1 KiB) into GT
+__device__ __forceinline__ void copy_gtile(const TileArgs& p, int64_t gt, int wave, uint32_t lane) {
+  const int64_t pb = (int64_t)p.nk * f6t::PANEL;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(reinterpret_cast<const char*>(p.G) + gt * pb), 0, f6t::PANEL, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int piece = wave * 6 + j;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (OFR_LDS void*)(uintptr_t)(GT + piece * 1024), 16, lane * 16,
+                                             piece * 1024, 0, 0);
+  }
+}
+// half h = step & 1 of query panel step >> 1 (stage 0) into QB slot buf: sub-block q = wave, its part0 rows
+// [128 h, 128 h + 128) (2 pieces) and part1 slots of those rows (1 piece) -- the HPB image E::abase reads
+__device__ __forceinline__ void copy_qhalf(const TileArgs& p, int64_t step, int buf, int wave, uint32_t lane) {
+  const int64_t pb = (int64_t)p.nk * f6t::PANEL, pnl = step >> 1;
+  const int h = (int)(step & 1);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(reinterpret_cast<const char*>(p.Q) + pnl * pb), 0, f6t::PANEL, 0x00020000);
+#pragma unroll
+  for (int part = 0; part < 3; ++part) {
+    const int src = wave * 6144 + (part < 2 ? h * 2048 + part * 1024 : 4096 + h * 1024);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        r, (OFR_LDS void*)(uintptr_t)(QB + buf * E::HPB + wave * 3072 + part * 1024), 16, lane * 16, src, 0, 0);
+  }
+}
+__device__ __forceinline__ void copy_qtables(const uint2* qtab, int64_t nq, int64_t step, int buf, int wave,
+                                             uint32_t lane) {
+  f6p::table_piece(qtab + step * TQH, 2 * (nq - step * TQH), QT + buf * 1024, wave, lane);
+}
+__device__ __forceinline__ void copy_gtables(const TileArgs& p, int64_t g0, int buf, int wave, uint32_t lane) {
+  f6p::table_piece(p.aux + g0, p.N - g0, GTB + buf * 2048, wave, lane);
+  f6p::table_piece(p.gscale + g0, p.N - g0, GTB + buf * 2048 + 1024, wave, lane);
+}
+__device__ __forceinline__ i32x8 frag8(uint32_t a0, uint32_t a1) {
+  const f6t::i32x6 f = E::frag_at(a0, a1);
+  i32x8 v;
+  v[0] = f[0]; v[1] = f[1]; v[2] = f[2]; v[3] = f[3]; v[4] = f[4]; v[5] = f[5]; v[6] = 0; v[7] = 0;
+  return v;
+}
+
+// LDS reads through integer addresses, volatile (as E::frag_at): hipcc makes a read through smem wait for
+// every LDS-DMA copy in flight (s_waitcnt vmcnt(0): the next step's copies, issued at the step's top), not
+// these; none of them reads a region a copy in flight writes
+__device__ __forceinline__ uint2 lds_u2(uint32_t a) {
+  const f6t::i32x2 v = *reinterpret_cast<volatile const OFR_LDS f6t::i32x2*>((uintptr_t)a);
+  return make_uint2((uint32_t)v[0], (uint32_t)v[1]);
+}
+__device__ __forceinline__ uint32_t lds_u32(uint32_t a) {
+  return *reinterpret_cast<volatile const OFR_LDS uint32_t*>((uintptr_t)a);
+}
+__device__ __forceinline__ float4 lds_f4(uint32_t a) {
+  const f6t::i32x4 v = *reinterpret_cast<volatile const OFR_LDS f6t::i32x4*>((uintptr_t)a);
+  return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
+}
+
+struct Pend {
+  int64_t q;   // < 0: none
+  int slot;
+  uint2 hv;
+};
+// the wave's list of the previous step (n entries, uniform) -> bucket slots; more than one entry per lane
+// (rare on large galleries) is flushed here whole
+__device__ __forceinline__ Pend flush_begin(const TileArgs& p, uint32_t hits, uint32_t n, int64_t g0, int64_t q0,
+                                            uint32_t lane) {
+  // slot is left unset where no atomic writes it (read only where q >= 0): a constant there made the
+  // compiler wait for every memory operation in flight (vmcnt(0)) before overwriting the atomic's
+  // destination register on the no-flush path
+  Pend pd;
+  pd.q = -1;
+  pd.hv = make_uint2(0u, 0u);
+  if (n > 64u) {
+    for (uint32_t e = lane; e < n; e += 64u) {
+      const uint2 hv = lds_u2(hits + e * 8u);
+      const int64_t q = q0 + (int)(hv.y >> 9);
+      if (q < p.B) {
+        const int slot = atomicAdd(p.count + q, 1);
+        if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(hv.x), (int)(g0 + (hv.y & 511u))};
+      }
+    }
+  } else if (lane < n) {
+    pd.hv = lds_u2(hits + lane * 8u);
+    pd.q = q0 + (int)(pd.hv.y >> 9);
+    if (pd.q < p.B) pd.slot = atomicAdd(p.count + pd.q, 1);
+    else pd.q = -1;
+  }
+  return pd;
+}
+__device__ __forceinline__ void flush_end(const TileArgs& p, int64_t g0, const Pend& pd) {
+  int slot = pd.slot;
+  asm volatile("" : "+v"(slot));   // first use of the atomic's answer here, not right behind the atomic
+  if (pd.q >= 0 && slot < p.cap)
+    p.bucket[pd.q * p.cap + slot] = Cand{__uint_as_float(pd.hv.x), (int)(g0 + (pd.hv.y & 511u))};
+}
+}  // namespace pp
+
+// theta keys -> the pass's per-query table (thetas as floats, -inf past B; the power-of-two query scales'
+// exponents), nq = round_up(B, 128) entries
+__global__ void prefix_tables_kernel(const uint32_t* theta, const float* qscale, int64_t B, int64_t nq, uint2* out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  float th = -__builtin_inff();
+  int eq = 0;
+  if (q < B) {
+    th = key_float(theta[q] | 0xffu);   // KEY_NONE -> NaN: every row kept
+    const uint32_t sb = __float_as_uint(qscale[q]);
+    eq = sb != 0u ? (int)((sb >> 23) & 0xffu) - 127 : 0;
+  }
+  out[q] = make_uint2(__float_as_uint(th), (uint32_t)eq);
+}
+
+// OFR_PP_PROBE (probe builds only, tools/probe_prefix_pass.py): bit 1 no bucket flush, bit 2 no compares
+// (the accumulators kept alive), bit 4 no MFMAs (zero accumulators)
+#ifndef OFR_PP_PROBE
+#define OFR_PP_PROBE 0
+#endif
+// p.ntg = ceil(N / 256) gallery tiles; steps of 128 queries, ceil(B / 128); item w = (tile w / ngrp, steps
+// [qg (w % ngrp), ...)).  qtab: prefix_tables_kernel's table.
+__global__ void __launch_bounds__(256, 2) prefix_pass_kernel(TileArgs p, const uint2* qtab, int64_t qg) {
+  using E = f6t::EngineW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63;
+  const int64_t nsteps = (p.B + pp::TQH - 1) / pp::TQH, nq = nsteps * pp::TQH;
+  const int64_t ngrp = (nsteps + qg - 1) / qg, items = p.ntg * ngrp;
+  int64_t w = blockIdx.x;
+  if (w >= items) return;
+  int scs;   // the lane's stage-0 block scale byte (its 32-feature block lane >> 4)
+  {
+    const uint32_t r0 = f6t::sload_bscale(p.bs, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    scs = f6t::lane_byte(r0, 8u * (lane >> 4));
+  }
+  const uint32_t ng32 = (uint32_t)ngrp, qg32 = (uint32_t)qg;
+  auto item_gt = [&](int64_t it) { return (int64_t)((uint32_t)it / ng32); };
+  auto item_s0 = [&](int64_t it) { return (int64_t)(((uint32_t)it % ng32) * qg32); };
+  auto item_s1 = [&](int64_t it) { const int64_t e = item_s0(it) + qg; return e < nsteps ? e : nsteps; };
+  // fragment bases: gallery tile (panel image, rows wave * 64 + 16 i) and the two half-panel slots
+  const E::Bases gbas = E::bbase(pp::GT), qbas0 = E::abase(pp::QB);
+  const uint32_t hits_a = pp::HITS + (uint32_t)wave * pp::HCAPW * 8u;   // the wave's hit list (LDS address)
+  const int g4 = (int)(lane >> 4) * 4, r16 = (int)(lane & 15);
+  // prologue
+  pp::copy_gtile(p, item_gt(w), wave, lane);
+  pp::copy_gtables(p, item_gt(w) * pp::TGR, 0, wave, lane);
+  pp::copy_qhalf(p, item_s0(w), 0, wave, lane);
+  pp::copy_qtables(qtab, nq, item_s0(w), 0, wave, lane);
+  int qb = 0, gb = 0;
+  bool gpend = false;                  // the next item's gallery tile: copied once every wave has read this one's
+  uint32_t cnt = 0;                    // this wave's hits of the previous step (uniform)
+  int64_t pg0 = 0, pq0 = 0;            // the previous step's tile row / query base (the list's entries)
+  pp::Pend pdb{-1, 0, make_uint2(0u, 0u)};   // entries whose atomics the previous step issued
+  int64_t pg1 = 0;                     // their tile row base
+  bool flushed = false;                // memory operations issued after the copies (vmcnt(1) at the top)
+  pp::i32x8 A[4];
+  const f6t::f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  for (;;) {
+    const int64_t gt = item_gt(w), s0 = item_s0(w), s1 = item_s1(w), wn = w + gridDim.x;
+    const bool more_items = wn < items;
+    const int64_t g0 = gt * pp::TGR;
+    const int nvalid = p.N - g0 < pp::TGR ? (int)(p.N - g0) : pp::TGR;
+    for (int64_t s = s0; s < s1; ++s) {
+      // this step's copies landed: they were issued before the previous step's bucket atomics, so with
+      // an atomic (or any later memory operation) issued since, vmcnt(1) proves them in order
+      if (flushed) f6t::wait_vm<1>();
+      else f6t::wait_vm<0>();
+      f6t::barrier();
+      // the entries whose slots the previous step's atomics reserved: written now, a step later, and
+      // before this step's copies are issued (so no store follows the copies)
+      if constexpr (!(OFR_PP_PROBE & 1)) pp::flush_end(p, pg1, pdb);
+      if (s == s0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t r0 = (uint32_t)(wave * 64 + 16 * i);
+          A[i] = pp::frag8(gbas.p0 + r0 * 16, ((i & 1) ? gbas.p1o : gbas.p1e) + r0 * 8);
+        }
+        if (more_items) gpend = true;
+      } else if (gpend) {   // every wave read its fragments of this item's tile before this step's barrier
+        pp::copy_gtile(p, item_gt(wn), wave, lane);
+        pp::copy_gtables(p, item_gt(wn) * pp::TGR, gb ^ 1, wave, lane);
+        gpend = false;
+      }
+      const int64_t sn = s + 1 < s1 ? s + 1 : (more_items ? item_s0(wn) : -1);
+      if (sn >= 0) {
+        pp::copy_qhalf(p, sn, qb ^ 1, wave, lane);
+        pp::copy_qtables(qtab, nq, sn, qb ^ 1, wave, lane);
+      }
+      const pp::Pend pd = (OFR_PP_PROBE & 1) ? pp::Pend{-1, 0, make_uint2(0u, 0u)}
+                                             : pp::flush_begin(p, hits_a, cnt, pg0, pq0, lane);
+      flushed = (OFR_PP_PROBE & 1) ? false : cnt > 0u;
+      // MFMAs: acc[i][c] = rows wave * 64 + 16 i, queries 16 c of the step
+      const uint32_t qta = pp::QT + (uint32_t)qb * 1024u + (uint32_t)r16 * 8u;   // the lane's column c at + 128 c
+      f6t::f32x4 acc[4][8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t qo = (uint32_t)qb * E::HPB;   // the step's half-panel slot
+        const pp::i32x8 b = pp::frag8(qbas0.p0 + qo + c * 256, ((c & 1) ? qbas0.p1o : qbas0.p1e) + qo + c * 128);
+        const int sbq = scs + (int)pp::lds_u32(qta + c * 128u + 4u);   // block byte + e_q (in [0, 191]: no carry)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if constexpr (OFR_PP_PROBE & 4) {
+            acc[i][c] = zero;
+            asm volatile("" :: "v"(b), "v"(A[i]), "v"(sbq));
+          } else {
+            acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], b, zero, 2, 2, 0, scs, 0, sbq);
+          }
+        }
+      }
+      // compares: per query column the min of its 16 rows' scores against theta
+      const uint32_t gta = pp::GTB + (uint32_t)gb * 2048u + (uint32_t)(wave * 64 + g4) * 4u;   // aux; scale at + 1024
+      float av[4][4], tp[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 a4 = pp::lds_f4(gta + 64u * i);
+        const float4 s4 = pp::lds_f4(gta + 1024u + 64u * i);
+        av[i][0] = a4.x; av[i][1] = a4.y; av[i][2] = a4.z; av[i][3] = a4.w;
+        tp[i][0] = s4.x + s4.x; tp[i][1] = s4.y + s4.y; tp[i][2] = s4.z + s4.z; tp[i][3] = s4.w + s4.w;
+      }
+      uint32_t hitc = 0;
+      if constexpr (OFR_PP_PROBE & 2) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) asm volatile("" :: "v"(acc[i][c]));
+      } else
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float th = __uint_as_float(pp::lds_u32(qta + c * 128u));
+        float m[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float x0 = __builtin_fmaf(-tp[i][0], acc[i][c][0], av[i][0]);
+          const float x1 = __builtin_fmaf(-tp[i][1], acc[i][c][1], av[i][1]);
+          const float x2 = __builtin_fmaf(-tp[i][2], acc[i][c][2], av[i][2]);
+          const float x3 = __builtin_fmaf(-tp[i][3], acc[i][c][3], av[i][3]);
+          m[i] = fminf(fminf(x0, x1), fminf(x2, x3));
+        }
+        const float mn = fminf(fminf(m[0], m[1]), fminf(m[2], m[3]));
+        hitc |= !(mn > th) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
+      }
+      uint32_t ncnt = 0;
+      if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform; ~2 kept pairs per step and wave on gallery data
+        // the scores again, from laundered row terms: the compiler would otherwise keep all 128 scores of the
+        // pass above alive for this rare path (common subexpressions)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(tp[i][r]), "+v"(av[i][r]));
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
+          const float th = __uint_as_float(pp::lds_u32(qta + c * 128u));
+          const int ql = c * 16 + r16;
+          const bool qok = (int64_t)s * pp::TQH + ql < p.B;
+          float sc[16];
+          uint32_t hm = 0;   // the lane's rows j = 4 i + r that pass
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int j = 4 * i + r;
+              sc[j] = __builtin_fmaf(-tp[i][r], acc[i][c][r], av[i][r]);
+              const int row = wave * 64 + 16 * i + g4 + r;
+              hm |= (!(sc[j] > th) && row < nvalid && qok) ? (1u << j) : 0u;
+            }
+          // one kept row per lane and round, in row order: a wave-uniform loop of (on gallery data) one round
+          for (;;) {
+            const bool act = hm != 0u;
+            const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
+            if (mk == 0) break;   // uniform
+            const int j = act ? __builtin_ctz(hm) : 0;
+            hm &= hm - 1u;
+            float v = sc[0];
+#pragma unroll
+            for (int jj = 1; jj < 16; ++jj) v = j == jj ? sc[jj] : v;
+            const int row = wave * 64 + 16 * (j >> 2) + g4 + (j & 3);
+            if (act) {
+              const uint32_t kb = __float_as_uint(key_score(score_key(v, 0)));
+              const uint32_t slot =
+                  ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+              if (slot < (uint32_t)pp::HCAPW) {   // volatile integer address: no wait for the copies in flight
+                f6t::i32x2 e;
+                e[0] = (int)kb;
+                e[1] = (int)(((uint32_t)ql << 9) | (uint32_t)row);
+                *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
+              } else {   // the list is full (small galleries keep a large share): straight to the bucket
+                const int64_t q = (int64_t)s * pp::TQH + ql;
+                const int bs = atomicAdd(p.count + q, 1);
+                if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
+              }
+            }
+            ncnt += (uint32_t)__builtin_popcountll(mk);
+          }
+        }
+      }
+      flushed = flushed || ncnt > (uint32_t)pp::HCAPW;   // direct bucket writes of an overflowing list
+      pdb = pd;
+      pg1 = pg0;
+      cnt = ncnt < (uint32_t)pp::HCAPW ? ncnt : (uint32_t)pp::HCAPW;
+      pg0 = g0;
+      pq0 = s * pp::TQH;
+      qb ^= 1;
+    }
+    if (gpend) {   // a one-step item: its fragment reads are behind every wave only after a barrier
+      __syncthreads();
+      pp::copy_gtile(p, item_gt(wn), wave, lane);
+      pp::copy_gtables(p, item_gt(wn) * pp::TGR, gb ^ 1, wave, lane);
+      gpend = false;
+      flushed = false;   // these copies follow the atomics: the next top waits for everything
+    }
+    if (!more_items) break;
+    w = wn;
+    gb ^= 1;
+  }
+  // the last two steps' hits
+  f6t::wait_vm<0>();
+  pp::flush_end(p, pg1, pdb);
+  const pp::Pend pd = pp::flush_begin(p, hits_a, cnt, pg0, pq0, lane);
+  pp::flush_end(p, pg0, pd);
+}
+
 // ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
 // One workgroup per 256-row gallery panel, wave w owns rows 32w..32w+31 against the (single)
 // 32-row query block, loading its fragments straight to VGPRs from the f6 tiled layout (each
@@ -1042,6 +1399,7 @@ struct MergeArgs {
   // (the prefix scores, within dS of the keys), so the bounds below use |q_m|^2 for |q|^2 and a key
   // bounds nothing from above (no ub_local).
   int64_t dpre;
+  int* evals;   // optional [B]: candidates re-ranked exactly per query (the merge's bytes: evals x d x 4)
 };
 
 // Best KC (distance, index) of the n candidates at src (16-byte aligned) into lists[0..KC),
@@ -1234,6 +1592,46 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   const float* qr = p.Q + q * p.ldq;
   double qq, dS;
   const int kk = p.k < KC ? p.k : KC;
+  const int64_t d4 = p.d >> 2;
+  const bool vec = ((p.ldq | p.ldg) & 3) == 0 && (((uintptr_t)p.Q | (uintptr_t)p.G) & 15) == 0;
+  // exact squared distance (distance.py:60, in fp64) of candidate cc, one wave (the sum in every lane)
+  auto exact_d2 = [&](const Cand& cc) -> double {
+    double a = 0;
+    const float* gr = p.G + (int64_t)cc.i * p.ldg;
+    int64_t j0 = 0;
+    if (vec) {
+      const float4* q4 = reinterpret_cast<const float4*>(qr);
+      const float4* g4 = reinterpret_cast<const float4*>(gr);
+      // DU float4 pairs in flight per lane (a lone query's merge is one block: its loop is bound by
+      // the memory latency); the sum runs in the same order as one float4 per iteration
+      constexpr int DU = 4;
+      for (int64_t j = lane; j < d4; j += 64 * DU) {
+        float4 x[DU], y[DU];
+#pragma unroll
+        for (int u = 0; u < DU; ++u) {
+          const int64_t jj = j + 64 * u;
+          x[u] = jj < d4 ? q4[jj] : make_float4(0.f, 0.f, 0.f, 0.f);
+          y[u] = jj < d4 ? g4[jj] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < DU; ++u) {
+          if (j + 64 * u < d4) {
+            const double e0 = (double)x[u].x - (double)y[u].x, e1 = (double)x[u].y - (double)y[u].y;
+            const double e2 = (double)x[u].z - (double)y[u].z, e3 = (double)x[u].w - (double)y[u].w;
+            a += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+          }
+        }
+      }
+      j0 = d4 * 4;
+    }
+    for (int64_t j = j0 + lane; j < p.d; j += 64) {
+      const double df = (double)qr[j] - (double)gr[j];
+      a += df * df;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    return a;
+  };
   if (p.mode == 2) {   // the selection of a mode-1 launch
     if (threadIdx.x < KC) lists[threadIdx.x] = p.sel[q * KC + threadIdx.x];
     qq = p.qd[q * 3 + 0];
@@ -1273,6 +1671,18 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     dS = dS * (1.0 + 1e-6) + 1e-300;
     if (p.mode == 1) {
       if (threadIdx.x < KC) p.sel[q * KC + threadIdx.x] = lists[threadIdx.x];
+      if (p.dpre > 0) {
+        // a prefix key bounds nothing from above: the exact squared distances of the first kk
+        // candidates do (round 6) -- k real rows of this shard lie that close, so the k-th smallest
+        // of these over the shards bounds the global k-th; the other shards' candidates whose prefix
+        // lower bound exceeds it are then never re-ranked (mode 2)
+        for (int c = wave; c < kk; c += 4) {
+          const Cand cc = lists[c];
+          const double a = cc.i != CAND_EMPTY && !overflow ? exact_d2(cc) : __builtin_inf();
+          if (lane == 0) exact[c] = a;
+        }
+        __syncthreads();
+      }
       if (threadIdx.x == 0) {
         p.qd[q * 3 + 0] = qq;
         p.qd[q * 3 + 1] = dS;
@@ -1280,19 +1690,27 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
         // upper bound of d^2 of the j-th candidate: its truncated key t is within 256 ulp below
         // the fp32 coarse score (|sc - t| <= |t| 2^-15, 2^-14 taken), S <= sc + dS, d^2 = S + |q|^2;
         // the lists are in ascending key order, so the bounds ascend too
-        for (int j = 0; j < kk; ++j) {
-          const Cand c = lists[j];
-          const double t = (double)c.d;
-          p.ub_local[q * kk + j] = c.i == CAND_EMPTY || overflow || p.dpre > 0   // a prefix key: no upper bound
-                                       ? __builtin_inf()
-                                       : (t + fabs(t) * 0x1p-14 + dS + qq) * (1.0 + 1e-12) + 1e-300;
+        if (p.dpre > 0) {   // the exact values, ascending (insertion sort of <= 16), a relative 1e-12 up
+          for (int j = 1; j < kk; ++j) {
+            const double v = exact[j];
+            int t = j - 1;
+            for (; t >= 0 && exact[t] > v; --t) exact[t + 1] = exact[t];
+            exact[t + 1] = v;
+          }
+          for (int j = 0; j < kk; ++j) p.ub_local[q * kk + j] = exact[j] * (1.0 + 1e-12) + 1e-300;
+        } else {
+          for (int j = 0; j < kk; ++j) {
+            const Cand c = lists[j];
+            const double t = (double)c.d;
+            p.ub_local[q * kk + j] = c.i == CAND_EMPTY || overflow
+                                         ? __builtin_inf()
+                                         : (t + fabs(t) * 0x1p-14 + dS + qq) * (1.0 + 1e-12) + 1e-300;
+          }
         }
       }
       return;
     }
   }
-  const int64_t d4 = p.d >> 2;
-  const bool vec = ((p.ldq | p.ldg) & 3) == 0 && (((uintptr_t)p.Q | (uintptr_t)p.G) & 15) == 0;
   // lower bound of d^2 of any row whose (truncated) coarse score is >= s, less a relative 1e-12
   // for the fp64 evaluation
   auto d2_lower = [&](double s) { return (s - dS + qq) - 1e-12 * (fabs(s) + dS + 2.0 * qq); };
@@ -1310,70 +1728,37 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   // exact fp64 distance (distance.py:60) of the candidates in coarse order, 4 per round (one per
   // wave); stop once the next candidate's lower bound exceeds the k-th exact distance so far:
   // it and every later one (and every row outside the list) are strictly farther
+  int nevals = 0;   // candidates re-ranked exactly (wave 0's count; MergeArgs::evals)
   for (int r = 0; r < KC / 4 && !skip_all; ++r) {
     const int c = 4 * r + wave;
     const Cand cc = lists[c];
-    double a = 0;
-    if (cc.i != CAND_EMPTY) {
-      const float* gr = p.G + (int64_t)cc.i * p.ldg;
-      int64_t j0 = 0;
-      if (vec) {
-        const float4* q4 = reinterpret_cast<const float4*>(qr);
-        const float4* g4 = reinterpret_cast<const float4*>(gr);
-        // DU float4 pairs in flight per lane (a lone query's merge is one block: its loop is bound by
-        // the memory latency); the sum runs in the same order as one float4 per iteration
-        constexpr int DU = 4;
-        for (int64_t j = lane; j < d4; j += 64 * DU) {   // distance.py:60, in fp64
-          float4 x[DU], y[DU];
-#pragma unroll
-          for (int u = 0; u < DU; ++u) {
-            const int64_t jj = j + 64 * u;
-            x[u] = jj < d4 ? q4[jj] : make_float4(0.f, 0.f, 0.f, 0.f);
-            y[u] = jj < d4 ? g4[jj] : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-#pragma unroll
-          for (int u = 0; u < DU; ++u) {
-            if (j + 64 * u < d4) {
-              const double e0 = (double)x[u].x - (double)y[u].x, e1 = (double)x[u].y - (double)y[u].y;
-              const double e2 = (double)x[u].z - (double)y[u].z, e3 = (double)x[u].w - (double)y[u].w;
-              a += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
-            }
-          }
-        }
-        j0 = d4 * 4;
-      }
-      for (int64_t j = j0 + lane; j < p.d; j += 64) {
-        const double df = (double)qr[j] - (double)gr[j];
-        a += df * df;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-    }
+    const double a = cc.i != CAND_EMPTY ? exact_d2(cc) : 0.0;
     if (lane == 0) exact[c] = cc.i != CAND_EMPTY ? sqrt(a) : __builtin_inf();
     __syncthreads();
     const int done = 4 * r + 4;
-    if (threadIdx.x == 0) {
+    if (wave == 0) {   // the stop test, on one wave: lane t ranks exact[t] among exact[0..done)
+      nevals += (lists[done - 4].i != CAND_EMPTY) + (lists[done - 3].i != CAND_EMPTY) +
+                (lists[done - 2].i != CAND_EMPTY) + (lists[done - 1].i != CAND_EMPTY);
       int st = 0;
       if (done < KC && done >= kk) {
         if (lists[done].i == CAND_EMPTY) {
           st = 1;
         } else {
-          double kth = __builtin_inf();   // kk-th smallest of exact[0..done)
-          for (int t = 0; t < done; ++t) {
-            const double v = exact[t];
-            int lt = 0, le = 0;
-            for (int u = 0; u < done; ++u) {
-              lt += exact[u] < v;
-              le += exact[u] <= v;
-            }
-            if (lt < kk && kk <= le) kth = v;
+          const double v = lane < done ? exact[lane] : __builtin_inf();   // kk-th smallest of exact[0..done)
+          int lt = 0, le = 0;
+          for (int u = 0; u < done; ++u) {
+            const double e = exact[u];
+            lt += e < v;
+            le += e <= v;
           }
+          const uint64_t m = __ballot(lane < done && lt < kk && kk <= le);   // lanes holding the kk-th value
+          const double kth = m ? __shfl(v, __ffsll((long long)m) - 1) : __builtin_inf();
           st = d2_lower((double)lists[done].d) > fmin(kth * kth, ubq);
         }
       } else if (done < KC && p.ub) {
         st = lists[done].i == CAND_EMPTY || d2_lower((double)lists[done].d) > ubq;
       }
-      stop_flag = st;
+      if (lane == 0) stop_flag = st;
     }
     __syncthreads();
     if (stop_flag) {
@@ -1382,10 +1767,12 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (wave == 0) {
     double* od = p.out_d + q * p.k;
     int64_t* oi = p.out_i + q * p.k;
-    sort_and_write<KC>(lists, exact, p.k, p.index_base, od, oi);
+    const double dk = sort_and_write_wave<KC>(lists, exact, p.k, p.index_base, od, oi);
+    if (p.evals && lane == 0) p.evals[q] = nevals;
+    if (lane != 0) return;
     // certificate.  Every row outside the KC candidates has coarse score >= tau, hence exact
     // score S = d^2 - |q|^2 >= tau - dS, i.e. d^2 >= bound = tau - dS + |q|^2 (less a relative
     // 1e-12 for the fp64 evaluation); the local top-k is exact iff d_k^2 < bound.  tau = the
@@ -1396,7 +1783,6 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     double bnd = __builtin_inf();
     if (overflow) bnd = -__builtin_inf();   // the bucket dropped kept rows: no bound
     else if (tk != KEY_NONE) bnd = d2_lower((double)key_score(tk));
-    const double dk = od[kk - 1];
     p.cert[q] = (dk == dk) && (dk * dk < bnd);
     if (p.bound) p.bound[q] = bnd;
   }
@@ -2037,11 +2423,14 @@ extern "C" const char* ofr_f6_sieve_kernel(void) {
 
 // name of the kernel the prefix tier's sieve pass (ofr_knn_f6p_sampled, B > 32) launches for pstages
 static bool f6p_persistent();
+static int f6p_engine();
 extern "C" const char* ofr_f6p_sieve_kernel(int pstages) {
   static const std::string names[2] = {
       "q8s::tile_kernel_f6p (persistent prefix pass: one workgroup per CU, 384-row gallery tile resident in LDS, "
       "16x16x128 fp6 MFMA)",
-      ""};
+      "q8s::prefix_pass_kernel (persistent one-stage prefix pass: two workgroups per CU, 64 x 128 wave tiles, "
+      "16x16x128 fp6 MFMA)"};
+  if (pstages == 1 && f6_shape() == 384 && f6p_persistent() && f6p_engine() == 2) return names[1].c_str();
   if (pstages >= 1 && pstages <= q8s::f6p::NSPMAX && f6_shape() == 384 && f6p_persistent())
     return names[0].c_str();
   return ofr_f6_sieve_kernel();
@@ -2076,6 +2465,12 @@ constexpr int F6W_SERP = 1;
 static bool f6p_persistent() {
   const char* e = getenv("OFR_F6P_PERSIST");
   return !(e && e[0] == '0');
+}
+// Engine of the one-stage prefix pass: 2 = prefix_pass_kernel (two workgroups per CU; default since round
+// 6), 1 = tile_kernel_f6p<1> (one wave per SIMD; the A/B reference).  OFR_F6P_ENGINE, read at every call.
+static int f6p_engine() {
+  const char* e = getenv("OFR_F6P_ENGINE");
+  return e && e[0] == '1' ? 1 : 2;
 }
 // CUs the persistent prefix pass leaves free (OFR_F6P_RESERVE, probe): work queued on other streams --
 // the previous batch's merge -- otherwise waits for the whole pass
@@ -2142,9 +2537,14 @@ static size_t f6_ws_core(int64_t B, int64_t N) {
 }
 static size_t f6_ws_qd(int64_t B) { return (size_t)round_up((int64_t)(B * q8s::KC * sizeof(Cand)), 256); }
 
-extern "C" size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N) {
-  return f6_ws_core(B, N) + f6_ws_qd(B) + (size_t)B * 3 * sizeof(double);
+// the merge's per-query count of exact re-ranks, after the split merge's qd [B][3]
+static size_t f6_ws_evals(int64_t B, int64_t N) {
+  return f6_ws_core(B, N) + f6_ws_qd(B) + (size_t)round_up(B * 3 * (int64_t)sizeof(double), 256);
 }
+extern "C" size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N) {
+  return f6_ws_evals(B, N) + (size_t)round_up(B * 4, 256);
+}
+extern "C" size_t ofr_knn_f6_merge_evals_offset(int64_t B, int64_t N) { return f6_ws_evals(B, N); }
 
 extern "C" size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N) {
   return B <= 32 ? (size_t)-1 : sieve_ws(B, N).count;
@@ -2268,6 +2668,21 @@ extern "C" int ofr_knn_f6_merge_pruned(void* stream, int stage, const float* Q, 
                      out_d, out_i, cert, bound, workspace, workspace_bytes, stage, ub);
 }
 
+extern "C" int ofr_knn_f6p_merge_pruned(void* stream, int stage, const float* Q, int64_t B, int64_t ldq,
+                                        const void* Qt, const float* qscale, const double* qstats, const float* G,
+                                        int64_t N, int64_t ldg, int64_t d, const void* Gt, const float* gscale,
+                                        const float* aux, const double* gmax, int k, int64_t index_base,
+                                        double* out_d, int64_t* out_i, int* cert, double* bound, double* ub,
+                                        void* workspace, size_t workspace_bytes, int pstages) {
+  OFR_CHECK_ARG(stage == 1 || stage == 2, "ofr_knn_f6p_merge_pruned: stage must be 1 (select) or 2 (re-rank)");
+  OFR_CHECK_ARG(ub != nullptr, "ofr_knn_f6p_merge_pruned: null ub");
+  OFR_CHECK_ARG(d >= 1 && pstages >= 1 && pstages <= f6t::stages(d),
+                "ofr_knn_f6p_merge_pruned: pstages must be in [1, ceil(d / 128)]");
+  return knn_f6_impl(stream, 2, Q, B, ldq, Qt, qscale, qstats, G, N, ldg, d, Gt, gscale, aux, gmax, k, index_base,
+                     out_d, out_i, cert, bound, workspace, workspace_bytes, stage, ub, nullptr, nullptr, nullptr,
+                     nullptr, pstages);
+}
+
 static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                        const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                        const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
@@ -2340,6 +2755,11 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
           hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, q8s::f6p::LDS_BYTES);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 prefix pass)");
         }
+        {
+          hipError_t e = hipFuncSetAttribute((const void*)q8s::prefix_pass_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, q8s::pp::LDS_BYTES);
+          if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(prefix_pass_kernel)");
+        }
         attr_done = true;
       }
       // sample pass: tile lists of every SIEVE_STRIDE-th gallery panel, or of the row sample -> thresholds
@@ -2383,6 +2803,24 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       }
       if (!(phases & 8)) {
         // sample + thresholds only
+      } else if (f6_shape() == 384 && a.nkp == 1 && a.nkp < f6t::stages(d) && !two && f6p_persistent() &&
+                 f6p_engine() == 2 && device_cus() > 0) {
+        // the one-stage prefix pass: two workgroups per CU (prefix_pass_kernel)
+        q8s::TileArgs wa = a;
+        wa.ntg = cdiv(N, q8s::pp::TGR);
+        const int64_t nsteps = cdiv(B, q8s::pp::TQH), nq = nsteps * q8s::pp::TQH;
+        // the per-query table lives in the sample lists' region, dead once the thresholds are set
+        OFR_CHECK_ARG((size_t)nq * sizeof(uint2) <= w.theta - w.lists, "ofr_knn_f6: workspace too small (prefix tables)");
+        uint2* qtab = reinterpret_cast<uint2*>(wsb + w.lists);
+        hipLaunchKernelGGL(q8s::prefix_tables_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, theta, a.qscale, B,
+                           nq, qtab);
+        OFR_LAUNCH_CHECK("f6 prefix_tables_kernel");
+        const int slots = 2 * std::max(1, device_cus() - f6p_reserve());
+        const int64_t qg = f6p_group(wa.ntg, nsteps, slots);
+        const int64_t items = wa.ntg * cdiv(nsteps, qg);
+        OFR_CHECK_ARG(items < 0x7fffffffLL, "ofr_knn_f6: grid too large");
+        const unsigned grid = (unsigned)std::min<int64_t>(items, slots);
+        hipLaunchKernelGGL(q8s::prefix_pass_kernel, dim3(grid), dim3(q8s::pp::NT), q8s::pp::LDS_BYTES, st, wa, qtab, qg);
       } else if (f6_shape() == 384 && a.nkp <= q8s::f6p::NSPMAX && a.nkp < f6t::stages(d) && !two &&
                  f6p_persistent() && device_cus() > 0) {
         // the prefix tier's short pass: persistent workgroups, the gallery tile resident (tile_kernel_f6p)
@@ -2430,6 +2868,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
     m.dpre = a.nkp < f6t::stages(d) ? (int64_t)a.nkp * f6t::BK : 0;
     m.sel = reinterpret_cast<Cand*>(wsb + f6_ws_core(B, N));
     m.qd = reinterpret_cast<double*>(wsb + f6_ws_core(B, N) + f6_ws_qd(B));
+    m.evals = reinterpret_cast<int*>(wsb + f6_ws_evals(B, N));
     if (merge_mode == 1) m.ub_local = ub;
     if (merge_mode == 2) m.ub = ub;
     if (sieve) {

@@ -157,6 +157,49 @@ __device__ __forceinline__ void sort_and_write(const Cand* lists, const double* 
   }
 }
 
+// The same on one whole wave (every lane of it calls this; round 6): lane c ranks candidate c against
+// the other KC -- ties, i.e. equal (distance, index) keys, occur only between empty entries and go by c,
+// as the insertion sort above keeps them -- and writes it at its rank if that is below k.  Returns the
+// k-th distance (min(k, KC)-th) in every lane.  The thread-0 form sorts a dynamically indexed array in
+// scratch memory (~120 dependent scratch moves per query); this one reads the KC entries from LDS.
+template <int KC>
+__device__ __forceinline__ double sort_and_write_wave(const Cand* lists, const double* exact, int k, int64_t index_base,
+                                                      double* out_d, int64_t* out_i) {
+  const int lane = threadIdx.x & 63;
+  double x = __builtin_inf();
+  int64_t xi = INT64_MAX;
+  if (lane < KC) {
+    const Cand cc = lists[lane];
+    if (cc.i != CAND_EMPTY) {
+      x = exact[lane];
+      xi = (int64_t)cc.i;
+    }
+  }
+  int rank = 0;
+#pragma unroll
+  for (int u = 0; u < KC; ++u) {
+    const Cand cu = lists[u];
+    const bool ok = cu.i != CAND_EMPTY;
+    const double y = ok ? exact[u] : __builtin_inf();
+    const int64_t yi = ok ? (int64_t)cu.i : INT64_MAX;
+    rank += nan_last_before(y, yi, x, xi) || (u < lane && !nan_last_before(x, xi, y, yi));
+  }
+  if (lane < KC && rank < k) {
+    const bool ok = xi != INT64_MAX;
+    out_d[rank] = ok ? x : __builtin_inf();
+    out_i[rank] = ok ? xi + index_base : -1;
+  }
+  for (int j = KC + lane; j < k; j += 64) {   // k > KC: nothing more to place
+    out_d[j] = __builtin_inf();
+    out_i[j] = -1;
+  }
+  const int kk = k < KC ? k : KC;
+  const uint64_t m = __ballot(lane < KC && rank == kk - 1);
+  const int src = m ? __ffsll((long long)m) - 1 : 0;
+  const double dk = __shfl(xi != INT64_MAX ? x : __builtin_inf(), src);
+  return m ? dk : __builtin_inf();
+}
+
 static inline int pick_kc(int k) { return k <= 8 ? 8 : 16; }
 
 }  // namespace ofr

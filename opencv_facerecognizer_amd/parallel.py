@@ -151,10 +151,11 @@ def merge_sharded(gallery, Qd, qq, k, index_base, out, group=None, workspace=Non
     squared distance, and each rank re-ranks only the candidates that can still fall below it
     (stage 2): a rank that holds none of a query's neighbours skips its exact re-rank (the rows it
     skips are farther than k rows of another rank, so the global top-k and the certificate of
-    certify_sharded are unchanged).  Other tiers: the local merge.  workspace: the one phase 1 ran
-    on (the gallery's by default).  Returns out."""
+    certify_sharded are unchanged).  The prefix tier f6p (round 6) too: its keys bound no distance from
+    above, so stage 1 takes the exact squared distances of each rank's first k candidates instead.  Other
+    tiers: the local merge.  workspace: the one phase 1 ran on (the gallery's by default).  Returns out."""
     _, ws = world(group)
-    if ws == 1 or qq["tier"] != "f6":
+    if ws == 1 or qq["tier"] not in ("f6", "f6p"):
         return gallery.search_q8_phase(2, Qd, qq, k, index_base=index_base, out=out, workspace=workspace)
     B = Qd.shape[0]
     ub_local = torch.empty((B, k), dtype=torch.float64, device=Qd.device)
@@ -424,20 +425,24 @@ class DeviceComm:
     def __exit__(self, *exc):
         self.close()
 
-    def knn(self, galleries, queries, k, tiers=("f6x2", 2)):
+    def knn(self, galleries, queries, k, tiers=("f6x2", 2), prefix=True):
         """galleries[r]: the FloatGallery of shard r (on devices[r], global row offset in
         .index_base, default 0 for one shard); queries[r]: the centred fp32 query rows [B][ld] on
         devices[r] (the same batch on every device).  tiers: the finer stages the open queries may
         take before the exact pass ("f6x2" and / or 2 = int8 x2; built on the galleries if missing).
+        prefix: run the prefix tier f6p first when the galleries have one (prefix_stages(); a sharded
+        caller makes it the same on every shard: parallel.share_block_scales).
         Returns per device (out_d, out_i, cert); self.last_tier_counts = open queries after fp6,
-        after f6x2, after int8 x2, and the number the exact pass ran (-1: stage not run)."""
+        after f6x2, after int8 x2, and the number the exact pass ran (-1: stage not run);
+        self.last_prefix_open = open queries after the prefix tier (-1: not run)."""
         import ctypes
         from . import _lib
         lib = _lib.load()
         B, d = int(queries[0].shape[0]), galleries[0].d
         shards = (_lib.KnnShard * len(galleries))()
         counts = np.full(4, -1, dtype=np.int64)
-        keep = [counts]
+        popen = np.full(1, -1, dtype=np.int64)
+        keep = [counts, popen]
         for r, (g, Qd) in enumerate(zip(galleries, queries)):
             with torch.cuda.device(Qd.device):
                 qq = g.quantize_queries(Qd, tier="f6")
@@ -471,7 +476,16 @@ class DeviceComm:
                     s.gscale8, s.gmax8 = t8["scale"].data_ptr(), t8["gmax"].data_ptr()
                 if r == 0:
                     s.tier_counts = counts.ctypes.data
-                keep.append((qq, ws, out_d, out_i, cert))
+                    s.prefix_open = popen.ctypes.data
+                qp = None
+                if prefix and g.prefix_stages() and g.row_sample():
+                    qp = g.quantize_queries(Qd, tier="f6p")
+                    tp = g._tier_gallery("f6p")
+                    s.pstages = tp["pst"]
+                    s.Qtp, s.qscalep, s.qstatsp = qp["Qs"].data_ptr(), qp["scale"].data_ptr(), qp["stats"].data_ptr()
+                    s.paux, s.spaux = tp["paux"].data_ptr(), tp["spaux"].data_ptr()
+                keep.append((qq, ws, out_d, out_i, cert, qp))
         _lib.call("ofr_knn_sharded", self.handle, ctypes.cast(shards, ctypes.c_void_p), B, d, k)
         self.last_tier_counts = [int(x) for x in counts]
-        return [(o[2], o[3], o[4]) for o in keep[1:]]
+        self.last_prefix_open = int(popen[0])
+        return [(o[2], o[3], o[4]) for o in keep[2:]]

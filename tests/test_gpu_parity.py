@@ -1010,7 +1010,7 @@ def test_topk_merge_certify_kernel():
     assert rc.min() == 0 and rc.max() == 1
 
 
-@pytest.mark.parametrize("data", ["separated", "sphere", "crowded"])
+@pytest.mark.parametrize("data", ["separated", "sphere", "crowded", "prefix"])
 def test_knn_sharded_c_abi_one_device(monkeypatch, data):
     """ofr_comm_init_all + ofr_knn_sharded (single process, RCCL) on this box's one device: the fp6
     tier, the all-gather, the global certificate and the tier chain of uncertified queries (f6x2,
@@ -1031,6 +1031,9 @@ def test_knn_sharded_c_abi_one_device(monkeypatch, data):
         U = r.normal(0, 1, (2000, 64))
         G = c + 100.0 * U / np.linalg.norm(U, axis=1, keepdims=True)
         Q = c + r.normal(0, 1e-6, (100, 64))
+    elif data == "prefix":   # Fisherfaces-like: identity variance in the leading 64 features (round 6)
+        from test_gpu_prefix import _lda_like
+        G, Q = _lda_like(1000, 10, 1280, 300, seed=11)
     else:   # test_knn_f6x2_certifies_crowded_clusters' data
         r = _rng(3)
         mu = r.normal(0, 1, (200, 128))
@@ -1043,9 +1046,24 @@ def test_knn_sharded_c_abi_one_device(monkeypatch, data):
     with DeviceComm([0]) as comm:
         (dd, ii, cert), = comm.knn([g], [g.query_rows(Q)], k)
         counts = comm.last_tier_counts
+        popen = comm.last_prefix_open
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
     c = cert.cpu().numpy()
-    if data == "separated":
+    if data == "prefix":
+        # the prefix tier ran first (its own exchange and global certificate) and certified every query
+        assert g.prefix_stages() >= 1 and popen == 0 and counts[0] == 0, (g.prefix_stages(), popen, counts)
+        assert c.min() == 1
+        # forced on isotropic rows: the prefix tier certifies nothing, the fp6 tier takes every query
+        G2 = _rng(12).normal(0, 20, (4000, 1280)).astype(np.float32).astype(np.float64)
+        Q2 = (G2[_rng(13).integers(0, 4000, 100)] + _rng(14).normal(0, 1, (100, 1280))).astype(np.float32).astype(np.float64)
+        monkeypatch.setenv("OFR_F6_PREFIX", "1")
+        g2 = FloatGallery(G2, _lib.METRIC_EUCLIDEAN)
+        with DeviceComm([0]) as comm:
+            (d2, i2, c2), = comm.knn([g2], [g2.query_rows(Q2)], k)
+            assert comm.last_prefix_open == len(Q2) and comm.last_tier_counts[0] >= 0, (
+                comm.last_prefix_open, comm.last_tier_counts)
+        _check_search("EuclideanDistance", Q2, G2, d2.cpu().numpy(), i2.cpu().numpy(), k)
+    elif data == "separated":
         assert c.min() == 1 and counts == [0, -1, -1, -1]
     elif data == "sphere":
         assert c.max() == 0 and counts[0] == len(Q) and counts[3] == counts[2] == counts[1] == len(Q), counts

@@ -85,6 +85,28 @@ def _worker(rank, ws, port, out):
         skipped = int(torch.isinf(loc[0][:, 0]).sum())
         (rd, ri), rc = certify_sharded(g, Qd, qb, K, loc, g.index_base)
         res["pruned"] = (pd.cpu().numpy(), pi.cpu().numpy(), pc, rd.cpu().numpy(), ri.cpu().numpy(), rc, skipped)
+        # round 6: the prefix tier on a sharded gallery whose shards ALONE would choose different prefixes
+        # (the choice now comes from all-reduced block sums, so both ranks start at f6p and their
+        # collectives match), and its pruned split merge (ofr_knn_f6p_merge_pruned) against the plain one
+        from opencv_facerecognizer_amd._device import FloatGallery
+        Q, G, y = _split_prefix_data()
+        clf = _classifier("EuclideanDistance")
+        clf.compute(list(G), y)
+        clf.shard()
+        g = clf._gallery()
+        own = FloatGallery.choose_prefix(g.block_sums().cpu().numpy(), g.d, g.N)   # this shard's own choice
+        d, i = clf.search(Q)
+        res["prefix"] = (d, i, g.prefix_stages(), own, g.last_start_tier, tuple(g.last_fallbacks))
+        Qd = g.query_rows(Q)
+        qa = g.quantize_queries(Qd, tier="f6p")
+        plain = g.search_q8_phase(3, Qd, qa, K, g.index_base)
+        (pd, pi), pc = certify_sharded(g, Qd, qa, K, plain, g.index_base)
+        qb = g.quantize_queries(Qd, tier="f6p")
+        loc = g.search_q8_phase(1, Qd, qb, K, g.index_base)
+        merge_sharded(g, Qd, qb, K, g.index_base, loc)
+        skipped = int(torch.isinf(loc[0][:, 0]).sum())
+        (rd, ri), rc = certify_sharded(g, Qd, qb, K, loc, g.index_base)
+        res["prefix_pruned"] = (pd.cpu().numpy(), pi.cpu().numpy(), pc, rd.cpu().numpy(), ri.cpu().numpy(), rc, skipped)
         # the fused model path: Fisherfaces projection + sharded certified search
         from ocvfacerec.facerec.feature import Fisherfaces
         from ocvfacerec.facerec.model import PredictableModel
@@ -112,6 +134,21 @@ def _identity_blocks():
     G = protos[np.arange(4000) // 10] + r.normal(0, 1, (4000, 48))
     Q = protos[r.integers(0, 400, 300)] + r.normal(0, 1, (300, 48))
     return Q.astype(np.float32).astype(np.float64), G.astype(np.float32).astype(np.float64), np.arange(4000) // 10
+
+
+def _split_prefix_data():
+    """2 x 150 identities x 10 rows, d = 1,280: the first half's identities differ in the leading 64
+    features (a Fisherfaces-like profile: alone its shard chooses a one-stage prefix), the second half's
+    isotropically (alone: no prefix); together the leading blocks still dominate (prefix 1)."""
+    r = np.random.default_rng(76)
+    d, nid, per = 1280, 150, 10
+    Ca = np.zeros((nid, d))
+    Ca[:, :64] = r.normal(0, 60, (nid, 64))
+    Cb = r.normal(0, 6, (nid, d))
+    C = np.concatenate([Ca, Cb])
+    G = C[np.arange(2 * nid * per) // per] + r.normal(0, 3, (2 * nid * per, d))
+    Q = C[r.integers(0, 2 * nid, 300)] + r.normal(0, 3, (300, d))
+    return Q.astype(np.float32).astype(np.float64), G.astype(np.float32).astype(np.float64), np.arange(2 * nid * per) // per
 
 
 def _faces():
@@ -292,3 +329,25 @@ def test_sharded_adaptive_start_tier_matches_fixed_chain():
     oracle_i = np.argsort(O.pairwise("EuclideanDistance", *_crowded()[:2]), axis=1, kind="stable")[:, :2]
     got = res[0]["1"][1][0][1]
     assert (np.sort(got, 1) == np.sort(oracle_i, 1)).mean() > 0.99   # exact top-2 (up to oracle near-ties)
+
+
+@pytest.mark.timeout(600)
+def test_sharded_prefix_tier_shared_choice_and_pruned_merge(sharded):
+    """Round 6 (VERDICT r5 do-this #6): shards that alone would pick different prefix
+    lengths pick the same one (all-reduced block sums), both start the batch at f6p, the global top-k
+    equals the oracle's; the pruned split merge of the prefix tier (exact d^2 of each rank's first k
+    candidates as the upper bounds) gives the plain merge's results and certificate counts while the
+    rank that does not hold a query's identity skips its re-rank."""
+    Q, G, _ = _split_prefix_data()
+    r0, r1 = sharded[0]["prefix"], sharded[1]["prefix"]
+    assert {r0[3], r1[3]} == {0, 1}, (r0[3], r1[3])                 # the shards' own choices differ
+    assert r0[2] == r1[2] == 1, (r0[2], r1[2])                       # the shared choice
+    assert r0[4] == r1[4] == "f6p" and r0[5] == r1[5], (r0[4:], r1[4:])
+    assert np.array_equal(r0[1], r1[1]) and np.array_equal(r0[0], r1[0])
+    _check_search("EuclideanDistance", Q, G, r0[0], r0[1], K)
+    for rank in (0, 1):
+        pd, pi, pc, rd, ri, rc, skipped = sharded[rank]["prefix_pruned"]
+        assert np.array_equal(pi, ri) and np.array_equal(pd, rd)
+        assert list(pc) == list(rc)
+        assert skipped >= 60, (rank, skipped)                        # ~half the queries live on the other rank
+    _check_search("EuclideanDistance", Q, G, sharded[0]["prefix_pruned"][3], sharded[0]["prefix_pruned"][4], K)

@@ -148,7 +148,8 @@ def test_sieve_complete_vs_exact_scores_headline_shape(w, tier):
     sd = torch.from_numpy(s).to(dev)
     thf = _key_float(theta.index_select(0, sd).cpu().numpy())
     cnt = count.index_select(0, sd).cpu().numpy()
-    assert np.all((cnt >= 16) & (cnt <= g.SIEVE_CAP)), cnt
+    # f6p: theta is the row sample's 2nd best key (SIEVE_RANK_PREFIX), so ~2 x 64 rows are kept, some fewer than 16
+    assert np.all((cnt >= (16 if ns is None else 2)) & (cnt <= g.SIEVE_CAP)), cnt
     nst = -(-d // 128)
     dm = d if ns is None else min(d, 128 * ns)          # the features the pass scores
     table = _e2m3_table(dev)
@@ -204,7 +205,7 @@ def test_sieve_complete_vs_exact_scores_headline_shape(w, tier):
         assert missing.size == 0, (j, s[j], missing[:10], len(need), cnt[j])
         wrong = np.intersect1d(np.concatenate(allowed_hi[j]), kept)
         assert wrong.size == 0, (j, s[j], wrong[:10])
-    assert n_must >= 16 * 64                                           # the test is not vacuous
+    assert n_must >= (16 if ns is None else 4) * 64                    # the test is not vacuous
 
 
 def _clustered(n_id, per, d, B, seed):

@@ -22,6 +22,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = os.path.join(ROOT, "gpurun_out", "prof")
 
 
+def sieve_engine(name):
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.sieve_engine(name)
+
+
 def counters(kname):
     agg = collections.defaultdict(list)
     for p in ("p1", "p2", "p3", "p4", "p5"):
@@ -59,7 +65,9 @@ def main():
                    "search": search,
                    "w": "trained" if "trained" in cfg.get("workload", "") else "random",
                    # the tier the timed steps started at (f6p: the prefix tier's pass)
-                   "tier": max((bench.get("start_tiers") or {"": 0}).items(), key=lambda t: t[1])[0] or search},
+                   "tier": max((bench.get("start_tiers") or {"": 0}).items(), key=lambda t: t[1])[0] or search,
+                   # the sieve kernel the bench's roofline names (bench.sieve_engine)
+                   "engine": sieve_engine(bench["roofline"].get("kernel"))},
         # bench.committed_traffic takes the newest summary of its config (file names do not order rounds)
         "measured_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
         "kernel": " + ".join(knames), "launches": min(v["launches"] for v in per.values()), "rocprof_avg_ns": avg_ns,
