@@ -176,7 +176,11 @@ def committed_traffic(cfg):
 
 
 class StepPipeline:
-    """The timed step's schedule over a sequence of query batches:
+    """The timed step's schedule over a sequence of query batches.  Default since round 6
+    (merge_at "after"): one kernel at a time, in the order sample pass s, sieve pass s, merge s-1 (side
+    stream, behind the sieve pass), preparation s+1 (main stream, behind that merge), with the host's
+    certificate read of batch s-1 (a sync of the side stream only) issued after preparation s+1 is queued.
+    merge_at "sieve" (rounds 3-5):
 
       main stream  tile pass of batch s (behind its preparation): its sample pass + thresholds, then
                    its sieve pass;
@@ -197,12 +201,21 @@ class StepPipeline:
 
     NBUF, NWS = 3, 2
 
-    def __init__(self, device, prep, tiles, merge, finish, overlap=True, prep_behind=None):
+    def __init__(self, device, prep, tiles, merge, finish, overlap=True, prep_behind=None, merge_at=None):
         self.prep_fn, self.tiles_fn, self.merge_fn, self.finish_fn = prep, tiles, merge, finish
         # prep_behind "tiles" (default): batch s+1's preparation waits for tile pass s and runs alone;
         # "sample": it waits only for sample pass s and shares the chip with sieve pass s
         self.prep_behind = prep_behind or os.environ.get("OFR_BENCH_PREP", "tiles")
         assert self.prep_behind in ("tiles", "sample"), self.prep_behind
+        # merge_at "after" (default, round 6): merge s-1 behind sieve pass s, then batch s+1's preparation
+        # on the main stream behind that merge -- every kernel alone on the chip, and the host's certificate
+        # read (side stream, up to the merge) never leaves the GPU without queued work.  Neither the
+        # persistent prefix pass (two workgroups per CU) nor the projection leaves a CU room for merge
+        # blocks: run beside the sieve pass, the merge held its CUs and the pass (whose work items are
+        # dealt statically) ended with its last workgroups: 0.83 -> 1.59 ms for 0.47 ms of merge
+        # (profiles/r06_merge_at_ab.txt).  "sieve": merge s-1 under sieve pass s (rounds 3-5).
+        self.merge_at = merge_at or os.environ.get("OFR_BENCH_MERGE", "after")
+        assert self.merge_at in ("after", "sieve"), self.merge_at
         self.main = torch.cuda.current_stream(device)
         self.side = torch.cuda.Stream(device=device) if overlap else self.main
         self.ws = [Workspace() for _ in range(self.NWS)]
@@ -210,6 +223,7 @@ class StepPipeline:
         self.ev_merged = [torch.cuda.Event() for _ in range(self.NWS)]    # workspace's merge done (side)
         self.ev_tiles = torch.cuda.Event()                                # latest tile pass done (main)
         self.ev_sample = torch.cuda.Event()                               # latest sample pass done (main)
+        self.ev_done = [torch.cuda.Event() for _ in range(self.NBUF)]     # buffer's fallback done (side)
         # the side stream starts behind everything the main stream has queued (gallery and tier builds,
         # the query images, buffer fills): an unrecorded event is no dependency, and once the caching
         # allocator stops calling hipMalloc (which synchronises) nothing else would order the first
@@ -217,14 +231,14 @@ class StepPipeline:
         if self.side is not self.main:
             self.side.wait_stream(self.main)
 
-    def _prep(self, s, ev):
-        with torch.cuda.stream(self.side):
+    def _prep(self, s, ev, stream=None):
+        with torch.cuda.stream(stream or self.side):
             if ev:
                 ev[0].record()
             self.prep_fn(s % self.NBUF)
             if ev:
                 ev[1].record()
-            self.ev_ready[s % self.NBUF].record(self.side)
+            self.ev_ready[s % self.NBUF].record(stream or self.side)
 
     def _finish(self, s):
         with torch.cuda.stream(self.side):
@@ -233,7 +247,8 @@ class StepPipeline:
     def _merge(self, s, ev):
         j, w = s % self.NBUF, s % self.NWS
         with torch.cuda.stream(self.side):
-            self.side.wait_event(self.ev_sample)            # behind the next batch's sample pass
+            # behind the next batch's sample pass ("sieve") or its whole tile pass ("after")
+            self.side.wait_event(self.ev_sample if self.merge_at == "sieve" else self.ev_tiles)
             if ev:
                 ev[5].record()
             self.merge_fn(j, self.ws[w])
@@ -258,12 +273,24 @@ class StepPipeline:
             self.ev_sample.record(self.main)
             if ev[s]:
                 ev[s][6].record(self.main)
-            if s >= 1:                                      # merge s-1 under sieve pass s
+            if s >= 1 and self.merge_at == "sieve":         # merge s-1 under sieve pass s
                 self._merge(s - 1, ev[s - 1])
             self.tiles_fn(j, self.ws[w], "sieve")
             if ev[s]:
                 ev[s][2].record(self.main)
             self.ev_tiles.record(self.main)
+            if self.merge_at == "after":
+                if s >= 1:                                  # merge s-1 behind tile pass s
+                    self._merge(s - 1, ev[s - 1])
+                if s + 1 < steps:                           # preparation s+1 behind that merge, on main
+                    if s >= 1:
+                        self.main.wait_event(self.ev_merged[(s - 1) % self.NWS])
+                    self.main.wait_event(self.ev_done[(s + 1) % self.NBUF])   # its buffer's fallback done
+                    self._prep(s + 1, ev[s + 1], stream=self.main)
+                if s >= 1:
+                    res = self._finish(s - 1)
+                    self.ev_done[(s - 1) % self.NBUF].record(self.side)
+                continue
             if s >= 1:
                 res = self._finish(s - 1)
             self.side.wait_event(self.ev_tiles if self.prep_behind == "tiles" else self.ev_sample)
@@ -272,6 +299,7 @@ class StepPipeline:
         if steps:
             self._merge(steps - 1, ev[steps - 1])
             res = self._finish(steps - 1)
+            self.ev_done[(steps - 1) % self.NBUF].record(self.side)
         # the caller's stream sees everything the side stream did
         self.main.wait_stream(self.side)
         return res

@@ -1,7 +1,8 @@
 """bench.py's StepPipeline (the timed step's schedule): the tile pass of batch s on the
-main stream (sample pass, then sieve pass), batch s-1's merge on a side stream behind sample pass s,
-batch s+1's preparation behind tile pass s, batch s-1's certificate read and fallback tiers enqueued
-before batch s+1's preparation, three query buffers and two search workspaces.  Every batch's final top-k must equal the one-shot search of the same batch
+main stream (sample pass, then sieve pass), batch s-1's merge on a side stream behind sample pass s
+(merge_at "sieve") or behind the whole tile pass s (merge_at "after", with batch s+1's preparation on
+the main stream behind that merge), batch s-1's certificate read and fallback tiers, three query
+buffers and two search workspaces.  Every batch's final top-k must equal the one-shot search of the same batch
 (quantize, ofr_knn_f6 phases 1+2, fallback tiers) on the default stream -- bit for bit: the schedule
 changes only which stream runs a kernel and which buffer it reads."""
 import os
@@ -31,10 +32,12 @@ def _setup(noise, N=20_000, d=512, side=32, per=10, B=512, batches=5):
     return P, g, X
 
 
+@pytest.mark.parametrize("merge_at", ["after", "sieve"])
 @pytest.mark.parametrize("noise", [12.0, 40.0])
-def test_step_pipeline_matches_one_shot(noise):
+def test_step_pipeline_matches_one_shot(noise, merge_at):
     """noise 40: crowded identities, so the fallback tiers run inside finish() while the next tile
-    pass and the next preparation are in flight."""
+    pass and the next preparation are in flight.  merge_at "after" (the default since round 6): the
+    merge behind the tile pass and the next preparation on the main stream behind it."""
     from bench import StepPipeline
     P, g, X = _setup(noise)
     k, dev = 3, torch.device("cuda", 0)
@@ -76,7 +79,7 @@ def test_step_pipeline_matches_one_shot(noise):
         got.append((b["batch"], b["out"][0].clone(), b["out"][1].clone()))
         return b["out"]
 
-    pipe = StepPipeline(dev, prep, tiles, merge, finish)
+    pipe = StepPipeline(dev, prep, tiles, merge, finish, merge_at=merge_at)
     assert pipe.side is not pipe.main
     pipe.run(len(X))
     torch.cuda.synchronize()
