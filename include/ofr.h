@@ -248,7 +248,7 @@ int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int6
 /* Prefix tier f6p: ofr_knn_f6_sampled whose sample and sieve passes score only the
  * first pstages 128-feature stages of the same tiles (1 <= pstages <= ceil(d / 128)).  aux / saux are
  * the PREFIX terms |g_m|^2 of the rows and of the row sample (ofr_row_aux over the first
- * min(d, 128 pstages) features, saux[j] = aux[64 j]); gmax is the f6 tier's.  A row's squared distance
+ * min(d, 128 pstages) features, saux[j] = aux[64 j]); Gt/gscale/gmax: see below.  A row's squared distance
  * is at least that of its first features, so the certificate and the bound (-> the merge's exact fp64
  * re-rank of the full rows) hold as for ofr_knn_f6; on features whose discriminating variance sits in
  * the leading columns (Fisherfaces / Eigenfaces output, eigenvalues descending) it certifies at a
@@ -258,6 +258,21 @@ int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int64_t B, int6
 int ofr_f6_quantize_rows_prefix(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int pstages,
                                 void* tiles, size_t tiles_bytes, float* scale, double* stats,
                                 const uint8_t* bscale);
+/* The prefix tier's OWN gallery tiles (round 6): the first pstages stages of each row in the f6 tiled layout of
+ * pstages stages per 256-row panel (ofr_f6p_tiles_bytes(R, pstages) bytes), quantized from the first
+ * min(d, 128 pstages) features with power-of-two row scales (exact in the MFMA's E8M0 operand scale: the pass
+ * folds 2 s_g and -|g_m|^2 into the MFMA) and their prefix stats; ofr_f6p_quantize_rows also writes the maxima
+ * of those stats and of paux (the prefix terms |g_m|^2, ofr_row_aux): the f6p tier's gmax.  _at: rows
+ * [row0, row0 + R) of a tile buffer (append).                                                              */
+size_t ofr_f6p_tiles_bytes(int64_t R, int pstages);
+int ofr_f6p_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int64_t row0,
+                             int pstages, void* tiles, size_t tiles_bytes, float* scale, double* stats,
+                             const uint8_t* bscale);
+int ofr_f6p_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int pstages, void* tiles,
+                          size_t tiles_bytes, float* scale, double* stats, const float* paux, double* maxima,
+                          const uint8_t* bscale);
+/* ofr_knn_f6p_sampled (and ofr_knn_f6p_merge_pruned): Gt, gscale, gmax are the prefix tier's own gallery tiles,
+ * scales and maxima above (round 6; round 5 read the f6 tiles); St / sscale: the f6 tier's row sample.     */
 int ofr_knn_f6p_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                         const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg, int64_t d,
                         const void* Gt, const float* gscale, const float* aux, const double* gmax, int k,
@@ -563,6 +578,11 @@ typedef struct ofr_knn_shard {
   const float* paux;        /* the shard rows' prefix terms |g_m|^2 (ofr_row_aux over min(d, 128 pstages)) */
   const float* spaux;       /* the row sample's prefix terms */
   int64_t* prefix_open;     /* optional out [1] (shard 0): queries the prefix tier left open */
+  /* the prefix tier's own gallery tiles of the shard's rows (ofr_f6p_quantize_rows: pstages stages per
+     panel, power-of-two row scales), their row scales and maxima -- needed when pstages > 0 (round 6) */
+  const void* Gtp;
+  const float* gscalep;
+  const double* gmaxp;
 } ofr_knn_shard;
 int ofr_comm_init_all(int ndev, const int* devices, ofr_comm** comm);
 int ofr_comm_destroy(ofr_comm* comm);

@@ -317,10 +317,16 @@ class FloatGallery:
                 call("ofr_f6_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, ptr(g["Gs"]),
                      g["Gs"].numel(), ptr(g["scale"]), ptr(g["stats"]), ptr(self.bscale))
                 self._sample_rows(g, N0, N1)
-            elif tier == "f6p":                        # tiles shared with f6 (extended above): the prefix terms
+            elif tier == "f6p":                        # its own compact tiles + the prefix terms (the row sample:
                 call("ofr_row_aux", stream(), _lib.METRIC_EUCLIDEAN, ptr(self._Gbuf[N0:]), n, g["pdim"], self.ld,
-                     ptr(g["paux"][N0:]))
+                     ptr(g["paux"][N0:]))              # the f6 tier's, extended above)
+                call("ofr_f6p_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, g["pst"],
+                     ptr(g["Gs"]), g["Gs"].numel(), ptr(g["scale"]), ptr(g["stats"]), ptr(self.bscale))
                 g["spaux"] = self._prefix_sample_aux(g["paux"], N1)
+                g6 = self.q8["f6"]
+                g["St"], g["sscale"] = g6["St"], g6["sscale"]
+                call("ofr_q8_maxima", stream(), ptr(g["stats"]), ptr(g["paux"]), N1, ptr(g["gmax"]))
+                continue
             elif tier == "f6x2":                       # the first slice is the f6 tier's, extended above
                 call("ofr_f6x2_quantize_rows_at", stream(), ptr(self.G[N0:]), n, self.d, self.ld, N0, None,
                      ptr(g["Gs2"]), g["Gs2"].numel(), ptr(g["scale"]), ptr(g["stats"]), ptr(self.bscale))
@@ -568,15 +574,23 @@ class FloatGallery:
             st = torch.empty((cap, 3), dtype=torch.float64, device=dev_)
             gmax = torch.empty(4, dtype=torch.float64, device=dev_)
             extra = {}
-            if tier == "f6p":                     # the f6 tier's tiles, sample and maxima + the prefix terms
+            if tier == "f6p":
+                # its own compact tiles of the first pst stages (ofr_f6p_quantize_rows: power-of-two row scales,
+                # prefix stats, maxima of those and of the prefix terms) and the f6 tier's row sample (St, sscale)
+                # for the thresholds; built after f6, so append extends the sample first
                 g6 = self._tier_gallery("f6")
-                pdim = min(self.d, 128 * self.prefix_stages())
+                pst = self.prefix_stages()
+                pdim = min(self.d, 128 * pst)
                 if pdim < 1:
                     raise RuntimeError("f6p: this gallery has no prefix tier (prefix_stages() == 0)")
                 paux = torch.empty(cap, dtype=torch.float32, device=dev_)
                 call("ofr_row_aux", stream(), _lib.METRIC_EUCLIDEAN, ptr(self.G), self.N, pdim, self.ld, ptr(paux))
-                self.q8[tier] = dict(g6, paux=paux, pdim=pdim, pst=self.prefix_stages(),
-                                     spaux=self._prefix_sample_aux(paux, self.N))
+                nbytes = _lib.load().ofr_f6p_tiles_bytes(cap, pst)
+                Gp = torch.empty(nbytes, dtype=torch.uint8, device=dev_)
+                call("ofr_f6p_quantize_rows", stream(), ptr(self.G), self.N, self.d, self.ld, pst, ptr(Gp), nbytes,
+                     ptr(gs), ptr(st), ptr(paux), ptr(gmax), ptr(self._block_scales()))
+                self.q8[tier] = dict(Gs=Gp, scale=gs, stats=st, gmax=gmax, ld=0, paux=paux, pdim=pdim, pst=pst,
+                                     spaux=self._prefix_sample_aux(paux, self.N), St=g6["St"], sscale=g6["sscale"])
                 return self.q8[tier]
             if tier == "f6":
                 lib = _lib.load()

@@ -71,6 +71,10 @@ SIGNATURES = {
                                    c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                    c_vp, c_sz, c_vp]),
     "ofr_f6_quantize_rows_prefix": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_sz, c_vp, c_vp, c_vp]),
+    "ofr_f6p_tiles_bytes": (c_sz, [c_i64, c_int]),
+    "ofr_f6p_quantize_rows_at": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, c_sz, c_vp, c_vp, c_vp]),
+    "ofr_f6p_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp]),
     "ofr_knn_f6p_sampled": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                     c_vp, c_sz, c_vp, c_int]),
@@ -161,7 +165,7 @@ class KnnShard(ctypes.Structure):
                 ("gmax8", c_vp), ("tier_counts", c_vp), ("St", c_vp), ("Ns", c_i64), ("sscale", c_vp), ("saux", c_vp),
                 ("St2", c_vp), ("bscale", c_vp),
                 ("pstages", c_int), ("Qtp", c_vp), ("qscalep", c_vp), ("qstatsp", c_vp), ("paux", c_vp),
-                ("spaux", c_vp), ("prefix_open", c_vp)]
+                ("spaux", c_vp), ("prefix_open", c_vp), ("Gtp", c_vp), ("gscalep", c_vp), ("gmaxp", c_vp)]
 
 
 class OfrError(RuntimeError):

@@ -345,8 +345,10 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
   for (int p = 0; p < P; ++p) {
     const ofr_knn_shard& s = shards[p];
     OFR_CHECK_ARG(s.pstages == pst, "ofr_knn_sharded: pstages differs between shards (choose it from all-reduced sums)");
-    OFR_CHECK_ARG(pst == 0 || (s.Qtp && s.qscalep && s.qstatsp && s.paux && s.spaux && s.St),
-                  "ofr_knn_sharded: the prefix tier needs Qtp, qscalep, qstatsp, paux, spaux and the row sample St");
+    OFR_CHECK_ARG(pst == 0 || (s.Qtp && s.qscalep && s.qstatsp && s.paux && s.spaux && s.St && s.Gtp && s.gscalep &&
+                               s.gmaxp),
+                  "ofr_knn_sharded: the prefix tier needs Qtp, qscalep, qstatsp, paux, spaux, its gallery tiles Gtp, "
+                  "gscalep, gmaxp and the row sample St");
   }
   OFR_CHECK_ARG(pst >= 0 && pst <= cdiv(d, 128), "ofr_knn_sharded: pstages must be in [0, ceil(d / 128)]");
   const bool prefix = pst > 0 && pst < cdiv(d, 128);   // a prefix of every stage is the fp6 tier itself
@@ -361,12 +363,12 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
     char* ws = (char*)s.workspace;
     int rc;
     if (prefix) {
-      rc = ofr_knn_f6p_sampled(s.stream, 1, s.Q, B, s.ldq, s.Qtp, s.qscalep, s.qstatsp, s.G, s.N, s.ldg, d, s.Gt,
-                               s.gscale, s.paux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr, s.St, s.Ns,
+      rc = ofr_knn_f6p_sampled(s.stream, 1, s.Q, B, s.ldq, s.Qtp, s.qscalep, s.qstatsp, s.G, s.N, s.ldg, d, s.Gtp,
+                               s.gscalep, s.paux, s.gmaxp, k, s.index_base, nullptr, nullptr, nullptr, nullptr, s.St, s.Ns,
                                s.sscale, s.spaux, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N), s.bscale, pst);
       if (rc) return rc;
-      rc = ofr_knn_f6p_merge_pruned(s.stream, 1, s.Q, B, s.ldq, s.Qtp, s.qscalep, s.qstatsp, s.G, s.N, s.ldg, d, s.Gt,
-                                    s.gscale, s.paux, s.gmax, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
+      rc = ofr_knn_f6p_merge_pruned(s.stream, 1, s.Q, B, s.ldq, s.Qtp, s.qscalep, s.qstatsp, s.G, s.N, s.ldg, d, s.Gtp,
+                                    s.gscalep, s.paux, s.gmaxp, k, s.index_base, nullptr, nullptr, nullptr, nullptr,
                                     (double*)(ws + L[p].ubl), ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N), pst);
       if (rc) return rc;
       continue;
@@ -415,7 +417,7 @@ extern "C" int ofr_knn_sharded(ofr_comm* c, const ofr_knn_shard* shards, int64_t
                        (const double*)(ws + L[p].ubr), P, B, k, ub);
     OFR_LAUNCH_CHECK("kth_bound_kernel");
     int rc = prefix ? ofr_knn_f6p_merge_pruned(s.stream, 2, s.Q, B, s.ldq, s.Qtp, s.qscalep, s.qstatsp, s.G, s.N,
-                                               s.ldg, d, s.Gt, s.gscale, s.paux, s.gmax, k, s.index_base, ld_, li_,
+                                               s.ldg, d, s.Gtp, s.gscalep, s.paux, s.gmaxp, k, s.index_base, ld_, li_,
                                                lc_, lb_, ub, ws + L[p].knn, ofr_knn_f6_workspace_bytes(B, s.N), pst)
                     : ofr_knn_f6_merge_pruned(s.stream, 2, s.Q, B, s.ldq, s.Qt, s.qscale, s.qstats, s.G, s.N, s.ldg, d,
                                               s.Gt, s.gscale, s.aux, s.gmax, k, s.index_base, ld_, li_, lc_, lb_, ub,

@@ -523,19 +523,23 @@ struct EngineW {
   };
 
   template <int W, int NSEG = 1>
+  // gnst: stages per panel of the gallery tiles when they differ from the queries' (the prefix tier's
+  // compact gallery tiles, round 6; < 0: nst)
   static __device__ __forceinline__ void feed_init(Feed& f, const char* G, int64_t N, const char* Q, int64_t qp,
                                                    int64_t nst, int64_t gt, const char* G2 = nullptr,
-                                                   const char* Q2 = nullptr, const uint32_t* bs = nullptr) {
+                                                   const char* Q2 = nullptr, const uint32_t* bs = nullptr,
+                                                   int64_t gnst = -1) {
     f.bs = bs;
     const int64_t h0 = 3 * gt, p0 = h0 >> 1;
-    const int64_t pb = nst * (int64_t)PANEL;                 // bytes per 256-row panel
+    const int64_t qb = nst * (int64_t)PANEL;                 // bytes per 256-row query panel
+    const int64_t pb = (gnst < 0 ? nst : gnst) * (int64_t)PANEL;   // ... gallery panel
     const int64_t rem = panels(N) * pb - p0 * pb;
     const int64_t rec = rem < 2 * pb ? rem : 2 * pb;         // reads past the gallery return zeros
     f.rg = __builtin_amdgcn_make_buffer_rsrc((void*)(G + p0 * pb), 0, (int)rec, 0x00020000);
-    f.rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * pb), 0, (int)pb, 0x00020000);
+    f.rq = __builtin_amdgcn_make_buffer_rsrc((void*)(Q + qp * qb), 0, (int)qb, 0x00020000);
     if constexpr (NSEG == 3) {
       f.rg2 = __builtin_amdgcn_make_buffer_rsrc((void*)(G2 + p0 * pb), 0, (int)rec, 0x00020000);
-      f.rq2 = __builtin_amdgcn_make_buffer_rsrc((void*)(Q2 + qp * pb), 0, (int)pb, 0x00020000);
+      f.rq2 = __builtin_amdgcn_make_buffer_rsrc((void*)(Q2 + qp * qb), 0, (int)qb, 0x00020000);
     }
 #pragma unroll
     for (int j = 0; j < GPW; ++j) {

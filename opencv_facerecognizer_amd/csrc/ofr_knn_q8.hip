@@ -74,6 +74,9 @@ struct TileArgs {
   // stages run per segment: nk / NSEG, or fewer -- the prefix tier f6p scores only the first nkp
   // stages of the tiles (nk stays their layout)
   int nkp;
+  // stages per 256-row panel of the GALLERY tiles the prefix passes read (round 6: the prefix tier's own
+  // compact tiles, ofr_f6p_quantize_rows, hold only its nkp stages; every other pass: nk)
+  int gnk;
 };
 
 // ---- keys of the tile epilogue (ofr_keys.h: order-preserving u32 keys, med3 key lists) ----
@@ -365,7 +368,7 @@ __device__ __forceinline__ void f6w_main(const TileArgs& p, int64_t g0, int64_t 
   E::Feed f;
   E::feed_init<W, NSEG>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), q0 / f6t::TQ,
                         p.nk / NSEG, g0 / E::TGW, reinterpret_cast<const char*>(p.G2),
-                        reinterpret_cast<const char*>(p.Q2), p.bs);
+                        reinterpret_cast<const char*>(p.Q2), p.bs, p.gnk / NSEG);
   E::mainloop<W, NSEG>(f, p.nkp, acc);
 }
 
@@ -542,7 +545,7 @@ __device__ __forceinline__ void mfma0a(const f6t::i32x6& a, const f6t::i32x6& b,
 template <int W, int NSP>
 __device__ __forceinline__ void copy_gallery(const TileArgs& p, int64_t gt) {
   E::Feed f;
-  E::feed_init<W, 1>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), 0, p.nk, gt);
+  E::feed_init<W, 1>(f, reinterpret_cast<const char*>(p.G), p.N, reinterpret_cast<const char*>(p.Q), 0, p.gnk, gt);
 #pragma unroll
   for (int s = 0; s < NSP; ++s) {
     const uint32_t so = GS + s * E::GSLOT, ko = (uint32_t)s * f6t::PANEL;
@@ -943,7 +946,7 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 // wave's pieces of the stage-0 image of gallery panel gt (24 pieces of 1 KiB) into GT
 __device__ __forceinline__ void copy_gtile(const TileArgs& p, int64_t gt, int wave, uint32_t lane) {
-  const int64_t pb = (int64_t)p.nk * f6t::PANEL;
+  const int64_t pb = (int64_t)p.gnk * f6t::PANEL;
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(reinterpret_cast<const char*>(p.G) + gt * pb), 0, f6t::PANEL, 0x00020000);
 #pragma unroll
@@ -1053,12 +1056,24 @@ __global__ void prefix_tables_kernel(const uint32_t* theta, const float* qscale,
 }
 
 // OFR_PP_PROBE (probe builds only, tools/probe_prefix_pass.py): bit 1 no bucket flush, bit 2 no compares
-// (the accumulators kept alive), bit 4 no MFMAs (zero accumulators)
+// (the accumulators kept alive), bit 4 no MFMAs (zero accumulators), bit 8 no hit path (the compares' hit
+// masks computed and dropped)
 #ifndef OFR_PP_PROBE
 #define OFR_PP_PROBE 0
 #endif
 // p.ntg = ceil(N / 256) gallery tiles; steps of 128 queries, ceil(B / 128); item w = (tile w / ngrp, steps
 // [qg (w % ngrp), ...)).  qtab: prefix_tables_kernel's table.
+//
+// FOLD (round 6, the default engine 3): the gallery rows' power-of-two scales (the prefix tier's own tiles,
+// ofr_f6p_quantize_rows) join the gallery operand's E8M0 scale with the factor 2 (per lane: its A row), and
+// -|g_m|^2 is the MFMA's accumulator input (per lane: its 4 output rows, one register set per row block for
+// every query column), so the MFMA writes D = 2 s_g s_q (q~.g~) - |g_m|^2 = -(the coarse score) itself:
+// the compares are one max per score (v_max3) and one compare per query column, against -theta, instead of
+// an fma and a min per score (tools/probe_prefix_pass.py: the compares and their hit path were 0.55 of the
+// pass's 0.84 ms).  The hit path tests the 16 rows of a flagged column block row by row with one ballot
+// each (no per-lane select chains).  The scores differ from FOLD = false's fma(-2 s_g, acc, aux) by the
+// accumulation order of one fp32 rounding: the merge's bound for the prefix tier carries 2^-14 aux for it.
+template <bool FOLD>
 __global__ void __launch_bounds__(256, 2) prefix_pass_kernel(TileArgs p, const uint2* qtab, int64_t qg) {
   using E = f6t::EngineW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1096,6 +1111,11 @@ __global__ void __launch_bounds__(256, 2) prefix_pass_kernel(TileArgs p, const u
   bool flushed = false;                // memory operations issued after the copies (vmcnt(1) at the top)
   pp::i32x8 A[4];
   const f6t::f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  // FOLD, per item: the accumulator inputs (-|g_m|^2 of the lane's output rows of each row block; -inf past
+  // N), the gallery operand scales (block byte + e_g + 1 of the lane's A row) and the lane's valid rows
+  f6t::f32x4 Cin[4];
+  int sa[4];
+  uint32_t vmask = 0;
   for (;;) {
     const int64_t gt = item_gt(w), s0 = item_s0(w), s1 = item_s1(w), wn = w + gridDim.x;
     const bool more_items = wn < items;
@@ -1115,6 +1135,25 @@ __global__ void __launch_bounds__(256, 2) prefix_pass_kernel(TileArgs p, const u
         for (int i = 0; i < 4; ++i) {
           const uint32_t r0 = (uint32_t)(wave * 64 + 16 * i);
           A[i] = pp::frag8(gbas.p0 + r0 * 16, ((i & 1) ? gbas.p1o : gbas.p1e) + r0 * 8);
+        }
+        if constexpr (FOLD) {
+          const uint32_t gtb = pp::GTB + (uint32_t)gb * 2048u;
+          vmask = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 a4 = pp::lds_f4(gtb + (uint32_t)(wave * 64 + 16 * i + g4) * 4u);
+            const int rb = wave * 64 + 16 * i + g4;
+            Cin[i][0] = rb + 0 < nvalid ? -a4.x : -__builtin_inff();
+            Cin[i][1] = rb + 1 < nvalid ? -a4.y : -__builtin_inff();
+            Cin[i][2] = rb + 2 < nvalid ? -a4.z : -__builtin_inff();
+            Cin[i][3] = rb + 3 < nvalid ? -a4.w : -__builtin_inff();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) vmask |= rb + r < nvalid ? 1u << (4 * i + r) : 0u;
+            // the lane's A row wave * 64 + 16 i + r16: its scale 2^e (0 past N: e = 0)
+            const uint32_t sb = pp::lds_u32(gtb + 1024u + (uint32_t)(wave * 64 + 16 * i + r16) * 4u);
+            const int eg = sb != 0u ? (int)((sb >> 23) & 0xffu) - 127 : 0;
+            sa[i] = scs + eg + 1;   // block byte (64..127) + e_g (-64..64) + 1: in [1, 192]
+          }
         }
         if (more_items) gpend = true;
       } else if (gpend) {   // every wave read its fragments of this item's tile before this step's barrier
@@ -1143,95 +1182,171 @@ __global__ void __launch_bounds__(256, 2) prefix_pass_kernel(TileArgs p, const u
           if constexpr (OFR_PP_PROBE & 4) {
             acc[i][c] = zero;
             asm volatile("" :: "v"(b), "v"(A[i]), "v"(sbq));
+          } else if constexpr (FOLD) {
+            acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], b, Cin[i], 2, 2, 0, sa[i], 0, sbq);
           } else {
             acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], b, zero, 2, 2, 0, scs, 0, sbq);
           }
         }
       }
-      // compares: per query column the min of its 16 rows' scores against theta
-      const uint32_t gta = pp::GTB + (uint32_t)gb * 2048u + (uint32_t)(wave * 64 + g4) * 4u;   // aux; scale at + 1024
-      float av[4][4], tp[4][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float4 a4 = pp::lds_f4(gta + 64u * i);
-        const float4 s4 = pp::lds_f4(gta + 1024u + 64u * i);
-        av[i][0] = a4.x; av[i][1] = a4.y; av[i][2] = a4.z; av[i][3] = a4.w;
-        tp[i][0] = s4.x + s4.x; tp[i][1] = s4.y + s4.y; tp[i][2] = s4.z + s4.z; tp[i][3] = s4.w + s4.w;
-      }
-      uint32_t hitc = 0;
-      if constexpr (OFR_PP_PROBE & 2) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) asm volatile("" :: "v"(acc[i][c]));
-      } else
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const float th = __uint_as_float(pp::lds_u32(qta + c * 128u));
-        float m[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float x0 = __builtin_fmaf(-tp[i][0], acc[i][c][0], av[i][0]);
-          const float x1 = __builtin_fmaf(-tp[i][1], acc[i][c][1], av[i][1]);
-          const float x2 = __builtin_fmaf(-tp[i][2], acc[i][c][2], av[i][2]);
-          const float x3 = __builtin_fmaf(-tp[i][3], acc[i][c][3], av[i][3]);
-          m[i] = fminf(fminf(x0, x1), fminf(x2, x3));
-        }
-        const float mn = fminf(fminf(m[0], m[1]), fminf(m[2], m[3]));
-        hitc |= !(mn > th) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
-      }
       uint32_t ncnt = 0;
-      if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform; ~2 kept pairs per step and wave on gallery data
-        // the scores again, from laundered row terms: the compiler would otherwise keep all 128 scores of the
-        // pass above alive for this rare path (common subexpressions)
+      if constexpr (FOLD) {
+        // compares: per query column the max of its 16 rows' D = -score against -theta (NaN theta: "keep
+        // every row", passes); v_max3 trees
+        uint32_t hitc = 0;
+        if constexpr (OFR_PP_PROBE & 2) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int c = 0; c < 8; ++c)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(tp[i][r]), "+v"(av[i][r]));
+            for (int i = 0; i < 4; ++i) asm volatile("" :: "v"(acc[i][c]));
+        } else
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
           const float th = __uint_as_float(pp::lds_u32(qta + c * 128u));
-          const int ql = c * 16 + r16;
-          const bool qok = (int64_t)s * pp::TQH + ql < p.B;
-          float sc[16];
-          uint32_t hm = 0;   // the lane's rows j = 4 i + r that pass
+          // IEEE maximum (NaN-propagating; no NaN here): v_maximum3_f32 straight on the MFMA results -- fmaxf
+          // (maxnum) would first quiet each of them (a v_max_f32 x, x per score)
+          auto mx3 = [](float a, float b, float d) {
+            return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), d);
+          };
+          const f6t::f32x4 &a0 = acc[0][c], &a1 = acc[1][c], &a2 = acc[2][c], &a3 = acc[3][c];
+          const float t0 = mx3(a0[0], a0[1], a0[2]), t1 = mx3(a0[3], a1[0], a1[1]), t2 = mx3(a1[2], a1[3], a2[0]);
+          const float t3 = mx3(a2[1], a2[2], a2[3]), t4 = mx3(a3[0], a3[1], a3[2]);
+          const float mx = __builtin_elementwise_maximum(mx3(t0, t1, t2), mx3(t3, t4, a3[3]));
+          hitc |= !(mx < -th) ? (1u << c) : 0u;
+        }
+        if constexpr (OFR_PP_PROBE & 8) {
+          asm volatile("" ::"v"(hitc));
+          hitc = 0;
+        }
+        if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform; ~1 kept pair per step and wave on gallery data
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int c = 0; c < 8; ++c) {
+            if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
+            const float nth = -__uint_as_float(pp::lds_u32(qta + c * 128u));
+            // lane-derived payloads from a laundered lane index: computed from threadIdx.x they are loop
+            // invariants, and the compiler hoisted all 128 (column, row) payloads out of the loops and
+            // spilled them (531 VGPRs)
+            uint32_t lid = lane;
+            asm volatile("" : "+v"(lid));
+            const int ql = c * 16 + (int)(lid & 15u);
+            const int rg4 = (int)(lid >> 4) * 4;
+            const uint32_t okm = (int64_t)s * pp::TQH + ql < p.B ? vmask : 0u;
+            // row by row: one compare and one ballot each; the passing lanes take consecutive list slots
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int j = 4 * i + r;
-              sc[j] = __builtin_fmaf(-tp[i][r], acc[i][c][r], av[i][r]);
-              const int row = wave * 64 + 16 * i + g4 + r;
-              hm |= (!(sc[j] > th) && row < nvalid && qok) ? (1u << j) : 0u;
-            }
-          // one kept row per lane and round, in row order: a wave-uniform loop of (on gallery data) one round
-          for (;;) {
-            const bool act = hm != 0u;
-            const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
-            if (mk == 0) break;   // uniform
-            const int j = act ? __builtin_ctz(hm) : 0;
-            hm &= hm - 1u;
-            float v = sc[0];
-#pragma unroll
-            for (int jj = 1; jj < 16; ++jj) v = j == jj ? sc[jj] : v;
-            const int row = wave * 64 + 16 * (j >> 2) + g4 + (j & 3);
-            if (act) {
-              const uint32_t kb = __float_as_uint(key_score(score_key(v, 0)));
-              const uint32_t slot =
-                  ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-              if (slot < (uint32_t)pp::HCAPW) {   // volatile integer address: no wait for the copies in flight
-                f6t::i32x2 e;
-                e[0] = (int)kb;
-                e[1] = (int)(((uint32_t)ql << 9) | (uint32_t)row);
-                *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
-              } else {   // the list is full (small galleries keep a large share): straight to the bucket
-                const int64_t q = (int64_t)s * pp::TQH + ql;
-                const int bs = atomicAdd(p.count + q, 1);
-                if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
+            for (int j = 0; j < 16; ++j) {
+              const float v = acc[j >> 2][c][j & 3];
+              const bool pass = !(v < nth) && (okm & (1u << j)) != 0u;
+              const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+              if (mk == 0) continue;   // uniform
+              if (pass) {
+                const uint32_t kb = __float_as_uint(key_score(score_key(-v, 0)));
+                const int row = wave * 64 + 16 * (j >> 2) + rg4 + (j & 3);
+                const uint32_t slot = ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                if (slot < (uint32_t)pp::HCAPW) {   // volatile integer address: no wait for the copies in flight
+                  f6t::i32x2 e;
+                  e[0] = (int)kb;
+                  e[1] = (int)(((uint32_t)ql << 9) | (uint32_t)row);
+                  *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
+                } else {   // the list is full (small galleries keep a large share): straight to the bucket
+                  const int64_t q = (int64_t)s * pp::TQH + ql;
+                  const int bs = atomicAdd(p.count + q, 1);
+                  if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
+                }
               }
+              ncnt += (uint32_t)__builtin_popcountll(mk);
             }
-            ncnt += (uint32_t)__builtin_popcountll(mk);
+          }
+        }
+      } else {
+        // compares: per query column the min of its 16 rows' scores against theta
+        const uint32_t gta = pp::GTB + (uint32_t)gb * 2048u + (uint32_t)(wave * 64 + g4) * 4u;   // aux; scale at + 1024
+        float av[4][4], tp[4][4];
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 a4 = pp::lds_f4(gta + 64u * i);
+          const float4 s4 = pp::lds_f4(gta + 1024u + 64u * i);
+          av[i][0] = a4.x; av[i][1] = a4.y; av[i][2] = a4.z; av[i][3] = a4.w;
+          tp[i][0] = s4.x + s4.x; tp[i][1] = s4.y + s4.y; tp[i][2] = s4.z + s4.z; tp[i][3] = s4.w + s4.w;
+        }
+        uint32_t hitc = 0;
+        if constexpr (OFR_PP_PROBE & 2) {
+  #pragma unroll
+          for (int c = 0; c < 8; ++c)
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("" :: "v"(acc[i][c]));
+        } else
+  #pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float th = __uint_as_float(pp::lds_u32(qta + c * 128u));
+          float m[4];
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float x0 = __builtin_fmaf(-tp[i][0], acc[i][c][0], av[i][0]);
+            const float x1 = __builtin_fmaf(-tp[i][1], acc[i][c][1], av[i][1]);
+            const float x2 = __builtin_fmaf(-tp[i][2], acc[i][c][2], av[i][2]);
+            const float x3 = __builtin_fmaf(-tp[i][3], acc[i][c][3], av[i][3]);
+            m[i] = fminf(fminf(x0, x1), fminf(x2, x3));
+          }
+          const float mn = fminf(fminf(m[0], m[1]), fminf(m[2], m[3]));
+          hitc |= !(mn > th) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
+        }
+          if constexpr (OFR_PP_PROBE & 8) {
+          asm volatile("" ::"v"(hitc));
+          hitc = 0;
+        }
+        if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform; ~2 kept pairs per step and wave on gallery data
+          // the scores again, from laundered row terms: the compiler would otherwise keep all 128 scores of the
+          // pass above alive for this rare path (common subexpressions)
+  #pragma unroll
+          for (int i = 0; i < 4; ++i)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(tp[i][r]), "+v"(av[i][r]));
+  #pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
+            const float th = __uint_as_float(pp::lds_u32(qta + c * 128u));
+            const int ql = c * 16 + r16;
+            const bool qok = (int64_t)s * pp::TQH + ql < p.B;
+            float sc[16];
+            uint32_t hm = 0;   // the lane's rows j = 4 i + r that pass
+  #pragma unroll
+            for (int i = 0; i < 4; ++i)
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int j = 4 * i + r;
+                sc[j] = __builtin_fmaf(-tp[i][r], acc[i][c][r], av[i][r]);
+                const int row = wave * 64 + 16 * i + g4 + r;
+                hm |= (!(sc[j] > th) && row < nvalid && qok) ? (1u << j) : 0u;
+              }
+            // one kept row per lane and round, in row order: a wave-uniform loop of (on gallery data) one round
+            for (;;) {
+              const bool act = hm != 0u;
+              const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
+              if (mk == 0) break;   // uniform
+              const int j = act ? __builtin_ctz(hm) : 0;
+              hm &= hm - 1u;
+              float v = sc[0];
+  #pragma unroll
+              for (int jj = 1; jj < 16; ++jj) v = j == jj ? sc[jj] : v;
+              const int row = wave * 64 + 16 * (j >> 2) + g4 + (j & 3);
+              if (act) {
+                const uint32_t kb = __float_as_uint(key_score(score_key(v, 0)));
+                const uint32_t slot =
+                    ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                if (slot < (uint32_t)pp::HCAPW) {   // volatile integer address: no wait for the copies in flight
+                  f6t::i32x2 e;
+                  e[0] = (int)kb;
+                  e[1] = (int)(((uint32_t)ql << 9) | (uint32_t)row);
+                  *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
+                } else {   // the list is full (small galleries keep a large share): straight to the bucket
+                  const int64_t q = (int64_t)s * pp::TQH + ql;
+                  const int bs = atomicAdd(p.count + q, 1);
+                  if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
+                }
+              }
+              ncnt += (uint32_t)__builtin_popcountll(mk);
+            }
           }
         }
       }
@@ -1303,7 +1418,7 @@ __global__ void __launch_bounds__(512) stream_kernel_f6(TileArgs p) {
     gtab[threadIdx.x][0] = ok ? p.aux[g] : 0.f;
     gtab[threadIdx.x][1] = ok ? p.gscale[g] : 0.f;
   }
-  const char* gpan = reinterpret_cast<const char*>(p.G) + gt * (int64_t)p.nk * f6t::PANEL;
+  const char* gpan = reinterpret_cast<const char*>(p.G) + gt * (int64_t)p.gnk * f6t::PANEL;
   const char* qpan = reinterpret_cast<const char*>(p.Q);
   const int nsteps = 2 * p.nkp, grow = wave * 32 + r32;   // nkp <= nk: the prefix tier's first stages
   f6t::f32x16 acc;
@@ -1667,7 +1782,10 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
     // dS(q): |S - S~| <= dS for every row, S = d^2 - |q|^2
     const double qa = p.qstats[q * 3 + 0], qe = p.qstats[q * 3 + 1], qt = p.qstats[q * 3 + 2];
     const double A = p.gmax[0], E = p.gmax[1], T = p.gmax[2], auxmax = p.gmax[3];
-    dS = 2.0 * (qa * E + qe * A + qe * E + qt * T) + 0x1p-20 * (auxmax + 2.0 * qa * A) + 2.0 * p.gamma * qa * A;
+    // the prefix tier's pass adds -aux inside the MFMA's fp32 accumulation (prefix_pass_kernel<true>: at most
+    // 129 roundings of partial sums <= aux + sum|products|, <= 129 2^-24 aux < 2^-17 aux) -- 2^-14 there
+    const double auxe = p.dpre > 0 ? 0x1p-14 : 0x1p-20;
+    dS = 2.0 * (qa * E + qe * A + qe * E + qt * T) + auxe * auxmax + 0x1p-20 * (2.0 * qa * A) + 2.0 * p.gamma * qa * A;
     dS = dS * (1.0 + 1e-6) + 1e-300;
     if (p.mode == 1) {
       if (threadIdx.x < KC) p.sel[q * KC + threadIdx.x] = lists[threadIdx.x];
@@ -2332,6 +2450,41 @@ extern "C" int ofr_f6_quantize_rows_prefix(void* stream, const float* X, int64_t
   return OFR_OK;
 }
 
+// The prefix tier's own gallery tiles (round 6): the first pstages 128-feature stages of each row in the
+// f6 tiled layout of pstages stages per panel (ofr_f6p_tiles_bytes), quantized from the first
+// dm = min(d, 128 pstages) features with a POWER-OF-TWO row scale s = 2^e (the least with max|x_k / 2^e_k|
+// <= 7.5 s) and their prefix stats (a = ||x~_m||, e = ||x_m - x~_m||).  A power-of-two s is exact in the
+// MFMA's E8M0 operand scale, so the prefix pass folds 2 s_g into the gallery operand and -|g_m|^2 into the
+// accumulator input: its output IS the negated coarse score (prefix_pass_kernel<true>).  The f6 tiers keep
+// their fp32 row scales (a finer cut of the full rows).
+extern "C" size_t ofr_f6p_tiles_bytes(int64_t R, int pstages) {
+  return pstages >= 1 ? (size_t)f6t::panels(R > 0 ? R : 1) * (size_t)pstages * (size_t)f6t::PANEL : 0;
+}
+
+extern "C" int ofr_f6p_quantize_rows_at(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int64_t row0,
+                                        int pstages, void* tiles, size_t tiles_bytes, float* scale, double* stats,
+                                        const uint8_t* bscale) {
+  OFR_CHECK_ARG(R >= 0 && d >= 1 && ldx >= d && row0 >= 0, "ofr_f6p_quantize_rows_at: bad sizes");
+  OFR_CHECK_ARG(pstages >= 1 && pstages <= f6t::stages(d), "ofr_f6p_quantize_rows_at: pstages in [1, ceil(d / 128)]");
+  if (R == 0) return OFR_OK;
+  OFR_CHECK_ARG(X && tiles && scale && stats, "ofr_f6p_quantize_rows_at: null pointer");
+  OFR_CHECK_ARG(row0 + R < 0x7fffffffLL, "ofr_f6p_quantize_rows_at: too many rows");
+  OFR_CHECK_ARG(tiles_bytes >= ofr_f6p_tiles_bytes(row0 + R, pstages), "ofr_f6p_quantize_rows_at: tile buffer too small");
+  OFR_CHECK_ARG((uintptr_t)tiles % 16 == 0, "ofr_f6p_quantize_rows_at: tiles must be 16-byte aligned");
+  OFR_CHECK_ARG(bscale_ok(bscale), "ofr_f6p_quantize_rows_at: bscale must be 4-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t dm = std::min<int64_t>(d, (int64_t)pstages * f6t::BK);
+  hipLaunchKernelGGL(q8s::quantize_f6_kernel<false>, dim3((unsigned)R), dim3(256), 0, st, X, ldx, dm, (int64_t)pstages,
+                     row0, (char*)tiles, scale, stats, nullptr, bscale, (int64_t)pstages, 1);
+  OFR_LAUNCH_CHECK("f6p quantize_kernel (gallery)");
+  const int64_t end = row0 + R;
+  if (end % 256) {
+    hipLaunchKernelGGL(q8s::f6_zero_tail, dim3(256), dim3(256), 0, st, (char*)tiles, end, (int64_t)pstages);
+    OFR_LAUNCH_CHECK("f6 zero_tail");
+  }
+  return OFR_OK;
+}
+
 extern "C" int ofr_q8_maxima(void* stream, const double* stats, const float* aux, int64_t R, double* maxima) {
   OFR_CHECK_ARG(R >= 0 && stats && maxima, "ofr_q8_maxima: bad arguments");
   hipLaunchKernelGGL(q8s::maxima_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, stats, aux, R, maxima);
@@ -2345,6 +2498,16 @@ extern "C" int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int
   const int rc = ofr_f6_quantize_rows_at(stream, X, R, d, ldx, 0, tiles, tiles_bytes, scale, stats, bscale);
   if (rc || R == 0 || !maxima) return rc;
   return ofr_q8_maxima(stream, stats, aux, R, maxima);
+}
+
+// ofr_f6p_quantize_rows_at from row 0, then the maxima of the prefix stats and of the prefix terms
+// paux (|g_m|^2, ofr_row_aux over the first min(d, 128 pstages) features): the f6p tier's gmax
+extern "C" int ofr_f6p_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, int pstages,
+                                     void* tiles, size_t tiles_bytes, float* scale, double* stats, const float* paux,
+                                     double* maxima, const uint8_t* bscale) {
+  const int rc = ofr_f6p_quantize_rows_at(stream, X, R, d, ldx, 0, pstages, tiles, tiles_bytes, scale, stats, bscale);
+  if (rc || R == 0 || !maxima) return rc;
+  return ofr_q8_maxima(stream, stats, paux, R, maxima);
 }
 
 extern "C" int ofr_f6x2_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles1,
@@ -2425,12 +2588,15 @@ extern "C" const char* ofr_f6_sieve_kernel(void) {
 static bool f6p_persistent();
 static int f6p_engine();
 extern "C" const char* ofr_f6p_sieve_kernel(int pstages) {
-  static const std::string names[2] = {
+  static const std::string names[3] = {
       "q8s::tile_kernel_f6p (persistent prefix pass: one workgroup per CU, 384-row gallery tile resident in LDS, "
       "16x16x128 fp6 MFMA)",
-      "q8s::prefix_pass_kernel (persistent one-stage prefix pass: two workgroups per CU, 64 x 128 wave tiles, "
-      "16x16x128 fp6 MFMA)"};
-  if (pstages == 1 && f6_shape() == 384 && f6p_persistent() && f6p_engine() == 2) return names[1].c_str();
+      "q8s::prefix_pass_kernel<false> (persistent one-stage prefix pass: two workgroups per CU, 64 x 128 wave tiles, "
+      "16x16x128 fp6 MFMA)",
+      "q8s::prefix_pass_kernel<true> (persistent one-stage prefix pass: two workgroups per CU, 64 x 128 wave tiles, "
+      "16x16x128 fp6 MFMA with the row scales and -|g_m|^2 folded in: D = -score)"};
+  if (pstages == 1 && f6_shape() == 384 && f6p_persistent() && f6p_engine() >= 2)
+    return names[f6p_engine() - 1].c_str();
   if (pstages >= 1 && pstages <= q8s::f6p::NSPMAX && f6_shape() == 384 && f6p_persistent())
     return names[0].c_str();
   return ofr_f6_sieve_kernel();
@@ -2466,11 +2632,13 @@ static bool f6p_persistent() {
   const char* e = getenv("OFR_F6P_PERSIST");
   return !(e && e[0] == '0');
 }
-// Engine of the one-stage prefix pass: 2 = prefix_pass_kernel (two workgroups per CU; default since round
-// 6), 1 = tile_kernel_f6p<1> (one wave per SIMD; the A/B reference).  OFR_F6P_ENGINE, read at every call.
+// Engine of the one-stage prefix pass: 3 = prefix_pass_kernel<true> (two workgroups per CU, row scales and
+// prefix terms folded into the MFMA; default), 2 = prefix_pass_kernel<false> (the same pass with the fma
+// epilogue), 1 = tile_kernel_f6p<1> (one wave per SIMD).  2 and 1: A/B references.  OFR_F6P_ENGINE, read at
+// every call.
 static int f6p_engine() {
   const char* e = getenv("OFR_F6P_ENGINE");
-  return e && e[0] == '1' ? 1 : 2;
+  return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 3;
 }
 // CUs the persistent prefix pass leaves free (OFR_F6P_RESERVE, probe): work queued on other streams --
 // the previous batch's merge -- otherwise waits for the whole pass
@@ -2597,9 +2765,10 @@ extern "C" int ofr_knn_f6_sampled(void* stream, int phases, const float* Q, int6
 }
 
 // Prefix tier f6p: ofr_knn_f6_sampled with the sample and sieve passes scoring only the
-// first pstages 128-feature stages of the same tiles.  aux / saux are the PREFIX terms |g_m|^2 of the
-// rows and of the row sample (ofr_row_aux over the first min(d, 128 pstages) features); gmax is the f6
-// tier's (its aux maximum bounds the prefix terms).  Every row's squared distance is at least its
+// first pstages 128-feature stages.  Gt / gscale / gmax: the prefix tier's own compact gallery tiles
+// (ofr_f6p_quantize_rows: pstages stages per panel, power-of-two row scales, prefix stats and maxima);
+// St / sscale: the f6 tier's row sample (its first stages).  aux / saux are the PREFIX terms |g_m|^2 of
+// the rows and of the row sample (ofr_row_aux over the first min(d, 128 pstages) features).  Every row's squared distance is at least its
 // prefix distance, so the certificate holds as for f6; the B x N coarse work shrinks by pstages / nst.
 extern "C" int ofr_knn_f6p_sampled(void* stream, int phases, const float* Q, int64_t B, int64_t ldq, const void* Qt,
                                    const float* qscale, const double* qstats, const float* G, int64_t N, int64_t ldg,
@@ -2711,6 +2880,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   a.nk = (int)f6t::stages(d) * (two ? 3 : 1);
   // prefix tier: the first pstages stages (one slice only); otherwise every stage of each segment
   a.nkp = pstages > 0 && !two && pstages < f6t::stages(d) ? pstages : (int)f6t::stages(d);
+  // the prefix tier's gallery tiles are its own compact ones (pstages stages per panel, round 6)
+  a.gnk = a.nkp < (int)f6t::stages(d) ? a.nkp : a.nk;
   a.G2 = (const int8_t*)Gt2; a.Q2 = (const int8_t*)Qt2;
   a.bs = reinterpret_cast<const uint32_t*>(bscale);
   if (!a.bs) {
@@ -2732,6 +2903,8 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
   uint32_t* armed = reinterpret_cast<uint32_t*>(wsb + w.armed);
   OFR_CHECK_ARG(a.ntq * a.ntg < 0x7fffffffLL, "ofr_knn_f6: grid too large");
   OFR_CHECK_ARG(f6_shape() > 0, "ofr_knn_f6: OFR_F6_SHAPE must be 384 (default) or 16");
+  if (a.gnk != a.nk && sieve && f6_shape() != 384)
+    return fail(OFR_E_UNSUPPORTED, "ofr_knn_f6p: the prefix tier's compact gallery tiles need OFR_F6_SHAPE=384");
   if (phases & 1) phases |= 12;   // phase 1 = sample + thresholds (4), then the sieve (8)
   if (phases & 12) {
     if (!sieve) {   // HBM regime: one 32-query block, gallery streamed straight to VGPRs
@@ -2756,8 +2929,11 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(f6 prefix pass)");
         }
         {
-          hipError_t e = hipFuncSetAttribute((const void*)q8s::prefix_pass_kernel,
+          hipError_t e = hipFuncSetAttribute((const void*)q8s::prefix_pass_kernel<false>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, q8s::pp::LDS_BYTES);
+          if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)q8s::prefix_pass_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    q8s::pp::LDS_BYTES);
           if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(prefix_pass_kernel)");
         }
         attr_done = true;
@@ -2804,7 +2980,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       if (!(phases & 8)) {
         // sample + thresholds only
       } else if (f6_shape() == 384 && a.nkp == 1 && a.nkp < f6t::stages(d) && !two && f6p_persistent() &&
-                 f6p_engine() == 2 && device_cus() > 0) {
+                 f6p_engine() >= 2 && device_cus() > 0) {
         // the one-stage prefix pass: two workgroups per CU (prefix_pass_kernel)
         q8s::TileArgs wa = a;
         wa.ntg = cdiv(N, q8s::pp::TGR);
@@ -2820,7 +2996,12 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         const int64_t items = wa.ntg * cdiv(nsteps, qg);
         OFR_CHECK_ARG(items < 0x7fffffffLL, "ofr_knn_f6: grid too large");
         const unsigned grid = (unsigned)std::min<int64_t>(items, slots);
-        hipLaunchKernelGGL(q8s::prefix_pass_kernel, dim3(grid), dim3(q8s::pp::NT), q8s::pp::LDS_BYTES, st, wa, qtab, qg);
+        if (f6p_engine() == 3)
+          hipLaunchKernelGGL(q8s::prefix_pass_kernel<true>, dim3(grid), dim3(q8s::pp::NT), q8s::pp::LDS_BYTES, st, wa,
+                             qtab, qg);
+        else
+          hipLaunchKernelGGL(q8s::prefix_pass_kernel<false>, dim3(grid), dim3(q8s::pp::NT), q8s::pp::LDS_BYTES, st, wa,
+                             qtab, qg);
       } else if (f6_shape() == 384 && a.nkp <= q8s::f6p::NSPMAX && a.nkp < f6t::stages(d) && !two &&
                  f6p_persistent() && device_cus() > 0) {
         // the prefix tier's short pass: persistent workgroups, the gallery tile resident (tile_kernel_f6p)

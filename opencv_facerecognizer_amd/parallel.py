@@ -484,6 +484,7 @@ class DeviceComm:
                     s.pstages = tp["pst"]
                     s.Qtp, s.qscalep, s.qstatsp = qp["Qs"].data_ptr(), qp["scale"].data_ptr(), qp["stats"].data_ptr()
                     s.paux, s.spaux = tp["paux"].data_ptr(), tp["spaux"].data_ptr()
+                    s.Gtp, s.gscalep, s.gmaxp = tp["Gs"].data_ptr(), tp["scale"].data_ptr(), tp["gmax"].data_ptr()
                 keep.append((qq, ws, out_d, out_i, cert, qp))
         _lib.call("ofr_knn_sharded", self.handle, ctypes.cast(shards, ctypes.c_void_p), B, d, k)
         self.last_tier_counts = [int(x) for x in counts]

@@ -92,8 +92,10 @@ def test_prefix_sieve_keeps_every_row_below_theta():
     bs = g._block_scales()
     f = torch.pow(2.0, bs.double() - 127.0).repeat_interleave(32)[:d]
     Vq = _decode_panels(qq["Qs"], 0, -(-B // 256), nst, d, table)[:B, :m] * f[:m]
-    gt = g._tier_gallery("f6p")
-    Vg = _decode_panels(gt["Gs"], 0, -(-N // 256), nst, d, table)[:N, :m] * f[:m]
+    gt = g._tier_gallery("f6p")              # its own compact tiles: pst stages per panel
+    Vg = _decode_panels(gt["Gs"], 0, -(-N // 256), pst, d, table, pst)[:N, :m] * f[:m]
+    gsc = gt["scale"][:N]
+    assert torch.equal(gsc, torch.exp2(torch.round(torch.log2(gsc)))), "row scales must be powers of two"
     sq, gs = qq["scale"].double(), gt["scale"][:N].double()
     paux = gt["paux"][:N].double()
     # the prefix terms are |g_m|^2 of the stored rows
@@ -102,7 +104,9 @@ def test_prefix_sieve_keeps_every_row_below_theta():
     t = 2.0 * sq[:, None] * gs[None, :]
     S = paux[None, :] - t * dot
     gamma = (2 * nst + 64) * 2.0 ** -23
-    band = t * (gamma * (Vq.abs() @ Vg.abs().t()) + 2.0 ** -22 * dot.abs()) + 2.0 ** -22 * (paux[None, :] + S.abs())
+    # the pass adds -paux inside the MFMA's fp32 accumulation: the certificate's 2^-14 paux
+    band = (t * (gamma * (Vq.abs() @ Vg.abs().t()) + 2.0 ** -22 * dot.abs()) + 2.0 ** -14 * paux[None, :]
+            + 2.0 ** -22 * S.abs())
     thf = torch.from_numpy(_key_float(theta.cpu().numpy())).to(dev)
     below = (S < thf[:, None] - band).cpu().numpy()
     above = (S > thf[:, None] + band).cpu().numpy()
@@ -182,9 +186,13 @@ def test_prefix_tier_extended_by_append():
 
 @pytest.mark.parametrize("pst,B,n_id", [(1, 300, 2003), (2, 700, 1501), (2, 4096, 997)])
 def test_persistent_prefix_pass_matches_per_tile_pass(monkeypatch, pst, B, n_id):
-    """tile_kernel_f6p (persistent, the default for pstages <= 2) keeps exactly the rows, with exactly the
-    keys, of tile_kernel_f6w on the same prefix (OFR_F6P_PERSIST=0): the same MFMAs in the same order and
-    the same compares.  Partial last gallery tile and query panel; B = 4096: 16 query panels per item."""
+    """tile_kernel_f6p (persistent, pstages = 2) keeps exactly the rows, with exactly the keys, of
+    tile_kernel_f6w on the same prefix (OFR_F6P_PERSIST=0): the same MFMAs in the same order and the same
+    compares.  pstages = 1 runs prefix_pass_kernel<true> (round 6), whose MFMA adds -|g_m|^2 inside its fp32
+    accumulation: its keys are within 2^-14 |g_m|^2 (the certificate's term) of f6w's, and a row kept by
+    only one of the two passes lies within that band of theta.  The exact outputs (distances, indices,
+    certificates) are equal either way.  Partial last gallery tile and query panel; B = 4096: 16 query
+    panels per item."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
     monkeypatch.setenv("OFR_F6_PREFIX", str(pst))
@@ -192,6 +200,8 @@ def test_persistent_prefix_pass_matches_per_tile_pass(monkeypatch, pst, B, n_id)
     g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
     assert g.prefix_stages() == pst
     Qd = g.query_rows(Q)
+    monkeypatch.setenv("OFR_F6P_PERSIST", "1")
+    folded = pst == 1 and "<true>" in _lib.load().ofr_f6p_sieve_kernel(1).decode()   # the default engine
     state, res = {}, {}
     for mode in ("1", "0"):
         monkeypatch.setenv("OFR_F6P_PERSIST", mode)
@@ -210,10 +220,26 @@ def test_persistent_prefix_pass_matches_per_tile_pass(monkeypatch, pst, B, n_id)
             pairs.append((r[o], kk[o]))
         state[mode] = (count, pairs)
         res[mode] = (out[0].cpu().numpy(), out[1].cpu().numpy(), qq["cert"].cpu().numpy().copy())
-    assert np.array_equal(state["1"][0], state["0"][0])
-    for b in range(B):
-        assert np.array_equal(state["1"][1][b][0], state["0"][1][b][0]), b
-        assert np.array_equal(state["1"][1][b][1].view(np.uint32), state["0"][1][b][1].view(np.uint32)), b
+    if not folded:
+        assert np.array_equal(state["1"][0], state["0"][0])
+        for b in range(B):
+            assert np.array_equal(state["1"][1][b][0], state["0"][1][b][0]), b
+            assert np.array_equal(state["1"][1][b][1].view(np.uint32), state["0"][1][b][1].view(np.uint32)), b
+    else:
+        from test_gpu_sieve import _key_float
+        paux = g._tier_gallery("f6p")["paux"][:g.N].double().cpu().numpy()
+        th = _key_float(theta.cpu().numpy())
+        n_diff = 0
+        for b in range(B):
+            (ra, ka), (rb, kb) = state["1"][1][b], state["0"][1][b]
+            common, ia, ib = np.intersect1d(ra, rb, return_indices=True)
+            tol = 2.0 ** -14 * paux[common] + 2.0 ** -14 * np.abs(kb[ib].astype(np.float64))   # + the key truncation
+            assert np.all(np.abs(ka[ia].astype(np.float64) - kb[ib].astype(np.float64)) <= tol), b
+            for r in np.setxor1d(ra, rb):   # kept by one pass only: at theta up to the band
+                n_diff += 1
+                k_any = ka[ra == r] if r in ra else kb[rb == r]
+                assert abs(float(k_any[0]) - th[b]) <= 2.0 ** -14 * paux[r] + 2.0 ** -14 * abs(th[b]), (b, r)
+        assert n_diff <= B, n_diff
     for j in range(3):
         assert np.array_equal(res["1"][j], res["0"][j])
     assert res["1"][2].all()

@@ -118,8 +118,8 @@ def _decode_panels(tiles, p0, p1, nst, d, table, ns=None):
 @pytest.mark.parametrize("w,tier", [("random", "f6"), ("trained", "f6"), ("trained", "f6p")])
 def test_sieve_complete_vs_exact_scores_headline_shape(w, tier):
     """tier f6p (round 6): the headline's own pass -- the prefix tier on the persistent sieve kernel,
-    scoring the first pstages (choose_prefix) stages of the same tiles with the prefix terms |g_m|^2
-    as the rows' aux and power-of-two query scales."""
+    scoring the prefix tier's own compact tiles of the first pstages (choose_prefix) stages (power-of-two
+    row scales and -|g_m|^2 folded into the MFMA) against power-of-two-scaled queries."""
     from opencv_facerecognizer_amd._device import round_up
     from opencv_facerecognizer_amd.synthetic import (SEED, IdentityBank, build_gallery, build_projection,
                                                      build_trained_projection)
@@ -180,14 +180,17 @@ def test_sieve_complete_vs_exact_scores_headline_shape(w, tier):
     thf_d = torch.from_numpy(thf).to(dev)
     for p0 in range(0, npan, PCH):
         p1 = min(npan, p0 + PCH)
-        Vg = _decode_panels(gt["Gs"], p0, p1, nst, d, table, ns)
+        # f6p: the prefix tier's own compact tiles (ns stages per panel, power-of-two row scales)
+        Vg = _decode_panels(gt["Gs"], p0, p1, nst if ns is None else ns, d, table, ns)
         r0, r1 = p0 * 256, min(N, p1 * 256)
         Vg = Vg[:r1 - r0] * f
         dot = Vq @ Vg.t()                             # exact: multiples of 2^-6, |sum| < 2^53 ulp range
         sab = Vqa @ Vg.abs().t()
         t = 2.0 * sq[:, None] * gscale[None, r0:r1]
         S = aux[None, r0:r1] - t * dot                # the exact coarse score of the fp6 codes
-        band = t * (gamma * sab + 2.0 ** -22 * dot.abs()) + 2.0 ** -22 * (aux[None, r0:r1].abs() + S.abs())
+        # f6p: the pass adds -aux inside the MFMA's fp32 accumulation (the certificate's 2^-14 aux)
+        auxe = 2.0 ** -22 if ns is None else 2.0 ** -14
+        band = t * (gamma * sab + 2.0 ** -22 * dot.abs()) + auxe * aux[None, r0:r1].abs() + 2.0 ** -22 * S.abs()
         below = S < thf_d[:, None] - band             # must be kept
         above = S > thf_d[:, None] + band             # must not be kept
         for j in range(64):
