@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--d", type=int, default=9999)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--check-rows", type=int, default=64)
-    ap.add_argument("--engines", default="i8,s4,s5,s5p")
+    ap.add_argument("--engines", default="i8")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -69,7 +69,11 @@ def main():
     tmp = os.path.join(tempfile.mkdtemp(prefix="bench_proj_"), "y")   # outputs are large: not under gpurun_out
     for eng in a.engines.split(","):
         # "lib=<path>": the default engine of another build of the library (same-box A/B)
-        env = dict(os.environ, OFR_LIB=eng[4:]) if eng.startswith("lib=") else dict(os.environ, OFR_PROJ_ENGINE=eng)
+        # "lib=<path>": another build of the library (same-box A/B); other names: OFR_PROJ_ENGINE
+        if eng.startswith("lib="):
+            env = dict(os.environ, OFR_LIB=eng[4:])
+        else:
+            env = dict(os.environ, OFR_PROJ_ENGINE=eng)
         key = f"{len(res['engines'])}:{eng}"
         out = f"{tmp}_{len(res['engines'])}"
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--out", out, "--batch", str(a.batch), "--D",
