@@ -939,8 +939,9 @@ constexpr int QB = GT + f6t::PANEL;            // [2] half-panel images (E::HPB 
 constexpr int QT = QB + 2 * E::HPB;            // [2][128] (theta as a float, the query's scale exponent)
 constexpr int GTB = QT + 2 * 1024;             // [2] {f32 aux [256], f32 scale [256]}
 constexpr int HITS = GTB + 2 * 2048;           // [4][HCAPW] (key bits, ql << 9 | row)
-constexpr int HCAPW = 768;
-constexpr int LDS_BYTES = HITS + 4 * HCAPW * 8;
+constexpr int HCAPW = 256;                     // a wave's hits per step (~1 on gallery data; past it: atomics)
+constexpr int SCR = HITS + 4 * HCAPW * 8;      // [4][4 KiB] per wave: a flagged column's 16 scores per lane
+constexpr int LDS_BYTES = SCR + 4 * 4096;
 static_assert(LDS_BYTES <= 81920, "two workgroups per CU");
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
@@ -1219,26 +1220,38 @@ __global__ void __launch_bounds__(256, 2) prefix_pass_kernel(TileArgs p, const u
           hitc = 0;
         }
         if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform; ~1 kept pair per step and wave on gallery data
+          // Hit path: per flagged column block, the lane's 16-row pass mask by VALU compares alone (no ballot or
+          // branch per row: testing the rows one ballot at a time cost half the pass, tools/probe_prefix_pass.py
+          // probe bit 8), then a wave-uniform loop over the lanes' set bits, one kept row per lane and round (on
+          // gallery data one round); the kept score is read back from the wave's LDS scratch by its row index.
+          // lane-derived payloads from a laundered lane index: computed from threadIdx.x they are loop
+          // invariants, and the compiler hoisted the (column, row) payloads out of the loops and spilled them
+          uint32_t lid = lane;
+          asm volatile("" : "+v"(lid));
+          const uint32_t scr = pp::SCR + (uint32_t)wave * 4096u + (lid & 63u) * 16u;
+          const int rg4 = (int)(lid >> 4) * 4;
 #pragma unroll
           for (int c = 0; c < 8; ++c) {
             if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
             const float nth = -__uint_as_float(pp::lds_u32(qta + c * 128u));
-            // lane-derived payloads from a laundered lane index: computed from threadIdx.x they are loop
-            // invariants, and the compiler hoisted all 128 (column, row) payloads out of the loops and
-            // spilled them (531 VGPRs)
-            uint32_t lid = lane;
-            asm volatile("" : "+v"(lid));
             const int ql = c * 16 + (int)(lid & 15u);
-            const int rg4 = (int)(lid >> 4) * 4;
-            const uint32_t okm = (int64_t)s * pp::TQH + ql < p.B ? vmask : 0u;
-            // row by row: one compare and one ballot each; the passing lanes take consecutive list slots
+            uint32_t hm = 0;   // rows j = 4 i + r of this lane that pass
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-              const float v = acc[j >> 2][c][j & 3];
-              const bool pass = !(v < nth) && (okm & (1u << j)) != 0u;
-              const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
-              if (mk == 0) continue;   // uniform
-              if (pass) {
+            for (int j = 0; j < 16; ++j) hm |= !(acc[j >> 2][c][j & 3] < nth) ? (1u << j) : 0u;
+            hm &= (int64_t)s * pp::TQH + ql < p.B ? vmask : 0u;
+            if (hm) {   // the lane's scores of this column into its scratch (read back by row index below)
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<volatile OFR_LDS f6t::f32x4*>((uintptr_t)(scr + 1024u * i)) = acc[i][c];
+            }
+            for (;;) {   // wave-uniform: one kept row per lane and round
+              const bool act = hm != 0u;
+              const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
+              if (mk == 0) break;
+              if (act) {
+                const int j = __builtin_ctz(hm);
+                hm &= hm - 1u;
+                const float v = __uint_as_float(pp::lds_u32(scr + 1024u * (uint32_t)(j >> 2) + 4u * (uint32_t)(j & 3)));
                 const uint32_t kb = __float_as_uint(key_score(score_key(-v, 0)));
                 const int row = wave * 64 + 16 * (j >> 2) + rg4 + (j & 3);
                 const uint32_t slot = ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
