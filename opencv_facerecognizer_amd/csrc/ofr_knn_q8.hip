@@ -1389,6 +1389,195 @@ __global__ void __launch_bounds__(256, 2) prefix_pass_kernel(TileArgs p, const u
   pp::flush_end(p, pg0, pd);
 }
 
+// ---- prefix tier's sieve pass, wave-decoupled (round 6, engine 4) ------------------------------------
+// prefix_pass_kernel<true> shares each 128-query half panel between its 4 waves through LDS, so every step
+// ends in a workgroup barrier, and a wave that finds hits (~1 kept pair per wave-step on gallery data) makes
+// the other three wait: rocprofv3 counted the waves parked 0.52 of their cycles, 0.29 without the hit path
+// (profiles/r06_prefix_pass_pmc.txt).  Here every wave runs alone: it owns 64 gallery rows of the work
+// item's 256-row tile (its A fragments, row scales and prefix terms in registers for the item) and walks
+// the item's 64-query steps loading each step's 4 query fragments and its thresholds straight from L2
+// into VGPRs (the 4 waves of a workgroup read the same steps about together: L1 hits), no LDS staging
+// and no barrier; the next step's fragments are loaded right behind this step's MFMAs, under its compares.
+// Per step: 16 MFMAs 16x16x128 (row scales 2 s_g in the gallery operand's E8M0 scale, -|g_m|^2 as the
+// accumulator input: D = -score), per query column one v_maximum3 tree and one compare, the hit path of
+// prefix_pass_kernel<true> into a wave-private LDS list, flushed to the buckets once per work item.
+namespace pw {
+constexpr int NT = 256;
+constexpr int TGR = 256;              // gallery rows per work item (one panel of the compact tiles)
+constexpr int TQS = 64;               // queries per step
+constexpr int HCAPW = 256;            // a wave's kept pairs per work item (~32 on gallery data; past it: atomics)
+constexpr int HITS = 0;               // [4][HCAPW] (key bits, query << 6 | row of the wave's 64)
+constexpr int SCR = HITS + 4 * HCAPW * 8;   // [4][4 KiB] a flagged column's 16 scores per lane
+constexpr int LDS_BYTES = SCR + 4 * 4096;
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// the fragment of rows [row, row + 16) (lane l: row + l % 16, 32-feature block l / 16) of the 256-row panel at
+// byte pbase of an f6 tiled buffer, stage 0: part0 16 B and part1 8 B (p1_slot) of sub-block l / 16
+__device__ __forceinline__ i32x8 gfrag(__amdgpu_buffer_rsrc_t r, uint32_t pbase, uint32_t row, uint32_t lane) {
+  const uint32_t q = lane >> 4, rr = row + (lane & 15u);
+  const uint32_t o0 = pbase + q * 6144u + rr * 16u;
+  const uint32_t o1 = pbase + q * 6144u + 4096u + (rr ^ ((q & 1u) << 4)) * 8u;
+  const f6t::i32x4 a = __builtin_bit_cast(f6t::i32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)o0, 0, 0));
+  const f6t::i32x2 b = __builtin_bit_cast(f6t::i32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)o1, 0, 0));
+  i32x8 v;
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = 0; v[7] = 0;
+  return v;
+}
+}  // namespace pw
+
+// p.ntg = ceil(N / 256) gallery tiles; steps of 64 queries, ceil(B / 64); item w = (tile w / ngrp, steps
+// [qg (w % ngrp), ...)), dealt to the workgroups by stride; each wave walks the same items on its own.
+// qtab: prefix_tables_kernel's table over round_up(B, 64) queries (theta as a float, -inf past B; e_q).
+__global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const uint2* qtab, int64_t qg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63;
+  const int64_t nsteps = (p.B + pw::TQS - 1) / pw::TQS;
+  const int64_t ngrp = (nsteps + qg - 1) / qg, items = p.ntg * ngrp;
+  if ((int64_t)blockIdx.x >= items) return;
+  int scs;   // the lane's stage-0 block scale byte (its 32-feature block lane >> 4)
+  {
+    const uint32_t r0 = f6t::sload_bscale(p.bs, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    scs = f6t::lane_byte(r0, 8u * (lane >> 4));
+  }
+  // buffer descriptors: the compact gallery tiles, the query tiles (stage stride nk), the row terms, the table
+  const int64_t gpb = (int64_t)p.gnk * f6t::PANEL, qpb = (int64_t)p.nk * f6t::PANEL;
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.G, 0, (int)(f6t::panels(p.N) * gpb), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.Q, 0, (int)(f6t::panels(p.B) * qpb), 0x00020000);
+  const __amdgpu_buffer_rsrc_t raux = __builtin_amdgcn_make_buffer_rsrc((void*)p.aux, 0, (int)(p.N * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc((void*)p.gscale, 0, (int)(p.N * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rtab = __builtin_amdgcn_make_buffer_rsrc((void*)qtab, 0, (int)(nsteps * pw::TQS * 8),
+                                                                         0x00020000);
+  const uint32_t hits_a = pw::HITS + (uint32_t)wave * pw::HCAPW * 8u;   // the wave's kept pairs (LDS address)
+  const int g4 = (int)(lane >> 4) * 4, r16 = (int)(lane & 15);
+  const uint32_t ng32 = (uint32_t)ngrp, qg32 = (uint32_t)qg;
+  for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const int64_t gt = (int64_t)((uint32_t)w / ng32), s0 = (int64_t)(((uint32_t)w % ng32) * qg32);
+    const int64_t s1 = s0 + qg < nsteps ? s0 + qg : nsteps;
+    const int64_t g0 = gt * pw::TGR + wave * 64;   // the wave's first row
+    const int nvalid = p.N - g0 < 64 ? (int)(p.N - g0) : 64;
+    if (nvalid <= 0) continue;   // uniform: the last tile's empty quarters
+    // the item's gallery operands: A fragments of row blocks i, accumulator inputs -|g_m|^2 (-inf past N) of the
+    // lane's output rows, operand scales block byte + e_g + 1 of the lane's A rows, the valid-row mask
+    pw::i32x8 A[4];
+    f6t::f32x4 Cin[4];
+    int sa[4];
+    uint32_t vmask = 0;
+    const uint32_t gpan = (uint32_t)(gt * gpb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      A[i] = pw::gfrag(rg, gpan, (uint32_t)(wave * 64 + 16 * i), lane);
+      const int rb = 16 * i + g4;
+      const f6t::i32x4 a4 = __builtin_bit_cast(
+          f6t::i32x4, __builtin_amdgcn_raw_buffer_load_b128(raux, (int)((g0 + rb) * 4), 0, 0));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Cin[i][r] = rb + r < nvalid ? -__int_as_float(a4[r]) : -__builtin_inff();
+        vmask |= rb + r < nvalid ? 1u << (4 * i + r) : 0u;
+      }
+      const uint32_t sb = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsc, (int)((g0 + 16 * i + r16) * 4), 0, 0);
+      const int eg = sb != 0u ? (int)((sb >> 23) & 0xffu) - 127 : 0;
+      sa[i] = scs + eg + 1;   // block byte (64..127) + e_g (-64..64) + 1: in [1, 192]
+    }
+    // the first step's query fragments and table entries (lane: query 64 s + 16 c + l % 16)
+    auto qload = [&](int64_t st, pw::i32x8 (&b)[4], uint2 (&t)[4]) {
+      const uint32_t qpan = (uint32_t)((st >> 2) * qpb), qrow = (uint32_t)((st & 3) * 64);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        b[c] = pw::gfrag(rq, qpan, qrow + 16u * c, lane);
+        const f6t::i32x2 e = __builtin_bit_cast(
+            f6t::i32x2, __builtin_amdgcn_raw_buffer_load_b64(rtab, (int)((st * pw::TQS + 16 * c + r16) * 8), 0, 0));
+        t[c] = make_uint2((uint32_t)e[0], (uint32_t)e[1]);
+      }
+    };
+    pw::i32x8 B[4];
+    uint2 tb[4];
+    qload(s0, B, tb);
+    uint32_t ncnt = 0;   // kept pairs of this item in the wave's list (uniform)
+    for (int64_t st = s0; st < s1; ++st) {
+      float th[4];
+      f6t::f32x4 acc[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        th[c] = __uint_as_float(tb[c].x);
+        const int sbq = scs + (int)tb[c].y;   // block byte + e_q (in [0, 191]: no carry)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], B[c], Cin[i], 2, 2, 0, sa[i], 0, sbq);
+      }
+      if (st + 1 < s1) qload(st + 1, B, tb);   // the next step's operands, under this step's compares
+      uint32_t hitc = 0;
+      auto mx3 = [](float a, float b, float d) {
+        return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), d);
+      };
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const f6t::f32x4 &a0 = acc[0][c], &a1 = acc[1][c], &a2 = acc[2][c], &a3 = acc[3][c];
+        const float t0 = mx3(a0[0], a0[1], a0[2]), t1 = mx3(a0[3], a1[0], a1[1]), t2 = mx3(a1[2], a1[3], a2[0]);
+        const float t3 = mx3(a2[1], a2[2], a2[3]), t4 = mx3(a3[0], a3[1], a3[2]);
+        const float mx = __builtin_elementwise_maximum(mx3(t0, t1, t2), mx3(t3, t4, a3[3]));
+        hitc |= !(mx < -th[c]) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
+      }
+      if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform
+        uint32_t lid = lane;   // laundered: the payloads are not hoisted out of the loops (spills)
+        asm volatile("" : "+v"(lid));
+        const uint32_t scr = pw::SCR + (uint32_t)wave * 4096u + (lid & 63u) * 16u;
+        const int rg4 = (int)(lid >> 4) * 4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
+          const float nth = -th[c];
+          const int64_t q = st * pw::TQS + 16 * c + (int)(lid & 15u);
+          uint32_t hm = 0;   // rows j = 4 i + r of this lane that pass
+#pragma unroll
+          for (int j = 0; j < 16; ++j) hm |= !(acc[j >> 2][c][j & 3] < nth) ? (1u << j) : 0u;
+          hm &= q < p.B ? vmask : 0u;
+          if (hm) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              *reinterpret_cast<volatile OFR_LDS f6t::f32x4*>((uintptr_t)(scr + 1024u * i)) = acc[i][c];
+          }
+          for (;;) {   // wave-uniform: one kept row per lane and round
+            const bool act = hm != 0u;
+            const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
+            if (mk == 0) break;
+            if (act) {
+              const int j = __builtin_ctz(hm);
+              hm &= hm - 1u;
+              const float v = __uint_as_float(pp::lds_u32(scr + 1024u * (uint32_t)(j >> 2) + 4u * (uint32_t)(j & 3)));
+              const uint32_t kb = __float_as_uint(key_score(score_key(-v, 0)));
+              const int row = 16 * (j >> 2) + rg4 + (j & 3);   // of the wave's 64
+              const uint32_t slot = ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+              if (slot < (uint32_t)pw::HCAPW) {
+                f6t::i32x2 e;
+                e[0] = (int)kb;
+                e[1] = (int)(((uint32_t)q << 6) | (uint32_t)row);
+                *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
+              } else {   // the list is full (small galleries keep a large share): straight to the bucket
+                const int bs = atomicAdd(p.count + q, 1);
+                if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
+              }
+            }
+            ncnt += (uint32_t)__builtin_popcountll(mk);
+          }
+        }
+      }
+    }
+    // the item's kept pairs -> bucket slots and entries
+    const uint32_t n = ncnt < (uint32_t)pw::HCAPW ? ncnt : (uint32_t)pw::HCAPW;
+    for (uint32_t e = lane; e < n; e += 64u) {
+      const uint2 hv = pp::lds_u2(hits_a + e * 8u);
+      const int64_t q = (int64_t)(hv.y >> 6);
+      const int slot = atomicAdd(p.count + q, 1);
+      if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(hv.x), (int)(g0 + (hv.y & 63u))};
+    }
+  }
+}
+
 // ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
 // One workgroup per 256-row gallery panel, wave w owns rows 32w..32w+31 against the (single)
 // 32-row query block, loading its fragments straight to VGPRs from the f6 tiled layout (each
@@ -2601,13 +2790,15 @@ extern "C" const char* ofr_f6_sieve_kernel(void) {
 static bool f6p_persistent();
 static int f6p_engine();
 extern "C" const char* ofr_f6p_sieve_kernel(int pstages) {
-  static const std::string names[3] = {
+  static const std::string names[4] = {
       "q8s::tile_kernel_f6p (persistent prefix pass: one workgroup per CU, 384-row gallery tile resident in LDS, "
       "16x16x128 fp6 MFMA)",
       "q8s::prefix_pass_kernel<false> (persistent one-stage prefix pass: two workgroups per CU, 64 x 128 wave tiles, "
       "16x16x128 fp6 MFMA)",
       "q8s::prefix_pass_kernel<true> (persistent one-stage prefix pass: two workgroups per CU, 64 x 128 wave tiles, "
-      "16x16x128 fp6 MFMA with the row scales and -|g_m|^2 folded in: D = -score)"};
+      "16x16x128 fp6 MFMA with the row scales and -|g_m|^2 folded in: D = -score)",
+      "q8s::prefix_wave_kernel (persistent one-stage prefix pass, waves decoupled: 64 x 64 wave steps, query "
+      "fragments straight from L2, no barriers; 16x16x128 fp6 MFMA with the row scales and -|g_m|^2 folded in)"};
   if (pstages == 1 && f6_shape() == 384 && f6p_persistent() && f6p_engine() >= 2)
     return names[f6p_engine() - 1].c_str();
   if (pstages >= 1 && pstages <= q8s::f6p::NSPMAX && f6_shape() == 384 && f6p_persistent())
@@ -2645,13 +2836,14 @@ static bool f6p_persistent() {
   const char* e = getenv("OFR_F6P_PERSIST");
   return !(e && e[0] == '0');
 }
-// Engine of the one-stage prefix pass: 3 = prefix_pass_kernel<true> (two workgroups per CU, row scales and
-// prefix terms folded into the MFMA; default), 2 = prefix_pass_kernel<false> (the same pass with the fma
-// epilogue), 1 = tile_kernel_f6p<1> (one wave per SIMD).  2 and 1: A/B references.  OFR_F6P_ENGINE, read at
-// every call.
+// Engine of the one-stage prefix pass: 4 = prefix_wave_kernel (waves decoupled, no barriers; default: 0.49 vs
+// 0.63-0.66 ms alone, profiles/r06_prefix_engines_ab.txt), 3 = prefix_pass_kernel<true> (two workgroups per CU
+// sharing query panels through LDS, row scales and prefix terms folded into the MFMA), 2 =
+// prefix_pass_kernel<false> (the same pass with the fma epilogue), 1 = tile_kernel_f6p<1> (one wave per SIMD).
+// 1-3: A/B references.  OFR_F6P_ENGINE, read at every call.
 static int f6p_engine() {
   const char* e = getenv("OFR_F6P_ENGINE");
-  return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 3;
+  return e && e[0] >= '1' && e[0] <= '3' ? e[0] - '0' : 4;
 }
 // CUs the persistent prefix pass leaves free (OFR_F6P_RESERVE, probe): work queued on other streams --
 // the previous batch's merge -- otherwise waits for the whole pass
@@ -3009,7 +3201,18 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         const int64_t items = wa.ntg * cdiv(nsteps, qg);
         OFR_CHECK_ARG(items < 0x7fffffffLL, "ofr_knn_f6: grid too large");
         const unsigned grid = (unsigned)std::min<int64_t>(items, slots);
-        if (f6p_engine() == 3)
+        if (f6p_engine() == 4) {   // wave-decoupled: 64-query steps, its own table length and grouping
+          const int64_t ns4 = cdiv(B, q8s::pw::TQS), nq4 = ns4 * q8s::pw::TQS;
+          OFR_CHECK_ARG((size_t)nq4 * sizeof(uint2) <= w.theta - w.lists, "ofr_knn_f6: workspace too small (prefix tables)");
+          hipLaunchKernelGGL(q8s::prefix_tables_kernel, dim3((unsigned)cdiv(nq4, 256)), dim3(256), 0, st, theta,
+                             a.qscale, B, nq4, qtab);
+          OFR_LAUNCH_CHECK("f6 prefix_tables_kernel");
+          const int64_t qg4 = f6p_group(wa.ntg, ns4, slots);
+          const int64_t items4 = wa.ntg * cdiv(ns4, qg4);
+          OFR_CHECK_ARG(items4 < 0x7fffffffLL, "ofr_knn_f6: grid too large");
+          hipLaunchKernelGGL(q8s::prefix_wave_kernel, dim3((unsigned)std::min<int64_t>(items4, slots)), dim3(q8s::pw::NT),
+                             q8s::pw::LDS_BYTES, st, wa, qtab, qg4);
+        } else if (f6p_engine() == 3)
           hipLaunchKernelGGL(q8s::prefix_pass_kernel<true>, dim3(grid), dim3(q8s::pp::NT), q8s::pp::LDS_BYTES, st, wa,
                              qtab, qg);
         else

@@ -201,7 +201,7 @@ def test_persistent_prefix_pass_matches_per_tile_pass(monkeypatch, pst, B, n_id)
     assert g.prefix_stages() == pst
     Qd = g.query_rows(Q)
     monkeypatch.setenv("OFR_F6P_PERSIST", "1")
-    folded = pst == 1 and "<true>" in _lib.load().ofr_f6p_sieve_kernel(1).decode()   # the default engine
+    folded = pst == 1 and "folded" in _lib.load().ofr_f6p_sieve_kernel(1).decode()   # the default engine
     state, res = {}, {}
     for mode in ("1", "0"):
         monkeypatch.setenv("OFR_F6P_PERSIST", mode)
