@@ -40,7 +40,9 @@ def main():
     Qd = P.project(bank.images(ids, seed=SEED + 99), shift64=g.shift64)
     qq = g.quantize_queries(Qd, tier="f6p")
     for e in [x for x in a.engines.split(",") if x]:
+        e, _, occ = e.partition(":")  # "4:3" = engine 4 at 3 workgroups per CU
         os.environ["OFR_F6P_ENGINE"] = e
+        os.environ["OFR_F6P_OCC"] = occ or "2"
         ms = []
         for rep in range(a.reps + 2):
             g.search_q8_phase(4, Qd, qq, 1)
@@ -54,7 +56,7 @@ def main():
         kept = g.sieve_counts(B)
         m = float(np.median(ms))
         ops = 2.0 * B * N * min(d, 128 * g.prefix_stages())
-        print(json.dumps({"tag": a.tag, "lib": os.environ.get("OFR_LIB", "in-tree"), "engine": int(e),
+        print(json.dumps({"tag": a.tag, "lib": os.environ.get("OFR_LIB", "in-tree"), "engine": int(e), "occ": int(occ or 2),
                           "pass_ms_median": m, "pass_ms_min": float(min(ms)), "pass_ms_max": float(max(ms)),
                           "frac_fp6_peak": ops / (m * 1e-3) / 10e15, "kept_mean": float(kept.double().mean()),
                           "kept_max": int(kept.max()), "pstages": g.prefix_stages()}), flush=True)
