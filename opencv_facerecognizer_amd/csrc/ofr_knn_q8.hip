@@ -1897,11 +1897,18 @@ __global__ void __launch_bounds__(256) sieve_arm_kernel(uint32_t* armed, int* co
 // k-th; (3) sort by (distance, index) and the certificate.
 // SMALL: the sieve's buckets (~120-260 rows per query): block_best_small and 4 KC list entries of LDS
 // instead of block_best's 256 KC (32 KiB), so 4x as many merge blocks fit a CU.
-template <bool SMALL>
-__global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
+// COOP (round 6, the default): each candidate's exact distance is summed by the whole block -- every
+// thread holds its 10 float4 of the query row in registers for the block's life (d <= 10,240) and issues
+// its 10 float4 of the candidate row at once, one block reduction per candidate -- and the stop test runs
+// after every candidate, not every fourth: one HBM round trip per re-rank, no query re-reads from L2.
+// The per-candidate sum order differs from the wave form (!COOP), so the two give distances within one
+// fp64 rounding of each other; one library uses one form for every tier.
+template <bool SMALL, bool COOP>
+__global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
   __shared__ Cand lists[(SMALL ? 4 : 256) * KC];
   __shared__ double exact[KC];
   __shared__ double red[4];
+  __shared__ double red2[2][4];
   __shared__ int stop_flag;
   const int64_t q = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1948,6 +1955,78 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
     return a;
+  };
+  // COOP: the block's query row, float4 j = threadIdx.x + 256 u, held when d fits (MQ float4 per thread)
+  constexpr int MQ = 10;
+  const bool qres = vec && d4 <= 256 * MQ && (p.mode != 1 || p.dpre > 0);   // (mode 1 of f6: no re-rank)
+  float4 qv[MQ];
+  // buffer loads of float4 j = threadIdx.x + 256 u of a row's first d4 float4: one 32-bit offset per load
+  // (no 64-bit addresses), and the range check returns zeros past d4 (the offset in voffset: the check
+  // covers voffset + offset, not soffset)
+  auto row_load = [&](const float* row, int64_t n4, float4* v, auto nu) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), 0, (int)(n4 * 16), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < decltype(nu)::value; ++u)
+      v[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)((threadIdx.x + 256 * u) * 16), 0, 0));
+  };
+  using NQ = std::integral_constant<int, MQ>;
+  using NC = std::integral_constant<int, 4>;   // float4 per thread and chunk past MQ
+  auto load_query = [&]() { row_load(qr, d4, qv, NQ{}); };   // right before the re-rank (not live during the selection)
+  int rb = 0;   // red2 buffer of the next block reduction (two: one barrier per reduction)
+  // COOP: exact squared distance of gallery row `row`, the whole block (block-uniform call; the sum in
+  // every thread): per thread its float4 in u order, the scalar tail, then lanes by xor shuffles and the
+  // four waves in a fixed order
+  auto exact_block = [&](int row) -> double {
+    row = __builtin_amdgcn_readfirstlane(row);   // block-uniform: a scalar buffer descriptor
+    const float* gr = p.G + (int64_t)row * p.ldg;
+    double a = 0;
+    if (qres) {
+      float4 y[MQ];
+      row_load(gr, d4, y, NQ{});   // every load issued at once: one HBM round trip per candidate
+#pragma unroll
+      for (int u = 0; u < MQ; ++u) {   // padding lanes add (0 - 0)^2 = 0 exactly
+        // laundered: else the compiler hoists the 40 fp64 conversions of the query out of the candidate
+        // loop (80 VGPRs, 218 in all)
+        float4 x = qv[u];
+        asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
+        const double e0 = (double)x.x - (double)y[u].x, e1 = (double)x.y - (double)y[u].y;
+        const double e2 = (double)x.z - (double)y[u].z, e3 = (double)x.w - (double)y[u].w;
+        a += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+      }
+      for (int64_t j = d4 * 4 + threadIdx.x; j < p.d; j += 256) {
+        const double df = (double)qr[j] - (double)gr[j];
+        a += df * df;
+      }
+    } else {
+      int64_t j0 = 0;
+      if (vec) {   // d > 10,240: the query re-read per chunk of 1,024 float4
+        for (int64_t c0 = 0; c0 < d4; c0 += 256 * NC::value) {
+          float4 x[NC::value], y[NC::value];
+          const int64_t n4 = d4 - c0 < 256 * NC::value ? d4 - c0 : 256 * NC::value;
+          row_load(qr + 4 * c0, n4, x, NC{});
+          row_load(gr + 4 * c0, n4, y, NC{});
+#pragma unroll
+          for (int u = 0; u < NC::value; ++u) {
+            const double e0 = (double)x[u].x - (double)y[u].x, e1 = (double)x[u].y - (double)y[u].y;
+            const double e2 = (double)x[u].z - (double)y[u].z, e3 = (double)x[u].w - (double)y[u].w;
+            a += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+          }
+        }
+        j0 = d4 * 4;
+      }
+      for (int64_t j = j0 + threadIdx.x; j < p.d; j += 256) {
+        const double df = (double)qr[j] - (double)gr[j];
+        a += df * df;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    double* rr = red2[rb];
+    rb ^= 1;
+    if (lane == 0) rr[wave] = a;
+    __syncthreads();
+    return (rr[0] + rr[1]) + (rr[2] + rr[3]);
   };
   if (p.mode == 2) {   // the selection of a mode-1 launch
     if (threadIdx.x < KC) lists[threadIdx.x] = p.sel[q * KC + threadIdx.x];
@@ -1996,10 +2075,19 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
         // candidates do (round 6) -- k real rows of this shard lie that close, so the k-th smallest
         // of these over the shards bounds the global k-th; the other shards' candidates whose prefix
         // lower bound exceeds it are then never re-ranked (mode 2)
-        for (int c = wave; c < kk; c += 4) {
-          const Cand cc = lists[c];
-          const double a = cc.i != CAND_EMPTY && !overflow ? exact_d2(cc) : __builtin_inf();
-          if (lane == 0) exact[c] = a;
+        if constexpr (COOP) {
+          if (qres) load_query();
+          for (int c = 0; c < kk; ++c) {   // block-uniform: lists (after a barrier) and overflow
+            const Cand cc = lists[c];
+            const double a = cc.i != CAND_EMPTY && !overflow ? exact_block(cc.i) : __builtin_inf();
+            if (threadIdx.x == 0) exact[c] = a;
+          }
+        } else {
+          for (int c = wave; c < kk; c += 4) {
+            const Cand cc = lists[c];
+            const double a = cc.i != CAND_EMPTY && !overflow ? exact_d2(cc) : __builtin_inf();
+            if (lane == 0) exact[c] = a;
+          }
         }
         __syncthreads();
       }
@@ -2049,7 +2137,42 @@ __global__ void __launch_bounds__(256) merge_kernel(MergeArgs p) {
   // wave); stop once the next candidate's lower bound exceeds the k-th exact distance so far:
   // it and every later one (and every row outside the list) are strictly farther
   int nevals = 0;   // candidates re-ranked exactly (wave 0's count; MergeArgs::evals)
-  for (int r = 0; r < KC / 4 && !skip_all; ++r) {
+  if constexpr (COOP) {
+    // one candidate at a time; lane c of every wave keeps exact[c] (mine), so the stop test needs no
+    // LDS round trip: the same test as the wave form's, after every candidate
+    double mine = __builtin_inf(), best = __builtin_inf();
+    if (qres && !skip_all) load_query();
+    int c = 0;
+    for (; c < KC && !skip_all; ++c) {
+      const Cand cc = lists[c];   // block-uniform
+      if (cc.i == CAND_EMPTY) break;   // every later one is empty too
+      if (c > 0) {
+        double lim = ubq;
+        if (c >= kk) {
+          double kth = best;
+          if (kk > 1) {   // the kk-th smallest of exact[0..c): lane t ranks its value among them
+            const double v = lane < c ? mine : __builtin_inf();
+            int lt = 0, le = 0;
+            for (int u = 0; u < c; ++u) {
+              const double e = __shfl(mine, u);
+              lt += e < v;
+              le += e <= v;
+            }
+            const uint64_t m = __ballot(lane < c && lt < kk && kk <= le);
+            kth = m ? __shfl(v, __ffsll((long long)m) - 1) : __builtin_inf();
+          }
+          lim = fmin(kth * kth, ubq);
+        }
+        if (d2_lower((double)cc.d) > lim) break;
+      }
+      const double e = sqrt(exact_block(cc.i));
+      if (lane == c) mine = e;
+      best = fmin(best, e);
+      ++nevals;
+    }
+    if (wave == 0 && lane < KC) exact[lane] = lane < c ? mine : __builtin_inf();
+  }
+  for (int r = 0; r < (COOP ? 0 : KC / 4) && !skip_all; ++r) {
     const int c = 4 * r + wave;
     const Cand cc = lists[c];
     const double a = cc.i != CAND_EMPTY ? exact_d2(cc) : 0.0;
@@ -2527,6 +2650,17 @@ static int q8_tiles(hipStream_t st, q8s::TileArgs a) {
   return OFR_OK;
 }
 
+// the merge's re-rank form (OFR_MERGE_ENGINE: 1 = one wave per candidate, four per round, probe;
+// default the block-cooperative form)
+template <bool SMALL>
+static void launch_merge(hipStream_t st, const q8s::MergeArgs& m) {
+  const char* e = getenv("OFR_MERGE_ENGINE");
+  if (e && e[0] == '1')
+    hipLaunchKernelGGL((q8s::merge_kernel<SMALL, false>), dim3((unsigned)m.B), dim3(256), 0, st, m);
+  else
+    hipLaunchKernelGGL((q8s::merge_kernel<SMALL, true>), dim3((unsigned)m.B), dim3(256), 0, st, m);
+}
+
 extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, int64_t ldq,
                           const int8_t* Qs, const float* qscale, const double* qstats, const float* G, int64_t N,
                           int64_t ldg, int64_t d, const int8_t* Gs, int64_t ld, const float* gscale,
@@ -2561,7 +2695,7 @@ extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, 
   if (phases & 2) {
     OFR_CHECK_ARG(out_d && out_i && cert, "ofr_knn_q8: null output");
     q8s::MergeArgs m{a.cand, a.ntg, B, Q, ldq, G, ldg, d, qstats, gmax, 0.0, k, index_base, out_d, out_i, cert, bound};
-    hipLaunchKernelGGL(q8s::merge_kernel<false>, dim3((unsigned)B), dim3(256), 0, st, m);
+    launch_merge<false>(st, m);
     OFR_LAUNCH_CHECK("q8 merge_kernel");
   }
   return OFR_OK;
@@ -3283,9 +3417,9 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       m.T = q8s::PM;
     }
     if (sieve)
-      hipLaunchKernelGGL(q8s::merge_kernel<true>, dim3((unsigned)B), dim3(256), 0, st, m);
+      launch_merge<true>(st, m);
     else
-      hipLaunchKernelGGL(q8s::merge_kernel<false>, dim3((unsigned)B), dim3(256), 0, st, m);
+      launch_merge<false>(st, m);
     OFR_LAUNCH_CHECK("f6 merge_kernel");
   }
   return OFR_OK;
