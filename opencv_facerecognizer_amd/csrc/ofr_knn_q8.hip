@@ -1521,6 +1521,10 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
         const float mx = __builtin_elementwise_maximum(mx3(t0, t1, t2), mx3(t3, t4, a3[3]));
         hitc |= !(mx < -th[c]) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
       }
+      if constexpr (OFR_PP_PROBE & 8) {   // probe: compares kept, hits dropped
+        if (hitc == 0xdeadu) asm volatile("" ::: "memory");
+        continue;
+      }
       if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform
         uint32_t lid = lane;   // laundered: the payloads are not hoisted out of the loops (spills)
         asm volatile("" : "+v"(lid));
@@ -2606,6 +2610,23 @@ static int64_t f6p_group(int64_t ntg, int64_t ntq, int cus) {
   return best;
 }
 
+// query steps per work item of the wave-decoupled prefix pass: the largest ceil(ntq / 2^j) that deals
+// every workgroup about 24 items or more, but 8 steps at least.  Swept at B = 4,096 on galleries of one
+// rank's share at G = 1/2/4/8 (profiles/r06_prefix_group_ab.txt): the best step counts were 16 / 8-16 / 8 /
+// 4-8; one item per workgroup (64 steps at N = 125k) measured 3x slower (0.45 vs 0.15 ms).
+static int64_t f6p_group_wave(int64_t ntg, int64_t ntq, int slots) {
+  if (const char* e = getenv("OFR_F6P_GROUP")) {   // probe override
+    const int64_t v = atoll(e);
+    if (v >= 1) return v < ntq ? v : ntq;
+  }
+  int64_t qg = ntq;
+  for (int64_t div = 1; div <= ntq; div *= 2) {
+    qg = (ntq + div - 1) / div;
+    if (ntg * ((ntq + qg - 1) / qg) >= 24 * (int64_t)slots || qg <= 8) break;
+  }
+  return qg;
+}
+
 static int64_t q8_min_ld(int slices, int64_t d) { return slices == 1 ? round_up(d, 128) : 2 * round_up(d, 64); }
 
 extern "C" int ofr_q8_quantize_rows(void* stream, int slices, const float* X, int64_t R, int64_t d, int64_t ldx,
@@ -3327,9 +3348,11 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         // the per-query table lives in the sample lists' region, dead once the thresholds are set
         OFR_CHECK_ARG((size_t)nq * sizeof(uint2) <= w.theta - w.lists, "ofr_knn_f6: workspace too small (prefix tables)");
         uint2* qtab = reinterpret_cast<uint2*>(wsb + w.lists);
-        hipLaunchKernelGGL(q8s::prefix_tables_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, theta, a.qscale, B,
-                           nq, qtab);
-        OFR_LAUNCH_CHECK("f6 prefix_tables_kernel");
+        if (f6p_engine() != 4) {
+          hipLaunchKernelGGL(q8s::prefix_tables_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, theta, a.qscale,
+                             B, nq, qtab);
+          OFR_LAUNCH_CHECK("f6 prefix_tables_kernel");
+        }
         const int slots = 2 * std::max(1, device_cus() - f6p_reserve());
         const int64_t qg = f6p_group(wa.ntg, nsteps, slots);
         const int64_t items = wa.ntg * cdiv(nsteps, qg);
@@ -3341,7 +3364,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
           hipLaunchKernelGGL(q8s::prefix_tables_kernel, dim3((unsigned)cdiv(nq4, 256)), dim3(256), 0, st, theta,
                              a.qscale, B, nq4, qtab);
           OFR_LAUNCH_CHECK("f6 prefix_tables_kernel");
-          const int64_t qg4 = f6p_group(wa.ntg, ns4, slots);
+          const int64_t qg4 = f6p_group_wave(wa.ntg, ns4, slots);
           const int64_t items4 = wa.ntg * cdiv(ns4, qg4);
           OFR_CHECK_ARG(items4 < 0x7fffffffLL, "ofr_knn_f6: grid too large");
           hipLaunchKernelGGL(q8s::prefix_wave_kernel, dim3((unsigned)std::min<int64_t>(items4, slots)), dim3(q8s::pw::NT),
