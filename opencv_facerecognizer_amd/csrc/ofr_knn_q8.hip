@@ -1428,6 +1428,8 @@ __device__ __forceinline__ i32x8 gfrag(__amdgpu_buffer_rsrc_t r, uint32_t pbase,
 // p.ntg = ceil(N / 256) gallery tiles; steps of 64 queries, ceil(B / 64); item w = (tile w / ngrp, steps
 // [qg (w % ngrp), ...)), dealt to the workgroups by stride; each wave walks the same items on its own.
 // qtab: prefix_tables_kernel's table over round_up(B, 64) queries (theta as a float, -inf past B; e_q).
+// PF: query steps in flight (1, the default: the next step's loads under this step's compares; 2: probe)
+template <int PF>
 __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const uint2* qtab, int64_t qg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1493,82 +1495,100 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
         t[c] = make_uint2((uint32_t)e[0], (uint32_t)e[1]);
       }
     };
-    pw::i32x8 B[4];
-    uint2 tb[4];
-    qload(s0, B, tb);
     uint32_t ncnt = 0;   // kept pairs of this item in the wave's list (uniform)
-    for (int64_t st = s0; st < s1; ++st) {
-      float th[4];
-      f6t::f32x4 acc[4][4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        th[c] = __uint_as_float(tb[c].x);
-        const int sbq = scs + (int)tb[c].y;   // block byte + e_q (in [0, 191]: no carry)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], B[c], Cin[i], 2, 2, 0, sa[i], 0, sbq);
-      }
-      if (st + 1 < s1) qload(st + 1, B, tb);   // the next step's operands, under this step's compares
-      uint32_t hitc = 0;
-      auto mx3 = [](float a, float b, float d) {
-        return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), d);
-      };
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const f6t::f32x4 &a0 = acc[0][c], &a1 = acc[1][c], &a2 = acc[2][c], &a3 = acc[3][c];
-        const float t0 = mx3(a0[0], a0[1], a0[2]), t1 = mx3(a0[3], a1[0], a1[1]), t2 = mx3(a1[2], a1[3], a2[0]);
-        const float t3 = mx3(a2[1], a2[2], a2[3]), t4 = mx3(a3[0], a3[1], a3[2]);
-        const float mx = __builtin_elementwise_maximum(mx3(t0, t1, t2), mx3(t3, t4, a3[3]));
-        hitc |= !(mx < -th[c]) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
-      }
-      if constexpr (OFR_PP_PROBE & 8) {   // probe: compares kept, hits dropped
-        if (hitc == 0xdeadu) asm volatile("" ::: "memory");
-        continue;
-      }
-      if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform
-        uint32_t lid = lane;   // laundered: the payloads are not hoisted out of the loops (spills)
-        asm volatile("" : "+v"(lid));
-        const uint32_t scr = pw::SCR + (uint32_t)wave * 4096u + (lid & 63u) * 16u;
-        const int rg4 = (int)(lid >> 4) * 4;
-#pragma unroll
+    // one step: its MFMAs on the fragments in B / tb, then the load of step st + PF into them (PF buffers in
+    // flight: the L2 latency of a step's 12 loads spans PF - 1 other steps' work), then the compares and hits
+    auto step = [&](int64_t st, pw::i32x8 (&B)[4], uint2 (&tb)[4]) {
+        float th[4];
+        f6t::f32x4 acc[4][4];
+  #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
-          const float nth = -th[c];
-          const int64_t q = st * pw::TQS + 16 * c + (int)(lid & 15u);
-          uint32_t hm = 0;   // rows j = 4 i + r of this lane that pass
-#pragma unroll
-          for (int j = 0; j < 16; ++j) hm |= !(acc[j >> 2][c][j & 3] < nth) ? (1u << j) : 0u;
-          hm &= q < p.B ? vmask : 0u;
-          if (hm) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              *reinterpret_cast<volatile OFR_LDS f6t::f32x4*>((uintptr_t)(scr + 1024u * i)) = acc[i][c];
-          }
-          for (;;) {   // wave-uniform: one kept row per lane and round
-            const bool act = hm != 0u;
-            const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
-            if (mk == 0) break;
-            if (act) {
-              const int j = __builtin_ctz(hm);
-              hm &= hm - 1u;
-              const float v = __uint_as_float(pp::lds_u32(scr + 1024u * (uint32_t)(j >> 2) + 4u * (uint32_t)(j & 3)));
-              const uint32_t kb = __float_as_uint(key_score(score_key(-v, 0)));
-              const int row = 16 * (j >> 2) + rg4 + (j & 3);   // of the wave's 64
-              const uint32_t slot = ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-              if (slot < (uint32_t)pw::HCAPW) {
-                f6t::i32x2 e;
-                e[0] = (int)kb;
-                e[1] = (int)(((uint32_t)q << 6) | (uint32_t)row);
-                *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
-              } else {   // the list is full (small galleries keep a large share): straight to the bucket
-                const int bs = atomicAdd(p.count + q, 1);
-                if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
-              }
+          th[c] = __uint_as_float(tb[c].x);
+          const int sbq = scs + (int)tb[c].y;   // block byte + e_q (in [0, 191]: no carry)
+  #pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], B[c], Cin[i], 2, 2, 0, sa[i], 0, sbq);
+        }
+        if (st + PF < s1) qload(st + PF, B, tb);   // the operands PF steps on, under this step's compares
+        if constexpr (OFR_PP_PROBE & 2) {   // probe: no compares (the MFMA results consumed by an empty asm)
+  #pragma unroll
+          for (int c = 0; c < 4; ++c)
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(acc[i][c]));
+          return;
+        }
+        uint32_t hitc = 0;
+        auto mx3 = [](float a, float b, float d) {
+          return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), d);
+        };
+  #pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const f6t::f32x4 &a0 = acc[0][c], &a1 = acc[1][c], &a2 = acc[2][c], &a3 = acc[3][c];
+          const float t0 = mx3(a0[0], a0[1], a0[2]), t1 = mx3(a0[3], a1[0], a1[1]), t2 = mx3(a1[2], a1[3], a2[0]);
+          const float t3 = mx3(a2[1], a2[2], a2[3]), t4 = mx3(a3[0], a3[1], a3[2]);
+          const float mx = __builtin_elementwise_maximum(mx3(t0, t1, t2), mx3(t3, t4, a3[3]));
+          hitc |= !(mx < -th[c]) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
+        }
+        if constexpr (OFR_PP_PROBE & 8) {   // probe: compares kept (their mask consumed by an empty asm), hits dropped
+          asm volatile("" ::"v"(hitc));
+          return;
+        }
+        if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform
+          uint32_t lid = lane;   // laundered: the payloads are not hoisted out of the loops (spills)
+          asm volatile("" : "+v"(lid));
+          const uint32_t scr = pw::SCR + (uint32_t)wave * 4096u + (lid & 63u) * 16u;
+          const int rg4 = (int)(lid >> 4) * 4;
+  #pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
+            const float nth = -th[c];
+            const int64_t q = st * pw::TQS + 16 * c + (int)(lid & 15u);
+            uint32_t hm = 0;   // rows j = 4 i + r of this lane that pass
+  #pragma unroll
+            for (int j = 0; j < 16; ++j) hm |= !(acc[j >> 2][c][j & 3] < nth) ? (1u << j) : 0u;
+            hm &= q < p.B ? vmask : 0u;
+            if (hm) {
+  #pragma unroll
+              for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<volatile OFR_LDS f6t::f32x4*>((uintptr_t)(scr + 1024u * i)) = acc[i][c];
             }
-            ncnt += (uint32_t)__builtin_popcountll(mk);
+            for (;;) {   // wave-uniform: one kept row per lane and round
+              const bool act = hm != 0u;
+              const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
+              if (mk == 0) break;
+              if (act) {
+                const int j = __builtin_ctz(hm);
+                hm &= hm - 1u;
+                const float v = __uint_as_float(pp::lds_u32(scr + 1024u * (uint32_t)(j >> 2) + 4u * (uint32_t)(j & 3)));
+                const uint32_t kb = __float_as_uint(key_score(score_key(-v, 0)));
+                const int row = 16 * (j >> 2) + rg4 + (j & 3);   // of the wave's 64
+                const uint32_t slot = ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                if (slot < (uint32_t)pw::HCAPW) {
+                  f6t::i32x2 e;
+                  e[0] = (int)kb;
+                  e[1] = (int)(((uint32_t)q << 6) | (uint32_t)row);
+                  *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
+                } else {   // the list is full (small galleries keep a large share): straight to the bucket
+                  const int bs = atomicAdd(p.count + q, 1);
+                  if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
+                }
+              }
+              ncnt += (uint32_t)__builtin_popcountll(mk);
+            }
           }
         }
+    };
+    pw::i32x8 B0[4], B1[4];
+    uint2 t0[4], t1[4];
+    qload(s0, B0, t0);
+    if constexpr (PF == 1) {
+      for (int64_t st = s0; st < s1; ++st) step(st, B0, t0);
+    } else {
+      if (s0 + 1 < s1) qload(s0 + 1, B1, t1);
+      for (int64_t st = s0; st < s1; st += 2) {
+        step(st, B0, t0);
+        if (st + 1 < s1) step(st + 1, B1, t1);
       }
     }
     // the item's kept pairs -> bucket slots and entries
@@ -3367,8 +3387,13 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
           const int64_t qg4 = f6p_group_wave(wa.ntg, ns4, slots);
           const int64_t items4 = wa.ntg * cdiv(ns4, qg4);
           OFR_CHECK_ARG(items4 < 0x7fffffffLL, "ofr_knn_f6: grid too large");
-          hipLaunchKernelGGL(q8s::prefix_wave_kernel, dim3((unsigned)std::min<int64_t>(items4, slots)), dim3(q8s::pw::NT),
-                             q8s::pw::LDS_BYTES, st, wa, qtab, qg4);
+          const dim3 g4((unsigned)std::min<int64_t>(items4, slots));
+          // probe OFR_F6P_PREFETCH=2: two steps in flight (242 VGPRs) measured equal (profiles/r06_prefix_wave_parts.txt)
+          const char* pf = getenv("OFR_F6P_PREFETCH");
+          if (pf && pf[0] == '2')
+            hipLaunchKernelGGL(q8s::prefix_wave_kernel<2>, g4, dim3(q8s::pw::NT), q8s::pw::LDS_BYTES, st, wa, qtab, qg4);
+          else
+            hipLaunchKernelGGL(q8s::prefix_wave_kernel<1>, g4, dim3(q8s::pw::NT), q8s::pw::LDS_BYTES, st, wa, qtab, qg4);
         } else if (f6p_engine() == 3)
           hipLaunchKernelGGL(q8s::prefix_pass_kernel<true>, dim3(grid), dim3(q8s::pp::NT), q8s::pp::LDS_BYTES, st, wa,
                              qtab, qg);
