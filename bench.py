@@ -143,7 +143,7 @@ def cpu_baseline(P, gallery, Xq, N_total, seconds):
 def sieve_engine(name):
     """Short name of the sieve-pass kernel a roofline / PMC record refers to (the committed traffic of one
     engine is never attributed to another)."""
-    for e in ("prefix_pass_kernel", "tile_kernel_f6p", "tile_kernel_f6w", "tile_kernel_f6s", "tile_kernel<1>",
+    for e in ("prefix_wave_kernel", "prefix_pass_kernel", "tile_kernel_f6p", "tile_kernel_f6w", "tile_kernel_f6s", "tile_kernel<1>",
               "knn_tile_kernel"):
         if e in (name or ""):
             return e

@@ -8,5 +8,5 @@ TAG=${1:-r02_final}
 BENCH_ARGS="${BENCH_ARGS:-}" TEST_TIMEOUT=700 BENCH_TIMEOUT=500 bash tools/gpu_round.sh $TAG || exit $?
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.txt 2>&1 || exit $?
 [ "${PROF:-1}" = "1" ] || exit 0
-bash tools/prof_search.sh || exit $?
+bash tools/prof_search.sh ${PROF_K:-} || exit $?
 echo "prof done: run python tools/pmc_summary.py $TAG locally after the merge"
