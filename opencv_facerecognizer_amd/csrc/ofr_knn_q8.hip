@@ -1403,12 +1403,10 @@ __global__ void __launch_bounds__(256, 2) prefix_pass_kernel(TileArgs p, const u
 // prefix_pass_kernel<true> into a wave-private LDS list, flushed to the buckets once per work item.
 namespace pw {
 constexpr int NT = 256;
-constexpr int TGR = 256;              // gallery rows per work item (one panel of the compact tiles)
-constexpr int TQS = 64;               // queries per step
 constexpr int HCAPW = 256;            // a wave's kept pairs per work item (~32 on gallery data; past it: atomics)
 constexpr int HITS = 0;               // [4][HCAPW] (key bits, query << 6 | row of the wave's 64)
-constexpr int SCR = HITS + 4 * HCAPW * 8;   // [4][4 KiB] a flagged column's 16 scores per lane
-constexpr int LDS_BYTES = SCR + 4 * 4096;
+constexpr int SCR = HITS + 4 * HCAPW * 8;   // [4][RB KiB] a flagged column's 4 RB scores per lane
+constexpr int lds_bytes(int rb) { return SCR + 4 * 1024 * rb; }
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 // the fragment of rows [row, row + 16) (lane l: row + l % 16, 32-feature block l / 16) of the 256-row panel at
@@ -1425,17 +1423,24 @@ __device__ __forceinline__ i32x8 gfrag(__amdgpu_buffer_rsrc_t r, uint32_t pbase,
 }
 }  // namespace pw
 
-// p.ntg = ceil(N / 256) gallery tiles; steps of 64 queries, ceil(B / 64); item w = (tile w / ngrp, steps
-// [qg (w % ngrp), ...)), dealt to the workgroups by stride; each wave walks the same items on its own.
-// qtab: prefix_tables_kernel's table over round_up(B, 64) queries (theta as a float, -inf past B; e_q).
+// RB row blocks of 16 gallery rows per wave, QB query blocks of 16 per step (RB x QB = 16 MFMAs per step):
+// <8, 2> = 128 rows x 32 queries (the default: half the query-fragment loads per MFMA of <4, 4>), <4, 4> =
+// 64 rows x 64 queries (OFR_F6P_WAVE=4).  An item is 4 RB 16 gallery rows (256 or 512: one or two panels of the compact
+// tiles) and a group of qg steps, ceil(N / (64 RB)) x ceil(nsteps / qg) items dealt to the workgroups by
+// stride; each wave walks the same items on its own.  qtab: prefix_tables_kernel's table over
+// round_up(B, 16 QB) queries (theta as a float, -inf past B; e_q).
 // PF: query steps in flight (1, the default: the next step's loads under this step's compares; 2: probe)
-template <int PF>
+template <int RB, int QB, int PF>
 __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const uint2* qtab, int64_t qg) {
+  static_assert((RB == 4 && QB == 4) || (RB == 8 && QB == 2), "wave tile shapes");
+  constexpr int WR = 16 * RB, TGI = 4 * WR, TQ = 16 * QB;   // rows per wave, rows per item, queries per step
+  constexpr int RSH = RB == 4 ? 6 : 7;                        // hit payload: (query << RSH) | row of the wave's
+  constexpr uint32_t WSCR = 1024u * RB;                       // the wave's LDS scratch (a column's scores)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t lane = threadIdx.x & 63;
-  const int64_t nsteps = (p.B + pw::TQS - 1) / pw::TQS;
-  const int64_t ngrp = (nsteps + qg - 1) / qg, items = p.ntg * ngrp;
+  const int64_t nsteps = (p.B + TQ - 1) / TQ, ntg = (p.N + TGI - 1) / TGI;
+  const int64_t ngrp = (nsteps + qg - 1) / qg, items = ntg * ngrp;
   if ((int64_t)blockIdx.x >= items) return;
   int scs;   // the lane's stage-0 block scale byte (its 32-feature block lane >> 4)
   {
@@ -1451,7 +1456,7 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
       (void*)p.Q, 0, (int)(f6t::panels(p.B) * qpb), 0x00020000);
   const __amdgpu_buffer_rsrc_t raux = __builtin_amdgcn_make_buffer_rsrc((void*)p.aux, 0, (int)(p.N * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc((void*)p.gscale, 0, (int)(p.N * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rtab = __builtin_amdgcn_make_buffer_rsrc((void*)qtab, 0, (int)(nsteps * pw::TQS * 8),
+  const __amdgpu_buffer_rsrc_t rtab = __builtin_amdgcn_make_buffer_rsrc((void*)qtab, 0, (int)(nsteps * TQ * 8),
                                                                          0x00020000);
   const uint32_t hits_a = pw::HITS + (uint32_t)wave * pw::HCAPW * 8u;   // the wave's kept pairs (LDS address)
   const int g4 = (int)(lane >> 4) * 4, r16 = (int)(lane & 15);
@@ -1459,19 +1464,19 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
   for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
     const int64_t gt = (int64_t)((uint32_t)w / ng32), s0 = (int64_t)(((uint32_t)w % ng32) * qg32);
     const int64_t s1 = s0 + qg < nsteps ? s0 + qg : nsteps;
-    const int64_t g0 = gt * pw::TGR + wave * 64;   // the wave's first row
-    const int nvalid = p.N - g0 < 64 ? (int)(p.N - g0) : 64;
-    if (nvalid <= 0) continue;   // uniform: the last tile's empty quarters
+    const int64_t g0 = gt * TGI + wave * WR;   // the wave's first row
+    const int nvalid = p.N - g0 < WR ? (int)(p.N - g0) : WR;
+    if (nvalid <= 0) continue;   // uniform: the last item's empty quarters
     // the item's gallery operands: A fragments of row blocks i, accumulator inputs -|g_m|^2 (-inf past N) of the
     // lane's output rows, operand scales block byte + e_g + 1 of the lane's A rows, the valid-row mask
-    pw::i32x8 A[4];
-    f6t::f32x4 Cin[4];
-    int sa[4];
+    pw::i32x8 A[RB];
+    f6t::f32x4 Cin[RB];
+    int sa[RB];
     uint32_t vmask = 0;
-    const uint32_t gpan = (uint32_t)(gt * gpb);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      A[i] = pw::gfrag(rg, gpan, (uint32_t)(wave * 64 + 16 * i), lane);
+    for (int i = 0; i < RB; ++i) {
+      const uint32_t wr = (uint32_t)(wave * WR + 16 * i);   // row of the item: panel wr >> 8, row wr & 255
+      A[i] = pw::gfrag(rg, (uint32_t)((gt * (TGI / 256) + (wr >> 8)) * gpb), wr & 255u, lane);
       const int rb = 16 * i + g4;
       const f6t::i32x4 a4 = __builtin_bit_cast(
           f6t::i32x4, __builtin_amdgcn_raw_buffer_load_b128(raux, (int)((g0 + rb) * 4), 0, 0));
@@ -1484,103 +1489,112 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
       const int eg = sb != 0u ? (int)((sb >> 23) & 0xffu) - 127 : 0;
       sa[i] = scs + eg + 1;   // block byte (64..127) + e_g (-64..64) + 1: in [1, 192]
     }
-    // the first step's query fragments and table entries (lane: query 64 s + 16 c + l % 16)
-    auto qload = [&](int64_t st, pw::i32x8 (&b)[4], uint2 (&t)[4]) {
-      const uint32_t qpan = (uint32_t)((st >> 2) * qpb), qrow = (uint32_t)((st & 3) * 64);
+    // a step's query fragments and table entries (lane: query TQ s + 16 c + l % 16)
+    auto qload = [&](int64_t st, pw::i32x8 (&b)[QB], uint2 (&t)[QB]) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        b[c] = pw::gfrag(rq, qpan, qrow + 16u * c, lane);
+      for (int c = 0; c < QB; ++c) {
+        const int64_t qr = st * TQ + 16 * c;   // panel qr >> 8, row qr & 255
+        b[c] = pw::gfrag(rq, (uint32_t)((qr >> 8) * qpb), (uint32_t)(qr & 255), lane);
         const f6t::i32x2 e = __builtin_bit_cast(
-            f6t::i32x2, __builtin_amdgcn_raw_buffer_load_b64(rtab, (int)((st * pw::TQS + 16 * c + r16) * 8), 0, 0));
+            f6t::i32x2, __builtin_amdgcn_raw_buffer_load_b64(rtab, (int)((qr + r16) * 8), 0, 0));
         t[c] = make_uint2((uint32_t)e[0], (uint32_t)e[1]);
       }
     };
     uint32_t ncnt = 0;   // kept pairs of this item in the wave's list (uniform)
     // one step: its MFMAs on the fragments in B / tb, then the load of step st + PF into them (PF buffers in
-    // flight: the L2 latency of a step's 12 loads spans PF - 1 other steps' work), then the compares and hits
-    auto step = [&](int64_t st, pw::i32x8 (&B)[4], uint2 (&tb)[4]) {
-        float th[4];
-        f6t::f32x4 acc[4][4];
-  #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          th[c] = __uint_as_float(tb[c].x);
-          const int sbq = scs + (int)tb[c].y;   // block byte + e_q (in [0, 191]: no carry)
-  #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], B[c], Cin[i], 2, 2, 0, sa[i], 0, sbq);
-        }
-        if (st + PF < s1) qload(st + PF, B, tb);   // the operands PF steps on, under this step's compares
-        if constexpr (OFR_PP_PROBE & 2) {   // probe: no compares (the MFMA results consumed by an empty asm)
-  #pragma unroll
-          for (int c = 0; c < 4; ++c)
-  #pragma unroll
-            for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(acc[i][c]));
-          return;
-        }
-        uint32_t hitc = 0;
-        auto mx3 = [](float a, float b, float d) {
-          return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), d);
-        };
-  #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+    // flight: the L2 latency of a step's loads spans PF - 1 other steps' work), then the compares and hits
+    auto step = [&](int64_t st, pw::i32x8 (&B)[QB], uint2 (&tb)[QB]) {
+      float th[QB];
+      f6t::f32x4 acc[RB][QB];
+#pragma unroll
+      for (int c = 0; c < QB; ++c) {
+        th[c] = __uint_as_float(tb[c].x);
+        const int sbq = scs + (int)tb[c].y;   // block byte + e_q (in [0, 191]: no carry)
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+          acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], B[c], Cin[i], 2, 2, 0, sa[i], 0, sbq);
+      }
+      if (st + PF < s1) qload(st + PF, B, tb);   // the operands PF steps on, under this step's compares
+      if constexpr (OFR_PP_PROBE & 2) {   // probe: no compares (the MFMA results consumed by an empty asm)
+#pragma unroll
+        for (int c = 0; c < QB; ++c)
+#pragma unroll
+          for (int i = 0; i < RB; ++i) asm volatile("" ::"v"(acc[i][c]));
+        return;
+      }
+      uint32_t hitc = 0;
+      auto mx3 = [](float a, float b, float d) {
+        return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), d);
+      };
+#pragma unroll
+      for (int c = 0; c < QB; ++c) {
+        float mx;
+        if constexpr (RB == 4) {
           const f6t::f32x4 &a0 = acc[0][c], &a1 = acc[1][c], &a2 = acc[2][c], &a3 = acc[3][c];
           const float t0 = mx3(a0[0], a0[1], a0[2]), t1 = mx3(a0[3], a1[0], a1[1]), t2 = mx3(a1[2], a1[3], a2[0]);
           const float t3 = mx3(a2[1], a2[2], a2[3]), t4 = mx3(a3[0], a3[1], a3[2]);
-          const float mx = __builtin_elementwise_maximum(mx3(t0, t1, t2), mx3(t3, t4, a3[3]));
-          hitc |= !(mx < -th[c]) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
+          mx = __builtin_elementwise_maximum(mx3(t0, t1, t2), mx3(t3, t4, a3[3]));
+        } else {
+          float t[RB];
+#pragma unroll
+          for (int i = 0; i < RB; ++i)
+            t[i] = mx3(acc[i][c][0], acc[i][c][1], __builtin_elementwise_maximum(acc[i][c][2], acc[i][c][3]));
+          mx = mx3(mx3(t[0], t[1], t[2]), mx3(t[3], t[4], t[5]), __builtin_elementwise_maximum(t[6], t[7]));
         }
-        if constexpr (OFR_PP_PROBE & 8) {   // probe: compares kept (their mask consumed by an empty asm), hits dropped
-          asm volatile("" ::"v"(hitc));
-          return;
-        }
-        if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform
-          uint32_t lid = lane;   // laundered: the payloads are not hoisted out of the loops (spills)
-          asm volatile("" : "+v"(lid));
-          const uint32_t scr = pw::SCR + (uint32_t)wave * 4096u + (lid & 63u) * 16u;
-          const int rg4 = (int)(lid >> 4) * 4;
-  #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
-            const float nth = -th[c];
-            const int64_t q = st * pw::TQS + 16 * c + (int)(lid & 15u);
-            uint32_t hm = 0;   // rows j = 4 i + r of this lane that pass
-  #pragma unroll
-            for (int j = 0; j < 16; ++j) hm |= !(acc[j >> 2][c][j & 3] < nth) ? (1u << j) : 0u;
-            hm &= q < p.B ? vmask : 0u;
-            if (hm) {
-  #pragma unroll
-              for (int i = 0; i < 4; ++i)
-                *reinterpret_cast<volatile OFR_LDS f6t::f32x4*>((uintptr_t)(scr + 1024u * i)) = acc[i][c];
-            }
-            for (;;) {   // wave-uniform: one kept row per lane and round
-              const bool act = hm != 0u;
-              const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
-              if (mk == 0) break;
-              if (act) {
-                const int j = __builtin_ctz(hm);
-                hm &= hm - 1u;
-                const float v = __uint_as_float(pp::lds_u32(scr + 1024u * (uint32_t)(j >> 2) + 4u * (uint32_t)(j & 3)));
-                const uint32_t kb = __float_as_uint(key_score(score_key(-v, 0)));
-                const int row = 16 * (j >> 2) + rg4 + (j & 3);   // of the wave's 64
-                const uint32_t slot = ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-                if (slot < (uint32_t)pw::HCAPW) {
-                  f6t::i32x2 e;
-                  e[0] = (int)kb;
-                  e[1] = (int)(((uint32_t)q << 6) | (uint32_t)row);
-                  *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
-                } else {   // the list is full (small galleries keep a large share): straight to the bucket
-                  const int bs = atomicAdd(p.count + q, 1);
-                  if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
-                }
+        hitc |= !(mx < -th[c]) ? (1u << c) : 0u;   // NaN theta ("keep every row") passes
+      }
+      if constexpr (OFR_PP_PROBE & 8) {   // probe: compares kept (their mask consumed by an empty asm), hits dropped
+        asm volatile("" ::"v"(hitc));
+        return;
+      }
+      if (__builtin_amdgcn_ballot_w64(hitc != 0u)) {   // uniform
+        uint32_t lid = lane;   // laundered: the payloads are not hoisted out of the loops (spills)
+        asm volatile("" : "+v"(lid));
+        const uint32_t scr = pw::SCR + (uint32_t)wave * WSCR + (lid & 63u) * 16u;
+        const int rg4 = (int)(lid >> 4) * 4;
+#pragma unroll
+        for (int c = 0; c < QB; ++c) {
+          if (!__builtin_amdgcn_ballot_w64((hitc >> c) & 1u)) continue;   // uniform
+          const float nth = -th[c];
+          const int64_t q = st * TQ + 16 * c + (int)(lid & 15u);
+          uint32_t hm = 0;   // rows j = 4 i + r of this lane that pass
+#pragma unroll
+          for (int j = 0; j < 4 * RB; ++j) hm |= !(acc[j >> 2][c][j & 3] < nth) ? (1u << j) : 0u;
+          hm &= q < p.B ? vmask : 0u;
+          if (hm) {
+#pragma unroll
+            for (int i = 0; i < RB; ++i)
+              *reinterpret_cast<volatile OFR_LDS f6t::f32x4*>((uintptr_t)(scr + 1024u * i)) = acc[i][c];
+          }
+          for (;;) {   // wave-uniform: one kept row per lane and round
+            const bool act = hm != 0u;
+            const uint64_t mk = __builtin_amdgcn_ballot_w64(act);
+            if (mk == 0) break;
+            if (act) {
+              const int j = __builtin_ctz(hm);
+              hm &= hm - 1u;
+              const float v = __uint_as_float(pp::lds_u32(scr + 1024u * (uint32_t)(j >> 2) + 4u * (uint32_t)(j & 3)));
+              const uint32_t kb = __float_as_uint(key_score(score_key(-v, 0)));
+              const int row = 16 * (j >> 2) + rg4 + (j & 3);   // of the wave's WR
+              const uint32_t slot = ncnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+              if (slot < (uint32_t)pw::HCAPW) {
+                f6t::i32x2 e;
+                e[0] = (int)kb;
+                e[1] = (int)(((uint32_t)q << RSH) | (uint32_t)row);
+                *reinterpret_cast<volatile OFR_LDS f6t::i32x2*>((uintptr_t)(hits_a + slot * 8u)) = e;
+              } else {   // the list is full (small galleries keep a large share): straight to the bucket
+                const int bs = atomicAdd(p.count + q, 1);
+                if (bs < p.cap) p.bucket[q * p.cap + bs] = Cand{__uint_as_float(kb), (int)(g0 + row)};
               }
-              ncnt += (uint32_t)__builtin_popcountll(mk);
             }
+            ncnt += (uint32_t)__builtin_popcountll(mk);
           }
         }
+      }
     };
-    pw::i32x8 B0[4], B1[4];
-    uint2 t0[4], t1[4];
+    pw::i32x8 B0[QB], B1[QB];
+    uint2 t0[QB], t1[QB];
     qload(s0, B0, t0);
     if constexpr (PF == 1) {
       for (int64_t st = s0; st < s1; ++st) step(st, B0, t0);
@@ -1595,9 +1609,9 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
     const uint32_t n = ncnt < (uint32_t)pw::HCAPW ? ncnt : (uint32_t)pw::HCAPW;
     for (uint32_t e = lane; e < n; e += 64u) {
       const uint2 hv = pp::lds_u2(hits_a + e * 8u);
-      const int64_t q = (int64_t)(hv.y >> 6);
+      const int64_t q = (int64_t)(hv.y >> RSH);
       const int slot = atomicAdd(p.count + q, 1);
-      if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(hv.x), (int)(g0 + (hv.y & 63u))};
+      if (slot < p.cap) p.bucket[q * p.cap + slot] = Cand{__uint_as_float(hv.x), (int)(g0 + (hv.y & (uint32_t)(WR - 1)))};
     }
   }
 }
@@ -2634,7 +2648,7 @@ static int64_t f6p_group(int64_t ntg, int64_t ntq, int cus) {
 // every workgroup about 24 items or more, but 8 steps at least.  Swept at B = 4,096 on galleries of one
 // rank's share at G = 1/2/4/8 (profiles/r06_prefix_group_ab.txt): the best step counts were 16 / 8-16 / 8 /
 // 4-8; one item per workgroup (64 steps at N = 125k) measured 3x slower (0.45 vs 0.15 ms).
-static int64_t f6p_group_wave(int64_t ntg, int64_t ntq, int slots) {
+static int64_t f6p_group_wave(int64_t ntg, int64_t ntq, int slots, int per_wg) {
   if (const char* e = getenv("OFR_F6P_GROUP")) {   // probe override
     const int64_t v = atoll(e);
     if (v >= 1) return v < ntq ? v : ntq;
@@ -2642,7 +2656,7 @@ static int64_t f6p_group_wave(int64_t ntg, int64_t ntq, int slots) {
   int64_t qg = ntq;
   for (int64_t div = 1; div <= ntq; div *= 2) {
     qg = (ntq + div - 1) / div;
-    if (ntg * ((ntq + qg - 1) / qg) >= 24 * (int64_t)slots || qg <= 8) break;
+    if (ntg * ((ntq + qg - 1) / qg) >= per_wg * (int64_t)slots || qg <= 8) break;
   }
   return qg;
 }
@@ -2972,7 +2986,7 @@ extern "C" const char* ofr_f6p_sieve_kernel(int pstages) {
       "16x16x128 fp6 MFMA)",
       "q8s::prefix_pass_kernel<true> (persistent one-stage prefix pass: two workgroups per CU, 64 x 128 wave tiles, "
       "16x16x128 fp6 MFMA with the row scales and -|g_m|^2 folded in: D = -score)",
-      "q8s::prefix_wave_kernel (persistent one-stage prefix pass, waves decoupled: 64 x 64 wave steps, query "
+      "q8s::prefix_wave_kernel (persistent one-stage prefix pass, waves decoupled: 128 x 32 wave steps, query "
       "fragments straight from L2, no barriers; 16x16x128 fp6 MFMA with the row scales and -|g_m|^2 folded in)"};
   if (pstages == 1 && f6_shape() == 384 && f6p_persistent() && f6p_engine() >= 2)
     return names[f6p_engine() - 1].c_str();
@@ -3378,22 +3392,32 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
         const int64_t items = wa.ntg * cdiv(nsteps, qg);
         OFR_CHECK_ARG(items < 0x7fffffffLL, "ofr_knn_f6: grid too large");
         const unsigned grid = (unsigned)std::min<int64_t>(items, slots);
-        if (f6p_engine() == 4) {   // wave-decoupled: 64-query steps, its own table length and grouping
-          const int64_t ns4 = cdiv(B, q8s::pw::TQS), nq4 = ns4 * q8s::pw::TQS;
+        if (f6p_engine() == 4) {   // wave-decoupled: its own step length, table length and grouping
+          // 128 gallery rows x 32 queries per wave step (default: half the query-fragment loads per MFMA,
+          // 0.51 -> 0.40 ms at 1M, profiles/r06_prefix_wave_shape_ab.txt); OFR_F6P_WAVE=4: 64 x 64
+          const char* wv = getenv("OFR_F6P_WAVE");
+          const bool w8 = !(wv && wv[0] == '4');
+          const int64_t tq = w8 ? 32 : 64, tgi = w8 ? 512 : 256;
+          const int64_t ns4 = cdiv(B, tq), nq4 = ns4 * tq, ntg4 = cdiv(N, tgi);
           OFR_CHECK_ARG((size_t)nq4 * sizeof(uint2) <= w.theta - w.lists, "ofr_knn_f6: workspace too small (prefix tables)");
           hipLaunchKernelGGL(q8s::prefix_tables_kernel, dim3((unsigned)cdiv(nq4, 256)), dim3(256), 0, st, theta,
                              a.qscale, B, nq4, qtab);
           OFR_LAUNCH_CHECK("f6 prefix_tables_kernel");
-          const int64_t qg4 = f6p_group_wave(wa.ntg, ns4, slots);
-          const int64_t items4 = wa.ntg * cdiv(ns4, qg4);
+          const int64_t qg4 = f6p_group_wave(ntg4, ns4, slots, w8 ? 12 : 24);
+          const int64_t items4 = ntg4 * cdiv(ns4, qg4);
           OFR_CHECK_ARG(items4 < 0x7fffffffLL, "ofr_knn_f6: grid too large");
           const dim3 g4((unsigned)std::min<int64_t>(items4, slots));
           // probe OFR_F6P_PREFETCH=2: two steps in flight (242 VGPRs) measured equal (profiles/r06_prefix_wave_parts.txt)
           const char* pf = getenv("OFR_F6P_PREFETCH");
-          if (pf && pf[0] == '2')
-            hipLaunchKernelGGL(q8s::prefix_wave_kernel<2>, g4, dim3(q8s::pw::NT), q8s::pw::LDS_BYTES, st, wa, qtab, qg4);
+          if (w8)
+            hipLaunchKernelGGL((q8s::prefix_wave_kernel<8, 2, 1>), g4, dim3(q8s::pw::NT), q8s::pw::lds_bytes(8), st, wa,
+                               qtab, qg4);
+          else if (pf && pf[0] == '2')
+            hipLaunchKernelGGL((q8s::prefix_wave_kernel<4, 4, 2>), g4, dim3(q8s::pw::NT), q8s::pw::lds_bytes(4), st, wa,
+                               qtab, qg4);
           else
-            hipLaunchKernelGGL(q8s::prefix_wave_kernel<1>, g4, dim3(q8s::pw::NT), q8s::pw::LDS_BYTES, st, wa, qtab, qg4);
+            hipLaunchKernelGGL((q8s::prefix_wave_kernel<4, 4, 1>), g4, dim3(q8s::pw::NT), q8s::pw::lds_bytes(4), st, wa,
+                               qtab, qg4);
         } else if (f6p_engine() == 3)
           hipLaunchKernelGGL(q8s::prefix_pass_kernel<true>, dim3(grid), dim3(q8s::pp::NT), q8s::pp::LDS_BYTES, st, wa,
                              qtab, qg);

@@ -40,8 +40,9 @@ ALLOWED = {
 # spills go to VGPR lanes (v_writelane), not memory.  The round-6 folded prefix pass spilled 531 VGPRs of
 # hoisted hit payloads until its lane index was laundered per column block.
 NO_SCRATCH = [
-    "void ofr::q8s::prefix_wave_kernel<1>(",
-    "void ofr::q8s::prefix_wave_kernel<2>(",
+    "void ofr::q8s::prefix_wave_kernel<4, 4, 1>(",
+    "void ofr::q8s::prefix_wave_kernel<4, 4, 2>(",
+    "void ofr::q8s::prefix_wave_kernel<8, 2, 1>(",
     "void ofr::q8s::prefix_pass_kernel<true>(",
     "void ofr::q8s::prefix_pass_kernel<false>(",
 ]
