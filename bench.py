@@ -214,8 +214,11 @@ class StepPipeline:
         # blocks: run beside the sieve pass, the merge held its CUs and the pass (whose work items are
         # dealt statically) ended with its last workgroups: 0.83 -> 1.59 ms for 0.47 ms of merge
         # (profiles/r06_merge_at_ab.txt).  "sieve": merge s-1 under sieve pass s (rounds 3-5).
+        # "sample": merge s-1 beside sample pass s (both behind preparation s), sieve pass s behind both, then
+        # preparation s+1 -- the short sample pass and the HBM-bound merge share the chip, everything else
+        # runs alone
         self.merge_at = merge_at or os.environ.get("OFR_BENCH_MERGE", "after")
-        assert self.merge_at in ("after", "sieve"), self.merge_at
+        assert self.merge_at in ("after", "sieve", "sample"), self.merge_at
         self.main = torch.cuda.current_stream(device)
         self.side = torch.cuda.Stream(device=device) if overlap else self.main
         self.ws = [Workspace() for _ in range(self.NWS)]
@@ -247,8 +250,13 @@ class StepPipeline:
     def _merge(self, s, ev):
         j, w = s % self.NBUF, s % self.NWS
         with torch.cuda.stream(self.side):
-            # behind the next batch's sample pass ("sieve") or its whole tile pass ("after")
-            self.side.wait_event(self.ev_sample if self.merge_at == "sieve" else self.ev_tiles)
+            # behind the next batch's sample pass ("sieve"), its preparation ("sample") or its whole tile pass
+            # ("after")
+            if self.merge_at == "sample":   # (the tile pass too: the last batch has no next preparation)
+                self.side.wait_event(self.ev_tiles)
+                self.side.wait_event(self.ev_ready[(s + 1) % self.NBUF])
+            else:
+                self.side.wait_event(self.ev_sample if self.merge_at == "sieve" else self.ev_tiles)
             if ev:
                 ev[5].record()
             self.merge_fn(j, self.ws[w])
@@ -269,18 +277,22 @@ class StepPipeline:
             self.main.wait_event(self.ev_merged[w])         # merge s-2 done with this workspace
             if ev[s]:
                 ev[s][4].record(self.main)
+            if s >= 1 and self.merge_at == "sample":        # merge s-1 beside sample pass s
+                self._merge(s - 1, ev[s - 1])
             self.tiles_fn(j, self.ws[w], "sample")
             self.ev_sample.record(self.main)
             if ev[s]:
                 ev[s][6].record(self.main)
             if s >= 1 and self.merge_at == "sieve":         # merge s-1 under sieve pass s
                 self._merge(s - 1, ev[s - 1])
+            if s >= 1 and self.merge_at == "sample":        # sieve pass s alone: behind merge s-1
+                self.main.wait_event(self.ev_merged[(s - 1) % self.NWS])
             self.tiles_fn(j, self.ws[w], "sieve")
             if ev[s]:
                 ev[s][2].record(self.main)
             self.ev_tiles.record(self.main)
-            if self.merge_at == "after":
-                if s >= 1:                                  # merge s-1 behind tile pass s
+            if self.merge_at in ("after", "sample"):
+                if s >= 1 and self.merge_at == "after":     # merge s-1 behind tile pass s
                     self._merge(s - 1, ev[s - 1])
                 if s + 1 < steps:                           # preparation s+1 behind that merge, on main
                     if s >= 1:
