@@ -1616,6 +1616,140 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
   }
 }
 
+// ---- the prefix tier's sample pass as a wave pass (round 6) -------------------------------------------
+// The sieve threshold of the prefix tier is the rank-th best prefix score (rank <= 2 here) over the row
+// sample (every 64th gallery row, the f6 tier's sample tiles and row scales, the prefix terms spaux).  The
+// 32x32x64 tile kernel with its top-16 epilogue took 0.09 ms for a 15.6k-row sample at B = 4,096 (992
+// workgroups, fixed costs per tile); here the prefix_wave_kernel<8, 2> layout -- each wave 128 sample rows
+// resident, 32-query steps from L2 -- with no hit path: per query column each lane keeps the two best of its
+// 32 scores, two shuffles combine the column's 4 lane groups, and the wave writes the (best, second) keys of
+// its 128 rows per query to keys[q][T] (T = ceil(Ns / 128)); sieve_threshold2_kernel takes the rank-th of
+// each query's 2 T keys.  The gallery scales are the f6 tier's (not powers of two): score = fma(-2 s_g, acc,
+// aux) after an MFMA with the block scales only, as prefix_pass_kernel<false>.
+namespace sw {
+constexpr int RB = 8, QB = 2, WR = 128, TGI = 512, TQ = 32;
+}
+__global__ void __launch_bounds__(256, 2) sample_wave_kernel(TileArgs p, uint2* keys, int64_t T, int64_t qg) {
+  using namespace sw;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63;
+  const int64_t nsteps = (p.B + TQ - 1) / TQ, ntg = (p.N + TGI - 1) / TGI;
+  const int64_t ngrp = (nsteps + qg - 1) / qg, items = ntg * ngrp;
+  if ((int64_t)blockIdx.x >= items) return;
+  int scs;   // the lane's stage-0 block scale byte (its 32-feature block lane >> 4)
+  {
+    const uint32_t r0 = f6t::sload_bscale(p.bs, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    scs = f6t::lane_byte(r0, 8u * (lane >> 4));
+  }
+  // the sample's and the queries' tiles: full-depth f6 tiled buffers (stage stride nk), stage 0 read
+  const int64_t pb = (int64_t)p.nk * f6t::PANEL;
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)p.G, 0, (int)(f6t::panels(p.N) * pb),
+                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)p.Q, 0, (int)(f6t::panels(p.B) * pb),
+                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t raux = __builtin_amdgcn_make_buffer_rsrc((void*)p.aux, 0, (int)(p.N * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc((void*)p.gscale, 0, (int)(p.N * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rqs = __builtin_amdgcn_make_buffer_rsrc((void*)p.qscale, 0, (int)(p.B * 4), 0x00020000);
+  const int g4 = (int)(lane >> 4) * 4, r16 = (int)(lane & 15);
+  const uint32_t ng32 = (uint32_t)ngrp, qg32 = (uint32_t)qg;
+  for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const int64_t gt = (int64_t)((uint32_t)w / ng32), s0 = (int64_t)(((uint32_t)w % ng32) * qg32);
+    const int64_t s1 = s0 + qg < nsteps ? s0 + qg : nsteps;
+    const int64_t g0 = gt * TGI + wave * WR;   // the wave's first sample row
+    const int nvalid = p.N - g0 < WR ? (int)(p.N - g0) : WR;
+    if (nvalid <= 0) continue;   // uniform
+    const int64_t tw = gt * 4 + wave;   // the wave's 128-row list index
+    pw::i32x8 A[RB];
+    float av[RB][4], tp[RB][4];   // the lane's output rows: prefix term (+inf past Ns), 2 s_g
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const uint32_t wr = (uint32_t)(wave * WR + 16 * i);
+      A[i] = pw::gfrag(rg, (uint32_t)((gt * (TGI / 256) + (wr >> 8)) * pb), wr & 255u, lane);
+      const int rb = 16 * i + g4;
+      const f6t::i32x4 a4 = __builtin_bit_cast(
+          f6t::i32x4, __builtin_amdgcn_raw_buffer_load_b128(raux, (int)((g0 + rb) * 4), 0, 0));
+      const f6t::i32x4 s4 = __builtin_bit_cast(
+          f6t::i32x4, __builtin_amdgcn_raw_buffer_load_b128(rsc, (int)((g0 + rb) * 4), 0, 0));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = rb + r < nvalid;
+        av[i][r] = ok ? __int_as_float(a4[r]) : __builtin_inff();
+        tp[i][r] = ok ? 2.0f * __int_as_float(s4[r]) : 0.0f;
+      }
+    }
+    auto qload = [&](int64_t st, pw::i32x8 (&b)[QB], int (&sq)[QB]) {
+#pragma unroll
+      for (int c = 0; c < QB; ++c) {
+        const int64_t qr = st * TQ + 16 * c;
+        b[c] = pw::gfrag(rq, (uint32_t)((qr >> 8) * pb), (uint32_t)(qr & 255), lane);
+        const uint32_t sb = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rqs, (int)((qr + r16) * 4), 0, 0);
+        sq[c] = scs + (sb != 0u ? (int)((sb >> 23) & 0xffu) - 127 : 0);   // block byte + e_q
+      }
+    };
+    pw::i32x8 B[QB];
+    int sq[QB];
+    qload(s0, B, sq);
+    const f6t::f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t st = s0; st < s1; ++st) {
+      f6t::f32x4 acc[RB][QB];
+#pragma unroll
+      for (int c = 0; c < QB; ++c)
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+          acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[i], B[c], zero, 2, 2, 0, scs, 0, sq[c]);
+      if (st + 1 < s1) qload(st + 1, B, sq);
+#pragma unroll
+      for (int c = 0; c < QB; ++c) {
+        float m1 = __builtin_inff(), m2 = __builtin_inff();   // the lane's two best scores
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = __builtin_fmaf(-tp[i][r], acc[i][c][r], av[i][r]);
+            m2 = fminf(m2, fmaxf(m1, x));
+            m1 = fminf(m1, x);
+          }
+#pragma unroll
+        for (int o = 16; o < 64; o <<= 1) {   // the column's 4 lane groups (rows 4 (l / 16) + ...)
+          const float b1 = __shfl_xor(m1, o), b2 = __shfl_xor(m2, o);
+          m2 = fminf(fmaxf(m1, b1), fminf(m2, b2));
+          m1 = fminf(m1, b1);
+        }
+        const int64_t q = st * TQ + 16 * c + r16;
+        if (lane < 16 && q < p.B) keys[q * T + tw] = make_uint2(score_key(m1, 0), score_key(m2, 0));
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t arm_token(int64_t B);   // below (the sieve's arm token)
+// Thresholds from sample_wave_kernel's key pairs: theta[q] = the rank-th (1 or 2) smallest of the query's 2 T
+// keys; resets the bucket counts and arms the sieve (as sieve_threshold_kernel).  One wave per query.
+__global__ void __launch_bounds__(256) sieve_threshold2_kernel(const uint2* keys, int64_t T, uint32_t* theta, int* count,
+                                                               int64_t B, int rank, uint32_t* armed) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *armed = arm_token(B);
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= B) return;
+  uint32_t k1 = KEY_NONE, k2 = KEY_NONE;
+  for (int64_t e = lane; e < T; e += 64) {
+    const uint2 v = keys[q * T + e];   // v.x <= v.y
+    k2 = umin(umax(k1, v.x), umin(k2, v.y));
+    k1 = umin(k1, v.x);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t b1 = (uint32_t)__shfl_xor((int)k1, o), b2 = (uint32_t)__shfl_xor((int)k2, o);
+    k2 = umin(umax(k1, b1), umin(k2, b2));
+    k1 = umin(k1, b1);
+  }
+  if (lane == 0) {
+    theta[q] = rank <= 1 ? k1 : k2;
+    count[q] = 0;
+  }
+}
+
 // ---- small batches (B <= 32): HBM-streaming fp6 pass --------------------------------------
 // One workgroup per 256-row gallery panel, wave w owns rows 32w..32w+31 against the (single)
 // 32-row query block, loading its fragments straight to VGPRs from the f6 tiled layout (each
@@ -3348,19 +3482,39 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
       }
       s.gg = s.ntg < q8s::GROUP_G ? s.ntg : q8s::GROUP_G;
       s.cand = reinterpret_cast<Cand*>(wsb + w.lists);
+      const bool prefix = a.nkp < f6t::stages(d);
+      const int rank = std::max(k, prefix && rows ? f6p_rank() : sieve_rank(rows));
+      // the prefix tier's one-stage sample as a wave pass (sample_wave_kernel; OFR_F6P_SAMPLE=tiles: the tile pass)
+      const char* spe = getenv("OFR_F6P_SAMPLE");
+      const bool swave = (phases & 4) && prefix && rows && a.nkp == 1 && !two && rank <= 2 && f6_shape() == 384 &&
+                         device_cus() > 0 && !(spe && spe[0] == 't');
       if (!(phases & 4)) {
         // sieve only: the thresholds of a preceding phases-4 call are in the workspace
+      } else if (swave) {
+        const int64_t T = cdiv(s.N, (int64_t)q8s::sw::WR);
+        OFR_CHECK_ARG((size_t)B * T * sizeof(uint2) <= w.theta - w.lists, "ofr_knn_f6: workspace too small (sample keys)");
+        uint2* skeys = reinterpret_cast<uint2*>(wsb + w.lists);
+        const int slots = 2 * std::max(1, device_cus());
+        const int64_t nst = cdiv(B, (int64_t)q8s::sw::TQ), ntgs = cdiv(s.N, (int64_t)q8s::sw::TGI);
+        const int64_t qgs = f6p_group_wave(ntgs, nst, slots, 12);
+        const int64_t itm = ntgs * cdiv(nst, qgs);
+        OFR_CHECK_ARG(itm < 0x7fffffffLL, "ofr_knn_f6: grid too large (sample)");
+        hipLaunchKernelGGL(q8s::sample_wave_kernel, dim3((unsigned)std::min<int64_t>(itm, slots)), dim3(256), 0, st, s,
+                           skeys, T, qgs);
+        OFR_LAUNCH_CHECK("f6p sample_wave_kernel");
+        hipLaunchKernelGGL(q8s::sieve_threshold2_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, skeys, T, theta,
+                           count, B, rank, armed);
+        OFR_LAUNCH_CHECK("f6p sieve_threshold2_kernel");
       } else if (two)
         hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW, 3>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
                            f6t::LDS, st, s);
       else
         hipLaunchKernelGGL((q8s::tile_kernel_f6<F6_NW>), dim3((unsigned)(s.ntq * s.ntg)), dim3(F6_NW * 64),
                            f6t::LDS, st, s);
-      if (phases & 4) {
+      if ((phases & 4) && !swave) {
         OFR_LAUNCH_CHECK("f6 tile_kernel (sieve sample)");
-        const bool prefix = a.nkp < f6t::stages(d);
         hipLaunchKernelGGL(q8s::sieve_threshold_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, s.cand, s.ntg,
-                           theta, count, B, std::max(k, prefix && rows ? f6p_rank() : sieve_rank(rows)), armed);
+                           theta, count, B, rank, armed);
         OFR_LAUNCH_CHECK("f6 sieve_threshold_kernel");
       }
       a.theta = theta;

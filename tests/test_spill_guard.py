@@ -43,6 +43,7 @@ NO_SCRATCH = [
     "void ofr::q8s::prefix_wave_kernel<4, 4, 1>(",
     "void ofr::q8s::prefix_wave_kernel<4, 4, 2>(",
     "void ofr::q8s::prefix_wave_kernel<8, 2, 1>(",
+    "ofr::q8s::sample_wave_kernel(",
     "void ofr::q8s::prefix_pass_kernel<true>(",
     "void ofr::q8s::prefix_pass_kernel<false>(",
 ]
