@@ -684,8 +684,13 @@ def main():
     gallery = build_gallery(P, bank, args.per_id, n0, nl, N, d, ld, device)
     gq = torch.Generator(device=device)
     gq.manual_seed(SEED + 7)
-    ids_q = torch.randint(0, n_ids, (B,), generator=gq, device=device)
-    Xq = bank.images(ids_q, seed=SEED + 99)
+    # one distinct query batch per pipeline buffer (identities and pixel noise differ): consecutive timed steps
+    # never replay the same faces (round 6; before, every step searched one fixed batch)
+    ids_qs, Xqs = [], []
+    for jb in range(StepPipeline.NBUF):
+        ids_qs.append(torch.randint(0, n_ids, (B,), generator=gq, device=device))
+        Xqs.append(bank.images(ids_qs[-1], seed=SEED + 99 + jb))
+    ids_q, Xq = ids_qs[0], Xqs[0]
     Qd = torch.zeros((B, ld), dtype=torch.float32, device=device)
     out = (torch.empty((B, k), dtype=torch.float64, device=device), torch.empty((B, k), dtype=torch.int64, device=device))
     torch.cuda.synchronize()
@@ -717,7 +722,7 @@ def main():
         """Query batch -> centred fp32 search rows (+ the first tier's quantized rows) in buffer j."""
         b = bufs[j]
         if shard_prep:
-            P.project(Xq[b0:b1], shift64=gallery.shift64, out=b["Qd_loc"])   # this rank's faces
+            P.project(Xqs[j][b0:b1], shift64=gallery.shift64, out=b["Qd_loc"])   # this rank's faces
             if use_q8:
                 tier = gallery.start_tier(B) if tier0 == "f6" else tier0
                 starts.append(str(tier))
@@ -729,7 +734,7 @@ def main():
             else:
                 b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
         else:
-            P.project(Xq, shift64=gallery.shift64, out=b["Qd"])          # fp32(W^T x - c), exact int8 MFMA
+            P.project(Xqs[j], shift64=gallery.shift64, out=b["Qd"])      # fp32(W^T x - c), exact int8 MFMA
             if use_q8:       # the adaptive start tier (FloatGallery.start_tier; f6 here)
                 tier = gallery.start_tier(B) if tier0 == "f6" else tier0
                 starts.append(str(tier))
@@ -795,7 +800,7 @@ def main():
     ms_sieve = np.mean([e[6].elapsed_time(e[2]) for e in ev])     # its sieve pass (fp6; else the rest)
     ms_merge = np.mean([e[5].elapsed_time(e[3]) for e in ev])     # merge + certificate on the side stream
     idx = res[1][:, 0]
-    acc = float(((idx // args.per_id) == ids_q).double().mean().item())
+    acc = float(((idx // args.per_id) == ids_qs[last]).double().mean().item())   # the last batch's identities
     kept = (gallery.sieve_counts(B, pipe.ws[(args.steps - 1) % StepPipeline.NWS]) if args.search == "f6"
             else None)                                                  # last step's fp6 sieve (this rank)
     kept = None if kept is None else {"mean": float(kept.double().mean()), "max": int(kept.max()),
@@ -933,7 +938,7 @@ def main():
                       f" -- prefix tier f6p: coarse scores of the first {128 * pst} features, certified by the "
                       f"projection bound" if pst else ""),
                       "q8": "i8 (int8 MFMA coarse scores, certified; fp64 exact re-rank)",
-                      "fp32": "f32 (fp32 MFMA scores, fp64 exact re-rank)"}[args.search], "data": "synthetic",
+                      "fp32": "f32 (fp32 MFMA scores, fp64 exact re-rank)"}[args.search], "data": "synthetic", "query_batches_cycled": StepPipeline.NBUF,
             "config": {"workload": "configs[2]: Fisherfaces projection + 1-NN, 1M-image gallery (100k ids x 10), "
                                    "100x100 faces, d=9999, B=4096 queries/step, Euclidean, k=1, W = "
                                    + ("Fisherfaces() trained on configs[1]'s 100k faces (10k ids x 10)"
