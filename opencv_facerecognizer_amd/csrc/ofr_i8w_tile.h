@@ -25,6 +25,11 @@
 #pragma once
 #include "ofr_common.h"
 
+// OFR_PROJ_PROBE (probe builds only, tools/build_proj_probes.sh; results WRONG, timing only): bit 1 no barriers
+// in the main loop, bit 2 no stage copies in the main loop, bit 4 no fragment reads in the main loop
+#ifndef OFR_PROJ_PROBE
+#define OFR_PROJ_PROBE 0
+#endif
 namespace ofr {
 namespace i8w {
 
@@ -151,27 +156,28 @@ __device__ __forceinline__ void mainloop(const Feed& f, int nk, i32x4 (&acc)[NA]
     auto row = [&](auto ii) {
       constexpr int i = decltype(ii)::value;
       constexpr bool AG = i < NAA;
+      constexpr bool BAR = !(OFR_PROJ_PROBE & 1), CPY = !(OFR_PROJ_PROBE & 2);
       if constexpr (i == 2) {   // barrier A: B(s) consumed (its reads, rows 22-23 of s - 1, are older than row 0's)
         asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if constexpr (BAR) __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (i == NA - 2) {   // barrier B: A(s+1), B(s+1) landed; A(s) consumed
         wait_vm<APW + BPW>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if constexpr (BAR) __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (i % 4 == 0 && i <= 12) acopy<W, (i % 4 == 0 && i <= 12 ? 2 + i / 4 : 0)>(f, va, g2, k2);
-      if constexpr (i % 4 == 2 && i <= 14) bcopy<W, (i % 4 == 2 && i <= 14 ? i / 4 : 0)>(f, vb, q0, k2);
-      if constexpr (i == NA - 2) acopy<W, 0>(f, va, g0, k3);
+      if constexpr (CPY && i % 4 == 0 && i <= 12) acopy<W, (i % 4 == 0 && i <= 12 ? 2 + i / 4 : 0)>(f, va, g2, k2);
+      if constexpr (CPY && i % 4 == 2 && i <= 14) bcopy<W, (i % 4 == 2 && i <= 14 ? i / 4 : 0)>(f, vb, q0, k2);
+      if constexpr (CPY && i == NA - 2) acopy<W, 0>(f, va, g0, k3);
       if constexpr (i == NA - 1) {
         // rows 22 and 23 run together (below)
       } else if constexpr (i == NA - 2) {
         a[0] = frag<0>(an);   // s + 1's A[0] into A[21]'s slot
         mfma<false>(a[1], b[0], acc[22][0]); mfma<false>(a[2], b[0], acc[23][0]); b[0] = frag<W * 64 + 0>(bn);
         mfma<false>(a[1], b[1], acc[22][1]); mfma<false>(a[2], b[1], acc[23][1]); b[1] = frag<W * 64 + 16>(bn);
-        acopy<W, 1>(f, va, g0, k3);
+        if constexpr (CPY) acopy<W, 1>(f, va, g0, k3);
         mfma<false>(a[1], b[2], acc[22][2]); mfma<false>(a[2], b[2], acc[23][2]); b[2] = frag<W * 64 + 32>(bn);
         mfma<false>(a[1], b[3], acc[22][3]); mfma<false>(a[2], b[3], acc[23][3]); b[3] = frag<W * 64 + 48>(bn);
         a[1] = frag<16>(an);  // s + 1's A[1] into A[22]'s slot
