@@ -1889,7 +1889,12 @@ struct MergeArgs {
   // bounds nothing from above (no ub_local).
   int64_t dpre;
   int* evals;   // optional [B]: candidates re-ranked exactly per query (the merge's bytes: evals x d x 4)
+  // deep continuation (round 6; sieve buckets, mode 0, the block-cooperative re-rank): a query the best 16
+  // candidates do not certify re-ranks the bucket's next 16 by key, and so on (at most DEEP_ROUNDS), until
+  // its k-th exact distance clears the bound of the rows it has not re-ranked or the bucket runs out
+  int deep;
 };
+constexpr int DEEP_ROUNDS = 32;
 
 // Best KC (distance, index) of the n candidates at src (16-byte aligned) into lists[0..KC),
 // ascending; one 256-thread block.  16 B per lane and load (two candidates), fully coalesced,
@@ -1948,6 +1953,48 @@ __device__ __forceinline__ void block_best_small(const Cand* src, int64_t n, Can
   for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
     const Cand c = src[e];
     if (better_f(c.d, c.i, L.d[KC - 1], L.i[KC - 1])) L.insert(c.d, c.i);
+  }
+  for (int off = 1; off < 64; off <<= 1) {
+    float od[KC];
+    int oi[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      od[j] = __shfl_xor(L.d[j], off);
+      oi[j] = __shfl_xor(L.i[j], off);
+    }
+    L.merge(od, oi);
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0 && wave > 0) {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) lists[wave * KC + j] = Cand{L.d[j], L.i[j]};
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      float od[KC];
+      int oi[KC];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        od[j] = lists[w * KC + j].d;
+        oi[j] = lists[w * KC + j].i;
+      }
+      L.merge(od, oi);
+    }
+#pragma unroll
+    for (int j = 0; j < KC; ++j) lists[j] = Cand{L.d[j], L.i[j]};
+  }
+  __syncthreads();
+}
+
+// block_best_small over the entries strictly after `after` in (distance, index) order: the next KC (the deep
+// continuation of the merge walks a bucket 16 candidates at a time)
+__device__ __forceinline__ void block_best_small_after(const Cand* src, int64_t n, Cand* lists, Cand after) {
+  TopList<KC> L;
+  L.init();
+  for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+    const Cand c = src[e];
+    if (better_f(after.d, after.i, c.d, c.i) && better_f(c.d, c.i, L.d[KC - 1], L.i[KC - 1])) L.insert(c.d, c.i);
   }
   for (int off = 1; off < 64; off <<= 1) {
     float od[KC];
@@ -2309,6 +2356,7 @@ __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
   // wave); stop once the next candidate's lower bound exceeds the k-th exact distance so far:
   // it and every later one (and every row outside the list) are strictly farther
   int nevals = 0;   // candidates re-ranked exactly (wave 0's count; MergeArgs::evals)
+  bool deep_need = false;   // the first 16 candidates, all re-ranked, do not certify (block-uniform)
   if constexpr (COOP) {
     // one candidate at a time; lane c of every wave keeps exact[c] (mine), so the stop test needs no
     // LDS round trip: the same test as the wave form's, after every candidate
@@ -2343,6 +2391,28 @@ __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
       ++nevals;
     }
     if (wave == 0 && lane < KC) exact[lane] = lane < c ? mine : __builtin_inf();
+    if constexpr (SMALL) {
+      // every thread decides alike from its registers (no barrier on the common, certified path): a stop
+      // before the 16th candidate certifies, an exhausted bucket cannot continue
+      if (p.deep && p.count && p.theta && p.mode == 0 && !overflow && !skip_all && c == KC) {
+        double kth = best;
+        if (kk > 1) {
+          const double v = mine;
+          int lt = 0, le = 0;
+          for (int u = 0; u < KC; ++u) {
+            const double e = __shfl(mine, u);
+            lt += e < v;
+            le += e <= v;
+          }
+          const uint64_t m = __ballot(lane < KC && lt < kk && kk <= le);
+          kth = m ? __shfl(v, __ffsll((long long)m) - 1) : __builtin_inf();
+        }
+        uint32_t tk = lists[KC - 1].i != CAND_EMPTY ? score_key(lists[KC - 1].d, 0) : KEY_NONE;
+        tk = umin(tk, p.theta[q]);
+        const double bnd = tk != KEY_NONE ? d2_lower((double)key_score(tk)) : __builtin_inf();
+        deep_need = !(kth == kth && kth * kth < bnd) && lists[KC - 1].i != CAND_EMPTY;
+      }
+    }
   }
   for (int r = 0; r < (COOP ? 0 : KC / 4) && !skip_all; ++r) {
     const int c = 4 * r + wave;
@@ -2381,6 +2451,85 @@ __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
       break;
     }
   }
+  uint32_t tk_deep = 0;   // the deep continuation's bound key (min(16th key of its last round, theta))
+  bool deep_ran = false;
+  if constexpr (SMALL && COOP) {
+    if (deep_need) {
+      __shared__ Cand run_l[KC];          // the best KC re-ranked so far, ascending by (distance, row)
+      __shared__ double run_e[KC];
+      __shared__ int dstate;
+      __shared__ uint32_t dtk;
+      // wave 0: run <- the best KC of run (unless fresh) and (lists, exact), by (distance, row)
+      auto merge_run = [&](bool fresh) {
+        double x = __builtin_inf();
+        int64_t xi = INT64_MAX;
+        if (lane < KC) {
+          if (!fresh && run_l[lane].i != CAND_EMPTY) {
+            x = run_e[lane];
+            xi = run_l[lane].i;
+          }
+        } else if (lane < 2 * KC) {
+          const Cand cc = lists[lane - KC];
+          if (cc.i != CAND_EMPTY && exact[lane - KC] == exact[lane - KC] && exact[lane - KC] < __builtin_inf()) {
+            x = exact[lane - KC];
+            xi = cc.i;
+          }
+        }
+        int rank = 0;
+        for (int u = 0; u < 2 * KC; ++u) {
+          const double y = __shfl(x, u);
+          const int64_t yi = __shfl(xi, u);
+          rank += better_d(y, yi, x, xi) || (y == x && yi == xi && u < lane);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 2 * KC && rank < KC) {
+          run_l[rank] = Cand{0.f, xi != INT64_MAX ? (int)xi : CAND_EMPTY};
+          run_e[rank] = x;
+        }
+      };
+      __syncthreads();   // exact[] of the first 16 written (wave 0)
+      if (wave == 0) merge_run(true);
+      __syncthreads();
+      for (int round = 0; round <= DEEP_ROUNDS; ++round) {
+        if (threadIdx.x == 0) {   // certified by the rows re-ranked so far?  (as the final certificate)
+          uint32_t tk = lists[KC - 1].i != CAND_EMPTY ? score_key(lists[KC - 1].d, 0) : KEY_NONE;
+          tk = umin(tk, p.theta[q]);
+          const double kth = run_l[kk - 1].i != CAND_EMPTY ? run_e[kk - 1] : __builtin_inf();
+          const double bnd = tk != KEY_NONE ? d2_lower((double)key_score(tk)) : __builtin_inf();
+          dtk = tk;
+          dstate = (kth == kth && kth * kth < bnd) ? 1 : (lists[KC - 1].i == CAND_EMPTY || round == DEEP_ROUNDS ? 2 : 0);
+        }
+        __syncthreads();
+        if (dstate != 0) break;   // block-uniform
+        deep_ran = true;
+        const Cand after = lists[KC - 1];
+        const double kth = run_l[kk - 1].i != CAND_EMPTY ? run_e[kk - 1] : __builtin_inf();
+        __syncthreads();   // every thread has `after` before the lists are replaced
+        block_best_small_after(p.cand + (size_t)q * p.cap, p.count[q], lists, after);
+        if (qres) load_query();   // re-read: the query registers are not live across the selection (spills)
+        double mine2 = __builtin_inf();
+        int c = 0;
+        for (; c < KC; ++c) {   // in key order, while a candidate's lower bound can still reach the k-th
+          const Cand cc = lists[c];
+          if (cc.i == CAND_EMPTY || d2_lower((double)cc.d) > kth * kth) break;
+          const double e = sqrt(exact_block(cc.i));
+          if (lane == c) mine2 = e;
+          ++nevals;
+        }
+        if (wave == 0 && lane < KC) exact[lane] = lane < c ? mine2 : __builtin_inf();
+        __syncthreads();
+        if (wave == 0) merge_run(false);
+        __syncthreads();
+      }
+      if (deep_ran) {   // the final sort takes the best KC re-ranked, the certificate the last round's bound
+        if (wave == 0 && lane < KC) {
+          lists[lane] = run_l[lane];
+          exact[lane] = run_e[lane];
+        }
+        tk_deep = dtk;
+      }
+    }
+  }
   __syncthreads();
   if (wave == 0) {
     double* od = p.out_d + q * p.k;
@@ -2395,6 +2544,7 @@ __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
     // A sharded search compares the GLOBAL k-th with every rank's bound instead (parallel.py).
     uint32_t tk = lists[KC - 1].i != CAND_EMPTY ? score_key(lists[KC - 1].d, 0) : KEY_NONE;
     if (p.theta) tk = umin(tk, p.theta[q]);
+    if (deep_ran) tk = tk_deep;
     double bnd = __builtin_inf();
     if (overflow) bnd = -__builtin_inf();   // the bucket dropped kept rows: no bound
     else if (tk != KEY_NONE) bnd = d2_lower((double)key_score(tk));
@@ -3626,6 +3776,11 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
     m.sel = reinterpret_cast<Cand*>(wsb + f6_ws_core(B, N));
     m.qd = reinterpret_cast<double*>(wsb + f6_ws_core(B, N) + f6_ws_qd(B));
     m.evals = reinterpret_cast<int*>(wsb + f6_ws_evals(B, N));
+    // the deep continuation (sieve buckets, the one-stage merge; OFR_MERGE_DEEP=0: off)
+    {
+      const char* e = getenv("OFR_MERGE_DEEP");
+      m.deep = sieve && merge_mode == 0 && !(e && e[0] == '0') ? 1 : 0;
+    }
     if (merge_mode == 1) m.ub_local = ub;
     if (merge_mode == 2) m.ub = ub;
     if (sieve) {

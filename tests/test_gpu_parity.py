@@ -346,10 +346,12 @@ def test_knn_f6x2_certifies_crowded_clusters(monkeypatch, k):
     """Clusters of 40 rows (sigma 0.5 around unit-variance centres, d = 128): the 16 candidates all lie
     in the query's cluster, within a fraction of the fp6 tier's bound of each other, so the fp6 tier
     certifies none; the two-slice tier (residual ~1/30 of fp6's) must certify them, with the oracle's
-    neighbours."""
+    neighbours.  The merge's deep continuation (round 6) would certify most of them at the fp6 tier
+    already (test_deep_merge_certifies_crowded_clusters): off here, so the tier chain runs."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
     monkeypatch.setenv("OFR_SEARCH", "auto")
+    monkeypatch.setenv("OFR_MERGE_DEEP", "0")
     r = _rng(3)
     d, K, per, B = 128, 200, 40, 300
     mu = r.normal(0, 1, (K, d))
@@ -361,6 +363,36 @@ def test_knn_f6x2_certifies_crowded_clusters(monkeypatch, k):
     assert fb[0] >= 0.9 * B and len(fb) >= 2 and fb[1] <= 0.02 * B, fb
     assert g.last_skipped.get("f6x2", 0) == 0
     _check_search("EuclideanDistance", Q, G, dd.cpu().numpy(), ii.cpu().numpy(), k)
+
+
+@pytest.mark.parametrize("k", [1, 4])
+def test_deep_merge_certifies_crowded_clusters(monkeypatch, k):
+    """The merge's deep continuation (round 6, merge_kernel MergeArgs::deep): on the crowded clusters
+    above, where the best 16 candidates never certify, the fp6 tier re-ranks each open query's bucket 16
+    candidates at a time until its k-th exact distance clears the bound of every row it has not re-ranked.
+    Most queries then certify at the first tier (k = 4 leaves 35 of 300 open on one box), and every answer
+    equals the tier chain's (deep off) and the oracle's."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(3)
+    d, K, per, B = 128, 200, 40, 300
+    mu = r.normal(0, 1, (K, d))
+    G = (mu[np.arange(K * per) % K] + r.normal(0, 0.5, (K * per, d))).astype(np.float32).astype(np.float64)
+    Q = (mu[r.integers(0, K, B)] + r.normal(0, 0.5, (B, d))).astype(np.float32).astype(np.float64)
+    res = {}
+    for deep in ("1", "0"):
+        monkeypatch.setenv("OFR_MERGE_DEEP", deep)
+        g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+        dd, ii = g.search(g.query_rows(Q), k)
+        res[deep] = (dd.cpu().numpy(), ii.cpu().numpy(), tuple(g.last_fallbacks))
+    assert res["0"][2][0] >= 0.9 * B, res["0"][2]                       # without: the fp6 tier certifies few
+    assert res["1"][2][0] <= 0.2 * B, res["1"][2]                       # with: most at the fp6 tier
+    # the same rows; distances equal up to the fp64 summation order of the exact pass that ended each query
+    # (the chain sends its last few queries to the fp32 pass, whose sum runs in another order)
+    assert np.array_equal(res["1"][1], res["0"][1])
+    np.testing.assert_allclose(res["1"][0], res["0"][0], rtol=1e-12, atol=0)
+    _check_search("EuclideanDistance", Q, G, res["1"][0], res["1"][1], k)
 
 
 def test_knn_f6_tier_certifies_separated_data(monkeypatch):
@@ -1017,10 +1049,11 @@ def test_knn_sharded_c_abi_one_device(monkeypatch, data):
     int8 x2, exact fp32), against the oracle.  'sphere' (equidistant rows) leaves every query
     uncertified by every quantized tier, forcing the exact pass; 'crowded' (tight clusters) is
     certified by f6x2 after fp6 fails -- with the same per-tier counts as the single-process
-    chain (FloatGallery.search)."""
+    chain (FloatGallery.search).  The merge's deep continuation is off: the chain is what runs here."""
     from opencv_facerecognizer_amd import _lib
     from opencv_facerecognizer_amd._device import FloatGallery
     from opencv_facerecognizer_amd.parallel import DeviceComm
+    monkeypatch.setenv("OFR_MERGE_DEEP", "0")
     r = _rng(41)
     if data == "separated":
         protos = r.normal(0, 30, (300, 96))
