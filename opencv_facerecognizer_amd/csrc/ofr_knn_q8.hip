@@ -1890,11 +1890,11 @@ struct MergeArgs {
   int64_t dpre;
   int* evals;   // optional [B]: candidates re-ranked exactly per query (the merge's bytes: evals x d x 4)
   // deep continuation (round 6; sieve buckets, mode 0, the block-cooperative re-rank): a query the best 16
-  // candidates do not certify re-ranks the bucket's next 16 by key, and so on (at most DEEP_ROUNDS), until
-  // its k-th exact distance clears the bound of the rows it has not re-ranked or the bucket runs out
+  // candidates do not certify re-ranks the bucket's next 16 by key, and so on (at most `deep` rounds), until
+  // its k-th exact distance clears the bound of the rows it has not re-ranked or the bucket runs out; 0: off
   int deep;
 };
-constexpr int DEEP_ROUNDS = 32;
+constexpr int DEEP_ROUNDS = 32;   // the default round cap
 
 // Best KC (distance, index) of the n candidates at src (16-byte aligned) into lists[0..KC),
 // ascending; one 256-thread block.  16 B per lane and load (two candidates), fully coalesced,
@@ -2490,14 +2490,14 @@ __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
       __syncthreads();   // exact[] of the first 16 written (wave 0)
       if (wave == 0) merge_run(true);
       __syncthreads();
-      for (int round = 0; round <= DEEP_ROUNDS; ++round) {
+      for (int round = 0; round <= p.deep; ++round) {
         if (threadIdx.x == 0) {   // certified by the rows re-ranked so far?  (as the final certificate)
           uint32_t tk = lists[KC - 1].i != CAND_EMPTY ? score_key(lists[KC - 1].d, 0) : KEY_NONE;
           tk = umin(tk, p.theta[q]);
           const double kth = run_l[kk - 1].i != CAND_EMPTY ? run_e[kk - 1] : __builtin_inf();
           const double bnd = tk != KEY_NONE ? d2_lower((double)key_score(tk)) : __builtin_inf();
           dtk = tk;
-          dstate = (kth == kth && kth * kth < bnd) ? 1 : (lists[KC - 1].i == CAND_EMPTY || round == DEEP_ROUNDS ? 2 : 0);
+          dstate = (kth == kth && kth * kth < bnd) ? 1 : (lists[KC - 1].i == CAND_EMPTY || round == p.deep ? 2 : 0);
         }
         __syncthreads();
         if (dstate != 0) break;   // block-uniform
@@ -3776,10 +3776,11 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
     m.sel = reinterpret_cast<Cand*>(wsb + f6_ws_core(B, N));
     m.qd = reinterpret_cast<double*>(wsb + f6_ws_core(B, N) + f6_ws_qd(B));
     m.evals = reinterpret_cast<int*>(wsb + f6_ws_evals(B, N));
-    // the deep continuation (sieve buckets, the one-stage merge; OFR_MERGE_DEEP=0: off)
+    // the deep continuation (sieve buckets, the one-stage merge; OFR_MERGE_DEEP=0: off, =N: N rounds at most)
     {
       const char* e = getenv("OFR_MERGE_DEEP");
-      m.deep = sieve && merge_mode == 0 && !(e && e[0] == '0') ? 1 : 0;
+      const int rounds = e && e[0] ? atoi(e) : q8s::DEEP_ROUNDS;
+      m.deep = sieve && merge_mode == 0 && rounds > 0 ? std::min(rounds, 4096) : 0;
     }
     if (merge_mode == 1) m.ub_local = ub;
     if (merge_mode == 2) m.ub = ub;

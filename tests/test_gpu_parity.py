@@ -381,8 +381,11 @@ def test_deep_merge_certifies_crowded_clusters(monkeypatch, k):
     G = (mu[np.arange(K * per) % K] + r.normal(0, 0.5, (K * per, d))).astype(np.float32).astype(np.float64)
     Q = (mu[r.integers(0, K, B)] + r.normal(0, 0.5, (B, d))).astype(np.float32).astype(np.float64)
     res = {}
-    for deep in ("1", "0"):
-        monkeypatch.setenv("OFR_MERGE_DEEP", deep)
+    for deep in ("1", "0"):   # "1": the default round cap (OFR_MERGE_DEEP unset)
+        if deep == "1":
+            monkeypatch.delenv("OFR_MERGE_DEEP", raising=False)
+        else:
+            monkeypatch.setenv("OFR_MERGE_DEEP", deep)
         g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
         dd, ii = g.search(g.query_rows(Q), k)
         res[deep] = (dd.cpu().numpy(), ii.cpu().numpy(), tuple(g.last_fallbacks))
