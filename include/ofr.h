@@ -219,6 +219,13 @@ size_t ofr_knn_f6_workspace_bytes(int64_t B, int64_t N);
  * HBM roofline                                                                                  */
 size_t ofr_knn_f6_merge_evals_offset(int64_t B, int64_t N);
 size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N);
+/* Round 6: the sieve's keep thresholds given instead of a sample pass -- per query the coarse-score bound
+ * smax[B] (fp64; NaN or +inf: keep every row), B > 32 -- for a following phases-8 (sieve) call on the same
+ * workspace: a query a tier left open is searched again keeping every row whose coarse score could still
+ * beat its k-th exact distance, smax = d_k^2 - |q|^2 + dS (FloatGallery._resieve), and the merge's deep
+ * continuation re-ranks those rows.  Replaces the same search as ofr_knn_f6 (classifier.py:104-119). */
+int ofr_knn_f6_set_thresholds(void* stream, const double* smax, int64_t B, int64_t N, void* workspace,
+                              size_t workspace_bytes);
 int ofr_f6_quantize_rows(void* stream, const float* X, int64_t R, int64_t d, int64_t ldx, void* tiles,
                          size_t tiles_bytes, float* scale, double* stats, const float* aux, double* maxima,
                          const uint8_t* bscale);

@@ -821,6 +821,8 @@ class FloatGallery:
         uncertified queries after each quantized tier that ran.  timings (a list, optional)
         receives (tier, queries, ms) per stage that ran (HIP events on the current stream)."""
         bad = open_rows(qq["cert"])
+        if qq["tier"] == "f6" and 0 < int(bad.numel()) <= self.RESIEVE_MAX and self.resieve_enabled():
+            bad = self._resieve(Qd, bad, k, out, index_base, qq)   # round 6: part of the fp6 tier
         counts = [int(bad.numel())]
         self.note_failures(qq["tier"], int(qq["B"]), counts[0])
         pending = {}                    # tier -> indices into the original batch waiting for it
@@ -858,6 +860,46 @@ class FloatGallery:
                 timings.append((str(tier), int(rows.numel()), ev[0].elapsed_time(ev[1])))
         self.last_fallbacks = tuple(counts)
         return counts[0]
+
+    # the fp6 tier's second sieve pass for the queries it left open (round 6): at most this many
+    RESIEVE_MAX = 256
+
+    @staticmethod
+    def resieve_enabled():
+        """OFR_RESIEVE=0 turns the fp6 tier's second sieve pass off (then also off when the merge's deep
+        continuation is: the second pass keeps rows for it to re-rank)."""
+        return os.environ.get("OFR_RESIEVE", "1") != "0" and os.environ.get("OFR_MERGE_DEEP", "32") != "0"
+
+    def _resieve(self, Qd, rows, k, out, index_base, qq):
+        """The fp6 tier again for the queries it left open (rows of the batch), keeping every gallery row
+        whose coarse score could still beat the query's k-th exact distance so far: smax = d_k^2 - |q|^2 + dS
+        (merge_kernel's d2_lower inverted, with 1e-9 of slack), set by ofr_knn_f6_set_thresholds instead of
+        the sample pass; the merge's deep continuation re-ranks the kept rows in key order until the
+        certificate holds.  A query whose sieve bucket overflows (32768 rows) stays open.  The batch is padded
+        to 33 rows (the sieve runs for B > 32; the pads repeat the first row).  Writes the results of the
+        queries it certifies into out and qq["cert"] / qq["bound"]; returns the rows still open."""
+        n = int(rows.numel())
+        pad = max(0, 33 - n)
+        prow = torch.cat([rows, rows[:1].expand(pad)]) if pad else rows
+        sub = Qd.index_select(0, prow).contiguous()
+        q2 = self.quantize_queries(sub, tier="f6")
+        dk = out[0].index_select(0, prow)[:, k - 1].double()
+        qn = (sub[:, : self.d].double() ** 2).sum(1)
+        dS = self._dS("f6", q2["stats"]) * (1.0 + 1e-6)
+        smax = (dk * dk - qn + dS) * (1.0 + 1e-9) + 1e-9 * (dk * dk + qn + dS)
+        smax = torch.where(torch.isfinite(smax), smax, torch.full_like(smax, float("inf")))
+        B2 = int(prow.numel())
+        lib = _lib.load()
+        ws = self.ws.get(lib.ofr_knn_f6_workspace_bytes(B2, self.N), Qd.device)
+        call("ofr_knn_f6_set_thresholds", stream(), ptr(smax), B2, self.N, ptr(ws), ws.numel())
+        d2, i2 = self.search_q8_phase(8 | 2, sub, q2, k, index_base, workspace=None)
+        ok = q2["cert"][:n] != 0
+        done = rows[ok]
+        out[0].index_copy_(0, done, d2[:n][ok])
+        out[1].index_copy_(0, done, i2[:n][ok])
+        qq["cert"].index_fill_(0, done, 1)
+        qq["bound"].index_copy_(0, done, q2["bound"][:n][ok])
+        return rows[~ok]
 
     # the k-th distance must clear the next tier's predicted bound by this factor of the bound's gain
     ROUTE_SLACK = 1.5

@@ -64,6 +64,7 @@ SIGNATURES = {
     "ofr_f6_sieve_kernel": (ctypes.c_char_p, []),
     "ofr_f6p_sieve_kernel": (ctypes.c_char_p, [c_int]),
     "ofr_knn_f6_sieve_counts_offset": (c_sz, [c_i64, c_i64]),
+    "ofr_knn_f6_set_thresholds": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_sz]),
     "ofr_f6_quantize_rows": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ofr_knn_f6": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp,
                            c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),

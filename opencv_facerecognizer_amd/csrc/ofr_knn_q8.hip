@@ -2098,6 +2098,29 @@ __global__ void __launch_bounds__(256) sieve_threshold_kernel(const Cand* lists,
 // and arms the flag).  A second sieve pass on the same thresholds (phases 8 called twice) would append
 // every kept row again, and duplicated candidates could certify a top-k that repeats one row: it is
 // made to overflow every bucket instead (uncertified, bound -inf).  One workgroup; disarms.
+// Given keep thresholds (round 6, ofr_knn_f6_set_thresholds): theta[q] = the smallest order key whose bucket's
+// lower end key_score(theta) is >= smax[q] (the sieve keeps every row whose coarse score is <= the upper end of
+// that bucket, and the certificate's bound from theta then covers smax); NaN or +inf: KEY_NONE (keep every row).
+// Resets the counts and arms one sieve pass of a B-query batch, as sieve_threshold_kernel does.
+__global__ void __launch_bounds__(256) set_thresholds_kernel(const double* smax, int64_t B, uint32_t* theta, int* count,
+                                                             uint32_t* armed) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *armed = arm_token(B);
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B) return;
+  const double v = smax[q];
+  uint32_t t = KEY_NONE;
+  if (v == v && v < 3.0e38) {
+    float f = (float)(v > -3.0e38 ? v : -3.0e38);
+    if ((double)f < v)   // the next float up
+      f = f == 0.0f ? __uint_as_float(1u) : __uint_as_float(__float_as_uint(f) + (f > 0.0f ? 1u : 0xffffffffu));
+    t = score_key(f, 0);
+    for (int it = 0; it < 2 && (double)key_score(t) < v && t < KEY_NONE - 0x1ffu; ++it) t += 0x100u;
+    if ((double)key_score(t) < v) t = KEY_NONE;
+  }
+  theta[q] = t;
+  count[q] = 0;
+}
+
 __global__ void __launch_bounds__(256) sieve_arm_kernel(uint32_t* armed, int* count, int64_t B, int cap) {
   // (a workspace never armed for this B holds anything: only the threshold kernel's token for B arms it;
   // uninitialised memory equals it with probability 2^-32)
@@ -3394,6 +3417,20 @@ extern "C" size_t ofr_knn_f6_merge_evals_offset(int64_t B, int64_t N) { return f
 
 extern "C" size_t ofr_knn_f6_sieve_counts_offset(int64_t B, int64_t N) {
   return B <= 32 ? (size_t)-1 : sieve_ws(B, N).count;
+}
+
+extern "C" int ofr_knn_f6_set_thresholds(void* stream, const double* smax, int64_t B, int64_t N, void* workspace,
+                                         size_t workspace_bytes) {
+  OFR_CHECK_ARG(B > 32 && N >= 1, "ofr_knn_f6_set_thresholds: the sieve runs for B > 32 (pad the batch)");
+  OFR_CHECK_ARG(smax && workspace, "ofr_knn_f6_set_thresholds: null pointer");
+  OFR_CHECK_ARG(workspace_bytes >= ofr_knn_f6_workspace_bytes(B, N), "ofr_knn_f6_set_thresholds: workspace too small");
+  const SieveWs w = sieve_ws(B, N);
+  char* wsb = reinterpret_cast<char*>(workspace);
+  hipLaunchKernelGGL(q8s::set_thresholds_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream, smax,
+                     B, reinterpret_cast<uint32_t*>(wsb + w.theta), reinterpret_cast<int*>(wsb + w.count),
+                     reinterpret_cast<uint32_t*>(wsb + w.armed));
+  OFR_LAUNCH_CHECK("set_thresholds_kernel");
+  return OFR_OK;
 }
 
 // the row sample of ofr_knn_f6_sampled

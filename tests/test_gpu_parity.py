@@ -398,6 +398,35 @@ def test_deep_merge_certifies_crowded_clusters(monkeypatch, k):
     _check_search("EuclideanDistance", Q, G, res["1"][0], res["1"][1], k)
 
 
+@pytest.mark.parametrize("k", [1, 4])
+def test_resieve_certifies_open_queries(monkeypatch, k):
+    """The fp6 tier's second sieve pass (round 6, FloatGallery._resieve + ofr_knn_f6_set_thresholds): for the
+    queries the deep merge leaves open (their buckets hold too few rows below the sample's threshold), a
+    sieve pass keeping every row whose coarse score could beat the k-th exact distance, then the deep merge
+    again.  On the crowded clusters: no more open queries than without it (usually none), the answers of the
+    tier chain and of the oracle."""
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    monkeypatch.delenv("OFR_MERGE_DEEP", raising=False)
+    r = _rng(3)
+    d, K, per, B = 128, 200, 40, 300
+    mu = r.normal(0, 1, (K, d))
+    G = (mu[np.arange(K * per) % K] + r.normal(0, 0.5, (K * per, d))).astype(np.float32).astype(np.float64)
+    Q = (mu[r.integers(0, K, B)] + r.normal(0, 0.5, (B, d))).astype(np.float32).astype(np.float64)
+    res = {}
+    for rs in ("1", "0"):
+        monkeypatch.setenv("OFR_RESIEVE", rs)
+        g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+        dd, ii = g.search(g.query_rows(Q), k)
+        res[rs] = (dd.cpu().numpy(), ii.cpu().numpy(), tuple(g.last_fallbacks))
+    print("open after fp6: resieve", res["1"][2], "without", res["0"][2])
+    assert res["1"][2][0] <= res["0"][2][0], (res["1"][2], res["0"][2])
+    assert np.array_equal(res["1"][1], res["0"][1])
+    np.testing.assert_allclose(res["1"][0], res["0"][0], rtol=1e-12, atol=0)
+    _check_search("EuclideanDistance", Q, G, res["1"][0], res["1"][1], k)
+
+
 def test_knn_f6_tier_certifies_separated_data(monkeypatch):
     """f6 tier on well-separated identities (integer prototypes, +-1 noise, 10 rows per identity so
     that the 16 candidates reach past the query's own identity): the fp6 tier alone must certify
