@@ -821,7 +821,7 @@ class FloatGallery:
         uncertified queries after each quantized tier that ran.  timings (a list, optional)
         receives (tier, queries, ms) per stage that ran (HIP events on the current stream)."""
         bad = open_rows(qq["cert"])
-        if qq["tier"] == "f6" and 0 < int(bad.numel()) <= self.RESIEVE_MAX and self.resieve_enabled():
+        if qq["tier"] == "f6" and 0 < int(bad.numel()) <= self.resieve_max() and self.resieve_enabled():
             bad = self._resieve(Qd, bad, k, out, index_base, qq)   # round 6: part of the fp6 tier
         counts = [int(bad.numel())]
         self.note_failures(qq["tier"], int(qq["B"]), counts[0])
@@ -863,6 +863,10 @@ class FloatGallery:
 
     # the fp6 tier's second sieve pass for the queries it left open (round 6): at most this many
     RESIEVE_MAX = 256
+
+    @classmethod
+    def resieve_max(cls):
+        return int(os.environ.get("OFR_RESIEVE_MAX", cls.RESIEVE_MAX))
 
     @staticmethod
     def resieve_enabled():
