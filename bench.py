@@ -881,8 +881,9 @@ def main():
             n_ev = float(ev_.double().sum())
             mb = n_ev * d * 4 + B * d * 4 + (float(kc.double().clamp(0, 32768).sum()) * 8 if kc is not None else 0.0)
             mm = float(np.median(ms_m))
-            merge_roof = {"kernel": "q8s::merge_kernel<true, true> (bucket best-16, exact fp64 re-rank of the "
-                                    "candidates by the whole block, one HBM round trip each, certificate)", "bound": "hbm", "ms_alone": mm,
+            merge_roof = {"kernel": "q8s::merge_kernel<true, true, false> (bucket best-16, exact fp64 re-rank of the "
+                                    "candidates by the whole block, one HBM round trip each, certificate) + "
+                                    "merge_kernel<true, true, true> (the deep continuation of open queries)", "bound": "hbm", "ms_alone": mm,
                           "exact_reranks_per_query": n_ev / B, "algorithmic_bytes": mb,
                           "achieved": mb / (mm * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                           "frac": mb / (mm * 1e-3) / PEAK_HBM}

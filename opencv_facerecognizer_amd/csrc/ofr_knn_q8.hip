@@ -2145,7 +2145,10 @@ __global__ void __launch_bounds__(256) sieve_arm_kernel(uint32_t* armed, int* co
 // after every candidate, not every fourth: one HBM round trip per re-rank, no query re-reads from L2.
 // The per-candidate sum order differs from the wave form (!COOP), so the two give distances within one
 // fp64 rounding of each other; one library uses one form for every tier.
-template <bool SMALL, bool COOP>
+// DEEP (sieve buckets, COOP): a second launch behind the plain one (launch_merge) for the queries it left
+// uncertified -- every other block returns at once -- which redoes the query's merge and then continues it
+// (MergeArgs::deep); kept out of the first launch, whose registers it would crowd (0.338 -> 0.364 ms).
+template <bool SMALL, bool COOP, bool DEEP = false>
 __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
   __shared__ Cand lists[(SMALL ? 4 : 256) * KC];
   __shared__ double exact[KC];
@@ -2153,6 +2156,9 @@ __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
   __shared__ double red2[2][4];
   __shared__ int stop_flag;
   const int64_t q = blockIdx.x;
+  if constexpr (DEEP) {   // certified, or a bucket that dropped rows: nothing to continue
+    if (p.cert[q] != 0 || !p.count || !p.theta || p.count[q] > p.cap || p.count[q] < 0) return;
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   bool overflow = false;
   const float* qr = p.Q + q * p.ldq;
@@ -2414,7 +2420,7 @@ __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
       ++nevals;
     }
     if (wave == 0 && lane < KC) exact[lane] = lane < c ? mine : __builtin_inf();
-    if constexpr (SMALL) {
+    if constexpr (SMALL && DEEP) {
       // every thread decides alike from its registers (no barrier on the common, certified path): a stop
       // before the 16th candidate certifies, an exhausted bucket cannot continue
       if (p.deep && p.count && p.theta && p.mode == 0 && !overflow && !skip_all && c == KC) {
@@ -2476,7 +2482,7 @@ __global__ void __launch_bounds__(256, COOP ? 4 : 1) merge_kernel(MergeArgs p) {
   }
   uint32_t tk_deep = 0;   // the deep continuation's bound key (min(16th key of its last round, theta))
   bool deep_ran = false;
-  if constexpr (SMALL && COOP) {
+  if constexpr (SMALL && COOP && DEEP) {
     if (deep_need) {
       __shared__ Cand run_l[KC];          // the best KC re-ranked so far, ascending by (distance, row)
       __shared__ double run_e[KC];
@@ -3017,10 +3023,15 @@ static int q8_tiles(hipStream_t st, q8s::TileArgs a) {
 template <bool SMALL>
 static void launch_merge(hipStream_t st, const q8s::MergeArgs& m) {
   const char* e = getenv("OFR_MERGE_ENGINE");
-  if (e && e[0] == '1')
+  if (e && e[0] == '1') {
     hipLaunchKernelGGL((q8s::merge_kernel<SMALL, false>), dim3((unsigned)m.B), dim3(256), 0, st, m);
-  else
-    hipLaunchKernelGGL((q8s::merge_kernel<SMALL, true>), dim3((unsigned)m.B), dim3(256), 0, st, m);
+    return;
+  }
+  hipLaunchKernelGGL((q8s::merge_kernel<SMALL, true>), dim3((unsigned)m.B), dim3(256), 0, st, m);
+  if constexpr (SMALL) {   // the deep continuation of what the plain merge left open (sieve buckets)
+    if (m.deep > 0 && m.mode == 0 && m.count && m.theta)
+      hipLaunchKernelGGL((q8s::merge_kernel<true, true, true>), dim3((unsigned)m.B), dim3(256), 0, st, m);
+  }
 }
 
 extern "C" int ofr_knn_q8(void* stream, int phases, int slices, const float* Q, int64_t B, int64_t ldq,
