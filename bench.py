@@ -217,8 +217,9 @@ class StepPipeline:
         # "sample": merge s-1 beside sample pass s (both behind preparation s), sieve pass s behind both, then
         # preparation s+1 -- the short sample pass and the HBM-bound merge share the chip, everything else
         # runs alone
+        # "prep": merge s-1 behind tile pass s on the side stream, beside preparation s+1 on the main one
         self.merge_at = merge_at or os.environ.get("OFR_BENCH_MERGE", "after")
-        assert self.merge_at in ("after", "sieve", "sample"), self.merge_at
+        assert self.merge_at in ("after", "sieve", "sample", "prep"), self.merge_at
         self.main = torch.cuda.current_stream(device)
         self.side = torch.cuda.Stream(device=device) if overlap else self.main
         self.ws = [Workspace() for _ in range(self.NWS)]
@@ -291,11 +292,11 @@ class StepPipeline:
             if ev[s]:
                 ev[s][2].record(self.main)
             self.ev_tiles.record(self.main)
-            if self.merge_at in ("after", "sample"):
-                if s >= 1 and self.merge_at == "after":     # merge s-1 behind tile pass s
+            if self.merge_at in ("after", "sample", "prep"):
+                if s >= 1 and self.merge_at in ("after", "prep"):   # merge s-1 behind tile pass s
                     self._merge(s - 1, ev[s - 1])
                 if s + 1 < steps:                           # preparation s+1 behind that merge, on main
-                    if s >= 1:
+                    if s >= 1 and self.merge_at != "prep":
                         self.main.wait_event(self.ev_merged[(s - 1) % self.NWS])
                     self.main.wait_event(self.ev_done[(s + 1) % self.NBUF])   # its buffer's fallback done
                     self._prep(s + 1, ev[s + 1], stream=self.main)

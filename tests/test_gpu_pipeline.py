@@ -32,7 +32,7 @@ def _setup(noise, N=20_000, d=512, side=32, per=10, B=512, batches=5):
     return P, g, X
 
 
-@pytest.mark.parametrize("merge_at", ["after", "sieve", "sample"])
+@pytest.mark.parametrize("merge_at", ["after", "sieve", "sample", "prep"])
 @pytest.mark.parametrize("noise", [12.0, 40.0])
 def test_step_pipeline_matches_one_shot(noise, merge_at):
     """noise 40: crowded identities, so the fallback tiers run inside finish() while the next tile
