@@ -427,6 +427,41 @@ def test_resieve_certifies_open_queries(monkeypatch, k):
     _check_search("EuclideanDistance", Q, G, res["1"][0], res["1"][1], k)
 
 
+def test_resieve_small_open_set_padding(monkeypatch):
+    """The second sieve pass on an open set smaller than the sieve's 33-query minimum (FloatGallery._resieve
+    pads it with repeats of its first query): 48 queries on the crowded clusters, the deep merge off so that
+    the fp6 tier leaves most of them open, then _resieve on the first 5 open rows only -- each certified
+    answer equals the oracle's, and the padded rows change nothing outside those 5."""
+    import torch
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import FloatGallery, open_rows
+    monkeypatch.setenv("OFR_SEARCH", "auto")
+    r = _rng(7)
+    d, K, per, B, k = 128, 200, 40, 48, 1
+    mu = r.normal(0, 1, (K, d))
+    G = (mu[np.arange(K * per) % K] + r.normal(0, 0.5, (K * per, d))).astype(np.float32).astype(np.float64)
+    Q = (mu[r.integers(0, K, B)] + r.normal(0, 0.5, (B, d))).astype(np.float32).astype(np.float64)
+    g = FloatGallery(G, _lib.METRIC_EUCLIDEAN)
+    Qd = g.query_rows(Q)
+    monkeypatch.setenv("OFR_MERGE_DEEP", "0")
+    qq = g.quantize_queries(Qd, tier="f6")
+    out = g.search_q8_phase(3, Qd, qq, k)
+    torch.cuda.synchronize()
+    bad = open_rows(qq["cert"])
+    assert int(bad.numel()) >= 5, int(bad.numel())
+    rows = bad[:5]
+    before_i = out[1].clone()
+    monkeypatch.delenv("OFR_MERGE_DEEP", raising=False)
+    still = g._resieve(Qd, rows, k, out, 0, qq)
+    torch.cuda.synchronize()
+    done = sorted(set(rows.cpu().tolist()) - set(still.cpu().tolist()))
+    assert len(done) >= 4, (rows.cpu().tolist(), still.cpu().tolist())
+    other = sorted(set(range(B)) - set(rows.cpu().tolist()))
+    assert torch.equal(out[1][other], before_i[other])
+    dd, ii = out[0].cpu().numpy()[done], out[1].cpu().numpy()[done]
+    _check_search("EuclideanDistance", Q[done], G, dd, ii, k)
+
+
 def test_knn_f6_tier_certifies_separated_data(monkeypatch):
     """f6 tier on well-separated identities (integer prototypes, +-1 noise, 10 rows per identity so
     that the 16 candidates reach past the query's own identity): the fp6 tier alone must certify
