@@ -1440,7 +1440,8 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t lane = threadIdx.x & 63;
   const int64_t nsteps = (p.B + TQ - 1) / TQ, ntg = (p.N + TGI - 1) / TGI;
-  const int64_t ngrp = (nsteps + qg - 1) / qg, items = ntg * ngrp;
+  // items in tile octets (ntg rounded up to 8): see the item map below
+  const int64_t ngrp = (nsteps + qg - 1) / qg, items = ((ntg + 7) & ~(int64_t)7) * ngrp;
   if ((int64_t)blockIdx.x >= items) return;
   int scs;   // the lane's stage-0 block scale byte (its 32-feature block lane >> 4)
   {
@@ -1462,7 +1463,12 @@ __global__ void __launch_bounds__(256, 2) prefix_wave_kernel(TileArgs p, const u
   const int g4 = (int)(lane >> 4) * 4, r16 = (int)(lane & 15);
   const uint32_t ng32 = (uint32_t)ngrp, qg32 = (uint32_t)qg;
   for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
-    const int64_t gt = (int64_t)((uint32_t)w / ng32), s0 = (int64_t)(((uint32_t)w % ng32) * qg32);
+    // item w: gallery tile (w / (8 ngrp)) 8 + w % 8, query group (w / 8) % ngrp -- the ngrp items of one tile
+    // are w, w + 8, ...: on workgroups of one XCD (workgroup b runs on XCD b % 8, the grid is a multiple of 8)
+    // at about one time, so the tile's fragments come from that XCD's L2 after the first (round 6)
+    const uint32_t wu = (uint32_t)w;
+    const int64_t gt = (int64_t)((wu / (8u * ng32)) * 8u + (wu & 7u)), s0 = (int64_t)(((wu >> 3) % ng32) * qg32);
+    if (gt >= ntg) continue;   // uniform: the last octet's missing tiles
     const int64_t s1 = s0 + qg < nsteps ? s0 + qg : nsteps;
     const int64_t g0 = gt * TGI + wave * WR;   // the wave's first row
     const int nvalid = p.N - g0 < WR ? (int)(p.N - g0) : WR;
@@ -3756,7 +3762,7 @@ static int knn_f6_impl(void* stream, int phases, const float* Q, int64_t B, int6
                              a.qscale, B, nq4, qtab);
           OFR_LAUNCH_CHECK("f6 prefix_tables_kernel");
           const int64_t qg4 = f6p_group_wave(ntg4, ns4, slots, w8 ? 12 : 24);
-          const int64_t items4 = ntg4 * cdiv(ns4, qg4);
+          const int64_t items4 = round_up(ntg4, 8) * cdiv(ns4, qg4);   // the kernel's tile octets
           OFR_CHECK_ARG(items4 < 0x7fffffffLL, "ofr_knn_f6: grid too large");
           const dim3 g4((unsigned)std::min<int64_t>(items4, slots));
           // probe OFR_F6P_PREFETCH=2: two steps in flight (242 VGPRs) measured equal (profiles/r06_prefix_wave_parts.txt)
