@@ -64,12 +64,12 @@ struct Args {
 // l: row 16 i + 4 (l / 16) + reg = block i / 8, slice (i % 8) / 2, feature (i % 2) * 16 + 4 (l / 16) + reg
 // of the block; image 64 W + 16 c + l % 16.  The epilogue combines the four slices exactly as
 // project_epilogue (the same fp64 operations in the same order: identical results).
-template <int W>
+template <int W, bool REG>
 __device__ __forceinline__ void project_w_body(const Args& p, int64_t ft, int64_t b0) {
   i8w::i32x4 acc[i8w::NA][i8w::NB];
   i8w::Feed f;
   i8w::feed_init(f, p.Aq, p.ldk, p.arows, ft * i8w::TA, p.X, p.ldx, p.B, b0);
-  i8w::mainloop<W>(f, p.nk, acc);
+  i8w::mainloop<W, REG>(f, p.nk, acc);
   const int lane = threadIdx.x & 63, l16 = lane & 15, g = lane >> 4;
   // Epilogue through the wave's own 32 KiB of LDS (free after the main loop's last barrier): per
   // projection block, its 8 x 4 accumulators are stored as they are (ds_write takes AGPR data) and read
@@ -140,16 +140,18 @@ __device__ __forceinline__ void project_w_body(const Args& p, int64_t ft, int64_
   }
 }
 
+// REG: the engine's register-staged stage copies (i8w::mainloop, OFR_PROJ_STAGE=reg) instead of LDS-DMA
+template <bool REG>
 __global__ void __launch_bounds__(i8w::NT, 1) project_q8w_kernel(Args p) {
   const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   int64_t ft, bt;
   i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
   const int64_t b0 = bt * i8w::TB;
   switch (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {   // the wave's role, compile time below
-    case 0: project_w_body<0>(p, ft, b0); break;
-    case 1: project_w_body<1>(p, ft, b0); break;
-    case 2: project_w_body<2>(p, ft, b0); break;
-    default: project_w_body<3>(p, ft, b0); break;
+    case 0: project_w_body<0, REG>(p, ft, b0); break;
+    case 1: project_w_body<1, REG>(p, ft, b0); break;
+    case 2: project_w_body<2, REG>(p, ft, b0); break;
+    default: project_w_body<3, REG>(p, ft, b0); break;
   }
 }
 
@@ -340,6 +342,15 @@ static bool getenv_flag_gemv() {
   return f;
 }
 
+// OFR_PROJ_STAGE: "reg" (register-staged stage copies) or "dma" (LDS-DMA); read once
+static bool proj_stage_reg() {
+  static const bool f = [] {
+    const char* e = getenv("OFR_PROJ_STAGE");
+    return e && strcmp(e, "reg") == 0;
+  }();
+  return f;
+}
+
 extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx, const int8_t* Aq,
                                     int64_t ldk, const double* scale, const double* K, int64_t d, const double* shift,
                                     void* Y, int64_t ldy, int y_dtype) {
@@ -353,8 +364,11 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   OFR_CHECK_ARG(ldy >= d, "ofr_project_u8_exact: ldy < d");
   static std::atomic<bool> attr_done{false};
   if (!attr_done.load(std::memory_order_acquire)) {
-    hipError_t e = hipFuncSetAttribute((const void*)q8::project_q8w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       q8::PROJ_LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)q8::project_q8w_kernel<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, q8::PROJ_LDS);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)q8::project_q8w_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              q8::PROJ_LDS);
     if (e != hipSuccess) return hip_status(e, "hipFuncSetAttribute(project_q8w)");
     attr_done.store(true, std::memory_order_release);
   }
@@ -394,8 +408,12 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   p.nk = (int)cdiv(D, i8w::BK);
   p.ntb = cdiv(B, i8w::TB);
   OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
-  hipLaunchKernelGGL(q8::project_q8w_kernel, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), q8::PROJ_LDS,
-                     (hipStream_t)stream, p);
+  if (proj_stage_reg())
+    hipLaunchKernelGGL(q8::project_q8w_kernel<true>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), q8::PROJ_LDS,
+                       (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(q8::project_q8w_kernel<false>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), q8::PROJ_LDS,
+                       (hipStream_t)stream, p);
   OFR_LAUNCH_CHECK("project_q8w_kernel");
   return OFR_OK;
 }

@@ -26,7 +26,8 @@ LIB = os.path.join(os.path.dirname(__file__), "..", "opencv_facerecognizer_amd",
 
 # demangled-name prefixes
 ZERO = [
-    "ofr::q8::project_q8w_kernel(",
+    "void ofr::q8::project_q8w_kernel<false>(",
+    "void ofr::q8::project_q8w_kernel<true>(",
     "void ofr::q8s::tile_kernel_f6w<1>(",
 ]
 # asm-MFMA kernels allowed to keep invariant spills, with upper bounds on the counts

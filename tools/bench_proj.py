@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--d", type=int, default=9999)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--check-rows", type=int, default=64)
-    ap.add_argument("--engines", default="i8")
+    ap.add_argument("--engines", default="dma,reg")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -73,7 +73,7 @@ def main():
         if eng.startswith("lib="):
             env = dict(os.environ, OFR_LIB=eng[4:])
         else:
-            env = dict(os.environ, OFR_PROJ_ENGINE=eng)
+            env = dict(os.environ, OFR_PROJ_ENGINE=eng, OFR_PROJ_STAGE=eng)   # stage copies: dma | reg
         key = f"{len(res['engines'])}:{eng}"
         out = f"{tmp}_{len(res['engines'])}"
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--out", out, "--batch", str(a.batch), "--D",
