@@ -218,8 +218,12 @@ class StepPipeline:
         # preparation s+1 -- the short sample pass and the HBM-bound merge share the chip, everything else
         # runs alone
         # "prep": merge s-1 behind tile pass s on the side stream, beside preparation s+1 on the main one
-        self.merge_at = merge_at or os.environ.get("OFR_BENCH_MERGE", "after")
-        assert self.merge_at in ("after", "sieve", "sample", "prep"), self.merge_at
+        self.merge_at = merge_at or os.environ.get("OFR_BENCH_MERGE", "tail")
+        # "tail" (the default since late round 6): as "after", but merge s-1 waits only for the full rounds of
+        # preparation s+1's projection and runs beside its last, partial round (144 of 1,680 tiles on 256 CUs:
+        # 112 CUs idle), the prep function taking a hook it calls between the two launches: 2.335 -> 2.29 ms
+        # per step (profiles/r06_merge_tail_ab.txt)
+        assert self.merge_at in ("after", "sieve", "sample", "prep", "tail"), self.merge_at
         self.main = torch.cuda.current_stream(device)
         self.side = torch.cuda.Stream(device=device) if overlap else self.main
         self.ws = [Workspace() for _ in range(self.NWS)]
@@ -227,6 +231,7 @@ class StepPipeline:
         self.ev_merged = [torch.cuda.Event() for _ in range(self.NWS)]    # workspace's merge done (side)
         self.ev_tiles = torch.cuda.Event()                                # latest tile pass done (main)
         self.ev_sample = torch.cuda.Event()                               # latest sample pass done (main)
+        self.ev_parta = torch.cuda.Event()                                # projection's full rounds done (tail)
         self.ev_done = [torch.cuda.Event() for _ in range(self.NBUF)]     # buffer's fallback done (side)
         # the side stream starts behind everything the main stream has queued (gallery and tier builds,
         # the query images, buffer fills): an unrecorded event is no dependency, and once the caching
@@ -235,11 +240,14 @@ class StepPipeline:
         if self.side is not self.main:
             self.side.wait_stream(self.main)
 
-    def _prep(self, s, ev, stream=None):
+    def _prep(self, s, ev, stream=None, hook=None):
         with torch.cuda.stream(stream or self.side):
             if ev:
                 ev[0].record()
-            self.prep_fn(s % self.NBUF)
+            if hook is None:
+                self.prep_fn(s % self.NBUF)
+            else:
+                self.prep_fn(s % self.NBUF, hook)
             if ev:
                 ev[1].record()
             self.ev_ready[s % self.NBUF].record(stream or self.side)
@@ -248,12 +256,19 @@ class StepPipeline:
         with torch.cuda.stream(self.side):
             return self.finish_fn(s % self.NBUF)
 
-    def _merge(self, s, ev):
+    def _merge_tail(self, s, ev):
+        """The prep hook of merge_at "tail" (called on the main stream between the projection's launches)."""
+        self.ev_parta.record(self.main)
+        self._merge(s, ev, after=self.ev_parta)
+
+    def _merge(self, s, ev, after=None):
         j, w = s % self.NBUF, s % self.NWS
         with torch.cuda.stream(self.side):
             # behind the next batch's sample pass ("sieve"), its preparation ("sample") or its whole tile pass
-            # ("after")
-            if self.merge_at == "sample":   # (the tile pass too: the last batch has no next preparation)
+            # ("after"); "tail": behind the full rounds of the next preparation's projection
+            if after is not None:
+                self.side.wait_event(after)
+            elif self.merge_at == "sample":   # (the tile pass too: the last batch has no next preparation)
                 self.side.wait_event(self.ev_tiles)
                 self.side.wait_event(self.ev_ready[(s + 1) % self.NBUF])
             else:
@@ -292,14 +307,16 @@ class StepPipeline:
             if ev[s]:
                 ev[s][2].record(self.main)
             self.ev_tiles.record(self.main)
-            if self.merge_at in ("after", "sample", "prep"):
-                if s >= 1 and self.merge_at in ("after", "prep"):   # merge s-1 behind tile pass s
-                    self._merge(s - 1, ev[s - 1])
+            if self.merge_at in ("after", "sample", "prep", "tail"):
+                tail = self.merge_at == "tail" and s >= 1 and s + 1 < steps
+                if s >= 1 and (self.merge_at in ("after", "prep") or (self.merge_at == "tail" and not tail)):
+                    self._merge(s - 1, ev[s - 1])           # merge s-1 behind tile pass s
                 if s + 1 < steps:                           # preparation s+1 behind that merge, on main
-                    if s >= 1 and self.merge_at != "prep":
+                    if s >= 1 and self.merge_at not in ("prep", "tail"):
                         self.main.wait_event(self.ev_merged[(s - 1) % self.NWS])
                     self.main.wait_event(self.ev_done[(s + 1) % self.NBUF])   # its buffer's fallback done
-                    self._prep(s + 1, ev[s + 1], stream=self.main)
+                    hook = (lambda s_=s: self._merge_tail(s_ - 1, ev[s_ - 1])) if tail else None
+                    self._prep(s + 1, ev[s + 1], stream=self.main, hook=hook)
                 if s >= 1:
                     res = self._finish(s - 1)
                     self.ev_done[(s - 1) % self.NBUF].record(self.side)
@@ -719,11 +736,16 @@ def main():
                  Qd_loc=torch.zeros((b1 - b0, ld), dtype=torch.float32, device=device) if shard_prep else None)
             for j in range(StepPipeline.NBUF)]
 
-    def prep(j):
-        """Query batch -> centred fp32 search rows (+ the first tier's quantized rows) in buffer j."""
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+
+    def prep(j, hook=None):
+        """Query batch -> centred fp32 search rows (+ the first tier's quantized rows) in buffer j.  hook
+        (StepPipeline merge_at "tail"): called between the projection's full rounds and its last round."""
         b = bufs[j]
         if shard_prep:
             P.project(Xqs[j][b0:b1], shift64=gallery.shift64, out=b["Qd_loc"])   # this rank's faces
+            if hook is not None:
+                hook()
             if use_q8:
                 tier = gallery.start_tier(B) if tier0 == "f6" else tier0
                 starts.append(str(tier))
@@ -735,11 +757,21 @@ def main():
             else:
                 b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
         else:
-            P.project(Xqs[j], shift64=gallery.shift64, out=b["Qd"])      # fp32(W^T x - c), exact int8 MFMA
+            nt = P.tile_count(B) if hook is not None else 0
+            if nt > ncu:   # the full rounds, the hook (the merge's launch, waiting for them), the last round
+                split = (nt - 1) // ncu * ncu
+                P.project(Xqs[j], shift64=gallery.shift64, out=b["Qd"], tiles=(0, split))
+                hook()
+                P.project(Xqs[j], shift64=gallery.shift64, out=b["Qd"], tiles=(split, nt))
+            else:
+                P.project(Xqs[j], shift64=gallery.shift64, out=b["Qd"])  # fp32(W^T x - c), exact int8 MFMA
+                if hook is not None:
+                    hook()
             if use_q8:       # the adaptive start tier (FloatGallery.start_tier; f6 here)
                 tier = gallery.start_tier(B) if tier0 == "f6" else tier0
                 starts.append(str(tier))
                 b["qq"] = gallery.quantize_queries(b["Qd"], b["qq"], tier=tier)
+                b["tier"] = tier
 
     def tiles(j, w, part):
         b = bufs[j]
@@ -800,6 +832,23 @@ def main():
     ms_sample = np.mean([e[4].elapsed_time(e[6]) for e in ev])    # its sample pass + thresholds
     ms_sieve = np.mean([e[6].elapsed_time(e[2]) for e in ev])     # its sieve pass (fp6; else the rest)
     ms_merge = np.mean([e[5].elapsed_time(e[3]) for e in ev])     # merge + certificate on the side stream
+    # the preparation alone (the last batch's projection + quantization again, same outputs): with merge_at
+    # "tail" the step's preparation events also span the merge run beside the projection's last round
+    ms_proj_alone = None
+    if not shard_prep and world == 1:
+        xs, tq = Xqs[last], bufs[last].get("tier", tier0)
+        ms_pa = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            P.project(xs, shift64=gallery.shift64, out=Qd)
+            if use_q8:
+                qq = gallery.quantize_queries(Qd, qq, tier=tq)
+            e1.record()
+            torch.cuda.synchronize()
+            ms_pa.append(e0.elapsed_time(e1))
+        ms_proj_alone = float(np.median(ms_pa))
+    ms_prep_roof = ms_proj_alone if ms_proj_alone is not None else ms_proj
     idx = res[1][:, 0]
     acc = float(((idx // args.per_id) == ids_qs[last]).double().mean().item())   # the last batch's identities
     kept = (gallery.sieve_counts(B, pipe.ws[(args.steps - 1) % StepPipeline.NWS]) if args.search == "f6"
@@ -979,7 +1028,8 @@ def main():
             "roofline_merge": merge_roof,
             "kernels_ms": {"project_u8_exact" + ("+quantize" if use_q8 else "") + ("+all_gather" if shard_prep else ""):
                            ms_proj, "knn_tiles": ms_tiles,
-                           "knn_merge_rerank" + ("+certificate" if use_q8 else ""): ms_merge},
+                           "knn_merge_rerank" + ("+certificate" if use_q8 else ""): ms_merge,
+                           "preparation_alone": ms_proj_alone},
             # the preparation beside the dominant kernel (round 5: the two take about the same time): the
             # exact projection W^T x of the batch's faces on the int8 MFMA, four W slices --
             # 2 D d int8 ops per face and slice, timed with the quantization by the preparation's events
@@ -987,15 +1037,15 @@ def main():
                 "kernel": "q8::project_q8w_kernel (ofr_project_u8_exact, 4 int8 slices of W) + quantization",
                 "bound": "mfma", "unit": "TOPS", "peak": PEAK_I8_MFMA / 1e12,
                 "algorithmic_ops_per_step": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d,
-                "achieved": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d / (ms_proj * 1e-3) / 1e12,
-                "frac": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d / (ms_proj * 1e-3) / PEAK_I8_MFMA,
-                "ms": ms_proj},
+                "achieved": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d / (ms_prep_roof * 1e-3) / 1e12,
+                "frac": 2.0 * 4 * (b1 - b0 if shard_prep else B) * D * d / (ms_prep_roof * 1e-3) / PEAK_I8_MFMA,
+                "ms": ms_prep_roof, "ms_source": "alone" if ms_proj_alone is not None else "step events"},
             # which of the two is longer per step: since the one-stage prefix pass, the preparation's
             # projection (roofline_preparation); `roofline` stays the search pass's (the path's own kernel)
             "dominant_by_time": {"kernel": ("q8::project_q8w_kernel (roofline_preparation)"
-                                            if ms_proj > (ms_sieve if args.search == "f6" else ms_tiles)
+                                            if ms_prep_roof > (ms_sieve if args.search == "f6" else ms_tiles)
                                             else "the search pass (roofline)"),
-                                 "preparation_ms": ms_proj,
+                                 "preparation_ms": ms_prep_roof,
                                  "search_pass_ms": ms_sieve if args.search == "f6" else ms_tiles},
             "uncertified_queries_per_step": (float(np.mean(fallbacks[-args.steps:])) if use_q8 else None),
             "start_tiers": ({t: starts[-args.steps:].count(t) for t in sorted(set(starts[-args.steps:]))}

@@ -64,7 +64,7 @@ int ofr_device_check(int device);      /* OFR_OK iff `device` is gfx950 */
  *          PCA.project          feature.py:114-116 (shift = P^T mu),
  *          LDA.project          feature.py:184-185, and the per-sample
  *          projection loops feature.py:104-108, 178-182, 231-235.
- * EXACT integer path on v_mfma_i32_32x32x32_i8: W is prepared once into four
+ * EXACT integer path on v_mfma_i32_16x16x64_i8: W is prepared once into four
  * int8 slices with a power-of-two scale per output feature
  * (W[i][j] = s_j (q1 + q2/2^7 + q3/2^14 + q4/2^21), exact for every fp32
  * element within 2^4 of its column maximum); (x-128) . q is accumulated in
@@ -81,6 +81,15 @@ int ofr_qproj_prepare(void* stream, int dtype, const void* Wt, int64_t d, int64_
 int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx,
                          const int8_t* Aq, int64_t ldk, const double* scale, const double* K,
                          int64_t d, const double* shift, void* Y, int64_t ldy, int y_dtype);
+/* The same product as a launch over tiles [t0, t1) of its grid (one tile per CU and round):
+ * ofr_project_u8_exact_tiles(B, d) = the tile count (0 when B <= 4 takes the split-K GEMV, which has
+ * no tiles); every tile writes its own outputs, so launches over a partition of [0, tiles) give
+ * ofr_project_u8_exact's output bit for bit (lets a caller run other work beside the last round). */
+int64_t ofr_project_u8_exact_tiles(int64_t B, int64_t d);
+int ofr_project_u8_exact_range(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx,
+                               const int8_t* Aq, int64_t ldk, const double* scale, const double* K,
+                               int64_t d, const double* shift, void* Y, int64_t ldy, int y_dtype,
+                               int64_t t0, int64_t t1);
 
 /* Gallery preparation ------------------------------------------------------
  * For the search kernels: aux[n] = ||G[n]||^2 (EUCLIDEAN) or 1/||G[n]|| (COSINE),

@@ -188,16 +188,25 @@ class Projection:
             return self._Wt_src[:, :self.D].double().t()
         return f64_dev(np.asarray(self.W_host, np.float64))
 
-    def project(self, Xd, shift64=None, out=None, f64=False):
-        """Xd: uint8 [B][ldx] device rows.  fp32 [B][ldy] (zero pad) or fp64 [B][d]."""
+    def project(self, Xd, shift64=None, out=None, f64=False, tiles=None):
+        """Xd: uint8 [B][ldx] device rows.  fp32 [B][ldy] (zero pad) or fp64 [B][d].
+        tiles=(t0, t1): only the grid's tiles [t0, t1) (ofr_project_u8_exact_range; see tile_count)."""
         B = Xd.shape[0]
         if out is None:
             out = torch.empty((B, self.d), dtype=torch.float64, device=Xd.device) if f64 else \
                 torch.zeros((B, self.ldy), dtype=torch.float32, device=Xd.device)
         ydt = _lib.DT_F64 if out.dtype == torch.float64 else _lib.DT_F32
-        call("ofr_project_u8_exact", stream(), ptr(Xd), B, self.D, Xd.shape[1], ptr(self.Aq), self.ldk,
-             ptr(self.scale), ptr(self.K), self.d, ptr(shift64), ptr(out), out.shape[1], ydt)
+        args = (stream(), ptr(Xd), B, self.D, Xd.shape[1], ptr(self.Aq), self.ldk, ptr(self.scale), ptr(self.K),
+                self.d, ptr(shift64), ptr(out), out.shape[1], ydt)
+        if tiles is None:
+            call("ofr_project_u8_exact", *args)
+        else:
+            call("ofr_project_u8_exact_range", *args, int(tiles[0]), int(tiles[1]))
         return out
+
+    def tile_count(self, B):
+        """Tiles of the projection grid for B faces (0: the B <= 4 GEMV, no tiles)."""
+        return int(_lib.load().ofr_project_u8_exact_tiles(B, self.d))
 
 
 def center_round(F64, shift64, ld, out=None):

@@ -39,6 +39,9 @@ SIGNATURES = {
     "ofr_qproj_prepare": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "ofr_project_u8_exact": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp,
                                      c_i64, c_int]),
+    "ofr_project_u8_exact_tiles": (c_i64, [c_i64, c_i64]),
+    "ofr_project_u8_exact_range": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                           c_vp, c_i64, c_int, c_i64, c_i64]),
     "ofr_center_round_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64]),
     "ofr_row_aux": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "ofr_col_mean": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp]),

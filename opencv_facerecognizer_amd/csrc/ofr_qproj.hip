@@ -56,6 +56,7 @@ struct Args {
   int y_f64;
   int nk;
   int64_t ntf, ntb, gg;
+  int64_t t0;   // first tile of this launch (ofr_project_u8_exact_range)
 };
 
 // The wide engine (ofr_i8w_tile.h, round 3): 384 slice rows (96 features x 4 slices) x 256 images, 4
@@ -143,7 +144,7 @@ __device__ __forceinline__ void project_w_body(const Args& p, int64_t ft, int64_
 // REG: the engine's register-staged stage copies (i8w::mainloop, OFR_PROJ_STAGE=reg) instead of LDS-DMA
 template <bool REG>
 __global__ void __launch_bounds__(i8w::NT, 1) project_q8w_kernel(Args p) {
-  const int64_t t = i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int64_t t = p.t0 + i8t::xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   int64_t ft, bt;
   i8t::tile_coords(t, p.gg, p.ntf, p.ntb, ft, bt);
   const int64_t b0 = bt * i8w::TB;
@@ -351,9 +352,9 @@ static bool proj_stage_reg() {
   return f;
 }
 
-extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx, const int8_t* Aq,
-                                    int64_t ldk, const double* scale, const double* K, int64_t d, const double* shift,
-                                    void* Y, int64_t ldy, int y_dtype) {
+static int project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx, const int8_t* Aq,
+                            int64_t ldk, const double* scale, const double* K, int64_t d, const double* shift, void* Y,
+                            int64_t ldy, int y_dtype, int64_t t0, int64_t t1) {
   OFR_CHECK_ARG(B >= 0 && D >= 1 && d >= 1, "ofr_project_u8_exact: bad sizes");
   OFR_CHECK_ARG(y_dtype == OFR_DT_F32 || y_dtype == OFR_DT_F64, "ofr_project_u8_exact: y_dtype must be F32 or F64");
   if (B == 0) return OFR_OK;
@@ -373,6 +374,7 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
     attr_done.store(true, std::memory_order_release);
   }
   if (B <= 4 && getenv_flag_gemv()) {
+    OFR_CHECK_ARG(t0 == 0 && t1 < 0, "ofr_project_u8_exact_range: B <= 4 takes the GEMV path (no tiles)");
     hipStream_t st = (hipStream_t)stream;
     const int64_t arows = cdiv(d, 64) * 256;
     int* part = nullptr;
@@ -408,14 +410,41 @@ extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, i
   p.nk = (int)cdiv(D, i8w::BK);
   p.ntb = cdiv(B, i8w::TB);
   OFR_CHECK_ARG(p.ntf * p.ntb < 0x7fffffffLL, "ofr_project_u8_exact: grid too large");
+  if (t1 < 0) t1 = p.ntf * p.ntb;
+  OFR_CHECK_ARG(t0 >= 0 && t0 <= t1 && t1 <= p.ntf * p.ntb, "ofr_project_u8_exact_range: tiles out of range");
+  if (t0 == t1) return OFR_OK;
+  p.t0 = t0;
   if (proj_stage_reg())
-    hipLaunchKernelGGL(q8::project_q8w_kernel<true>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), q8::PROJ_LDS,
+    hipLaunchKernelGGL(q8::project_q8w_kernel<true>, dim3((unsigned)(t1 - t0)), dim3(i8w::NT), q8::PROJ_LDS,
                        (hipStream_t)stream, p);
   else
-    hipLaunchKernelGGL(q8::project_q8w_kernel<false>, dim3((unsigned)(p.ntf * p.ntb)), dim3(i8w::NT), q8::PROJ_LDS,
+    hipLaunchKernelGGL(q8::project_q8w_kernel<false>, dim3((unsigned)(t1 - t0)), dim3(i8w::NT), q8::PROJ_LDS,
                        (hipStream_t)stream, p);
   OFR_LAUNCH_CHECK("project_q8w_kernel");
   return OFR_OK;
+}
+
+extern "C" int ofr_project_u8_exact(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx, const int8_t* Aq,
+                                    int64_t ldk, const double* scale, const double* K, int64_t d, const double* shift,
+                                    void* Y, int64_t ldy, int y_dtype) {
+  return project_u8_exact(stream, X, B, D, ldx, Aq, ldk, scale, K, d, shift, Y, ldy, y_dtype, 0, -1);
+}
+
+// The launch in two tile ranges (round 6): the tiles are dealt to the CUs in rounds of one tile per CU, so a
+// caller can run the full rounds and the last, partial round as two launches and put other work beside the
+// second (the bench's merge_at "tail").  Same tiles, same integers: identical outputs.
+extern "C" int64_t ofr_project_u8_exact_tiles(int64_t B, int64_t d) {
+  if (B <= 0 || d <= 0) return 0;
+  if (B <= 4 && getenv_flag_gemv()) return 0;
+  return cdiv(cdiv(d, 64) * 256, i8w::TA) * cdiv(B, i8w::TB);
+}
+
+extern "C" int ofr_project_u8_exact_range(void* stream, const uint8_t* X, int64_t B, int64_t D, int64_t ldx,
+                                          const int8_t* Aq, int64_t ldk, const double* scale, const double* K,
+                                          int64_t d, const double* shift, void* Y, int64_t ldy, int y_dtype,
+                                          int64_t t0, int64_t t1) {
+  OFR_CHECK_ARG(t1 >= 0, "ofr_project_u8_exact_range: t1 < 0");
+  return project_u8_exact(stream, X, B, D, ldx, Aq, ldk, scale, K, d, shift, Y, ldy, y_dtype, t0, t1);
 }
 
 extern "C" int ofr_center_round_f64(void* stream, const double* F, int64_t N, int64_t d, int64_t ldf,

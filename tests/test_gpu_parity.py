@@ -680,6 +680,36 @@ def test_projection_small_batch_gemv_identical(D, d):
             np.testing.assert_array_equal(small32, big32[s:s + B])
 
 
+@pytest.mark.parametrize("B,D,d", [(600, 10000, 130), (1000, 777, 450)])
+def test_projection_tile_ranges_identical(B, D, d):
+    """ofr_project_u8_exact_range: launches over a partition of the grid's tiles (the bench's merge_at
+    "tail" runs the last round as its own launch) give ofr_project_u8_exact's output bit for bit; empty and
+    out-of-range ranges; B <= 4 (the GEMV) has no tiles."""
+    import torch
+    from opencv_facerecognizer_amd import _lib
+    from opencv_facerecognizer_amd._device import Projection, f64_dev, u8_rows
+    r = _rng(B + D + d)
+    W = r.normal(0, 1.0 / np.sqrt(D), (D, d))
+    X = u8_rows(r.integers(0, 256, (B, D), dtype=np.uint8))
+    P = Projection(W)
+    c = f64_dev(r.normal(0, 3, d))
+    want = P.project(X, shift64=c).cpu().numpy()
+    want64 = P.project(X, shift64=c, f64=True).cpu().numpy()
+    nt = P.tile_count(B)
+    assert nt == -(-(-(-d // 64) * 256) // 384) * -(-B // 256)
+    for cuts in ([0, nt], [0, nt // 2, nt], [0, 1, nt - 1, nt], [0, 0, nt]):
+        got = torch.full(want.shape, float("nan"), dtype=torch.float32, device=X.device)
+        got64 = torch.full((B, d), float("nan"), dtype=torch.float64, device=X.device)
+        for t0, t1 in zip(cuts, cuts[1:]):
+            P.project(X, shift64=c, out=got, tiles=(t0, t1))
+            P.project(X, shift64=c, out=got64, tiles=(t0, t1))
+        np.testing.assert_array_equal(got.cpu().numpy()[:, :d], want[:, :d])
+        np.testing.assert_array_equal(got64.cpu().numpy(), want64)
+    with pytest.raises(_lib.OfrError):
+        P.project(X, shift64=c, tiles=(0, nt + 1))
+    assert P.tile_count(3) == 0
+
+
 def test_projection_fp32_weights_exact():
     """fp32 weights within 2^4 of their column maximum are represented exactly: the result equals the
     correctly rounded float64 dot product of the fp32 W."""

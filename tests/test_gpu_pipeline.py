@@ -32,7 +32,7 @@ def _setup(noise, N=20_000, d=512, side=32, per=10, B=512, batches=5):
     return P, g, X
 
 
-@pytest.mark.parametrize("merge_at", ["after", "sieve", "sample", "prep"])
+@pytest.mark.parametrize("merge_at", ["after", "sieve", "sample", "prep", "tail"])
 @pytest.mark.parametrize("noise", [12.0, 40.0])
 def test_step_pipeline_matches_one_shot(noise, merge_at):
     """noise 40: crowded identities, so the fallback tiers run inside finish() while the next tile
@@ -60,11 +60,18 @@ def test_step_pipeline_matches_one_shot(noise, merge_at):
     order = []           # batch index per preparation, in enqueue order
     got = []
 
-    def prep(j):
+    def prep(j, hook=None):
         s = len(order)
         order.append(s)
         bufs[j]["batch"] = s
-        P.project(X[s], shift64=g.shift64, out=bufs[j]["Qd"])
+        if hook is None:
+            P.project(X[s], shift64=g.shift64, out=bufs[j]["Qd"])
+        else:   # "tail": the projection in two tile ranges, the merge launched between them
+            nt = P.tile_count(B)
+            assert nt >= 2
+            P.project(X[s], shift64=g.shift64, out=bufs[j]["Qd"], tiles=(0, nt // 2))
+            hook()
+            P.project(X[s], shift64=g.shift64, out=bufs[j]["Qd"], tiles=(nt // 2, nt))
         bufs[j]["qq"] = g.quantize_queries(bufs[j]["Qd"], bufs[j]["qq"], tier="f6")
 
     def tiles(j, w, part):
