@@ -536,6 +536,22 @@ def feature_profile(gallery, rows=8192):
             "f6_residual_rel_median": float(np.median(rel)), "f6_residual_rel_max": float(rel.max()), "rows": n}
 
 
+def project_split(P, X, shift64, out, hook, device):
+    """The batch's exact projection into out; with a hook (StepPipeline merge_at "tail"): its full rounds of
+    tiles, the hook (which launches the previous batch's merge behind them), then the last, partial round."""
+    nt = P.tile_count(X.shape[0]) if hook is not None else 0
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    if nt > ncu:
+        split = (nt - 1) // ncu * ncu
+        P.project(X, shift64=shift64, out=out, tiles=(0, split))
+        hook()
+        P.project(X, shift64=shift64, out=out, tiles=(split, nt))
+    else:
+        P.project(X, shift64=shift64, out=out)
+        if hook is not None:
+            hook()
+
+
 def stress_run(P, bank, args, noise, device, N=None):
     """Crowded neighbours: the headline shape (1M gallery, B = 4096, d = 9999) with the pixel noise
     raised so that identities crowd together and the fp6 certificate fails; the uncertified queries
@@ -562,8 +578,8 @@ def stress_run(P, bank, args, noise, device, N=None):
 
     starts = []
 
-    def prep(j):
-        P.project(Xq, shift64=gallery.shift64, out=bufs[j]["Qd"])
+    def prep(j, hook=None):
+        project_split(P, Xq, gallery.shift64, bufs[j]["Qd"], hook, device)
         tier = gallery.start_tier(B)          # adaptive start (FloatGallery.start_tier): f6 unless it keeps failing
         if timed:
             starts.append(str(tier))
@@ -736,8 +752,6 @@ def main():
                  Qd_loc=torch.zeros((b1 - b0, ld), dtype=torch.float32, device=device) if shard_prep else None)
             for j in range(StepPipeline.NBUF)]
 
-    ncu = torch.cuda.get_device_properties(device).multi_processor_count
-
     def prep(j, hook=None):
         """Query batch -> centred fp32 search rows (+ the first tier's quantized rows) in buffer j.  hook
         (StepPipeline merge_at "tail"): called between the projection's full rounds and its last round."""
@@ -757,16 +771,7 @@ def main():
             else:
                 b["Qd"] = gather_rows(b["Qd_loc"])                        # RCCL all-gather
         else:
-            nt = P.tile_count(B) if hook is not None else 0
-            if nt > ncu:   # the full rounds, the hook (the merge's launch, waiting for them), the last round
-                split = (nt - 1) // ncu * ncu
-                P.project(Xqs[j], shift64=gallery.shift64, out=b["Qd"], tiles=(0, split))
-                hook()
-                P.project(Xqs[j], shift64=gallery.shift64, out=b["Qd"], tiles=(split, nt))
-            else:
-                P.project(Xqs[j], shift64=gallery.shift64, out=b["Qd"])  # fp32(W^T x - c), exact int8 MFMA
-                if hook is not None:
-                    hook()
+            project_split(P, Xqs[j], gallery.shift64, b["Qd"], hook, device)   # fp32(W^T x - c), exact int8 MFMA
             if use_q8:       # the adaptive start tier (FloatGallery.start_tier; f6 here)
                 tier = gallery.start_tier(B) if tier0 == "f6" else tier0
                 starts.append(str(tier))
@@ -807,7 +812,10 @@ def main():
         return b["out"]
 
     # OFR_BENCH_OVERLAP=0: everything on the main stream, in the same order
-    pipe = StepPipeline(device, prep, tiles, merge, finish, overlap=os.environ.get("OFR_BENCH_OVERLAP", "1") == "1")
+    # N > 1: "after" -- the merge's collectives (the pruned split merge's bound exchange) and the preparation's
+    # all-gathers stay strictly ordered on one communicator; "tail" would let them run on two streams at once
+    pipe = StepPipeline(device, prep, tiles, merge, finish, overlap=os.environ.get("OFR_BENCH_OVERLAP", "1") == "1",
+                        merge_at=None if world == 1 else os.environ.get("OFR_BENCH_MERGE", "after"))
     pipe.run(max(args.warmup, StepPipeline.NBUF))     # untimed; every buffer and workspace allocated
     torch.cuda.synchronize()
     if world > 1:
