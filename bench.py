@@ -176,8 +176,9 @@ def committed_traffic(cfg):
 
 
 class StepPipeline:
-    """The timed step's schedule over a sequence of query batches.  Default since round 6
-    (merge_at "after"): one kernel at a time, in the order sample pass s, sieve pass s, merge s-1 (side
+    """The timed step's schedule over a sequence of query batches.  Default since late round 6
+    (merge_at "tail", one GPU): as "after" below, except that merge s-1 runs beside the last, partial round of
+    preparation s+1's projection (prep's hook, project_split).  merge_at "after" (round 6; N > 1): one kernel at a time, in the order sample pass s, sieve pass s, merge s-1 (side
     stream, behind the sieve pass), preparation s+1 (main stream, behind that merge), with the host's
     certificate read of batch s-1 (a sync of the side stream only) issued after preparation s+1 is queued.
     merge_at "sieve" (rounds 3-5):
