@@ -11,7 +11,7 @@
 //     with a power-of-two scale s_j:  W[i][j] = s_j (q1 + q2/2^7 + q3/2^14 + q4/2^21)
 //     (exact for every fp32 element within 2^4 of the column maximum; the
 //     rest is truncated at 2^-28 of the column maximum);
-//   * x - 128 is an int8, so v_mfma_i32_32x32x32_i8 accumulates
+//   * x - 128 is an int8, so v_mfma_i32_16x16x64_i8 (the wide engine, ofr_i8w_tile.h) accumulates
 //     sum_i (x_i - 128) q_s[i][j] exactly in int32 (|sum| < 2^29);
 //   * the epilogue combines the four int32 sums and the exact offset
 //     128 * sum_i W[i][j] in fp64 without rounding (<= 50 significant bits),
